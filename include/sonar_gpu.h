@@ -1,0 +1,223 @@
+/*
+ * sonar_gpu.h -- C ABI of the MI355X (gfx950) implementation of the
+ * sonido-sonar per-frame DSP + alignment hot path.
+ *
+ * Library: sonido-sonar_amd/lib/libsonar_gpu.so (HIP kernels + C++ host code).
+ * Plain C types only: pointers, sizes, POD structs.  No torch, no HIP types.
+ *
+ * Every entry replaces one seam of the Go reference (RyanBlaney/sonido-sonar,
+ * paths relative to the repo root); INTEGRATION.md shows the cgo binding.
+ *
+ *   sonar_fingerprint          <- SpectralAnalyzer.ComputeSTFTWithWindow
+ *                                 (fingerprint/analyzers/spectral.go:385) fused with
+ *                                 MFCC.ComputeFrames (algorithms/spectral/mfcc.go:167),
+ *                                 the per-frame descriptors of
+ *                                 SpeechFeatureExtractor.extractSpectralFeatures
+ *                                 (fingerprint/extractors/speech.go:320) and
+ *                                 Energy.ComputeShortTimeEnergy (algorithms/temporal/energy.go:25)
+ *   sonar_pitch_yin            <- PitchDetector.DetectPitch per-frame YIN core
+ *                                 (algorithms/tonal/pitch_detection.go:225-420)
+ *   sonar_chroma_stft          <- MusicFeatureExtractor.extractChromaFeatures
+ *                                 (fingerprint/extractors/music.go:327) ->
+ *                                 ChromaSTFT.ComputeChroma (algorithms/chroma/chroma_stft.go:45)
+ *   sonar_ncc                  <- CrossCorrelation.Compute, NormalizedCrossCorrelation /
+ *                                 TimeDomain (algorithms/stats/correlation.go:131)
+ *   sonar_dtw                  <- DTWAlignment.Align (algorithms/stats/dtw.go:55)
+ *   sonar_generate_fingerprint <- FingerprintGenerator.GenerateFingerprint
+ *                                 (fingerprint/fingerprint.go:137)
+ *   sonar_align_features       <- AlignmentExtractor.ExtractAlignmentFeatures
+ *                                 (fingerprint/extractors/alignment.go:139)
+ *
+ * Conventions
+ *  - Every call returns SONAR_OK (0) or a negative SONAR_ERR_*; the message
+ *    (same text as the Go error where one exists) is in sonar_last_error(ctx).
+ *  - Buffers are owned by the caller.  With cfg->device_ptrs == 0 they are
+ *    host memory and the call is synchronous; with device_ptrs == 1 they are
+ *    device pointers on the ctx's device and the call is asynchronous on the
+ *    ctx stream (sonar_synchronize() waits).
+ *  - One ctx per OS thread / goroutine (the Go objects are not goroutine-safe
+ *    either).  Several ctxs may share one device.
+ */
+#ifndef SONAR_GPU_H
+#define SONAR_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SONAR_ABI_VERSION 1
+
+enum {
+  SONAR_OK = 0,
+  SONAR_ERR_INVALID = -1,      /* bad argument (message says which)            */
+  SONAR_ERR_TOO_SHORT = -2,    /* "signal too short for given window size ..."  */
+  SONAR_ERR_EMPTY = -3,        /* "empty signal" / "empty sequences provided"   */
+  SONAR_ERR_UNSUPPORTED = -4,  /* configuration not implemented on the GPU path */
+  SONAR_ERR_DEVICE = -5,       /* HIP runtime error                             */
+  SONAR_ERR_NOMEM = -6         /* device allocation failed                      */
+};
+
+/* window types: analyzers.WindowType (fingerprint/analyzers/windowing.go:13-23) */
+enum {
+  SONAR_WIN_HANN = 0, SONAR_WIN_HAMMING, SONAR_WIN_BLACKMAN, SONAR_WIN_BLACKMAN_HARRIS,
+  SONAR_WIN_KAISER, SONAR_WIN_TUKEY, SONAR_WIN_RECTANGULAR, SONAR_WIN_BARTLETT, SONAR_WIN_WELCH
+};
+
+enum { SONAR_F32 = 0, SONAR_F64 = 1 };              /* arithmetic / element types */
+enum { SONAR_FB_MEL = 0, SONAR_FB_BARK = 1 };       /* mel_scale.go / bark_scale.go */
+
+/* sonar_fp_cfg.flags: which outputs sonar_fingerprint produces */
+enum {
+  SONAR_FP_MFCC = 1u << 0,      /* out->mfcc       F x n_mfcc                        */
+  SONAR_FP_MAGNITUDE = 1u << 1, /* out->magnitude  F x (W/2+1)  (SpectrogramResult)  */
+  SONAR_FP_SPECTRAL = 1u << 2,  /* centroid..slope, flux (F-1), low/high energy ratio */
+  SONAR_FP_ZCR = 1u << 3,       /* out->zcr        F, on the pre-emphasised PCM       */
+  SONAR_FP_ENERGY = 1u << 4     /* out->energy     sonar_energy_frames(), pre-emphasised */
+};
+
+typedef struct sonar_ctx sonar_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+int sonar_create(int device, sonar_ctx** out);
+void sonar_destroy(sonar_ctx* ctx);
+const char* sonar_last_error(const sonar_ctx* ctx);
+int sonar_abi_version(void);
+/* Run on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the ctx-owned stream. */
+int sonar_set_stream(sonar_ctx* ctx, void* hip_stream);
+int sonar_synchronize(sonar_ctx* ctx);
+/* Average duration (ms) of the last `n` launches of the dominant kernel of
+ * the last call, measured with HIP events on the stream it ran on (bench). */
+int sonar_last_kernel_ms(sonar_ctx* ctx, double* ms);
+int sonar_enable_kernel_timing(sonar_ctx* ctx, int on);
+
+/* ---- sizes (same integer rules as the Go code) ------------------------ */
+/* (n - W)/H + 1, Go truncating division; <= 0 -> SONAR_ERR_TOO_SHORT
+ * (fingerprint/analyzers/spectral.go:409-412) */
+int64_t sonar_stft_frames(int64_t n, int32_t window_size, int32_t hop_size);
+/* Energy.ComputeShortTimeEnergy frame count, 0 when n < W or W,H <= 0 (energy.go:25-31) */
+int64_t sonar_energy_frames(int64_t n, int32_t window_size, int32_t hop_size);
+/* extractHarmonicFeatures frame count (1024/512), speech.go:469-471 */
+int64_t sonar_pitch_frames(int64_t n);
+
+/* ---- path A: fused STFT -> |X| -> filterbank -> ln -> DCT (+ descriptors) */
+typedef struct {
+  int32_t window_size;     /* STFT W (FFT size)                                     */
+  int32_t hop_size;        /* STFT H                                                */
+  int32_t window_type;     /* SONAR_WIN_*; always {Normalize, Symmetric} like spectral.go:415 */
+  int32_t sample_rate;     /* rate the algorithms see (0 reproduces GenerateFingerprint, F1) */
+  /* MFCCParams (mfcc.go:27-34); <=0 fields take the Go defaults of NewMFCCWithParams */
+  int32_t n_mfcc;
+  int32_t n_filters;
+  int32_t filterbank;      /* SONAR_FB_MEL / SONAR_FB_BARK                          */
+  int32_t use_lifter;
+  double low_freq;
+  double high_freq;
+  double lifter;
+  int32_t mfcc_input_power;/* 0: Compute() is fed |X| (speech.go:257); 1: fed |X|^2 (music.go:311, F5) */
+  int32_t energy_window;   /* ShortTimeEnergy frame size (extractor FeatureConfig.WindowSize) */
+  int32_t energy_hop;      /* ShortTimeEnergy hop                                   */
+  double preemph_alpha;    /* pre-emphasis for ZCR/energy (0.97 speech, pre_emphasis.go:116) */
+  uint32_t flags;          /* SONAR_FP_*                                            */
+  int32_t precision;       /* SONAR_F32 (throughput) / SONAR_F64 (parity)           */
+  int32_t pcm_dtype;       /* SONAR_F32 / SONAR_F64                                 */
+  int32_t out_dtype;       /* SONAR_F32 / SONAR_F64 element type of every output    */
+  int32_t device_ptrs;     /* 0: host buffers (sync); 1: device buffers (async)     */
+} sonar_fp_cfg;
+
+typedef struct {
+  void* mfcc;       /* F x n_mfcc                     */
+  void* magnitude;  /* F x (W/2+1)                    */
+  void* centroid;   /* F each ...                     */
+  void* rolloff;
+  void* bandwidth;
+  void* flatness;
+  void* crest;
+  void* slope;
+  void* flux;       /* F-1                            */
+  void* low_ratio;  /* F (per STFT frame)             */
+  void* high_ratio; /* F                              */
+  void* zcr;        /* F                              */
+  void* energy;     /* sonar_energy_frames(n, ew, eh) */
+} sonar_fp_out;
+
+void sonar_fp_cfg_default(sonar_fp_cfg* cfg);
+int sonar_fingerprint(sonar_ctx* ctx, const void* pcm, int64_t n, const sonar_fp_cfg* cfg,
+                      sonar_fp_out* out);
+
+/* ---- YIN per-frame core (frames of 1024 at hop 512, PitchDetector defaults).
+ * Writes the raw YIN result per frame (pitch Hz or 0, confidence 1-cmndf or 0)
+ * before the sequential octave-correction / median tracking, which the host
+ * layer (sonar_generate_fingerprint) applies.  pcm is float64. ----------- */
+int sonar_pitch_yin(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate,
+                    double* pitch_raw, double* conf_raw, int32_t* tau, int32_t device_ptrs);
+
+/* ---- chroma (music extractor): DC removal + pre-emphasis 0.95, frames of
+ * frame_size = n / n_frames at hop, normalised symmetric Hann, |DFT|^2 folded
+ * to 12 pitch classes over [80, 8000] Hz, unit-sum normalised. ----------- */
+int sonar_chroma_stft(sonar_ctx* ctx, const double* pcm, int64_t n, int64_t n_frames, int32_t hop,
+                      int32_t sample_rate, int32_t preprocess, double* chroma /* n_frames x 12 */,
+                      int32_t device_ptrs);
+
+/* ---- path B: normalized cross-correlation (float64) --------------------
+ * corr has 2L+1 entries, L = max(0, min(max_lag, na-1, nb-1)); metrics[10] =
+ * {peak_corr, peak_lag, peak_index, p_value, snr, sharpness, second_peak,
+ *  peak_to_sidelobe, overlap_length, num_lags} (correlation.go:131-200). */
+int sonar_ncc(sonar_ctx* ctx, const double* a, int64_t na, const double* b, int64_t nb,
+              int32_t max_lag, double* corr, double* metrics, int32_t device_ptrs);
+
+/* ---- path B: DTW (float64, Euclidean, symmetric2, optional Sakoe-Chiba band)
+ * q: nq x dim, r: nr x dim row-major.  path_* capacity >= nq + nr.  cost
+ * (nullable) receives costMatrix[1:] = nq x (nr+1) (dtw.go:96).  Path points
+ * are in forward order with cost = C[i][j] - C[i-1][j-1] (dtw.go:165-188). */
+int sonar_dtw(sonar_ctx* ctx, const double* q, int64_t nq, const double* r, int64_t nr, int32_t dim,
+              int32_t band, double* distance, int32_t* path_q, int32_t* path_r, double* path_cost,
+              int64_t* path_len, double* cost, int32_t device_ptrs);
+
+/* ---- host mirror of the Go API (C++ above the kernels) ------------------ */
+typedef struct sonar_result sonar_result;   /* named float64 arrays + scalars */
+
+typedef struct {              /* fingerprint.FingerprintConfig (fingerprint.go:29-35) */
+  int32_t window_size;        /* FingerprintConfig.WindowSize (STFT)                 */
+  int32_t hop_size;           /* FingerprintConfig.HopSize                            */
+  int32_t feature_window_size;/* FingerprintConfig.FeatureConfig.WindowSize (energy)  */
+  int32_t feature_hop_size;   /* FingerprintConfig.FeatureConfig.HopSize              */
+  int32_t enable_content_detect;
+  int32_t window_type;        /* content settings WindowType (all Hann in the tables) */
+  int32_t precision;          /* SONAR_F32 / SONAR_F64                                */
+} sonar_fingerprint_config;
+
+void sonar_fingerprint_config_default(sonar_fingerprint_config* cfg);  /* fingerprint.go:70-98 */
+
+/* AudioData{PCM, SampleRate, Metadata.ContentType}.  content_type is the raw
+ * metadata string ("music", "news", "talk", ... ; unknown strings -> content
+ * detection, F12).  Returns arrays named like ExtractedFeatures fields:
+ * "mfcc", "spectral_centroid", ..., "short_time_energy", "pitch_estimate", ... */
+int sonar_generate_fingerprint(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate,
+                               const char* content_type, const sonar_fingerprint_config* cfg,
+                               sonar_result** out);
+
+/* AlignmentExtractor.ExtractAlignmentFeatures on the energy (+ optional chroma)
+ * features of two fingerprints.  feature_sample_rate / hop / window are the
+ * extractor's FeatureConfig; max_lag_seconds as NewAlignmentExtractorWithMaxLag. */
+int sonar_align_features(sonar_ctx* ctx,
+                         const double* q_energy, int64_t nq_energy, const double* r_energy, int64_t nr_energy,
+                         const double* q_chroma, int64_t nq_chroma, const double* r_chroma, int64_t nr_chroma,
+                         int64_t q_pcm_len, int64_t r_pcm_len, int32_t sample_rate,
+                         int32_t feature_sample_rate, int32_t hop_size, int32_t window_size,
+                         double max_lag_seconds, sonar_result** out);
+
+/* result accessors: rows*cols float64 values, row-major; scalars are 1x1 */
+int sonar_result_get(const sonar_result* res, const char* name, const double** data, int64_t* rows,
+                     int64_t* cols);
+int sonar_result_count(const sonar_result* res);
+const char* sonar_result_name(const sonar_result* res, int index);
+void sonar_result_free(sonar_result* res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SONAR_GPU_H */

@@ -1,0 +1,75 @@
+// kernels.h -- launch interfaces between the C-ABI host layer (sonar_api.cpp)
+// and the HIP kernels (*.hip).  Device pointers only; all launches are async
+// on the given stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace sonar {
+
+// Fused per-frame kernel (fp_kernel.hip).  One block = 4 waves = one tile of
+// `tile_f` consecutive STFT frames; each wave computes whole-frame FFTs
+// (W = 128 * R real points as a 64*R-point complex FFT + real split) into an
+// LDS row per frame, then the block runs the per-frame epilogues with
+// lane = frame.
+struct FpParams {
+  const void* pcm;      // device, f32 or f64
+  int64_t n;            // samples
+  int pcm_f64;
+  int64_t F;            // STFT frames
+  int W, H;             // window / hop
+  int tile_f;           // frames (LDS rows) per tile
+  int stride;           // frames advanced per tile (= tile_f - r0)
+  int r0;               // 1 when row 0 only feeds spectral flux, else 0
+  int64_t ntiles;
+  const void* window;   // W coefficients, precision T
+  uint32_t flags;       // SONAR_FP_* bits (see sonar_gpu.h)
+  int store_mag;        // LDS rows hold |X| (1) or |X|^2 (0)
+  // filterbank + MFCC
+  int n_mels, n_mfcc;
+  int input_power;      // MFCC.Compute fed |X|^2 (F5) -> uses |X|^4
+  int n_groups;         // epilogue groups (256 / tile_f)
+  const int* mel_lo;    // [n_mels] first nonzero bin
+  const int* mel_hi;    // [n_mels] one past last nonzero bin
+  const int* mel_woff;  // [n_mels] offset into mel_w
+  const void* mel_w;    // packed nonzero weights (T)
+  const int* grp_off;   // [n_groups+1] ranges into grp_mels
+  const int* grp_mels;  // mel indices per group (balanced by nnz)
+  const void* dct;      // [n_mfcc][n_mels] (T)
+  const void* lift;     // [n_mfcc] lifter multipliers (T)
+  int sample_rate;
+  // outputs (device); element type double if out_f64 else float
+  int out_f64;
+  void* out_mfcc;
+  void* out_mag;
+  void* out_spec[10];   // centroid, rolloff, bandwidth, flatness, crest, slope, flux, low, high, (unused)
+  // LDS carve (bytes)
+  int lds_P, lds_logmel, lds_stage, lds_bytes;
+};
+
+int launch_fingerprint(const FpParams& p, int precision_f64, hipStream_t s);
+bool fingerprint_supported(int W);
+
+// ZCR + short-time energy on the pre-emphasised PCM (misc_kernels.hip)
+int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, double alpha, int sample_rate,
+               void* out, int out_f64, hipStream_t s);
+int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H, double alpha,
+                  void* out, int out_f64, hipStream_t s);
+// YIN raw per-frame results (misc_kernels.hip)
+int launch_yin(const double* pcm, int64_t n, int64_t frames, int sample_rate, double* pitch, double* conf,
+               int32_t* tau, hipStream_t s);
+// Chroma STFT (misc_kernels.hip)
+int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, const double* window,
+                  const double* trig, const int* chroma_map, double* out, hipStream_t s);
+int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, hipStream_t s);
+// NCC (align_kernels.hip)
+int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t L, double* norm_a,
+               double* norm_b, double* stats, double* corr, hipStream_t s);
+// DTW (align_kernels.hip): cost holds (nq+1) x (nr+1) doubles
+int launch_dtw(const double* q, int64_t nq, const double* r, int64_t nr, int dim, int band, double* cost,
+               uint8_t* dir, int32_t* rev_q, int32_t* rev_r, int64_t* plen, hipStream_t s);
+int launch_dtw_path_cost(const double* cost, int64_t nr, const int32_t* rev_q, const int32_t* rev_r,
+                         const int64_t* plen_dev, int64_t plen, int32_t* pq, int32_t* pr, double* pc,
+                         hipStream_t s);
+
+}  // namespace sonar

@@ -1,0 +1,249 @@
+// misc_kernels.hip -- per-frame side features of the hot path (gfx950).
+//
+//  zcr_kernel      ZeroCrossingRate.Compute on pre-emphasised frames
+//                  (algorithms/spectral/zero_crossing_rate.go:37-52, called at
+//                  fingerprint/extractors/speech.go:351-358)
+//  energy_kernel   Energy.ComputeShortTimeEnergy (algorithms/temporal/energy.go:25-50)
+//  yin_kernel      PitchDetector.detectPitchYin core (algorithms/tonal/pitch_detection.go:282-420)
+//  chroma_kernel   ChromaSTFT.ComputeChroma on one music-extractor frame
+//                  (algorithms/chroma/chroma_stft.go:45-138, fingerprint/extractors/music.go:327-376)
+//  dcpre_kernel    DCRemoval.Process + PreEmphasis.Process (music.go:245-259)
+//
+// Decision-bearing arithmetic (sign tests, sums feeding thresholds) is float64
+// with explicit _rn intrinsics: no FMA contraction, Go's evaluation order.
+#include "kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace sonar {
+
+namespace {
+// y[i] = x[i] - alpha * x[i-1], x[-1] = 0 (pre_emphasis.go:150-153), rounded like Go
+__device__ __forceinline__ double pre_x(const void* pcm, int f64, int64_t i) {
+  return f64 ? ((const double*)pcm)[i] : (double)((const float*)pcm)[i];
+}
+__device__ __forceinline__ double preemph(const void* pcm, int f64, int64_t i, double alpha) {
+  const double x = pre_x(pcm, f64, i);
+  const double prev = i > 0 ? pre_x(pcm, f64, i - 1) : 0.0;
+  return __dsub_rn(x, __dmul_rn(alpha, prev));
+}
+__device__ __forceinline__ void store_out(void* out, int f64, int64_t i, double v) {
+  if (f64) ((double*)out)[i] = v; else ((float*)out)[i] = (float)v;
+}
+}  // namespace
+
+// one wave per frame; crossing count is an exact integer reduction
+__global__ __launch_bounds__(256) void zcr_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H,
+                                                  double alpha, int sr, void* out, int out_f64) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= F) return;
+  const int64_t s = t * H;
+  int64_t e = s + W; if (e > n) e = n;
+  const int64_t len = e - s;
+  int cnt = 0;
+  for (int64_t i = s + 1 + lane; i < e; i += 64) {
+    const double a = preemph(pcm, pcm_f64, i - 1, alpha), b = preemph(pcm, pcm_f64, i, alpha);
+    cnt += ((a >= 0 && b < 0) || (a < 0 && b >= 0)) ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  if (lane == 0) {
+    double r = 0.0;
+    if (len >= 2) r = __ddiv_rn((double)cnt, __ddiv_rn((double)len, (double)sr));
+    store_out(out, out_f64, t, r);
+  }
+}
+
+// one thread per energy frame, sequential sum in Go's order
+__global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H,
+                                                     double alpha, void* out, int out_f64) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= Fe) return;
+  const int64_t s = t * H;
+  double ss = 0.0;
+  double prev = s > 0 ? pre_x(pcm, pcm_f64, s - 1) : 0.0;
+  for (int64_t j = s; j < s + W; ++j) {
+    const double x = pre_x(pcm, pcm_f64, j);
+    const double y = __dsub_rn(x, __dmul_rn(alpha, prev));
+    prev = x;
+    ss = __dadd_rn(ss, __dmul_rn(y, y));
+  }
+  store_out(out, out_f64, t, sqrt(__ddiv_rn(ss, (double)W)));
+}
+
+// YIN per 1024-sample frame at hop 512: one block of 256 threads per frame
+__constant__ double c_yin_win[1024];
+
+__global__ __launch_bounds__(256) void yin_kernel(const double* pcm, int64_t n, int64_t frames, int sr,
+                                                  double* pitch, double* conf, int32_t* tau_out) {
+  __shared__ double xw[1024];
+  __shared__ double diff[512];
+  __shared__ double cm[512];
+  const int64_t fi = blockIdx.x;
+  if (fi >= frames) return;
+  const int64_t s = fi * 512;
+  const bool full = (s + 1024 <= n);
+  if (!full) {   // DetectPitch rejects frames != WindowSize (pitch_detection.go:226)
+    if (threadIdx.x == 0) { pitch[fi] = 0; conf[fi] = 0; if (tau_out) tau_out[fi] = -2; }
+    return;
+  }
+  for (int i = threadIdx.x; i < 1024; i += 256) {  // applyPreEmphasis :296-310, window :289-291
+    const double x = pcm[s + i];
+    const double y = (i == 0) ? x : __dsub_rn(x, __dmul_rn(0.97, pcm[s + i - 1]));
+    xw[i] = __dmul_rn(y, c_yin_win[i]);
+  }
+  __syncthreads();
+  for (int tau = threadIdx.x; tau < 512; tau += 256) {  // difference function :353-362
+    double sum = 0.0;
+    for (int j = 0; j < 512; ++j) {
+      const double d = __dsub_rn(xw[j], xw[j + tau]);
+      sum = __dadd_rn(sum, __dmul_rn(d, d));
+    }
+    diff[tau] = sum;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    cm[0] = 1.0;                                        // CMNDF :365-371
+    double run = 0.0;
+    for (int tau = 1; tau < 512; ++tau) {
+      run = __dadd_rn(run, diff[tau]);
+      cm[tau] = __ddiv_rn(diff[tau], __ddiv_rn(run, (double)tau));
+    }
+    int mt = -1;                                        // first local minimum below 0.15 :374-383
+    for (int tau = 1; tau < 512; ++tau)
+      if (cm[tau] < 0.15 && tau + 1 < 512 && cm[tau] < cm[tau + 1]) { mt = tau; break; }
+    double p = 0.0, c = 0.0;
+    if (mt > 0) {
+      double period = (double)mt;                       // parabolicInterpolation :743-764
+      if (mt < 511) {
+        const double y1 = cm[mt - 1], y2 = cm[mt], y3 = cm[mt + 1];
+        const double a = __ddiv_rn(__dadd_rn(__dsub_rn(y1, __dmul_rn(2.0, y2)), y3), 2.0);
+        const double b = __ddiv_rn(__dsub_rn(y3, y1), 2.0);
+        if (a != 0.0) period = __dadd_rn((double)mt, __ddiv_rn(-b, __dmul_rn(2.0, a)));
+      }
+      const double f = __ddiv_rn((double)sr, period);
+      const double cf = __dsub_rn(1.0, cm[mt]);
+      if (f >= 80.0 && f <= 1000.0) { p = f; c = cf; }
+    }
+    pitch[fi] = p; conf[fi] = c;
+    if (tau_out) tau_out[fi] = mt;
+  }
+}
+
+// chroma of one frame per block: direct DFT of length fs (any fs), |X|^2 folded to 12 bins.
+// trig table (cos, sin of -2 pi m/fs) lives in global memory (L1/L2 resident).
+__global__ __launch_bounds__(256) void chroma_kernel(const double* y, int64_t n, int64_t frames, int hop, int fs,
+                                                     const double* win, const double* trig, const int* cmap,
+                                                     double* out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* seg = (double*)smem;                 // fs
+  double* pw = seg + fs;                        // K + 12
+  const int K = fs / 2 + 1;
+  const int64_t t = blockIdx.x;
+  if (t >= frames) return;
+  const int64_t s = t * hop;
+  for (int i = threadIdx.x; i < fs; i += blockDim.x) {
+    const double v = (s + i < n) ? y[s + i] : 0.0;   // zero pad (music.go:351-357)
+    seg[i] = v * win[i];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    double re = 0.0, im = 0.0;
+    int idx = 0;
+    for (int m = 0; m < fs; ++m) {
+      re += seg[m] * trig[2 * idx];
+      im += seg[m] * trig[2 * idx + 1];
+      idx += k; if (idx >= fs) idx -= fs;
+    }
+    const double mag = hypot(re, im);
+    pw[k] = mag * mag;
+  }
+  __syncthreads();
+  if (threadIdx.x < 12) {
+    double acc = 0.0;
+    for (int k = 0; k < K; ++k) if (cmap[k] == (int)threadIdx.x) acc += pw[k];  // ascending-k order
+    pw[K + threadIdx.x] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0.0;
+    for (int b = 0; b < 12; ++b) tot += pw[K + b];
+    for (int b = 0; b < 12; ++b) out[t * 12 + b] = (tot > 1e-10) ? pw[K + b] / tot : pw[K + b];
+  }
+}
+
+// DC blocker y[n] = x[n] - x[n-1] + R y[n-1] followed by pre-emphasis z = y[n] - a y[n-1].
+// Each thread produces a chunk of outputs after a WARM-sample warm-up from zero
+// state; R^WARM < 1e-17, so the result equals the sequential filter to fp64 rounding.
+__global__ __launch_bounds__(256) void dcpre_kernel(const double* x, int64_t n, double R, double alpha, double* z,
+                                                    int chunk, int warm) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t s = c * chunk;
+  if (s >= n) return;
+  const int64_t e = min(n, s + chunk);
+  int64_t i = s - warm - 1; if (i < 0) i = 0;
+  double x1 = 0.0, y1 = 0.0;
+  if (i > 0) x1 = x[i - 1];
+  double yprev = 0.0;
+  for (; i < e; ++i) {
+    const double xv = x[i];
+    const double yv = __dadd_rn(__dsub_rn(xv, x1), __dmul_rn(R, y1));
+    x1 = xv; y1 = yv;
+    if (i >= s) z[i] = __dsub_rn(yv, __dmul_rn(alpha, yprev));
+    yprev = yv;
+  }
+}
+
+int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, double alpha, int sr, void* out,
+               int out_f64, hipStream_t s) {
+  if (F <= 0) return 0;
+  hipLaunchKernelGGL(zcr_kernel, dim3((unsigned)((F + 3) / 4)), dim3(256), 0, s, pcm, pcm_f64, n, F, W, H, alpha,
+                     sr, out, out_f64);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H, double alpha, void* out,
+                  int out_f64, hipStream_t s) {
+  if (Fe <= 0) return 0;
+  hipLaunchKernelGGL(energy_kernel, dim3((unsigned)((Fe + 255) / 256)), dim3(256), 0, s, pcm, pcm_f64, n, Fe, W, H,
+                     alpha, out, out_f64);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_yin(const double* pcm, int64_t n, int64_t frames, int sr, double* pitch, double* conf, int32_t* tau,
+               hipStream_t s) {
+  static bool init = false;
+  if (!init) {   // symmetric Hann without normalisation, pitch_detection.go:314-318
+    double w[1024];
+    for (int i = 0; i < 1024; i++) w[i] = 0.5 * (1.0 - cos(2.0 * M_PI * (double)i / 1023.0));
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_yin_win), w, sizeof(w)) != hipSuccess) return -5;
+    init = true;
+  }
+  if (frames <= 0) return 0;
+  hipLaunchKernelGGL(yin_kernel, dim3((unsigned)frames), dim3(256), 0, s, pcm, n, frames, sr, pitch, conf, tau);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, const double* window,
+                  const double* trig, const int* cmap, double* out, hipStream_t s) {
+  if (frames <= 0) return 0;
+  const int K = fs / 2 + 1;
+  const size_t lds = sizeof(double) * ((size_t)fs + K + 12);
+  if (lds > 160 * 1024) return -4;
+  if (lds > 64 * 1024) hipFuncSetAttribute((const void*)chroma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(chroma_kernel, dim3((unsigned)frames), dim3(256), lds, s, y, n, frames, hop, fs, window, trig,
+                     cmap, out);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, hipStream_t s) {
+  if (n <= 0) return 0;
+  const int chunk = 2048, warm = 8192;
+  const int64_t nthreads = (n + chunk - 1) / chunk;
+  hipLaunchKernelGGL(dcpre_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, s, x, n, R, alpha, y, chunk,
+                     warm);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // namespace sonar

@@ -1,0 +1,560 @@
+// sonar_api.cpp -- the C ABI of include/sonar_gpu.h.
+//
+// Low-level entries (sonar_fingerprint, sonar_pitch_yin, sonar_chroma_stft,
+// sonar_ncc, sonar_dtw) validate exactly like the Go functions they replace,
+// stage host buffers when device_ptrs == 0, and launch the HIP kernels.
+// High-level entries (sonar_generate_fingerprint, sonar_align_features) are
+// the C++ restatement of the Go orchestration above those seams
+// (fingerprint/fingerprint.go:137-236, fingerprint/extractors/speech.go:135-550,
+// fingerprint/extractors/alignment.go:139-476).  There is no CPU fallback:
+// every numeric array comes from a GPU kernel; the host only builds tables
+// and runs the O(frames) sequential epilogues the Go code runs.
+#include "../../include/sonar_gpu.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "host_dsp.h"
+#include "kernels.h"
+
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t cap = 0;
+};
+
+struct FpTables {
+  void* window = nullptr;
+  int *mel_lo = nullptr, *mel_hi = nullptr, *mel_woff = nullptr, *grp_off = nullptr, *grp_mels = nullptr;
+  void *mel_w = nullptr, *dct = nullptr, *lift = nullptr;
+  int n_mels = 0, n_mfcc = 0;
+};
+
+struct sonar_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::map<std::string, DevBuf> bufs;
+  std::map<std::string, FpTables> fp_tables;
+  struct ChromaT { void* win; void* trig; void* map; };
+  std::map<std::string, ChromaT> chroma_tables;
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool ev_pending = false;
+  double last_ms = 0.0;
+};
+
+struct sonar_result {
+  struct Arr {
+    std::string name;
+    std::vector<double> v;
+    int64_t rows = 0, cols = 0;
+  };
+  std::vector<Arr> arrays;
+  void put(const std::string& name, std::vector<double> v, int64_t rows, int64_t cols) {
+    for (auto& a : arrays)
+      if (a.name == name) { a.v = std::move(v); a.rows = rows; a.cols = cols; return; }
+    arrays.push_back({name, std::move(v), rows, cols});
+  }
+  void scalar(const std::string& name, double x) { put(name, {x}, 1, 1); }
+  void vec(const std::string& name, const std::vector<double>& v) { put(name, v, (int64_t)v.size(), 1); }
+};
+
+namespace {
+
+int fail(sonar_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIP_TRY(ctx, call)                                                                   \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess) return fail(ctx, SONAR_ERR_DEVICE, std::string(#call ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+void* dbuf(sonar_ctx* c, const std::string& name, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  DevBuf& b = c->bufs[name];
+  if (b.cap < bytes) {
+    if (b.ptr) { hipStreamSynchronize(c->stream); hipFree(b.ptr); b.ptr = nullptr; b.cap = 0; }
+    if (hipMalloc(&b.ptr, bytes) != hipSuccess) { b.ptr = nullptr; return nullptr; }
+    b.cap = bytes;
+  }
+  return b.ptr;
+}
+
+template <typename T>
+void* upload(const std::vector<T>& v) {
+  void* p = nullptr;
+  size_t bytes = std::max<size_t>(16, v.size() * sizeof(T));
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  if (!v.empty()) hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+  return p;
+}
+void* upload_real(const std::vector<double>& v, bool f64) {
+  if (f64) return upload(v);
+  std::vector<float> f(v.begin(), v.end());
+  return upload(f);
+}
+
+int64_t go_frames(int64_t n, int W, int H) { return (n - W) / H + 1; }
+
+int tile_frames(int W, bool f64) {
+  const int K = W / 2 + 1;
+  const int esz = f64 ? 8 : 4;
+  int t = 32;
+  while (t > 8 && (int64_t)t * K * esz > 72 * 1024) t >>= 1;
+  const int R = W / 128;
+  const int FR = R >= 8 ? 1 : 8 / R;
+  while (t % (4 * FR) != 0) t <<= 1;
+  return t;
+}
+
+}  // namespace
+
+// ============================================================ context ====
+extern "C" {
+
+int sonar_abi_version(void) { return SONAR_ABI_VERSION; }
+
+int sonar_create(int device, sonar_ctx** out) {
+  if (!out) return SONAR_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SONAR_ERR_DEVICE;
+  if (device < 0 || device >= n) return SONAR_ERR_INVALID;
+  auto* c = new sonar_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return SONAR_ERR_DEVICE;
+  }
+  c->stream = c->own;
+  hipEventCreate(&c->ev0);
+  hipEventCreate(&c->ev1);
+  *out = c;
+  return SONAR_OK;
+}
+
+void sonar_destroy(sonar_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  for (auto& kv : c->bufs) if (kv.second.ptr) hipFree(kv.second.ptr);
+  for (auto& kv : c->fp_tables) {
+    FpTables& t = kv.second;
+    for (void* p : {(void*)t.window, (void*)t.mel_lo, (void*)t.mel_hi, (void*)t.mel_woff, (void*)t.grp_off,
+                    (void*)t.grp_mels, t.mel_w, t.dct, t.lift})
+      if (p) hipFree(p);
+  }
+  for (auto& kv : c->chroma_tables) { hipFree(kv.second.win); hipFree(kv.second.trig); hipFree(kv.second.map); }
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->own) hipStreamDestroy(c->own);
+  delete c;
+}
+
+const char* sonar_last_error(const sonar_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int sonar_set_stream(sonar_ctx* c, void* s) {
+  if (!c) return SONAR_ERR_INVALID;
+  c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
+  return SONAR_OK;
+}
+
+int sonar_synchronize(sonar_ctx* c) {
+  if (!c) return SONAR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return SONAR_OK;
+}
+
+int sonar_enable_kernel_timing(sonar_ctx* c, int on) {
+  if (!c) return SONAR_ERR_INVALID;
+  c->timing = on != 0;
+  return SONAR_OK;
+}
+
+int sonar_last_kernel_ms(sonar_ctx* c, double* ms) {
+  if (!c || !ms) return SONAR_ERR_INVALID;
+  if (c->ev_pending) {
+    HIP_TRY(c, hipEventSynchronize(c->ev1));
+    float f = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&f, c->ev0, c->ev1));
+    c->last_ms = f;
+    c->ev_pending = false;
+  }
+  *ms = c->last_ms;
+  return SONAR_OK;
+}
+
+int64_t sonar_stft_frames(int64_t n, int32_t W, int32_t H) {
+  if (n <= 0) return SONAR_ERR_EMPTY;
+  if (W <= 0 || H <= 0) return SONAR_ERR_INVALID;
+  const int64_t F = go_frames(n, W, H);
+  return F <= 0 ? SONAR_ERR_TOO_SHORT : F;
+}
+
+int64_t sonar_energy_frames(int64_t n, int32_t W, int32_t H) {
+  if (n < W || H <= 0 || W <= 0) return 0;
+  return (n - W) / H + 1;
+}
+
+int64_t sonar_pitch_frames(int64_t n) {
+  const int64_t F = (n - 1024) / 512 + 1;
+  return F < 0 ? 0 : F;
+}
+
+void sonar_fp_cfg_default(sonar_fp_cfg* c) {
+  std::memset(c, 0, sizeof(*c));
+  c->window_size = 1024;
+  c->hop_size = 256;
+  c->window_type = SONAR_WIN_HANN;
+  c->sample_rate = 44100;
+  c->n_mfcc = 13;
+  c->n_filters = 26;
+  c->filterbank = SONAR_FB_MEL;
+  c->use_lifter = 1;
+  c->lifter = 22.0;
+  c->preemph_alpha = 0.97;
+  c->flags = SONAR_FP_MFCC;
+  c->precision = SONAR_F32;
+  c->pcm_dtype = SONAR_F64;
+  c->out_dtype = SONAR_F64;
+}
+
+// ======================================================= sonar_fingerprint ==
+int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cfg* cfg, sonar_fp_out* out) {
+  if (!c || !cfg || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
+  // ComputeSTFTWithWindow validation order (spectral.go:386-412)
+  if (n <= 0 || !pcm) return fail(c, SONAR_ERR_EMPTY, "empty signal");
+  const int W = cfg->window_size, H = cfg->hop_size;
+  if (W <= 0) return fail(c, SONAR_ERR_INVALID, "window size must be positive");
+  if (H <= 0) return fail(c, SONAR_ERR_INVALID, "hop size must be positive");
+  const int64_t F = go_frames(n, W, H);
+  if (F <= 0) return fail(c, SONAR_ERR_TOO_SHORT, "signal too short for given window size and hop size");
+  const bool f64 = cfg->precision == SONAR_F64;
+  const bool pcm64 = cfg->pcm_dtype == SONAR_F64;
+  const bool o64 = cfg->out_dtype == SONAR_F64;
+  const uint32_t flags = cfg->flags;
+  const bool need_fft = flags & (SONAR_FP_MFCC | SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL);
+  if (need_fft && !sonar::fingerprint_supported(W))
+    return fail(c, SONAR_ERR_UNSUPPORTED, "window size " + std::to_string(W) +
+                                              " not supported by the GPU STFT (128, 256, 512, 1024, 2048)");
+  if (flags & SONAR_FP_SPECTRAL)
+    return fail(c, SONAR_ERR_UNSUPPORTED, "SONAR_FP_SPECTRAL epilogue not built yet");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const size_t esz_in = pcm64 ? 8 : 4, esz_out = o64 ? 8 : 4;
+  const bool dev = cfg->device_ptrs != 0;
+
+  const void* dpcm = pcm;
+  if (!dev) {
+    void* p = dbuf(c, "fp.pcm", (size_t)n * esz_in);
+    if (!p) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (pcm)");
+    HIP_TRY(c, hipMemcpyAsync(p, pcm, (size_t)n * esz_in, hipMemcpyHostToDevice, s));
+    dpcm = p;
+  }
+  const int K = W / 2 + 1;
+  // outputs (device staging when host pointers)
+  struct OutMap { void* host; void* devp; size_t bytes; };
+  std::vector<OutMap> copies;
+  auto out_ptr = [&](void* user, const char* name, size_t count) -> void* {
+    if (!user) return nullptr;
+    if (dev) return user;
+    void* d = dbuf(c, std::string("fp.out.") + name, count * esz_out);
+    if (d) copies.push_back({user, d, count * esz_out});
+    return d;
+  };
+  void* d_mfcc = (flags & SONAR_FP_MFCC) ? out_ptr(out->mfcc, "mfcc", (size_t)F * std::max(cfg->n_mfcc, 1)) : nullptr;
+  void* d_mag = (flags & SONAR_FP_MAGNITUDE) ? out_ptr(out->magnitude, "mag", (size_t)F * K) : nullptr;
+  if ((flags & SONAR_FP_MFCC) && !d_mfcc) return fail(c, SONAR_ERR_INVALID, "out->mfcc is null or allocation failed");
+  if ((flags & SONAR_FP_MAGNITUDE) && !d_mag) return fail(c, SONAR_ERR_INVALID, "out->magnitude is null");
+
+  if (need_fft) {
+    const int tile = tile_frames(W, f64);
+    const int r0 = 0;
+    sonar::FpParams p{};
+    p.pcm = dpcm; p.n = n; p.pcm_f64 = pcm64; p.F = F; p.W = W; p.H = H;
+    p.tile_f = tile; p.r0 = r0; p.stride = tile - r0;
+    p.ntiles = (F + p.stride - 1) / p.stride;
+    p.flags = flags;
+    p.store_mag = (flags & (SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL)) ? 1 : 0;
+    p.input_power = cfg->mfcc_input_power;
+    p.n_groups = 256 / tile;
+    p.sample_rate = cfg->sample_rate;
+    p.out_f64 = o64;
+    p.out_mfcc = d_mfcc;
+    p.out_mag = d_mag;
+    // tables, cached per configuration
+    char key[512];
+    std::snprintf(key, sizeof(key), "%d|%d|%d|%d|%d|%d|%.17g|%.17g|%d|%.17g|%d|%d", W, cfg->window_type,
+                  cfg->sample_rate, cfg->n_mfcc, cfg->n_filters, cfg->filterbank, cfg->low_freq, cfg->high_freq,
+                  cfg->use_lifter, cfg->lifter, (int)f64, tile);
+    auto it = c->fp_tables.find(key);
+    if (it == c->fp_tables.end()) {
+      FpTables t;
+      std::vector<double> win;
+      if (!sonar::host::make_window(cfg->window_type, W, true, true, 8.6, 0.5, win))
+        return fail(c, SONAR_ERR_INVALID, "failed to generate window: unsupported window type");
+      t.window = upload_real(win, f64);
+      sonar::host::MfccTables mt;
+      if (!sonar::host::make_mfcc_tables(cfg->sample_rate, cfg->n_mfcc, cfg->n_filters, cfg->filterbank, cfg->low_freq,
+                                         cfg->high_freq, cfg->use_lifter != 0, cfg->lifter, W, mt))
+        return fail(c, SONAR_ERR_INVALID, "failed to initialize MFCC: failed to create mel filter bank");
+      std::vector<int> off, mels;
+      sonar::host::balance_groups(mt, 256 / tile, off, mels);
+      t.mel_lo = (int*)upload(mt.lo); t.mel_hi = (int*)upload(mt.hi); t.mel_woff = (int*)upload(mt.woff);
+      t.grp_off = (int*)upload(off); t.grp_mels = (int*)upload(mels);
+      t.mel_w = upload_real(mt.w, f64); t.dct = upload_real(mt.dct, f64); t.lift = upload_real(mt.lift, f64);
+      t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc;
+      if (!t.window || !t.mel_lo || !t.mel_w || !t.dct || !t.lift) return fail(c, SONAR_ERR_NOMEM, "table upload failed");
+      it = c->fp_tables.emplace(key, t).first;
+    }
+    const FpTables& t = it->second;
+    p.window = t.window;
+    p.n_mels = t.n_mels; p.n_mfcc = t.n_mfcc;
+    p.mel_lo = t.mel_lo; p.mel_hi = t.mel_hi; p.mel_woff = t.mel_woff; p.mel_w = t.mel_w;
+    p.grp_off = t.grp_off; p.grp_mels = t.grp_mels; p.dct = t.dct; p.lift = t.lift;
+    const int esz = f64 ? 8 : 4;
+    auto al = [](int x) { return (x + 15) & ~15; };
+    p.lds_P = 0;
+    p.lds_logmel = al(tile * K * esz);
+    p.lds_stage = p.lds_logmel + al(tile * (t.n_mels + 1) * esz);
+    p.lds_bytes = p.lds_stage + al(tile * t.n_mfcc * esz);
+    if (p.lds_bytes > 160 * 1024) return fail(c, SONAR_ERR_UNSUPPORTED, "LDS budget exceeded");
+    if (c->timing) HIP_TRY(c, hipEventRecord(c->ev0, s));
+    const int rc = sonar::launch_fingerprint(p, f64, s);
+    if (rc != 0) return fail(c, SONAR_ERR_DEVICE, std::string("fingerprint kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (c->timing) { HIP_TRY(c, hipEventRecord(c->ev1, s)); c->ev_pending = true; }
+  }
+  if (flags & SONAR_FP_ZCR) {
+    void* d = out_ptr(out->zcr, "zcr", (size_t)F);
+    if (!d) return fail(c, SONAR_ERR_INVALID, "out->zcr is null");
+    if (sonar::launch_zcr(dpcm, pcm64, n, F, W, H, cfg->preemph_alpha, cfg->sample_rate, d, o64, s) != 0)
+      return fail(c, SONAR_ERR_DEVICE, "zcr launch failed");
+  }
+  if (flags & SONAR_FP_ENERGY) {
+    const int64_t Fe = sonar_energy_frames(n, cfg->energy_window, cfg->energy_hop);
+    if (Fe > 0) {
+      void* d = out_ptr(out->energy, "energy", (size_t)Fe);
+      if (!d) return fail(c, SONAR_ERR_INVALID, "out->energy is null");
+      if (sonar::launch_energy(dpcm, pcm64, n, Fe, cfg->energy_window, cfg->energy_hop, cfg->preemph_alpha, d, o64, s) != 0)
+        return fail(c, SONAR_ERR_DEVICE, "energy launch failed");
+    }
+  }
+  if (!dev) {
+    for (auto& m : copies) HIP_TRY(c, hipMemcpyAsync(m.host, m.devp, m.bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SONAR_OK;
+}
+
+// ========================================================= YIN, chroma ====
+int sonar_pitch_yin(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, double* pitch, double* conf, int32_t* tau,
+                    int32_t device_ptrs) {
+  if (!c) return SONAR_ERR_INVALID;
+  const int64_t F = sonar_pitch_frames(n);
+  if (F == 0) return SONAR_OK;
+  if (!pcm || !pitch || !conf) return fail(c, SONAR_ERR_INVALID, "null buffer");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const double* dp = pcm;
+  double *dpi = pitch, *dco = conf;
+  int32_t* dta = tau;
+  if (!device_ptrs) {
+    void* b = dbuf(c, "yin.pcm", n * 8);
+    dpi = (double*)dbuf(c, "yin.p", F * 8);
+    dco = (double*)dbuf(c, "yin.c", F * 8);
+    dta = tau ? (int32_t*)dbuf(c, "yin.t", F * 4) : nullptr;
+    if (!b || !dpi || !dco) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+    HIP_TRY(c, hipMemcpyAsync(b, pcm, n * 8, hipMemcpyHostToDevice, s));
+    dp = (const double*)b;
+  }
+  if (sonar::launch_yin(dp, n, F, sr, dpi, dco, dta, s) != 0) return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
+  if (!device_ptrs) {
+    HIP_TRY(c, hipMemcpyAsync(pitch, dpi, F * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(conf, dco, F * 8, hipMemcpyDeviceToHost, s));
+    if (tau) HIP_TRY(c, hipMemcpyAsync(tau, dta, F * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SONAR_OK;
+}
+
+int sonar_chroma_stft(sonar_ctx* c, const double* pcm, int64_t n, int64_t F, int32_t hop, int32_t sr, int32_t preprocess,
+                      double* chroma, int32_t device_ptrs) {
+  if (!c) return SONAR_ERR_INVALID;
+  if (!pcm || n <= 0 || F <= 0) return fail(c, SONAR_ERR_INVALID, "invalid input data");
+  if (hop <= 0) return fail(c, SONAR_ERR_INVALID, "hop size must be positive");
+  const int fs = (int)(n / F);                                    // music.go:331
+  if (fs <= 0) return fail(c, SONAR_ERR_INVALID, "window size must be positive");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const double* dp = pcm;
+  double* dout = chroma;
+  if (!device_ptrs) {
+    void* b = dbuf(c, "chroma.pcm", n * 8);
+    dout = (double*)dbuf(c, "chroma.out", F * 12 * 8);
+    if (!b || !dout) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+    HIP_TRY(c, hipMemcpyAsync(b, pcm, n * 8, hipMemcpyHostToDevice, s));
+    dp = (const double*)b;
+  }
+  const double* y = dp;
+  if (preprocess) {
+    double* yb = (double*)dbuf(c, "chroma.y", n * 8);
+    if (!yb) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+    if (sonar::launch_dc_preemph(dp, n, 0.995, 0.95, yb, s) != 0) return fail(c, SONAR_ERR_DEVICE, "dc launch failed");
+    y = yb;
+  }
+  const std::string key = std::to_string(fs) + "|" + std::to_string(sr);
+  auto it = c->chroma_tables.find(key);
+  if (it == c->chroma_tables.end()) {
+    std::vector<double> win;
+    sonar::host::make_window(SONAR_WIN_HANN, fs, true, true, 8.6, 0.5, win);
+    std::vector<int> map = sonar::host::chroma_map(fs, sr);
+    std::vector<double> trig(2 * (size_t)fs);
+    for (int m = 0; m < fs; m++) {
+      trig[2 * m] = std::cos(2.0 * M_PI * (double)m / (double)fs);
+      trig[2 * m + 1] = -std::sin(2.0 * M_PI * (double)m / (double)fs);
+    }
+    it = c->chroma_tables.emplace(key, sonar_ctx::ChromaT{upload(win), upload(trig), upload(map)}).first;
+  }
+  if (sonar::launch_chroma(y, n, F, hop, fs, (const double*)it->second.win, (const double*)it->second.trig,
+                           (const int*)it->second.map, dout, s) != 0)
+    return fail(c, SONAR_ERR_UNSUPPORTED, "chroma launch failed (frame size too large for LDS?)");
+  if (!device_ptrs) {
+    HIP_TRY(c, hipMemcpyAsync(chroma, dout, F * 12 * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SONAR_OK;
+}
+
+// ================================================================ NCC ====
+int sonar_ncc(sonar_ctx* c, const double* a, int64_t na, const double* b, int64_t nb, int32_t max_lag, double* corr,
+              double* metrics, int32_t device_ptrs) {
+  if (!c) return SONAR_ERR_INVALID;
+  if (na <= 0 || nb <= 0 || !a || !b) return fail(c, SONAR_ERR_EMPTY, "empty signals provided");
+  int64_t L = max_lag;                                            // calculateActualMaxLag :452-461
+  L = std::min<int64_t>(L, na - 1);
+  L = std::min<int64_t>(L, nb - 1);
+  L = std::max<int64_t>(L, 0);
+  const int64_t nl = 2 * L + 1;
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const double *da = a, *db = b;
+  if (!device_ptrs) {
+    double* pa = (double*)dbuf(c, "ncc.a", na * 8);
+    double* pb = (double*)dbuf(c, "ncc.b", nb * 8);
+    if (!pa || !pb) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+    HIP_TRY(c, hipMemcpyAsync(pa, a, na * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(pb, b, nb * 8, hipMemcpyHostToDevice, s));
+    da = pa; db = pb;
+  }
+  double* xa = (double*)dbuf(c, "ncc.xa", na * 8);
+  double* xb = (double*)dbuf(c, "ncc.xb", nb * 8);
+  double* st = (double*)dbuf(c, "ncc.stats", 64);
+  double* dc = (device_ptrs && corr) ? corr : (double*)dbuf(c, "ncc.corr", nl * 8);
+  if (!xa || !xb || !st || !dc) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev0, s));
+  if (sonar::launch_ncc(da, na, db, nb, L, xa, xb, st, dc, s) != 0) return fail(c, SONAR_ERR_DEVICE, "ncc launch failed");
+  if (c->timing) { HIP_TRY(c, hipEventRecord(c->ev1, s)); c->ev_pending = true; }
+  std::vector<double> hc(nl);
+  HIP_TRY(c, hipMemcpyAsync(hc.data(), dc, nl * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  if (corr && !device_ptrs) std::memcpy(corr, hc.data(), nl * 8);
+  if (metrics) {
+    const auto m = sonar::host::ncc_metrics(hc.data(), nl, L, na, nb);
+    const double v[10] = {m.peak_corr, (double)m.peak_lag, (double)m.peak_index, m.p_value, m.snr, m.sharpness,
+                          m.second_peak, m.psl, (double)m.overlap, (double)m.num_lags};
+    std::memcpy(metrics, v, sizeof(v));
+  }
+  return SONAR_OK;
+}
+
+// ================================================================ DTW ====
+int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_t nr, int32_t dim, int32_t band,
+              double* distance, int32_t* path_q, int32_t* path_r, double* path_cost, int64_t* path_len, double* cost,
+              int32_t device_ptrs) {
+  if (!c) return SONAR_ERR_INVALID;
+  if (nq <= 0 || nr <= 0 || !q || !r) return fail(c, SONAR_ERR_EMPTY, "empty sequences provided");
+  if (dim <= 0) return fail(c, SONAR_ERR_INVALID, "feature dimension must be positive");
+  if (nq + nr > (int64_t)INT32_MAX) return fail(c, SONAR_ERR_UNSUPPORTED, "sequence too long");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const double *dq = q, *dr = r;
+  if (!device_ptrs) {
+    double* pq = (double*)dbuf(c, "dtw.q", nq * dim * 8);
+    double* pr = (double*)dbuf(c, "dtw.r", nr * dim * 8);
+    if (!pq || !pr) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+    HIP_TRY(c, hipMemcpyAsync(pq, q, nq * dim * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(pr, r, nr * dim * 8, hipMemcpyHostToDevice, s));
+    dq = pq; dr = pr;
+  }
+  const size_t cells = (size_t)(nq + 1) * (size_t)(nr + 1);
+  double* C = (double*)dbuf(c, "dtw.C", cells * 8);
+  uint8_t* dir = (uint8_t*)dbuf(c, "dtw.dir", (size_t)nq * nr);
+  const int64_t cap = nq + nr + 1;
+  int32_t* rq = (int32_t*)dbuf(c, "dtw.rq", cap * 4);
+  int32_t* rr = (int32_t*)dbuf(c, "dtw.rr", cap * 4);
+  int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
+  if (!C || !dir || !rq || !rr || !pl) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (cost matrix)");
+  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev0, s));
+  if (sonar::launch_dtw(dq, nq, dr, nr, dim, band, C, dir, rq, rr, pl, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
+  if (c->timing) { HIP_TRY(c, hipEventRecord(c->ev1, s)); c->ev_pending = true; }
+  int64_t P = 0;
+  HIP_TRY(c, hipMemcpyAsync(&P, pl, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  int32_t* oq = path_q; int32_t* orr = path_r; double* oc = path_cost;
+  if (!device_ptrs) {
+    oq = (int32_t*)dbuf(c, "dtw.pq", cap * 4);
+    orr = (int32_t*)dbuf(c, "dtw.pr", cap * 4);
+    oc = (double*)dbuf(c, "dtw.pc", cap * 8);
+    if (!oq || !orr || !oc) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (path)");
+  }
+  if (sonar::launch_dtw_path_cost(C, nr, rq, rr, pl, P, oq, orr, oc, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "dtw path launch failed");
+  double cNM = 0;
+  HIP_TRY(c, hipMemcpyAsync(&cNM, C + (size_t)nq * (nr + 1) + nr, 8, hipMemcpyDeviceToHost, s));
+  if (!device_ptrs) {
+    if (path_q) HIP_TRY(c, hipMemcpyAsync(path_q, oq, P * 4, hipMemcpyDeviceToHost, s));
+    if (path_r) HIP_TRY(c, hipMemcpyAsync(path_r, orr, P * 4, hipMemcpyDeviceToHost, s));
+    if (path_cost) HIP_TRY(c, hipMemcpyAsync(path_cost, oc, P * 8, hipMemcpyDeviceToHost, s));
+    if (cost) HIP_TRY(c, hipMemcpyAsync(cost, C + (nr + 1), (size_t)nq * (nr + 1) * 8, hipMemcpyDeviceToHost, s));
+  } else if (cost) {
+    HIP_TRY(c, hipMemcpyAsync(cost, C + (nr + 1), (size_t)nq * (nr + 1) * 8, hipMemcpyDeviceToDevice, s));
+  }
+  HIP_TRY(c, hipStreamSynchronize(s));
+  if (path_len) *path_len = P;
+  if (distance) *distance = cNM / (double)P;                      // dtw.go:88-91
+  return SONAR_OK;
+}
+
+// ====================================================== result object ====
+int sonar_result_get(const sonar_result* r, const char* name, const double** data, int64_t* rows, int64_t* cols) {
+  if (!r || !name) return SONAR_ERR_INVALID;
+  for (const auto& a : r->arrays)
+    if (a.name == name) {
+      if (data) *data = a.v.data();
+      if (rows) *rows = a.rows;
+      if (cols) *cols = a.cols;
+      return SONAR_OK;
+    }
+  return SONAR_ERR_INVALID;
+}
+int sonar_result_count(const sonar_result* r) { return r ? (int)r->arrays.size() : 0; }
+const char* sonar_result_name(const sonar_result* r, int i) {
+  return (r && i >= 0 && i < (int)r->arrays.size()) ? r->arrays[i].name.c_str() : nullptr;
+}
+void sonar_result_free(sonar_result* r) { delete r; }
+
+}  // extern "C"

@@ -1,0 +1,323 @@
+"""ctypes binding of include/sonar_gpu.h (see package docstring)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))       # sonido-sonar_amd/
+_REPO = os.path.dirname(_PKG)
+LIB_PATH = os.path.join(_PKG, "lib", "libsonar_gpu.so")
+HEADER = os.path.join(_REPO, "include", "sonar_gpu.h")
+
+OK, ERR_INVALID, ERR_TOO_SHORT, ERR_EMPTY, ERR_UNSUPPORTED, ERR_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4, -5, -6
+FP_MFCC, FP_MAGNITUDE, FP_SPECTRAL, FP_ZCR, FP_ENERGY = 1, 2, 4, 8, 16
+F32, F64 = 0, 1
+WINDOWS = {"hann": 0, "hamming": 1, "blackman": 2, "blackman_harris": 3, "kaiser": 4,
+           "tukey": 5, "rectangular": 6, "bartlett": 7, "welch": 8}
+SPECTRAL_NAMES = ["centroid", "rolloff", "bandwidth", "flatness", "crest", "slope", "flux",
+                  "low_ratio", "high_ratio"]
+NCC_KEYS = ["peak_correlation", "peak_lag", "peak_index", "p_value", "snr", "sharpness",
+            "second_peak", "peak_to_sidelobe", "overlap_length", "num_lags"]
+
+
+def _exported_symbols():
+    with open(HEADER) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"\b(sonar_[a-z0-9_]+)\s*\(", txt)))
+
+
+EXPORTED_SYMBOLS = _exported_symbols()
+
+
+class SonarError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class FpConfig(C.Structure):
+    _fields_ = [("window_size", C.c_int32), ("hop_size", C.c_int32), ("window_type", C.c_int32),
+                ("sample_rate", C.c_int32), ("n_mfcc", C.c_int32), ("n_filters", C.c_int32),
+                ("filterbank", C.c_int32), ("use_lifter", C.c_int32), ("low_freq", C.c_double),
+                ("high_freq", C.c_double), ("lifter", C.c_double), ("mfcc_input_power", C.c_int32),
+                ("energy_window", C.c_int32), ("energy_hop", C.c_int32), ("preemph_alpha", C.c_double),
+                ("flags", C.c_uint32), ("precision", C.c_int32), ("pcm_dtype", C.c_int32),
+                ("out_dtype", C.c_int32), ("device_ptrs", C.c_int32)]
+
+
+class FpOut(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ["mfcc", "magnitude", "centroid", "rolloff", "bandwidth", "flatness",
+                                          "crest", "slope", "flux", "low_ratio", "high_ratio", "zcr", "energy"]]
+
+
+class FingerprintConfig(C.Structure):
+    _fields_ = [("window_size", C.c_int32), ("hop_size", C.c_int32), ("feature_window_size", C.c_int32),
+                ("feature_hop_size", C.c_int32), ("enable_content_detect", C.c_int32),
+                ("window_type", C.c_int32), ("precision", C.c_int32)]
+
+
+_lib = None
+_vp, _d, _i32p, _i64p = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
+
+
+def build():
+    """Compile libsonar_gpu.so in-tree for gfx950 (hipcc; no GPU needed)."""
+    subprocess.run(["make", "-s", "-j8", "-C", _PKG], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SonarError(ERR_DEVICE, f"{LIB_PATH} not built: run `make -C sonido-sonar_amd` "
+                                     "(there is no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    L.sonar_create.argtypes = [C.c_int, C.POINTER(_vp)]
+    L.sonar_destroy.argtypes = [_vp]
+    L.sonar_destroy.restype = None
+    L.sonar_last_error.argtypes = [_vp]
+    L.sonar_last_error.restype = C.c_char_p
+    L.sonar_set_stream.argtypes = [_vp, _vp]
+    L.sonar_synchronize.argtypes = [_vp]
+    L.sonar_last_kernel_ms.argtypes = [_vp, _d]
+    L.sonar_enable_kernel_timing.argtypes = [_vp, C.c_int]
+    for f in ("sonar_stft_frames", "sonar_energy_frames"):
+        getattr(L, f).argtypes = [C.c_int64, C.c_int32, C.c_int32]
+        getattr(L, f).restype = C.c_int64
+    L.sonar_pitch_frames.argtypes = [C.c_int64]
+    L.sonar_pitch_frames.restype = C.c_int64
+    L.sonar_fp_cfg_default.argtypes = [C.POINTER(FpConfig)]
+    L.sonar_fp_cfg_default.restype = None
+    L.sonar_fingerprint.argtypes = [_vp, _vp, C.c_int64, C.POINTER(FpConfig), C.POINTER(FpOut)]
+    L.sonar_pitch_yin.argtypes = [_vp, _vp, C.c_int64, C.c_int32, _vp, _vp, _vp, C.c_int32]
+    L.sonar_chroma_stft.argtypes = [_vp, _vp, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, C.c_int32]
+    L.sonar_ncc.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, _vp, _vp, C.c_int32]
+    L.sonar_dtw.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, _d, _vp, _vp, _vp, _i64p,
+                            _vp, C.c_int32]
+    L.sonar_fingerprint_config_default.argtypes = [C.POINTER(FingerprintConfig)]
+    L.sonar_fingerprint_config_default.restype = None
+    L.sonar_generate_fingerprint.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_char_p,
+                                             C.POINTER(FingerprintConfig), C.POINTER(_vp)]
+    L.sonar_align_features.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, _vp, C.c_int64, _vp, C.c_int64,
+                                       C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                       C.c_double, C.POINTER(_vp)]
+    L.sonar_result_get.argtypes = [_vp, C.c_char_p, C.POINTER(_d), _i64p, _i64p]
+    L.sonar_result_count.argtypes = [_vp]
+    L.sonar_result_name.argtypes = [_vp, C.c_int]
+    L.sonar_result_name.restype = C.c_char_p
+    L.sonar_result_free.argtypes = [_vp]
+    L.sonar_result_free.restype = None
+    _lib = L
+    return L
+
+
+def abi_version():
+    return lib().sonar_abi_version()
+
+
+def stft_frames(n, W, H):
+    return int(lib().sonar_stft_frames(n, W, H))
+
+
+def energy_frames(n, W, H):
+    return int(lib().sonar_energy_frames(n, W, H))
+
+
+def pitch_frames(n):
+    return int(lib().sonar_pitch_frames(n))
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class Context:
+    """One sonar_ctx (one HIP stream) on `device`."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = C.c_void_p()
+        rc = L.sonar_create(device, C.byref(h))
+        if rc != OK:
+            raise SonarError(rc, "sonar_create failed (no GPU visible?)")
+        self._h = h
+        self._L = L
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.sonar_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != OK:
+            raise SonarError(rc, self._L.sonar_last_error(self._h).decode())
+
+    # -- stream / timing -------------------------------------------------
+    def set_stream(self, stream_handle):
+        self._check(self._L.sonar_set_stream(self._h, C.c_void_p(stream_handle or 0) if stream_handle else None))
+
+    def synchronize(self):
+        self._check(self._L.sonar_synchronize(self._h))
+
+    def enable_kernel_timing(self, on=True):
+        self._check(self._L.sonar_enable_kernel_timing(self._h, int(on)))
+
+    def last_kernel_ms(self):
+        v = C.c_double()
+        self._check(self._L.sonar_last_kernel_ms(self._h, C.byref(v)))
+        return v.value
+
+    # -- path A ------------------------------------------------------------
+    @staticmethod
+    def config(**kw):
+        cfg = FpConfig()
+        lib().sonar_fp_cfg_default(C.byref(cfg))
+        for k, v in kw.items():
+            if k == "window_type" and isinstance(v, str):
+                v = WINDOWS[v]
+            setattr(cfg, k, v)
+        return cfg
+
+    def fingerprint(self, pcm, cfg: FpConfig):
+        """Host-buffer form: returns a dict of numpy arrays for the requested flags."""
+        pcm = np.ascontiguousarray(pcm, dtype=np.float64 if cfg.pcm_dtype == F64 else np.float32)
+        n = len(pcm)
+        cfg.device_ptrs = 0
+        F = stft_frames(n, cfg.window_size, cfg.hop_size) if n > 0 and cfg.window_size > 0 and cfg.hop_size > 0 else 0
+        od = np.float64 if cfg.out_dtype == F64 else np.float32
+        out, res = FpOut(), {}
+        if F > 0:
+            K = cfg.window_size // 2 + 1
+            nm = cfg.n_mfcc if cfg.n_mfcc > 0 else 13
+            if cfg.flags & FP_MFCC:
+                res["mfcc"] = np.zeros((F, nm), od)
+                out.mfcc = res["mfcc"].ctypes.data
+            if cfg.flags & FP_MAGNITUDE:
+                res["magnitude"] = np.zeros((F, K), od)
+                out.magnitude = res["magnitude"].ctypes.data
+            if cfg.flags & FP_SPECTRAL:
+                for nme in SPECTRAL_NAMES:
+                    res[nme] = np.zeros(max(F - 1, 0) if nme == "flux" else F, od)
+                    setattr(out, nme, res[nme].ctypes.data if res[nme].size else None)
+            if cfg.flags & FP_ZCR:
+                res["zcr"] = np.zeros(F, od)
+                out.zcr = res["zcr"].ctypes.data
+            if cfg.flags & FP_ENERGY:
+                fe = energy_frames(n, cfg.energy_window, cfg.energy_hop)
+                res["energy"] = np.zeros(fe, od)
+                out.energy = res["energy"].ctypes.data if fe > 0 else None
+        self._check(self._L.sonar_fingerprint(self._h, _ptr(pcm) if n else None, n, C.byref(cfg), C.byref(out)))
+        return res
+
+    def fingerprint_device(self, pcm_ptr, n, cfg: FpConfig, **out_ptrs):
+        """Device-pointer form (async on the ctx stream): out_ptrs name -> device address."""
+        cfg.device_ptrs = 1
+        out = FpOut()
+        for k, v in out_ptrs.items():
+            setattr(out, k, v)
+        self._check(self._L.sonar_fingerprint(self._h, C.c_void_p(pcm_ptr), n, C.byref(cfg), C.byref(out)))
+
+    def pitch_yin(self, pcm, sample_rate):
+        pcm = _f64(pcm)
+        F = pitch_frames(len(pcm))
+        p, c, t = np.zeros(F), np.zeros(F), np.zeros(F, np.int32)
+        self._check(self._L.sonar_pitch_yin(self._h, _ptr(pcm), len(pcm), sample_rate, _ptr(p), _ptr(c), _ptr(t), 0))
+        return p, c, t
+
+    def chroma_stft(self, pcm, n_frames, hop, sample_rate, preprocess=True):
+        pcm = _f64(pcm)
+        out = np.zeros((n_frames, 12))
+        self._check(self._L.sonar_chroma_stft(self._h, _ptr(pcm), len(pcm), n_frames, hop, sample_rate,
+                                              int(preprocess), _ptr(out), 0))
+        return out
+
+    # -- path B ------------------------------------------------------------
+    def ncc(self, a, b, max_lag):
+        a, b = _f64(a), _f64(b)
+        L = max(0, min(max_lag, len(a) - 1, len(b) - 1)) if len(a) and len(b) else 0
+        corr = np.zeros(2 * L + 1)
+        met = np.zeros(10)
+        self._check(self._L.sonar_ncc(self._h, _ptr(a) if len(a) else None, len(a), _ptr(b) if len(b) else None,
+                                      len(b), max_lag, _ptr(corr), _ptr(met), 0))
+        return corr, dict(zip(NCC_KEYS, met.tolist()))
+
+    def dtw(self, q, r, band=-1, want_cost=False):
+        q, r = _f64(q), _f64(r)
+        if q.ndim == 1:
+            q = q[:, None]
+        if r.ndim == 1:
+            r = r[:, None]
+        nq, d = q.shape if q.size else (0, 1)
+        nr = r.shape[0] if r.size else 0
+        cap = nq + nr + 1
+        pq, pr, pc = np.zeros(cap, np.int32), np.zeros(cap, np.int32), np.zeros(cap)
+        plen, dist = C.c_int64(), C.c_double()
+        cost = np.zeros((nq, nr + 1)) if want_cost else None
+        self._check(self._L.sonar_dtw(self._h, _ptr(q) if nq else None, nq, _ptr(r) if nr else None, nr, d, band,
+                                      C.byref(dist), _ptr(pq), _ptr(pr), _ptr(pc), C.byref(plen),
+                                      _ptr(cost) if want_cost else None, 0))
+        P = plen.value
+        return {"distance": dist.value, "path_q": pq[:P], "path_r": pr[:P], "path_cost": pc[:P], "cost": cost}
+
+    # -- Go API mirror -----------------------------------------------------
+    def _result(self, h):
+        L = self._L
+        out = {}
+        try:
+            for i in range(L.sonar_result_count(h)):
+                name = L.sonar_result_name(h, i).decode()
+                data, rows, cols = _d(), C.c_int64(), C.c_int64()
+                L.sonar_result_get(h, name.encode(), C.byref(data), C.byref(rows), C.byref(cols))
+                n = rows.value * cols.value
+                arr = np.ctypeslib.as_array(data, shape=(n,)).copy() if n else np.zeros(0)
+                out[name] = arr.reshape(rows.value, cols.value) if cols.value > 1 else arr
+        finally:
+            L.sonar_result_free(h)
+        return out
+
+    @staticmethod
+    def fingerprint_config(**kw):
+        cfg = FingerprintConfig()
+        lib().sonar_fingerprint_config_default(C.byref(cfg))
+        for k, v in kw.items():
+            setattr(cfg, k, v)
+        return cfg
+
+    def generate_fingerprint(self, pcm, sample_rate, content_type, cfg: FingerprintConfig = None):
+        pcm = _f64(pcm)
+        cfg = cfg or self.fingerprint_config()
+        h = C.c_void_p()
+        self._check(self._L.sonar_generate_fingerprint(self._h, _ptr(pcm) if len(pcm) else None, len(pcm),
+                                                       sample_rate, content_type.encode(), C.byref(cfg),
+                                                       C.byref(h)))
+        return self._result(h)
+
+    def align_features(self, q_energy, r_energy, q_chroma=None, r_chroma=None, q_pcm_len=0, r_pcm_len=0,
+                       sample_rate=44100, feature_sample_rate=44100, hop_size=256, window_size=1024,
+                       max_lag_seconds=60.0):
+        qe, re_ = _f64(q_energy), _f64(r_energy)
+        qc = _f64(q_chroma) if q_chroma is not None else np.zeros((0, 12))
+        rc = _f64(r_chroma) if r_chroma is not None else np.zeros((0, 12))
+        h = C.c_void_p()
+        self._check(self._L.sonar_align_features(
+            self._h, _ptr(qe) if len(qe) else None, len(qe), _ptr(re_) if len(re_) else None, len(re_),
+            _ptr(qc) if len(qc) else None, len(qc), _ptr(rc) if len(rc) else None, len(rc),
+            q_pcm_len, r_pcm_len, sample_rate, feature_sample_rate, hop_size, window_size, max_lag_seconds,
+            C.byref(h)))
+        return self._result(h)

@@ -1,0 +1,127 @@
+"""Path A parity on the GPU: ComputeSTFTWithWindow magnitude, MFCC.ComputeFrames,
+ZCR and ShortTimeEnergy vs the fp64 oracle (oracle/sonar_oracle.c).
+
+Tolerances (north_star: float features within 1e-4 relative):
+  * F64 kernels: 1e-9 relative to the frame's peak (magnitude) / MFCC L2 norm.
+  * F32 kernels: 1e-4 relative to the frame's MFCC L2 norm on well-conditioned
+    input (sweep + noise, every mel band populated); magnitude 2e-6 of frame peak.
+  * ZCR crossing counts: bit-exact (integer).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import sonar
+from sonar import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _sig(n, seed=0):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / 44100.0
+    return 0.5 * np.sin(2 * np.pi * 440 * t) + 0.1 * rng.standard_normal(n)
+
+
+def _rel_rows(a, b, norm):
+    return np.max(np.abs(a - b) / np.maximum(norm, 1e-30)[:, None])
+
+
+@pytest.mark.parametrize("W,H", [(1024, 256), (2048, 512), (512, 128), (256, 64), (1024, 1000), (128, 37)])
+@pytest.mark.parametrize("prec", [sonar.F64, sonar.F32])
+def test_magnitude_matches_oracle(ctx, W, H, prec):
+    x = _sig(W * 7 + 123)
+    cfg = ctx.config(window_size=W, hop_size=H, flags=sonar.FP_MAGNITUDE, precision=prec)
+    got = ctx.fingerprint(x, cfg)["magnitude"]
+    ref = O.stft_mag(x, W, H)
+    assert got.shape == ref.shape
+    tol = 1e-11 if prec == sonar.F64 else 2e-6
+    assert _rel_rows(got, ref, ref.max(axis=1)) < tol
+
+
+@pytest.mark.parametrize("win", ["hann", "hamming", "blackman", "blackman_harris", "kaiser", "tukey",
+                                 "rectangular", "bartlett", "welch"])
+def test_window_types(ctx, win):
+    x = _sig(1024 * 4)
+    cfg = ctx.config(window_size=1024, hop_size=256, window_type=win, flags=sonar.FP_MAGNITUDE,
+                     precision=sonar.F64)
+    got = ctx.fingerprint(x, cfg)["magnitude"]
+    ref = O.stft_mag(x, 1024, 256, window_type=win)
+    assert _rel_rows(got, ref, ref.max(axis=1)) < 1e-11
+
+
+def test_frame_count_and_short_signal_rules(ctx):
+    # Go truncating division: n in (W-H, W) gives one all-zero frame (spectral.go:409, :524-534)
+    assert sonar.stft_frames(1000, 1024, 256) == 1
+    assert sonar.stft_frames(768, 1024, 256) == sonar._abi.ERR_TOO_SHORT
+    x = _sig(1000)
+    got = ctx.fingerprint(x, ctx.config(flags=sonar.FP_MAGNITUDE, precision=sonar.F64))["magnitude"]
+    assert got.shape == (1, 513) and np.all(got == 0)
+    with pytest.raises(sonar.SonarError, match="signal too short"):
+        ctx.fingerprint(_sig(700), ctx.config(flags=sonar.FP_MAGNITUDE))
+    with pytest.raises(sonar.SonarError, match="empty signal"):
+        ctx.fingerprint(np.zeros(0), ctx.config())
+    with pytest.raises(sonar.SonarError, match="hop size must be positive"):
+        ctx.fingerprint(_sig(4096), ctx.config(hop_size=0))
+
+
+@pytest.mark.parametrize("sr,nm,nc,W", [(44100, 40, 13, 1024), (44100, 26, 13, 1024), (16000, 26, 13, 512),
+                                       (44100, 26, 13, 2048), (22050, 32, 20, 256)])
+def test_mfcc_f64_matches_oracle(ctx, sr, nm, nc, W):
+    x = _sig(W * 40)
+    H = W // 4
+    cfg = ctx.config(window_size=W, hop_size=H, sample_rate=sr, n_filters=nm, n_mfcc=nc, precision=sonar.F64)
+    got = ctx.fingerprint(x, cfg)["mfcc"]
+    ref = O.mfcc_frames(O.stft_mag(x, W, H), sr, n_coef=nc, n_mels=nm)
+    assert _rel_rows(got, ref, np.linalg.norm(ref, axis=1)) < 1e-9
+
+
+def test_mfcc_f32_headline_config(ctx):
+    """1 h config's arithmetic: sweep + 0.05 N(0,1), W=1024 H=256, 40 mels -> 13 MFCC, f32."""
+    x = synth.c2_hour(seconds=20.0)
+    cfg = ctx.config(window_size=1024, hop_size=256, sample_rate=44100, n_filters=40, n_mfcc=13,
+                     precision=sonar.F32, pcm_dtype=sonar.F32, out_dtype=sonar.F32)
+    got = ctx.fingerprint(x, cfg)["mfcc"].astype(np.float64)
+    ref = O.mfcc_frames(O.stft_mag(x.astype(np.float64), 1024, 256, nthreads=8), 44100, n_coef=13, n_mels=40)
+    assert got.shape == ref.shape == (3442, 13)
+    assert _rel_rows(got, ref, np.linalg.norm(ref, axis=1)) < 1e-4
+
+
+def test_mfcc_sample_rate_zero_constant(ctx):
+    """F1/F2: GenerateFingerprint runs NewMFCC(0, 13) -> all-zero filterbank -> constant MFCC."""
+    x = synth.sweep(2.0)
+    for prec in (sonar.F64, sonar.F32):
+        got = ctx.fingerprint(x, ctx.config(sample_rate=0, precision=prec))["mfcc"]
+        tol = 1e-9 if prec == sonar.F64 else 1e-4
+        assert np.allclose(got[:, 0], np.sqrt(26) * np.log(1e-10), rtol=0, atol=117.41 * tol)   # -117.409263
+        assert np.abs(got[:, 1:]).max() < 117.41 * tol
+
+
+def test_mfcc_music_power_input_and_bark(ctx):
+    x = _sig(1024 * 30)
+    mag = O.stft_mag(x, 1024, 256)
+    got = ctx.fingerprint(x, ctx.config(mfcc_input_power=1, precision=sonar.F64))["mfcc"]
+    ref = O.mfcc_frames(mag ** 2, 44100)          # music.go:311-317 feeds |X|^2 (F5)
+    assert _rel_rows(got, ref, np.linalg.norm(ref, axis=1)) < 1e-9
+    got = ctx.fingerprint(x, ctx.config(filterbank=1, precision=sonar.F64))["mfcc"]
+    ref = O.mfcc_frames(mag, 44100, kind="bark")
+    assert _rel_rows(got, ref, np.linalg.norm(ref, axis=1)) < 1e-9
+
+
+@pytest.mark.parametrize("pcm_dtype", [sonar.F64, sonar.F32])
+def test_zcr_bit_exact_and_energy(ctx, pcm_dtype):
+    x = _sig(1024 * 50, seed=3)
+    if pcm_dtype == sonar.F32:
+        x = x.astype(np.float32)
+    x64 = x.astype(np.float64)
+    cfg = ctx.config(flags=sonar.FP_ZCR | sonar.FP_ENERGY, energy_window=1024, energy_hop=256, sample_rate=16000,
+                     pcm_dtype=pcm_dtype)
+    got = ctx.fingerprint(x, cfg)
+    pre = O.preemphasis(x64, 0.97)
+    F = O.stft_frames(len(x), 1024, 256)
+    assert np.array_equal(got["zcr"], O.zcr_frames(pre, F, 1024, 256, 16000))
+    ref_e = O.short_time_energy(pre, 1024, 256)
+    assert np.array_equal(got["energy"], ref_e)   # same sequential float64 order -> bit-identical
+    # sr = 0 (F3): ZCR = crossings / (+Inf) = 0
+    got0 = ctx.fingerprint(x, ctx.config(flags=sonar.FP_ZCR, sample_rate=0, pcm_dtype=pcm_dtype))
+    assert np.all(got0["zcr"] == 0)

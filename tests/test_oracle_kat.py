@@ -1,0 +1,84 @@
+"""CPU: the oracle against analytic known answers and numpy.
+The Go reference has no tests/fixtures and cannot run here (no Go toolchain), so
+these KATs + numpy are what pin the oracle ("parity unpinned" w.r.t. Go)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from sonar import synth
+
+
+def test_fft_matches_numpy():
+    rng = np.random.default_rng(0)
+    for n in (8, 256, 1024, 2048, 255, 1000, 441):
+        x = rng.standard_normal(n)
+        assert np.max(np.abs(O.fft(x) - np.fft.fft(x))) < 1e-10 * n
+
+
+def test_hann_normalisation_factor():
+    w = O.window("hann", 1024)
+    raw = 0.5 * (1 - np.cos(2 * np.pi * np.arange(1024) / 1023))
+    assert w[512] / raw[512] == pytest.approx(1.6337911062772983, rel=1e-12)
+    assert np.mean(w ** 2) == pytest.approx(1.0, rel=1e-12)    # unit power gain (windowing.go:427-437)
+
+
+def test_mel_bin_points_and_nnz():
+    fb = O.filterbank(26, 1024, 44100, 0, 22050)
+    assert np.count_nonzero(fb) == 933
+    assert np.count_nonzero(O.filterbank(40, 1024, 44100, 0, 22050)) == 940
+    # integer bin points [0,2,5,8,11,15,19,24,...,392,449,512]: peak (weight 1) positions
+    peaks = [int(np.argmax(r)) for r in fb]
+    assert peaks[:6] == [2, 5, 8, 11, 15, 19] and peaks[-1] == 449
+
+
+def test_frame_count_10s():
+    assert O.stft_frames(441000, 1024, 256) == 1719
+    assert O.stft_frames(158_760_000, 1024, 256) == 620_153
+    assert O.stft_frames(13_230_000, 1024, 256) == 51_676
+    assert O.stft_frames(28_800_000, 512, 128) == 224_997
+
+
+def test_sample_rate_zero_mfcc_constant():
+    mag = O.stft_mag(synth.sweep(1.0), 1024, 256)
+    m = O.mfcc_frames(mag, 0)
+    assert np.allclose(m[:, 0], -117.409263, atol=1e-6)
+    assert np.abs(m[:, 1:]).max() < 1e-12
+
+
+def test_bin_centred_sine_energy_concentration():
+    k, W = 40, 1024
+    x = np.sin(2 * np.pi * k * np.arange(W * 4) / W)
+    mag = O.stft_mag(x, W, 256)
+    e = mag ** 2
+    assert np.all(e[:, k - 1:k + 2].sum(1) / e.sum(1) > 0.99)
+
+
+def test_ncc_delay_kat():
+    rng = np.random.default_rng(1)
+    s = np.convolve(rng.standard_normal(3000), np.ones(7), "same")
+    d = 25
+    corr, met = O.ncc(s[:2000], s[d:2000 + d] if False else np.concatenate([np.zeros(d), s[:2000 - d]]), 100)
+    assert met["peak_lag"] == d
+
+
+def test_dtw_identical_is_diagonal():
+    q = np.random.default_rng(2).random((50, 3))
+    r = O.dtw(q, q)
+    assert r["distance"] == 0.0
+    assert np.array_equal(r["path_q"], np.arange(50)) and np.array_equal(r["path_r"], np.arange(50))
+
+
+def test_chroma_a440_bin9():
+    # with a fine frame (fs = 8192 -> 5.4 Hz bins) 440 Hz folds to pitch class 9 (A);
+    # the music extractor's own frames are ~hop long (F6), far too coarse for this KAT
+    t = np.arange(8192 * 10) / 44100
+    x = np.sin(2 * np.pi * 440 * t)
+    c = O.chroma_frames(x, 10, 4096, 8192, 44100)
+    assert np.all(np.argmax(c[:-2], axis=1) == 9)
+
+
+def test_yin_finds_220hz():
+    sr = 16000
+    t = np.arange(1024) / sr
+    p, c, tau = O.yin_raw(np.sin(2 * np.pi * 220 * t), sr)
+    assert abs(p - 220) < 2 and c > 0.5
