@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""Benchmark of the sonido-sonar hot path on MI355X (see BASELINE.json / DESIGN.md).
+
+Headline: audio frames/sec of the fused STFT -> mel(40) -> MFCC(13) kernel
+(W=1024, H=256, 44.1 kHz, float32) on 1 h of synthetic PCM per GPU, PCM
+resident in HBM when timing starts.  Multi-GPU (torchrun, one process per
+GPU): every rank fingerprints its own 1 h stream (frames shard with no
+data-path collective -> "scaling": "weak"); the RCCL all-gather that
+reassembles the feature timeline runs once after the timed region and is
+reported separately.  Extra fields: DTW cells/sec (C3 size, float64, cost
+matrix in HBM), roofline of the dominant kernel, CPU baseline (the oracle,
+a float64 C restatement of the Go path, on a bounded sample).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "sonido-sonar_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import sonar  # noqa: E402
+from sonar import synth  # noqa: E402
+
+W, H, SR, N_MELS, N_MFCC = 1024, 256, 44100, 40, 13
+BYTES_PER_FRAME = 4 * H + 4 * N_MFCC            # PCM in (hop, f32) + MFCC out (f32)
+FLOPS_PER_FRAME = 31136                          # window + FFT + |X|^2 + mel + ln + DCT + lifter
+HBM_PEAK_GBS = 8000.0                            # MI355X_MICROARCH.md: 8 TB/s spec
+FP32_PEAK_TFS = 157.3                            # FP32 vector (= f32 MFMA) peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seconds", type=float, default=3600.0, help="audio seconds per GPU (1 h config)")
+    ap.add_argument("--dtw-len", type=int, default=51676, help="DTW sequence length (0 = skip); C3 = 51,676")
+    ap.add_argument("--dtw-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=0.0, help="force CPU-baseline sample length")
+    return ap.parse_args()
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        torch.distributed.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_pcm(seconds, rank, device):
+    """C2 recipe on the device: the 10 s sweep tiled + 0.05 N(0,1), float32."""
+    n = int(round(seconds * SR))
+    base = torch.tensor(synth.sweep(10.0), dtype=torch.float32, device=device)
+    reps = math.ceil(n / base.numel())
+    pcm = base.repeat(reps)[:n].contiguous()
+    g = torch.Generator(device=device)
+    g.manual_seed(1234 + rank)
+    pcm.add_(0.05 * torch.randn(n, generator=g, device=device, dtype=torch.float32))
+    return pcm
+
+
+def load_traffic():
+    """Per-launch HBM bytes of the fused kernel from the committed rocprofv3 PMC summary."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("fp_tile_kernel_hbm_bytes_per_launch")
+
+
+def cpu_baseline(seconds_hint):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = os.cpu_count() or 1
+    threads = min(threads, 16)      # the GPU box shares its CPUs: 16 is this job's share
+    probe = 60.0
+    x = synth.c2_hour(seconds=probe).astype(np.float64)
+    t0 = time.perf_counter()
+    m = O.stft_mag(x, W, H, nthreads=threads)
+    O.mfcc_frames(m, SR, n_coef=N_MFCC, n_mels=N_MELS)
+    dt = time.perf_counter() - t0
+    secs = seconds_hint or min(3600.0, max(probe, probe * 15.0 / max(dt, 1e-6)))   # ~15 s of CPU work
+    x = synth.c2_hour(seconds=secs).astype(np.float64)
+    t0 = time.perf_counter()
+    m = O.stft_mag(x, W, H, nthreads=threads)
+    O.mfcc_frames(m, SR, n_coef=N_MFCC, n_mels=N_MELS)
+    dt = time.perf_counter() - t0
+    return {"value": len(m) / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{secs:.0f} s of the C2 signal ({len(m)} frames), float64: STFT over {threads} threads "
+                      "(Go worker-pool shape), MFCC.ComputeFrames single-threaded, as in the Go path"}
+
+
+def bench_dtw(ctx, n, steps):
+    rng = np.random.default_rng(7)
+    q = rng.random((n, 12))
+    r = np.roll(q, 37, axis=0) + 0.01 * rng.random((n, 12))
+    ctx.dtw(q[:256], r[:256])       # warm-up / allocation of small buffers
+    ctx.dtw(q, r)                   # allocation of the (n+1)^2 cost matrix
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = ctx.dtw(q, r)
+    dt = (time.perf_counter() - t0) / steps
+    return {"dtw_cells_per_s": n * n / dt, "dtw_ms": dt * 1e3, "dtw_n": n, "dtw_dim": 12,
+            "dtw_path_len": int(len(res["path_q"]))}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup()
+    dev = torch.device("cuda", local)
+    pcm = make_pcm(args.seconds, rank, dev)
+    n = pcm.numel()
+    F = sonar.stft_frames(n, W, H)
+    out = torch.empty((F, N_MFCC), dtype=torch.float32, device=dev)
+    ctx = sonar.Context(local)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    cfg = ctx.config(window_size=W, hop_size=H, sample_rate=SR, n_filters=N_MELS, n_mfcc=N_MFCC,
+                     precision=sonar.F32, pcm_dtype=sonar.F32, out_dtype=sonar.F32, flags=sonar.FP_MFCC)
+
+    def step():
+        ctx.fingerprint_device(pcm.data_ptr(), n, cfg, mfcc=out.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.last_kernel_ms()              # drop warm-up event pairs
+    ctx.enable_kernel_timing(True)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    ctx.enable_kernel_timing(False)
+    kernel_ms = ctx.last_kernel_ms()
+    elapsed = max_over_ranks(elapsed, world)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = F * world / (elapsed / args.steps)
+
+    # RCCL all-gather of the MFCC timeline (reassembly of the N-stream feature
+    # timeline over xGMI), once, outside the timed region
+    gather_ms = None
+    if world > 1:
+        parts = [torch.empty_like(out) for _ in range(world)]
+        torch.cuda.synchronize()
+        barrier(world)
+        tg = time.perf_counter()
+        torch.distributed.all_gather(parts, out)
+        torch.cuda.synchronize()
+        gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3, world)
+        assert torch.equal(parts[rank], out)
+
+    extra = {}
+    if args.dtw_len > 0:
+        extra = bench_dtw(ctx, args.dtw_len, args.dtw_steps)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    achieved_gbs = F * BYTES_PER_FRAME / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic()
+    line = {
+        "metric": "audio frames/sec (STFT->MFCC, 1024/256)",
+        "value": value,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (C2: 10 s 100 Hz-10 kHz sweep tiled + 0.05 N(0,1), seeded per rank)",
+        "config": {"workload": "STFT(W=1024,H=256,Hann)->mel(40)->ln->DCT-II(13)->lifter(22) on 1 h of "
+                               "44.1 kHz float32 PCM per GPU", "frames_per_gpu": F, "samples_per_gpu": n,
+                   "parallelism": f"frame-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved_gbs / HBM_PEAK_GBS,
+                     "traffic": traffic, "kernel": "fp_tile_kernel<float,8>", "kernel_ms": kernel_ms,
+                     "algorithmic_bytes_per_frame": BYTES_PER_FRAME,
+                     "valu_tflops": F * FLOPS_PER_FRAME / (kernel_ms * 1e-3) / 1e12,
+                     "valu_frac": F * FLOPS_PER_FRAME / (kernel_ms * 1e-3) / 1e12 / FP32_PEAK_TFS},
+        "cpu_baseline": cpu,
+    }
+    if gather_ms is not None:
+        line["allgather_ms"] = gather_ms
+        line["allgather_bytes_per_rank"] = out.numel() * 4 * world
+    line.update(extra)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -134,7 +134,18 @@ int or_window(int type, int size, int symmetric, int normalize, double beta, dou
 /* UNPINNED: only the DFT definition X_k = sum x_n e^{-2 pi i kn/N} is  */
 /* relied on).  Radix-2 for powers of two, Bluestein otherwise.        */
 /* ------------------------------------------------------------------ */
+/* twiddles e^{-2 pi i k/n}, k < n/2, cached per thread (go-dsp also caches its factors) */
+static __thread double* tw_re = NULL;
+static __thread double* tw_im = NULL;
+static __thread int tw_n = 0;
+
 static void fft_pow2(double* re, double* im, int n, int inverse) {
+    if (n != tw_n) {
+        free(tw_re); free(tw_im);
+        tw_re = malloc(sizeof(double) * (n / 2 + 1)); tw_im = malloc(sizeof(double) * (n / 2 + 1));
+        for (int k = 0; k < n / 2; k++) { double a = -2.0 * M_PI * (double)k / (double)n; tw_re[k] = cos(a); tw_im[k] = sin(a); }
+        tw_n = n;
+    }
     for (int i = 1, j = 0; i < n; i++) {
         int bit = n >> 1;
         for (; j & bit; bit >>= 1) j ^= bit;
@@ -142,11 +153,9 @@ static void fft_pow2(double* re, double* im, int n, int inverse) {
         if (i < j) { double t = re[i]; re[i] = re[j]; re[j] = t; t = im[i]; im[i] = im[j]; im[j] = t; }
     }
     for (int len = 2; len <= n; len <<= 1) {
-        int half = len >> 1;
-        double sgn = inverse ? 1.0 : -1.0;
+        int half = len >> 1, step = n / len;
         for (int k = 0; k < half; k++) {
-            double ang = sgn * 2.0 * M_PI * (double)k / (double)len;
-            double wr = cos(ang), wi = sin(ang);
+            double wr = tw_re[k * step], wi = inverse ? -tw_im[k * step] : tw_im[k * step];
             for (int i = k; i < n; i += len) {
                 int j = i + half;
                 double xr = re[j] * wr - im[j] * wi;

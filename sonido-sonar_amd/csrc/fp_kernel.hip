@@ -8,21 +8,25 @@
 //   per-frame spectral descriptors            fingerprint/extractors/speech.go:320-367, :438-458
 //
 // Layout / schedule (see DESIGN.md "Kernel 1"):
-//  * one block = 256 threads = 4 waves = one tile of `tile_f` frames; blocks are
-//    persistent over a contiguous run of tiles (halo re-reads hit L2).
+//  * block = 256 threads = 4 independent waves; the twiddle tables are built once
+//    per block in LDS; afterwards no block barrier is used.  Every wave owns a
+//    contiguous run of frames (halo re-reads of the overlapping PCM hit L1/L2)
+//    and processes it in batches of NB frames; the next unit's PCM loads are
+//    issued before the current FFT so they stay in flight.
 //  * a wave computes FR frames at a time (FR = 8/R for R < 8): the W-point real
 //    FFT is a M = W/2 = 64*R point complex FFT of z[n] = x[2n] + i x[2n+1]:
 //      step 1: lane b holds z[64a+b] (a < R) -> R-point DFT in registers, twiddle w_M^{bc}
 //      step 2: 64-point DFT across lanes for every column c, done as 8 x 8:
 //              LDS exchange A, DFT8, twiddle w_64^{fg}, LDS exchange B, DFT8
-//      step 3: real split X_k = E_k + w_W^k O_k (partner bin M-k through LDS)
+//      step 3: real split X_k = E_k + w_W^k O_k (partner bin M-k by ds_bpermute)
 //    Exchanges use XOR-swizzled addresses chosen so every ds_write_b32 / ds_read_b32
-//    is bank-conflict-free (searched offline, tools/ in DESIGN.md).  The scratch
-//    is the frame's own LDS spectrum row, so a tile needs only tile_f * (M+1) words.
-//  * epilogue with lane = frame: thread (frame f, group g); group g owns a set of
-//    filterbank rows balanced by nonzero count (sparse triangle sums in Go's
-//    ascending-bin order), then the DCT rows g, g+G, ...; results are staged in
-//    LDS and written with coalesced stores.
+//    is bank-conflict-free (searched offline: tools/lds_banks.py).  The scratch
+//    is the frame's own LDS spectrum row.
+//  * batch epilogue with lane = (frame f, group g), NB frames x (64/NB) groups:
+//    group g owns a set of filterbank rows balanced by nonzero count (sparse
+//    triangle sums in Go's ascending-bin order), then DCT row g; descriptors are
+//    per-group partial sums over a bin chunk reduced with xor-shuffles; results
+//    are staged in LDS and written with coalesced stores.
 #include "kernels.h"
 #include "twiddles.h"
 
@@ -106,24 +110,74 @@ __device__ __forceinline__ void sincos_turns(double turns, T& c, T& s) {
 
 }  // namespace
 
-template <typename T, int R>
-__global__ __launch_bounds__(256, 2) void fp_tile_kernel(FpParams p) {
-  constexpr int FR = (R >= 8) ? 1 : 8 / R;   // frames per wave pass
+template <typename P> struct Vec2;
+template <> struct Vec2<float> { using type = float2; };
+template <> struct Vec2<double> { using type = double2; };
+
+template <typename T, typename P, int R, bool SPEC>
+__global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
+  constexpr int FR = (R >= 8) ? 1 : 8 / R;   // frames per FFT unit
   constexpr int V = R * FR;                   // values per lane
   constexpr int G = V / 8;                    // 8-column groups
   constexpr int M = 64 * R;                   // complex FFT size
   constexpr int K = M + 1;                    // bins per frame (LDS row stride)
+  constexpr int NB = FR > 4 ? FR : 4;         // frames per epilogue batch
+  constexpr int NG = 64 / NB;                 // epilogue lanes per frame
+  constexpr int UPB = NB / FR;                // units per batch
+  constexpr int PRE = SPEC ? FR : 0;          // rows before the batch (flux predecessor unit)
 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  T* Prow = reinterpret_cast<T*>(smem + p.lds_P);
-  T* logmel = reinterpret_cast<T*>(smem + p.lds_logmel);
-  T* stage = reinterpret_cast<T*>(smem + p.lds_stage);
-
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const T* win = reinterpret_cast<const T*>(p.window);
+  T* t1 = reinterpret_cast<T*>(smem + p.lds_tab_t1);   // [R][64] complex: w_M^{lane c}
+  T* t2 = reinterpret_cast<T*>(smem + p.lds_tab_t2);   // [64] complex: w_64^j
+  T* t3 = reinterpret_cast<T*>(smem + p.lds_tab_t3);   // [G*8][64] complex: w_W^k per lane slot
+  unsigned char* wbase = smem + p.lds_wave0 + wave * p.lds_wave_stride;
+  T* rows = reinterpret_cast<T*>(wbase);
+  T* logmel = reinterpret_cast<T*>(wbase + p.lds_logmel);
+  T* stage = reinterpret_cast<T*>(wbase + p.lds_stage);
 
-  // ---- per-lane constants, identical for every frame ----------------------
+  const int f2 = lane & 7, cl2 = lane >> 3;   // step-2 role: column cl2, f
+  const int g3 = lane >> 3, cl3 = lane & 7;   // step-3 role: lane = 8 g + cl
+
+  // ---- twiddle tables (double-evaluated, rounded to T), once per block ----
+  for (int i = threadIdx.x; i < R * 64; i += blockDim.x) {
+    const int c = i / 64, l = i % 64;
+    T cr, ci; sincos_turns<T>(-(double)((l * c) % M) / (double)M, cr, ci);
+    t1[2 * i] = cr; t1[2 * i + 1] = ci;
+  }
+  for (int i = threadIdx.x; i < 64; i += blockDim.x) {
+    T cr, ci; sincos_turns<T>(-(double)i / 64.0, cr, ci);
+    t2[2 * i] = cr; t2[2 * i + 1] = ci;
+  }
+  for (int i = threadIdx.x; i < G * 8 * 64; i += blockDim.x) {
+    const int slot = i / 64, l = i % 64;          // slot = gm*8 + h
+    const int gm = slot / 8, h = slot % 8;
+    const int col = 8 * gm + (l & 7), c = col % R;
+    const int k = c + R * (l >> 3) + 8 * R * h;
+    T cr, ci; sincos_turns<T>(-(double)k / (double)(2 * M), cr, ci);
+    t3[2 * i] = cr; t3[2 * i + 1] = ci;
+  }
+  // filterbank / DCT tables -> LDS (read by every epilogue lane, group-varying addresses)
+  int* e_lo = reinterpret_cast<int*>(smem + p.lds_tab_mel);
+  int* e_hi = e_lo + p.n_mels;
+  int* e_woff = e_hi + p.n_mels;
+  int* e_goff = e_woff + p.n_mels;
+  int* e_gmel = e_goff + (p.n_groups + 1);
+  T* e_w = reinterpret_cast<T*>(smem + p.lds_tab_w);
+  T* e_dct = reinterpret_cast<T*>(smem + p.lds_tab_dct);
+  T* e_lift = e_dct + p.n_mfcc * p.n_mels;
+  if (p.out_mfcc) {
+    for (int i = threadIdx.x; i < p.n_mels; i += blockDim.x) { e_lo[i] = p.mel_lo[i]; e_hi[i] = p.mel_hi[i]; e_woff[i] = p.mel_woff[i]; }
+    for (int i = threadIdx.x; i <= p.n_groups; i += blockDim.x) e_goff[i] = p.grp_off[i];
+    for (int i = threadIdx.x; i < p.n_mels; i += blockDim.x) e_gmel[i] = p.grp_mels[i];
+    for (int i = threadIdx.x; i < p.nnz; i += blockDim.x) e_w[i] = reinterpret_cast<const T*>(p.mel_w)[i];
+    for (int i = threadIdx.x; i < p.n_mfcc * p.n_mels; i += blockDim.x) e_dct[i] = reinterpret_cast<const T*>(p.dct)[i];
+    for (int i = threadIdx.x; i < p.n_mfcc; i += blockDim.x) e_lift[i] = reinterpret_cast<const T*>(p.lift)[i];
+  }
+  __syncthreads();
+
+  const T* win = reinterpret_cast<const T*>(p.window);
   T we[R], wo[R];                        // window at the lane's even/odd samples
 #pragma unroll
   for (int a = 0; a < R; a++) {
@@ -131,78 +185,85 @@ __global__ __launch_bounds__(256, 2) void fp_tile_kernel(FpParams p) {
     we[a] = win[n0];
     wo[a] = win[n0 + 1];
   }
-  T t1r[R], t1i[R];                      // w_M^{lane * c}
+
+  // ---- this wave's frame range and unit sequence ---------------------------
+  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  const int64_t f_begin = gw * p.frames_per_wave;
+  if (f_begin >= p.F) return;
+  const int64_t f_end = min(p.F, f_begin + p.frames_per_wave);
+  const int64_t nbatch = (f_end - f_begin + NB - 1) / NB;
+  const int pre = (SPEC && f_begin > 0) ? 1 : 0;
+  const int64_t nunits = pre + nbatch * UPB;
+  const bool fft_only = (p.flags >> 31) & 1u;
+
+  // unit i -> first frame, first row
+  auto unit_frame = [&](int64_t i) -> int64_t {
+    if (pre) { if (i == 0) return f_begin - FR; i -= 1; }
+    return f_begin + (i / UPB) * NB + (i % UPB) * FR;
+  };
+  auto unit_row = [&](int64_t i) -> int {
+    if (pre) { if (i == 0) return 0; i -= 1; }
+    return PRE + (int)(i % UPB) * FR;
+  };
+  // raw PCM of one unit (FR frames); validity is wave-uniform (depends on the frame only)
+  auto load_unit = [&](int64_t uf, T (&er)[FR][R], T (&od)[FR][R]) {
 #pragma unroll
-  for (int c = 0; c < R; c++) sincos_turns<T>(-(double)((lane * c) % M) / (double)M, t1r[c], t1i[c]);
-  const int f2 = lane & 7;               // step-2 role: column cl2 = lane >> 3, f = lane & 7
-  const int cl2 = lane >> 3;
-  T t2r[8], t2i[8];                      // w_64^{f * g}
+    for (int fr = 0; fr < FR; fr++) {
+      const int64_t t = uf + fr;
+      // Go skips frames whose end passes the signal (spectral.go:524-534): row stays all-zero
+      const bool valid = (t >= 0) && (t < p.F) && (t * p.H + p.W <= p.n);
+      const int64_t s0 = t * p.H;
+      if (valid) {
+        const P* base = reinterpret_cast<const P*>(p.pcm) + s0 + 2 * lane;
+        if ((s0 & 1) == 0) {       // 8 / 16-byte aligned pairs
+          using V2 = typename Vec2<P>::type;
 #pragma unroll
-  for (int g = 0; g < 8; g++) sincos_turns<T>(-(double)((f2 * g) % 64) / 64.0, t2r[g], t2i[g]);
-  const int g3 = lane >> 3;              // step-3 role: lane = 8 g + cl
-  const int cl3 = lane & 7;
-  T t3r[G][8], t3i[G][8];                // w_W^k for the lane's output bins
+          for (int a = 0; a < R; a++) {
+            const V2 v = *reinterpret_cast<const V2*>(base + 128 * a);
+            er[fr][a] = (T)v.x; od[fr][a] = (T)v.y;
+          }
+        } else {
 #pragma unroll
-  for (int gm = 0; gm < G; gm++) {
-    const int col = 8 * gm + cl3;
-    const int c = col % R;
+          for (int a = 0; a < R; a++) { er[fr][a] = (T)base[128 * a]; od[fr][a] = (T)base[128 * a + 1]; }
+        }
+      } else {
 #pragma unroll
-    for (int h = 0; h < 8; h++) {
-      const int k = c + R * g3 + 8 * R * h;
-      sincos_turns<T>(-(double)k / (double)(2 * M), t3r[gm][h], t3i[gm][h]);
+        for (int a = 0; a < R; a++) { er[fr][a] = 0; od[fr][a] = 0; }
+      }
     }
-  }
+  };
 
-  const int64_t chunk = (p.ntiles + gridDim.x - 1) / gridDim.x;
-  const int64_t tile_begin = (int64_t)blockIdx.x * chunk;
-  const int64_t tile_end = min(p.ntiles, tile_begin + chunk);
-  const int units = p.tile_f / FR;
+  T cur_e[FR][R], cur_o[FR][R];
+  load_unit(unit_frame(0), cur_e, cur_o);
 
-  for (int64_t tile = tile_begin; tile < tile_end; ++tile) {
-    const int64_t tb = tile * p.stride - p.r0;   // frame of LDS row 0
+  for (int64_t ui = 0; ui < nunits; ++ui) {
+    T nxt_e[FR][R], nxt_o[FR][R];
+    if (ui + 1 < nunits) load_unit(unit_frame(ui + 1), nxt_e, nxt_o);
+    const int64_t uf = unit_frame(ui);
+    const int rb = unit_row(ui);
+    T* S = rows + (int64_t)rb * K;              // scratch = the unit's own rows
 
-    // ======================= FFT phase: wave-private =======================
-    for (int u = wave; u < units; u += 4) {
-      const int rb = u * FR;
-      T* S = Prow + (int64_t)rb * K;             // scratch = the unit's own rows
-      bool any = false;
+    // ======================= FFT of FR frames ===============================
+    {
       T xr[FR][R], xi[FR][R];
 #pragma unroll
-      for (int fr = 0; fr < FR; fr++) {
-        const int64_t t = tb + rb + fr;
-        const bool exists = (t >= 0) && (t < p.F);
-        // Go skips frames whose end passes the signal (spectral.go:524-534): row stays all-zero
-        const bool valid = exists && (t * p.H + p.W <= p.n);
-        any |= exists;
-        const int64_t s0 = t * p.H;
+      for (int fr = 0; fr < FR; fr++)
 #pragma unroll
-        for (int a = 0; a < R; a++) {
-          const int64_t n0 = s0 + 2 * (64 * a + lane);
-          T e = 0, o = 0;
-          if (valid) {
-            e = load_pcm<T>(p.pcm, p.pcm_f64, n0);
-            o = load_pcm<T>(p.pcm, p.pcm_f64, n0 + 1);
-          }
-          xr[fr][a] = e * we[a];
-          xi[fr][a] = o * wo[a];
-        }
-      }
-      if (!any) continue;   // wave-uniform
-
+        for (int a = 0; a < R; a++) { xr[fr][a] = cur_e[fr][a] * we[a]; xi[fr][a] = cur_o[fr][a] * wo[a]; }
       // step 1: R-point DFT over a, twiddle w_M^{lane c}
 #pragma unroll
       for (int fr = 0; fr < FR; fr++) {
         dft_reg<T, R>(xr[fr], xi[fr]);
 #pragma unroll
         for (int c = 1; c < R; c++) {
+          const T wr = t1[2 * (c * 64 + lane)], wi = t1[2 * (c * 64 + lane) + 1];
           const T a_ = xr[fr][c], b_ = xi[fr][c];
-          xr[fr][c] = a_ * t1r[c] - b_ * t1i[c];
-          xi[fr][c] = a_ * t1i[c] + b_ * t1r[c];
+          xr[fr][c] = a_ * wr - b_ * wi;
+          xi[fr][c] = a_ * wi + b_ * wr;
         }
       }
-      // value for column col = fr*R + c  ->  flat index col
-      T yr[G][8], yi[G][8];
       // exchange A: write S[gm*512 + 64*cl + (lane ^ 8cl)], read S[gm*512 + 64*cl2 + ((8e+f2) ^ 8cl2)]
+      T yr[G][8], yi[G][8];
 #pragma unroll
       for (int plane = 0; plane < 2; plane++) {
 #pragma unroll
@@ -227,9 +288,11 @@ __global__ __launch_bounds__(256, 2) void fp_tile_kernel(FpParams p) {
         dft_reg<T, 8>(yr[gm], yi[gm]);
 #pragma unroll
         for (int g = 1; g < 8; g++) {
+          const int j = (f2 * g) & 63;
+          const T wr = t2[2 * j], wi = t2[2 * j + 1];
           const T a_ = yr[gm][g], b_ = yi[gm][g];
-          yr[gm][g] = a_ * t2r[g] - b_ * t2i[g];
-          yi[gm][g] = a_ * t2i[g] + b_ * t2r[g];
+          yr[gm][g] = a_ * wr - b_ * wi;
+          yi[gm][g] = a_ * wi + b_ * wr;
         }
       }
       // exchange B: write S[gm*512 + 64*cl2 + ((8g+f2) ^ (9cl2 & 63))], read with lane = 8g3 + cl3
@@ -255,110 +318,222 @@ __global__ __launch_bounds__(256, 2) void fp_tile_kernel(FpParams p) {
 #pragma unroll
       for (int gm = 0; gm < G; gm++) dft_reg<T, 8>(zr[gm], zi[gm]);
 
-      // real split: partner Z_fr[(M-k) mod M] through LDS (one plane at a time)
+      // real split needs the partner bin Z_fr[(M-k) mod M]
       T pr_[G][8], pi_[G][8];
+      if constexpr (G == 1) {
+        // partner is a fixed lane permutation: lane' = 8(7-g3) + fr R + (R-c) for c > 0,
+        // 8(8-g3) + fr R for c == 0 < g3, itself (register (8-h) & 7) for c == g3 == 0;
+        // source register 7-h.  ds_bpermute: no LDS allocation, no fences.
+        const int fr = cl3 / R, c = cl3 % R;
+        const bool self = (c == 0) && (g3 == 0);
+        const int src = (c > 0) ? (8 * (7 - g3) + fr * R + (R - c)) : (8 * ((8 - g3) & 7) + fr * R);
 #pragma unroll
-      for (int plane = 0; plane < 2; plane++) {
-#pragma unroll
-        for (int gm = 0; gm < G; gm++) {
-          const int col = 8 * gm + cl3, fr = col / R, c = col % R;
-#pragma unroll
-          for (int h = 0; h < 8; h++) {
-            const int k = c + R * g3 + 8 * R * h;
-            S[fr * M + k] = plane ? zi[gm][h] : zr[gm][h];
-          }
+        for (int h = 0; h < 8; h++) {
+          const T sr = __shfl(zr[0][7 - h], src, 64);
+          const T si = __shfl(zi[0][7 - h], src, 64);
+          pr_[0][h] = self ? zr[0][(8 - h) & 7] : sr;
+          pi_[0][h] = self ? zi[0][(8 - h) & 7] : si;
         }
-        wave_lds_sync();
+      } else {
 #pragma unroll
-        for (int gm = 0; gm < G; gm++) {
-          const int col = 8 * gm + cl3, fr = col / R, c = col % R;
+        for (int plane = 0; plane < 2; plane++) {
 #pragma unroll
-          for (int h = 0; h < 8; h++) {
-            const int k = c + R * g3 + 8 * R * h;
-            const T v = S[fr * M + ((M - k) & (M - 1))];
-            if (plane) pi_[gm][h] = v; else pr_[gm][h] = v;
+          for (int gm = 0; gm < G; gm++) {
+            const int col = 8 * gm + cl3, fr = col / R, c = col % R;
+#pragma unroll
+            for (int h = 0; h < 8; h++) {
+              const int k = c + R * g3 + 8 * R * h;
+              S[fr * M + k] = plane ? zi[gm][h] : zr[gm][h];
+            }
           }
+          wave_lds_sync();
+#pragma unroll
+          for (int gm = 0; gm < G; gm++) {
+            const int col = 8 * gm + cl3, fr = col / R, c = col % R;
+#pragma unroll
+            for (int h = 0; h < 8; h++) {
+              const int k = c + R * g3 + 8 * R * h;
+              const T v = S[fr * M + ((M - k) & (M - 1))];
+              if (plane) pi_[gm][h] = v; else pr_[gm][h] = v;
+            }
+          }
+          wave_lds_sync();
         }
-        wave_lds_sync();
       }
       // X_k = E + w O,  E = (A + B)/2, O = -i (A - B)/2, A = Z[k], B = conj(Z[M-k])
+      const bool mag = SPEC || p.out_mag;
 #pragma unroll
       for (int gm = 0; gm < G; gm++) {
         const int col = 8 * gm + cl3, fr = col / R, c = col % R;
-        T* row = Prow + (int64_t)(rb + fr) * K;
+        T* row = rows + (int64_t)(rb + fr) * K;
 #pragma unroll
         for (int h = 0; h < 8; h++) {
           const int k = c + R * g3 + 8 * R * h;
+          const int ti = 2 * ((gm * 8 + h) * 64 + lane);
+          const T wr = t3[ti], wi = t3[ti + 1];
           const T ar = zr[gm][h], ai = zi[gm][h];
           const T br = pr_[gm][h], bi = -pi_[gm][h];
           const T er = (T)0.5 * (ar + br), ei = (T)0.5 * (ai + bi);
           const T or_ = (T)0.5 * (ai - bi), oi = (T)-0.5 * (ar - br);
-          const T xr_ = er + (t3r[gm][h] * or_ - t3i[gm][h] * oi);
-          const T xi_ = ei + (t3r[gm][h] * oi + t3i[gm][h] * or_);
-          T pw = xr_ * xr_ + xi_ * xi_;
-          row[k] = p.store_mag ? sqrt(pw) : pw;
+          const T xr_ = er + (wr * or_ - wi * oi);
+          const T xi_ = ei + (wr * oi + wi * or_);
+          const T pw = xr_ * xr_ + xi_ * xi_;
+          row[k] = mag ? sqrt(pw) : pw;
           if (k == 0) {                 // Nyquist bin M = E_0 - O_0 (both real)
             const T xn = er - or_;
-            row[M] = p.store_mag ? fabs(xn) : xn * xn;
+            row[M] = mag ? fabs(xn) : xn * xn;
           }
         }
       }
+      wave_lds_sync();
     }
-    __syncthreads();
+#pragma unroll
+    for (int fr = 0; fr < FR; fr++)
+#pragma unroll
+      for (int a = 0; a < R; a++) { cur_e[fr][a] = nxt_e[fr][a]; cur_o[fr][a] = nxt_o[fr][a]; }
 
-    // ======================= epilogue: lane = frame ========================
-    const int nvalid_hi = (int)min((int64_t)p.tile_f, p.F - tb);   // rows < nvalid_hi exist
-    const int rlo = (tb + p.r0 < 0) ? (int)(-tb) : p.r0;           // first output row
+    // ======================= batch epilogue (lane = frame x group) ==========
+    const int64_t bi_ = pre ? ui - 1 : ui;
+    if (bi_ < 0 || (bi_ % UPB) != UPB - 1 || fft_only) continue;
+    const int64_t t0 = f_begin + (bi_ / UPB) * NB;        // first frame of the batch
+    const int nv = (int)min((int64_t)NB, f_end - t0);       // frames of the batch that exist
+    const int f = lane / NG, g = lane % NG;
+    const bool act = f < nv;
+    const T* row = rows + (int64_t)(PRE + f) * K;
+    const bool mag = SPEC || p.out_mag;
 
-    if (p.out_mag) {   // SpectrogramResult.Magnitude rows, coalesced flat copy
-      const int64_t first = tb + rlo;
-      const int64_t cnt = (int64_t)(nvalid_hi - rlo) * K;
-      for (int64_t i = threadIdx.x; i < cnt; i += 256) {
-        T v = Prow[(int64_t)rlo * K + i];
-        store_out<T>(p.out_mag, p.out_f64, first * K + i, p.store_mag ? v : sqrt(v));
-      }
+    if (p.out_mag) {   // SpectrogramResult.Magnitude rows: contiguous in LDS and in HBM
+      const int64_t cnt = (int64_t)nv * K;
+      for (int64_t i = lane; i < cnt; i += 64)
+        store_out<T>(p.out_mag, p.out_f64, t0 * K + i, rows[(int64_t)PRE * K + i]);
     }
-
     if (p.out_mfcc) {
-      const int f = threadIdx.x % p.tile_f;
-      const int grp = threadIdx.x / p.tile_f;
-      const T* wts = reinterpret_cast<const T*>(p.mel_w);
-      const bool act = (f >= rlo) && (f < nvalid_hi);
       if (act) {
-        const T* row = Prow + (int64_t)f * K;
-        for (int q = p.grp_off[grp]; q < p.grp_off[grp + 1]; ++q) {
-          const int m = p.grp_mels[q];
-          const int lo = p.mel_lo[m], hi = p.mel_hi[m];
-          const T* w = wts + p.mel_woff[m] - lo;
+        for (int q = e_goff[g]; q < e_goff[g + 1]; ++q) {
+          const int m = e_gmel[q];
+          const int lo = e_lo[m], hi = e_hi[m];
+          const T* w = e_w + e_woff[m] - lo;
           T s = 0;
-          for (int k = lo; k < hi; ++k) {
-            T pv = row[k];
-            if (p.store_mag) pv = pv * pv;        // |X|^2
-            if (p.input_power) pv = pv * pv;      // F5: Compute() squares |X|^2 again
-            s += pv * w[k];
+          // 8 independent LDS loads per step; lanes past `hi` add an exact 0 (Go adds
+          // zero-weight bins too), so the ascending-bin summation order is unchanged
+          for (int k = lo; k < hi; k += 8) {
+            T pv[8], wv[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) { pv[j] = row[k + j]; wv[j] = w[k + j]; }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+              T v = pv[j];
+              if (mag) v = v * v;                 // |X|^2
+              if (p.input_power) v = v * v;       // F5: Compute() squares |X|^2 again
+              v = (k + j < hi) ? v : (T)0;
+              s += v * ((k + j < hi) ? wv[j] : (T)0);
+            }
           }
           logmel[f * (p.n_mels + 1) + m] = (s > (T)0) ? dev_log(s) : dev_log((T)1e-10);
         }
       }
-      __syncthreads();
+      wave_lds_sync();
       if (act) {
-        const T* dct = reinterpret_cast<const T*>(p.dct);
-        const T* lift = reinterpret_cast<const T*>(p.lift);
         const T* lm = logmel + f * (p.n_mels + 1);
-        for (int kk = grp; kk < p.n_mfcc; kk += p.n_groups) {
-          const T* d = dct + kk * p.n_mels;
+        for (int kk = g; kk < p.n_mfcc; kk += NG) {
+          const T* d = e_dct + kk * p.n_mels;
           T s = 0;
-          for (int n = 0; n < p.n_mels; ++n) s += lm[n] * d[n];
-          stage[f * p.n_mfcc + kk] = s * lift[kk];
+          for (int n = 0; n < p.n_mels; n += 8) {
+            T a[8], b[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) { a[j] = lm[n + j]; b[j] = d[n + j]; }
+#pragma unroll
+            for (int j = 0; j < 8; j++) s += (n + j < p.n_mels) ? a[j] * b[j] : (T)0;
+          }
+          stage[f * p.n_mfcc + kk] = s * e_lift[kk];
         }
       }
-      __syncthreads();
-      const int64_t first = tb + rlo;
-      const int64_t cnt = (int64_t)(nvalid_hi - rlo) * p.n_mfcc;
-      for (int64_t i = threadIdx.x; i < cnt; i += 256)
-        store_out<T>(p.out_mfcc, p.out_f64, first * p.n_mfcc + i, stage[rlo * p.n_mfcc + i]);
+      wave_lds_sync();
+      const int cnt = nv * p.n_mfcc;
+      for (int i = lane; i < cnt; i += 64) store_out<T>(p.out_mfcc, p.out_f64, t0 * p.n_mfcc + i, stage[i]);
     }
-    __syncthreads();   // LDS rows are rewritten by the next tile
+    if constexpr (SPEC) {
+      // per-frame descriptors (speech.go:320-367, :438-458) from |X| in LDS.
+      // Each of the NG lanes of a frame reduces a chunk of bins; xor-shuffles combine.
+      const T* prev = row - K;                      // frame t-1 (row PRE-1+f), for flux
+      const int64_t t = t0 + f;
+      const bool has_prev = act && (t > 0);
+      constexpr int CH = (K + NG - 1) / NG;
+      const int k0 = g * CH, k1 = min(K, k0 + CH);
+      const T fscale = (T)((double)p.sample_rate / (double)((K - 1) * 2));   // freqBins[i] = i sr / (2(K-1))
+      const T inv_ln10 = (T)0.43429448190325182765;
+      T s_m = 0, s_fm = 0, s_m2 = 0, mx = 0, s_ln = 0, s_lo = 0, s_fx = 0;
+      double sx = 0, sy = 0, sxy = 0, sxx = 0;    // regression sums: f32 would cancel catastrophically
+      int n_ln = 0, n_sl = 0;
+      if (act) {
+#pragma unroll 4
+        for (int j = 0; j < CH; ++j) {
+          const int k = k0 + j;
+          if (k >= k1) break;
+          const T m = row[k];
+          const T fk = (T)k * fscale;
+          s_m += m; s_fm += fk * m; s_m2 += m * m;
+          if (m > mx) mx = m;
+          if (k < K / 4) s_lo += m * m;
+          if (m > (T)1e-10) {
+            const T lm = dev_log(m);
+            s_ln += lm; n_ln++;
+            if (fk > (T)0) {
+              const double x = (double)(dev_log(fk) * inv_ln10), y = (double)(lm * inv_ln10);
+              sx += x; sy += y; sxy += x * y; sxx += x * x; n_sl++;
+            }
+          }
+          if (has_prev) { const T d = m - prev[k]; if (d > (T)0) s_fx += d * d; }
+        }
+      }
+      auto red = [&](T v) { for (int o = NG / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64); return v; };
+      auto redd = [&](double v) { for (int o = NG / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64); return v; };
+      auto redi = [&](int v) { for (int o = NG / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64); return v; };
+      auto redmax = [&](T v) { for (int o = NG / 2; o > 0; o >>= 1) { const T u = __shfl_xor(v, o, 64); v = u > v ? u : v; } return v; };
+      const T S_m = red(s_m), S_fm = red(s_fm), S_m2 = red(s_m2), MX = redmax(mx), S_ln = red(s_ln);
+      const T S_lo = red(s_lo), S_fx = red(s_fx);
+      const double SX = redd(sx), SY = redd(sy), SXY = redd(sxy), SXX = redd(sxx);
+      const int N_ln = redi(n_ln), N_sl = redi(n_sl);
+      const T cen = (S_m == (T)0) ? (T)0 : S_fm / S_m;                       // spectral_centroid.go:18-41
+      T s_bw = 0;                                                            // spectral_bandwidth.go:22-47
+      if (act) {
+#pragma unroll 4
+        for (int j = 0; j < CH; ++j) { const int k = k0 + j; if (k >= k1) break; const T d = (T)k * fscale - cen; s_bw += d * d * row[k]; }
+      }
+      const T S_bw = red(s_bw);
+      // rolloff (spectral_rolloff.go:18-52): first k with cumulative m^2 >= 0.85 total
+      const T target = (T)0.85 * S_m2;
+      T incl = s_m2;                                                         // inclusive scan over the frame's lanes
+      for (int o = 1; o < NG; o <<= 1) { const T u = __shfl_up(incl, o, NG); if (g >= o) incl += u; }
+      T cum = incl - s_m2;
+      int ridx = 1 << 30;
+      if (act && S_m2 != (T)0)
+        for (int k = k0; k < k1; ++k) { cum += row[k] * row[k]; if (cum >= target) { ridx = k; break; } }
+      for (int o = NG / 2; o > 0; o >>= 1) { const int u = __shfl_xor(ridx, o, 64); ridx = u < ridx ? u : ridx; }
+      if (act && g == 0) {
+        const T fl_geo = N_ln > 0 ? exp(S_ln / (T)N_ln) : (T)0;              // spectral_flatness.go:31-73
+        const T am = S_m / (T)K;
+        T flat = 0;
+        if (N_ln > 0 && am > (T)1e-10) { flat = fl_geo / am; if (flat > (T)1) flat = 1; }
+        const T rms = sqrt(S_m2 / (T)K);                                     // spectral_crest.go:18-38
+        T slope = 0;                                                         // spectral_slope.go:23-63
+        if (N_sl >= 2) { const double dn = (double)N_sl * SXX - SX * SX; if (dn != 0.0) slope = (T)(((double)N_sl * SXY - SX * SY) / dn); }
+        T roll = 0;
+        if (S_m2 != (T)0) roll = (T)(ridx < K ? ridx : K - 1) * fscale;
+        const T vals[9] = {cen, roll, (S_m == (T)0) ? (T)0 : sqrt(S_bw / S_m), flat, rms == (T)0 ? (T)0 : MX / rms,
+                           slope, sqrt(S_fx), S_m2 > (T)0 ? S_lo / S_m2 : (T)0, S_m2 > (T)0 ? (S_m2 - S_lo) / S_m2 : (T)0};
+#pragma unroll
+        for (int d = 0; d < 9; d++) {
+          if (!p.out_spec[d]) continue;
+          if (d == 6) { if (t > 0) store_out<T>(p.out_spec[6], p.out_f64, t - 1, vals[6]); }
+          else store_out<T>(p.out_spec[d], p.out_f64, t, vals[d]);
+        }
+      }
+      // the batch's last frame is the next batch's flux predecessor
+      wave_lds_sync();
+      for (int i = lane; i < K; i += 64) rows[(int64_t)(PRE - 1) * K + i] = rows[(int64_t)(PRE + NB - 1) * K + i];
+      wave_lds_sync();
+    }
   }
 }
 
@@ -366,41 +541,49 @@ bool fingerprint_supported(int W) {
   return W == 128 || W == 256 || W == 512 || W == 1024 || W == 2048;
 }
 
-template <typename T, int R>
+template <typename T, typename P, int R, bool SPEC>
 static int launch_t(const FpParams& p, hipStream_t s) {
-  int dev = 0, ncu = 256;
-  hipGetDevice(&dev);
-  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  int64_t grid = (int64_t)ncu * 2;
-  if (grid > p.ntiles) grid = p.ntiles;
-  if (grid < 1) grid = 1;
-  auto kern = fp_tile_kernel<T, R>;
+  auto kern = fp_wave_kernel<T, P, R, SPEC>;
   if (p.lds_bytes > 64 * 1024)
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), p.lds_bytes, s, p);
+  const int64_t waves = (p.F + p.frames_per_wave - 1) / p.frames_per_wave;
+  const int64_t grid = (waves + p.waves_per_block - 1) / p.waves_per_block;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * p.waves_per_block), p.lds_bytes, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int launch_fingerprint(const FpParams& p, int f64, hipStream_t s) {
-  const int R = p.W / 128;
-  if (f64) {
-    switch (R) {
-      case 1: return launch_t<double, 1>(p, s);
-      case 2: return launch_t<double, 2>(p, s);
-      case 4: return launch_t<double, 4>(p, s);
-      case 8: return launch_t<double, 8>(p, s);
-      case 16: return launch_t<double, 16>(p, s);
-    }
-  } else {
-    switch (R) {
-      case 1: return launch_t<float, 1>(p, s);
-      case 2: return launch_t<float, 2>(p, s);
-      case 4: return launch_t<float, 4>(p, s);
-      case 8: return launch_t<float, 8>(p, s);
-      case 16: return launch_t<float, 16>(p, s);
-    }
+template <typename T, typename P, bool SPEC>
+static int launch_r(const FpParams& p, hipStream_t s) {
+  switch (p.W / 128) {
+    case 1: return launch_t<T, P, 1, SPEC>(p, s);
+    case 2: return launch_t<T, P, 2, SPEC>(p, s);
+    case 4: return launch_t<T, P, 4, SPEC>(p, s);
+    case 8: return launch_t<T, P, 8, SPEC>(p, s);
+    case 16: return launch_t<T, P, 16, SPEC>(p, s);
   }
   return -4;
+}
+
+template <typename T, typename P>
+static int launch_s(const FpParams& p, hipStream_t s) {
+  return (p.flags & 4u) ? launch_r<T, P, true>(p, s) : launch_r<T, P, false>(p, s);   // SONAR_FP_SPECTRAL
+}
+
+int launch_fingerprint(const FpParams& p, int f64, hipStream_t s) {
+  if (f64) return p.pcm_f64 ? launch_s<double, double>(p, s) : launch_s<double, float>(p, s);
+  return p.pcm_f64 ? launch_s<float, double>(p, s) : launch_s<float, float>(p, s);
+}
+
+// batch geometry shared with the host (LDS carve)
+int fp_batch_frames(int W) {
+  const int R = W / 128;
+  const int FR = R >= 8 ? 1 : 8 / R;
+  return FR > 4 ? FR : 4;
+}
+int fp_pre_rows(int W, int spec) {
+  const int R = W / 128;
+  const int FR = R >= 8 ? 1 : 8 / R;
+  return spec ? FR : 0;
 }
 
 }  // namespace sonar

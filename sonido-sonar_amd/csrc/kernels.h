@@ -7,28 +7,25 @@
 
 namespace sonar {
 
-// Fused per-frame kernel (fp_kernel.hip).  One block = 4 waves = one tile of
-// `tile_f` consecutive STFT frames; each wave computes whole-frame FFTs
-// (W = 128 * R real points as a 64*R-point complex FFT + real split) into an
-// LDS row per frame, then the block runs the per-frame epilogues with
-// lane = frame.
+// Fused per-frame kernel (fp_kernel.hip).  Every wave owns a contiguous range
+// of STFT frames and processes it in batches of NB frames: whole-frame FFTs
+// (W = 128 * R real points as a 64*R-point complex FFT + real split) into
+// wave-private LDS rows, then the batch epilogue with lane = (frame, group)
+// -- filterbank + ln + DCT (MFCC) and the spectral descriptors -- with no
+// block-level barrier after the twiddle tables are built.
 struct FpParams {
   const void* pcm;      // device, f32 or f64
   int64_t n;            // samples
   int pcm_f64;
   int64_t F;            // STFT frames
   int W, H;             // window / hop
-  int tile_f;           // frames (LDS rows) per tile
-  int stride;           // frames advanced per tile (= tile_f - r0)
-  int r0;               // 1 when row 0 only feeds spectral flux, else 0
-  int64_t ntiles;
+  int64_t frames_per_wave;   // multiple of the batch size
   const void* window;   // W coefficients, precision T
-  uint32_t flags;       // SONAR_FP_* bits (see sonar_gpu.h)
-  int store_mag;        // LDS rows hold |X| (1) or |X|^2 (0)
+  uint32_t flags;       // SONAR_FP_* bits (see sonar_gpu.h); bit 31: debug FFT-only
   // filterbank + MFCC
   int n_mels, n_mfcc;
   int input_power;      // MFCC.Compute fed |X|^2 (F5) -> uses |X|^4
-  int n_groups;         // epilogue groups (256 / tile_f)
+  int n_groups;         // epilogue groups per frame (64 / NB)
   const int* mel_lo;    // [n_mels] first nonzero bin
   const int* mel_hi;    // [n_mels] one past last nonzero bin
   const int* mel_woff;  // [n_mels] offset into mel_w
@@ -42,13 +39,19 @@ struct FpParams {
   int out_f64;
   void* out_mfcc;
   void* out_mag;
-  void* out_spec[10];   // centroid, rolloff, bandwidth, flatness, crest, slope, flux, low, high, (unused)
-  // LDS carve (bytes)
-  int lds_P, lds_logmel, lds_stage, lds_bytes;
+  void* out_spec[9];    // centroid, rolloff, bandwidth, flatness, crest, slope, flux(F-1), low, high
+  // LDS carve (bytes): shared twiddle tables, then one region per wave
+  int lds_tab_t1, lds_tab_t2, lds_tab_t3, lds_tab_mel, lds_tab_w, lds_tab_dct, lds_wave0, lds_wave_stride;
+  int nnz;              // packed filterbank weights
+  int lds_logmel, lds_stage;   // offsets inside a wave region (rows start at 0)
+  int lds_bytes;
+  int waves_per_block;
 };
 
 int launch_fingerprint(const FpParams& p, int precision_f64, hipStream_t s);
 bool fingerprint_supported(int W);
+int fp_batch_frames(int W);
+int fp_pre_rows(int W, int spec);
 
 // ZCR + short-time energy on the pre-emphasised PCM (misc_kernels.hip)
 int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, double alpha, int sample_rate,

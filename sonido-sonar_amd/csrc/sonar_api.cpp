@@ -34,7 +34,7 @@ struct FpTables {
   void* window = nullptr;
   int *mel_lo = nullptr, *mel_hi = nullptr, *mel_woff = nullptr, *grp_off = nullptr, *grp_mels = nullptr;
   void *mel_w = nullptr, *dct = nullptr, *lift = nullptr;
-  int n_mels = 0, n_mfcc = 0;
+  int n_mels = 0, n_mfcc = 0, nnz = 0;
 };
 
 struct sonar_ctx {
@@ -47,8 +47,10 @@ struct sonar_ctx {
   struct ChromaT { void* win; void* trig; void* map; };
   std::map<std::string, ChromaT> chroma_tables;
   bool timing = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool ev_pending = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;   // spare pair (kept for ABI simplicity)
+  // one event pair per timed launch since the last sonar_last_kernel_ms query
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  size_t ev_used = 0;
   double last_ms = 0.0;
 };
 
@@ -108,15 +110,23 @@ void* upload_real(const std::vector<double>& v, bool f64) {
 
 int64_t go_frames(int64_t n, int W, int H) { return (n - W) / H + 1; }
 
-int tile_frames(int W, bool f64) {
-  const int K = W / 2 + 1;
-  const int esz = f64 ? 8 : 4;
-  int t = 32;
-  while (t > 8 && (int64_t)t * K * esz > 72 * 1024) t >>= 1;
-  const int R = W / 128;
-  const int FR = R >= 8 ? 1 : 8 / R;
-  while (t % (4 * FR) != 0) t <<= 1;
-  return t;
+
+// brackets the dominant kernel of a call with a HIP event pair on its stream
+hipEvent_t timed_begin(sonar_ctx* c, hipStream_t s) {
+  if (!c->timing) return nullptr;
+  if (c->ev_used == c->ev_pool.size()) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return nullptr;
+    c->ev_pool.emplace_back(a, b);
+  }
+  auto& e = c->ev_pool[c->ev_used];
+  hipEventRecord(e.first, s);
+  return e.second;
+}
+void timed_end(sonar_ctx* c, hipStream_t s, hipEvent_t end) {
+  if (!end) return;
+  hipEventRecord(end, s);
+  c->ev_used++;
 }
 
 }  // namespace
@@ -157,6 +167,7 @@ void sonar_destroy(sonar_ctx* c) {
       if (p) hipFree(p);
   }
   for (auto& kv : c->chroma_tables) { hipFree(kv.second.win); hipFree(kv.second.trig); hipFree(kv.second.map); }
+  for (auto& e : c->ev_pool) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->own) hipStreamDestroy(c->own);
@@ -186,12 +197,16 @@ int sonar_enable_kernel_timing(sonar_ctx* c, int on) {
 
 int sonar_last_kernel_ms(sonar_ctx* c, double* ms) {
   if (!c || !ms) return SONAR_ERR_INVALID;
-  if (c->ev_pending) {
-    HIP_TRY(c, hipEventSynchronize(c->ev1));
-    float f = 0.f;
-    HIP_TRY(c, hipEventElapsedTime(&f, c->ev0, c->ev1));
-    c->last_ms = f;
-    c->ev_pending = false;
+  if (c->ev_used > 0) {   // average over every timed launch since the last query
+    HIP_TRY(c, hipEventSynchronize(c->ev_pool[c->ev_used - 1].second));
+    double sum = 0.0;
+    for (size_t i = 0; i < c->ev_used; ++i) {
+      float f = 0.f;
+      HIP_TRY(c, hipEventElapsedTime(&f, c->ev_pool[i].first, c->ev_pool[i].second));
+      sum += f;
+    }
+    c->last_ms = sum / (double)c->ev_used;
+    c->ev_used = 0;
   }
   *ms = c->last_ms;
   return SONAR_OK;
@@ -250,8 +265,6 @@ int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_c
   if (need_fft && !sonar::fingerprint_supported(W))
     return fail(c, SONAR_ERR_UNSUPPORTED, "window size " + std::to_string(W) +
                                               " not supported by the GPU STFT (128, 256, 512, 1024, 2048)");
-  if (flags & SONAR_FP_SPECTRAL)
-    return fail(c, SONAR_ERR_UNSUPPORTED, "SONAR_FP_SPECTRAL epilogue not built yet");
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const size_t esz_in = pcm64 ? 8 : 4, esz_out = o64 ? 8 : 4;
@@ -279,27 +292,36 @@ int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_c
   void* d_mag = (flags & SONAR_FP_MAGNITUDE) ? out_ptr(out->magnitude, "mag", (size_t)F * K) : nullptr;
   if ((flags & SONAR_FP_MFCC) && !d_mfcc) return fail(c, SONAR_ERR_INVALID, "out->mfcc is null or allocation failed");
   if ((flags & SONAR_FP_MAGNITUDE) && !d_mag) return fail(c, SONAR_ERR_INVALID, "out->magnitude is null");
+  void* d_spec[9] = {nullptr};
+  if (flags & SONAR_FP_SPECTRAL) {
+    void* user[9] = {out->centroid, out->rolloff, out->bandwidth, out->flatness, out->crest, out->slope,
+                     out->flux, out->low_ratio, out->high_ratio};
+    static const char* nm[9] = {"centroid", "rolloff", "bandwidth", "flatness", "crest", "slope", "flux", "low", "high"};
+    for (int d = 0; d < 9; d++) {
+      const size_t cnt = (d == 6) ? (size_t)std::max<int64_t>(F - 1, 0) : (size_t)F;
+      if (user[d] && cnt > 0) d_spec[d] = out_ptr(user[d], nm[d], cnt);
+    }
+  }
 
   if (need_fft) {
-    const int tile = tile_frames(W, f64);
-    const int r0 = 0;
+    const bool spec = (flags & SONAR_FP_SPECTRAL) != 0;
+    const int NB = sonar::fp_batch_frames(W);
+    const int PRE = sonar::fp_pre_rows(W, spec);
     sonar::FpParams p{};
     p.pcm = dpcm; p.n = n; p.pcm_f64 = pcm64; p.F = F; p.W = W; p.H = H;
-    p.tile_f = tile; p.r0 = r0; p.stride = tile - r0;
-    p.ntiles = (F + p.stride - 1) / p.stride;
     p.flags = flags;
-    p.store_mag = (flags & (SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL)) ? 1 : 0;
     p.input_power = cfg->mfcc_input_power;
-    p.n_groups = 256 / tile;
+    p.n_groups = 64 / NB;
     p.sample_rate = cfg->sample_rate;
     p.out_f64 = o64;
     p.out_mfcc = d_mfcc;
     p.out_mag = d_mag;
+    for (int d = 0; d < 9; d++) p.out_spec[d] = d_spec[d];
     // tables, cached per configuration
     char key[512];
     std::snprintf(key, sizeof(key), "%d|%d|%d|%d|%d|%d|%.17g|%.17g|%d|%.17g|%d|%d", W, cfg->window_type,
                   cfg->sample_rate, cfg->n_mfcc, cfg->n_filters, cfg->filterbank, cfg->low_freq, cfg->high_freq,
-                  cfg->use_lifter, cfg->lifter, (int)f64, tile);
+                  cfg->use_lifter, cfg->lifter, (int)f64, NB);
     auto it = c->fp_tables.find(key);
     if (it == c->fp_tables.end()) {
       FpTables t;
@@ -312,30 +334,48 @@ int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_c
                                          cfg->high_freq, cfg->use_lifter != 0, cfg->lifter, W, mt))
         return fail(c, SONAR_ERR_INVALID, "failed to initialize MFCC: failed to create mel filter bank");
       std::vector<int> off, mels;
-      sonar::host::balance_groups(mt, 256 / tile, off, mels);
+      sonar::host::balance_groups(mt, 64 / NB, off, mels);
       t.mel_lo = (int*)upload(mt.lo); t.mel_hi = (int*)upload(mt.hi); t.mel_woff = (int*)upload(mt.woff);
       t.grp_off = (int*)upload(off); t.grp_mels = (int*)upload(mels);
       t.mel_w = upload_real(mt.w, f64); t.dct = upload_real(mt.dct, f64); t.lift = upload_real(mt.lift, f64);
-      t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc;
+      t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc; t.nnz = (int)mt.w.size();
       if (!t.window || !t.mel_lo || !t.mel_w || !t.dct || !t.lift) return fail(c, SONAR_ERR_NOMEM, "table upload failed");
       it = c->fp_tables.emplace(key, t).first;
     }
     const FpTables& t = it->second;
     p.window = t.window;
-    p.n_mels = t.n_mels; p.n_mfcc = t.n_mfcc;
+    p.n_mels = t.n_mels; p.n_mfcc = t.n_mfcc; p.nnz = t.nnz;
     p.mel_lo = t.mel_lo; p.mel_hi = t.mel_hi; p.mel_woff = t.mel_woff; p.mel_w = t.mel_w;
     p.grp_off = t.grp_off; p.grp_mels = t.grp_mels; p.dct = t.dct; p.lift = t.lift;
+    // LDS carve: twiddle tables (shared), then one region per wave
     const int esz = f64 ? 8 : 4;
+    const int R = W / 128, FR = R >= 8 ? 1 : 8 / R, G = R * FR / 8;
     auto al = [](int x) { return (x + 15) & ~15; };
-    p.lds_P = 0;
-    p.lds_logmel = al(tile * K * esz);
-    p.lds_stage = p.lds_logmel + al(tile * (t.n_mels + 1) * esz);
-    p.lds_bytes = p.lds_stage + al(tile * t.n_mfcc * esz);
+    p.lds_tab_t1 = 0;
+    p.lds_tab_t2 = al(R * 64 * 2 * esz);
+    p.lds_tab_t3 = p.lds_tab_t2 + al(64 * 2 * esz);
+    p.lds_tab_mel = p.lds_tab_t3 + al(G * 8 * 64 * 2 * esz);
+    p.lds_tab_w = p.lds_tab_mel + al((4 * t.n_mels + p.n_groups + 1) * 4);
+    p.lds_tab_dct = p.lds_tab_w + al(std::max(t.nnz, 1) * esz);
+    p.lds_wave0 = p.lds_tab_dct + al((t.n_mfcc * t.n_mels + t.n_mfcc) * esz);
+    p.lds_logmel = al((PRE + NB) * K * esz);
+    p.lds_stage = p.lds_logmel + al(NB * (t.n_mels + 1) * esz);
+    p.lds_wave_stride = p.lds_stage + al(NB * t.n_mfcc * esz);
+    p.waves_per_block = 4;
+    while (p.waves_per_block > 1 && p.lds_wave0 + p.waves_per_block * p.lds_wave_stride > 160 * 1024) p.waves_per_block--;
+    p.lds_bytes = p.lds_wave0 + p.waves_per_block * p.lds_wave_stride;
     if (p.lds_bytes > 160 * 1024) return fail(c, SONAR_ERR_UNSUPPORTED, "LDS budget exceeded");
-    if (c->timing) HIP_TRY(c, hipEventRecord(c->ev0, s));
+    // frames per wave: about 12 resident waves per CU, equal shares, multiple of NB
+    int dev_cus = 256;
+    hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int64_t target_waves = (int64_t)dev_cus * 12;
+    int64_t fpw = (F + target_waves - 1) / target_waves;
+    fpw = std::max<int64_t>(NB, (fpw + NB - 1) / NB * NB);
+    p.frames_per_wave = fpw;
+    hipEvent_t tend = timed_begin(c, s);
     const int rc = sonar::launch_fingerprint(p, f64, s);
     if (rc != 0) return fail(c, SONAR_ERR_DEVICE, std::string("fingerprint kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
-    if (c->timing) { HIP_TRY(c, hipEventRecord(c->ev1, s)); c->ev_pending = true; }
+    timed_end(c, s, tend);
   }
   if (flags & SONAR_FP_ZCR) {
     void* d = out_ptr(out->zcr, "zcr", (size_t)F);
@@ -464,9 +504,9 @@ int sonar_ncc(sonar_ctx* c, const double* a, int64_t na, const double* b, int64_
   double* st = (double*)dbuf(c, "ncc.stats", 64);
   double* dc = (device_ptrs && corr) ? corr : (double*)dbuf(c, "ncc.corr", nl * 8);
   if (!xa || !xb || !st || !dc) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
-  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev0, s));
+  hipEvent_t tend = timed_begin(c, s);
   if (sonar::launch_ncc(da, na, db, nb, L, xa, xb, st, dc, s) != 0) return fail(c, SONAR_ERR_DEVICE, "ncc launch failed");
-  if (c->timing) { HIP_TRY(c, hipEventRecord(c->ev1, s)); c->ev_pending = true; }
+  timed_end(c, s, tend);
   std::vector<double> hc(nl);
   HIP_TRY(c, hipMemcpyAsync(hc.data(), dc, nl * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
@@ -507,10 +547,10 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
   int32_t* rr = (int32_t*)dbuf(c, "dtw.rr", cap * 4);
   int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
   if (!C || !dir || !rq || !rr || !pl) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (cost matrix)");
-  if (c->timing) HIP_TRY(c, hipEventRecord(c->ev0, s));
+  hipEvent_t tend = timed_begin(c, s);
   if (sonar::launch_dtw(dq, nq, dr, nr, dim, band, C, dir, rq, rr, pl, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
-  if (c->timing) { HIP_TRY(c, hipEventRecord(c->ev1, s)); c->ev_pending = true; }
+  timed_end(c, s, tend);
   int64_t P = 0;
   HIP_TRY(c, hipMemcpyAsync(&P, pl, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));

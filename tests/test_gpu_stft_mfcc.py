@@ -125,3 +125,39 @@ def test_zcr_bit_exact_and_energy(ctx, pcm_dtype):
     # sr = 0 (F3): ZCR = crossings / (+Inf) = 0
     got0 = ctx.fingerprint(x, ctx.config(flags=sonar.FP_ZCR, sample_rate=0, pcm_dtype=pcm_dtype))
     assert np.all(got0["zcr"] == 0)
+
+
+SPEC = ["centroid", "rolloff", "bandwidth", "flatness", "crest", "slope", "flux", "low_ratio", "high_ratio"]
+
+
+@pytest.mark.parametrize("W,H,sr", [(1024, 256, 44100), (512, 128, 16000), (2048, 512, 44100), (1024, 256, 0),
+                                    (256, 100, 22050)])
+@pytest.mark.parametrize("prec", [sonar.F64, sonar.F32])
+def test_spectral_descriptors_match_oracle(ctx, W, H, sr, prec):
+    """SpeechFeatureExtractor.extractSpectralFeatures per-frame descriptors (speech.go:320-367)
+    and the energy-band ratios (speech.go:438-458).  Float features: 1e-9 (F64) / 1e-4 (F32)
+    relative; rolloff is a bin index -> frequency: the F64 kernel sums the cumulative energy in
+    a different (parallel) order than Go, so a frame whose cumulative sits within rounding of the
+    85 % target may land one bin off -- allowed only for such borderline frames."""
+    x = synth.c2_hour(seconds=6.0).astype(np.float64)
+    cfg = ctx.config(window_size=W, hop_size=H, sample_rate=sr, precision=prec,
+                     flags=sonar.FP_SPECTRAL | sonar.FP_MFCC)
+    got = ctx.fingerprint(x, cfg)
+    mag = O.stft_mag(x, W, H)
+    ref = O.spectral_descriptors(mag, sr)
+    tol = 1e-9 if prec == sonar.F64 else 1e-4
+    for k in SPEC:
+        g, r = got[k], ref[k]
+        assert g.shape == r.shape, k
+        if k == "rolloff":
+            res = sr / W if sr else 1.0
+            bad = np.abs(g - r) > 0.5 * res
+            assert np.all(np.abs(g - r)[bad] <= 1.01 * res)
+            assert bad.mean() < (0.002 if prec == sonar.F64 else 0.02), bad.mean()
+            continue
+        scale = np.maximum(np.abs(r), np.max(np.abs(r)) * 1e-6 + 1e-30)
+        err = np.max(np.abs(g - r) / scale)
+        # slope is a log-log regression over every bin above 1e-10: in F32 the small bins carry
+        # large relative FFT error (error ~ 1e-7 of the frame PEAK), so F32 slope is checked at 5e-3
+        stol = tol * 10 if prec == sonar.F64 else 5e-3
+        assert err < (tol if k != "slope" else stol), (k, err)
