@@ -25,6 +25,9 @@
  *   sonar_dtw                  <- DTWAlignment.Align (algorithms/stats/dtw.go:55)
  *   sonar_generate_fingerprint <- FingerprintGenerator.GenerateFingerprint
  *                                 (fingerprint/fingerprint.go:137)
+ *   sonar_extract_speech_features <- SpeechFeatureExtractor.ExtractFeatures
+ *                                 (fingerprint/extractors/speech.go:135), the extractor
+ *                                 GenerateFingerprint builds for every content type
  *   sonar_align_features       <- AlignmentExtractor.ExtractAlignmentFeatures
  *                                 (fingerprint/extractors/alignment.go:139)
  *
@@ -191,6 +194,34 @@ typedef struct {              /* fingerprint.FingerprintConfig (fingerprint.go:2
 } sonar_fingerprint_config;
 
 void sonar_fingerprint_config_default(sonar_fingerprint_config* cfg);  /* fingerprint.go:70-98 */
+
+typedef struct {              /* config.FeatureConfig fields the speech extractor reads (config/config.go:13-38) */
+  int32_t sample_rate;        /* FeatureConfig.SampleRate (0 under GenerateFingerprint, F1)           */
+  int32_t window_size;        /* FeatureConfig.WindowSize: ShortTimeEnergy frames                     */
+  int32_t hop_size;           /* FeatureConfig.HopSize                                                */
+  int32_t stft_window_size;   /* spectrogram handed to ExtractFeatures (ComputeSTFTWithWindow W)     */
+  int32_t stft_hop_size;      /* ... and H                                                            */
+  int32_t window_type;
+  int32_t enable_mfcc;
+  int32_t enable_speech_features;
+  int32_t enable_temporal_features;
+  int32_t mfcc_coefficients;
+  int32_t is_news;
+  int32_t precision;          /* SONAR_F64 (parity, default) / SONAR_F32                              */
+} sonar_feature_config;
+
+void sonar_feature_config_default(sonar_feature_config* cfg);
+
+/* NewSpeechFeatureExtractor(cfg, is_news) + ExtractFeatures(STFT(pcm, W, H), pcm, sample_rate).
+ * Result arrays: "mfcc", "spectral_centroid" ... "spectral_flux", "zero_crossing_rate",
+ * "short_time_energy", "energy_variance", "loudness_range", "energy_entropy",
+ * "low_energy_ratio", "high_energy_ratio", "pitch_estimate", "pitch_confidence",
+ * "voicing_strength", "harmonic_ratio", "inharmonicity_ratio", "tonal_centroid",
+ * temporal ("rms_energy", "dynamic_range", "silence_ratio", "peak_amplitude",
+ * "average_amplitude", "onset_density", "attack_time", "envelope_shape") and speech
+ * ("is_speech", "voicing_probability", "spectral_tilt", "pause_duration") groups when enabled. */
+int sonar_extract_speech_features(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate,
+                                  const sonar_feature_config* cfg, sonar_result** out);
 
 /* AudioData{PCM, SampleRate, Metadata.ContentType}.  content_type is the raw
  * metadata string ("music", "news", "talk", ... ; unknown strings -> content

@@ -256,3 +256,149 @@ def align_xcorr_metrics(met, hop, sample_rate, max_lag):
     out = np.zeros(6)
     lib().or_align_xcorr_metrics(_p(m), hop, sample_rate, max_lag, _p(out))
     return dict(zip(["offset", "offset_seconds", "similarity", "confidence", "quality", "noise_level"], out.tolist()))
+
+
+# ---------------------------------------------------------------------------
+# Compositions of the Go orchestration (test infrastructure, pure Python over
+# the C primitives; restated from the Go source independently of the product)
+# ---------------------------------------------------------------------------
+
+def _median_pos(v):
+    f = sorted(x for x in v if x > 0)
+    if not f:
+        return 0.0
+    n = len(f)
+    return (f[n // 2 - 1] + f[n // 2]) / 2.0 if n % 2 == 0 else f[n // 2]
+
+
+class YinTrack:
+    """postProcessResult + updateTemporalTracking (pitch_detection.go:767-921)."""
+
+    def __init__(self):
+        self.hist, self.prev = [], 0.0
+
+    def step(self, p, c):
+        v = c
+        if p != 0.0 and self.hist:
+            rec = self.hist[-5:]
+            if len(rec) >= 3:
+                med = _median_pos(rec)
+                for r in (0.5, 2.0, 1.0 / 3.0, 3.0):
+                    ex = med * r
+                    with np.errstate(divide="ignore", invalid="ignore"):
+                        if abs(p - ex) / ex < 0.1:
+                            if abs(p - med) > abs(ex - med):
+                                p = ex
+                            break
+        if c < 0.5:
+            p, c, v = 0.0, 0.0, 0.0
+        self.hist.append(p)
+        self.hist = self.hist[-20:]
+        if len(self.hist) > 1:
+            rec = self.hist[-3:]
+            p = _median_pos(rec) if len(rec) >= 3 else 0.3 * p + 0.7 * self.prev
+        self.prev = p
+        return p, c, v
+
+
+def speech_features_reference(pcm, sample_rate, fc):
+    """SpeechFeatureExtractor.ExtractFeatures (fingerprint/extractors/speech.go:135-550), fp64.
+    fc: dict(sample_rate, window_size, hop_size, stft_window_size, stft_hop_size, enable_mfcc,
+    enable_speech_features, enable_temporal_features, mfcc_coefficients)."""
+    pcm = _f64(pcm)
+    csr = fc["sample_rate"]
+    W, H = fc["stft_window_size"], fc["stft_hop_size"]
+    mag = stft_mag(pcm, W, H, nthreads=8)
+    F = len(mag)
+    pre = preemphasis(pcm, 0.97)
+    out = {}
+    if fc["enable_mfcc"]:
+        out["mfcc"] = mfcc_frames(mag, csr, n_coef=fc["mfcc_coefficients"], n_mels=26)
+    d = spectral_descriptors(mag, csr)
+    for k in ["centroid", "rolloff", "bandwidth", "flatness", "crest", "slope"]:
+        out["spectral_" + k] = d[k]
+    if F > 1:
+        out["spectral_flux"] = d["flux"]
+    out["zero_crossing_rate"] = zcr_frames(pre, F, W, H, csr)
+    ste = short_time_energy(pre, fc["window_size"], fc["hop_size"])
+    # YIN raw on the pre-emphasised PCM
+    Fp = int(lib().or_pitch_frames(len(pre)))
+    raw = []
+    for i in range(Fp):
+        fr = pre[i * 512: i * 512 + 1024]
+        raw.append(yin_raw(fr, csr)[:2] if len(fr) == 1024 else None)
+    trk = YinTrack()
+    if fc["enable_speech_features"]:
+        n = len(pre)
+        sp = not (n < int(csr / 4))
+        cr = np.sum(((pre[:-1] >= 0) & (pre[1:] < 0)) | ((pre[:-1] < 0) & (pre[1:] >= 0)))
+        z = 0.0 if n <= 1 else cr / (n - 1)
+        if sp and (z < 0.01 or z > 0.3):
+            sp = False
+        if sp and np.sqrt(np.sum(pre * pre) / n) < 0.001:
+            sp = False
+        if sp:
+            fr = pre[:1024]
+            mc = 0.0
+            for lag in range(20, min(400, 512)):
+                c = np.sum(fr[:1024 - lag] * fr[lag:]) / (1024 - lag)
+                mc = max(mc, c)
+            en = np.sum(fr * fr) / 1024
+            if en > 0:
+                mc /= en
+            sp = mc > 0.1 and len(pre) >= 1024
+        out["is_speech"] = 1.0 if sp else 0.0
+        if sp:
+            vo = np.zeros(Fp)
+            for i, r in enumerate(raw):
+                if r is not None:
+                    vo[i] = trk.step(*r)[2]
+            out["voicing_probability"] = vo
+    pe, pc, vs = np.zeros(Fp), np.zeros(Fp), np.zeros(Fp)
+    for i, r in enumerate(raw):
+        if r is not None:
+            pe[i], pc[i], vs[i] = trk.step(*r)
+    out["pitch_estimate"], out["pitch_confidence"], out["voicing_strength"] = pe, pc, vs
+    out["harmonic_ratio"], out["inharmonicity_ratio"] = vs * 10.0, 1.0 - vs
+    out["tonal_centroid"] = np.where(pe > 0, pe, 0.0)
+    out["short_time_energy"] = ste
+    out["energy_variance"] = float(np.var(ste, ddof=1)) if len(ste) >= 2 else 0.0
+    ent = np.where(ste > 0, -ste * np.log(ste + 1e-10), 0.0)
+    lo = np.zeros(len(ste))
+    hi = np.zeros(len(ste))
+    m = min(len(ste), F)
+    lo[:m], hi[:m] = d["low_ratio"][:m], d["high_ratio"][:m]
+    out["energy_entropy"], out["low_energy_ratio"], out["high_energy_ratio"] = ent, lo, hi
+    return out
+
+
+def align_features_reference(qe, re_, qc, rc, q_pcm_len, r_pcm_len, sample_rate, feature_sample_rate, hop,
+                             max_lag_seconds):
+    """AlignmentExtractor.ExtractAlignmentFeatures (extractors/alignment.go:139-476), corr_energy + dtw_chroma."""
+    out = {}
+    max_lag_samples = int(max_lag_seconds * feature_sample_rate)
+    cands = []
+    if qe is not None and re_ is not None and len(qe) and len(re_):
+        mlf = min(max_lag_samples // hop if max_lag_samples >= 0 else -((-max_lag_samples) // hop),
+                  min(len(qe), len(re_)) - 1)
+        corr, met = ncc(qe, re_, mlf)
+        s = align_xcorr_metrics(met, hop, sample_rate, mlf)
+        out["correlations"], out["peak_lag"] = corr, met["peak_lag"]
+        cands.append((1, 1.0, s, None))
+    if qc is not None and rc is not None and len(qc) and len(rc):
+        r = dtw(qc, rc)
+        s = align_dtw_metrics(r, len(qc), len(rc), sample_rate)
+        out["dtw_distance"], out["dtw_path_query"], out["dtw_path_reference"] = r["distance"], r["path_q"], r["path_r"]
+        cands.append((2, 0.7, s, r))
+    best, bs = None, 0.0
+    for c in cands:
+        sc = c[1] * (0.4 * c[2]["confidence"] + 0.4 * c[2]["similarity"] + 0.2 * c[2]["quality"])
+        if sc > bs:
+            best, bs = c, sc
+    out["method"] = 0 if best is None else best[0]
+    if best is not None:
+        out["temporal_offset"] = best[2]["offset_seconds"]
+        out["offset_confidence"] = best[2]["confidence"]
+        out["alignment_similarity"] = best[2]["similarity"]
+        out["alignment_quality"] = best[2]["quality"]
+    return out

@@ -1,0 +1,72 @@
+// ctx.h -- internal state behind the opaque sonar_ctx / sonar_result handles,
+// shared by sonar_api.cpp (kernel-level entries) and go_api.cpp (Go-API mirror).
+#pragma once
+#include "../../include/sonar_gpu.h"
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t cap = 0;
+};
+
+struct FpTables {
+  void* window = nullptr;
+  int *mel_lo = nullptr, *mel_hi = nullptr, *mel_woff = nullptr, *grp_off = nullptr, *grp_mels = nullptr;
+  void *mel_w = nullptr, *dct = nullptr, *lift = nullptr;
+  int n_mels = 0, n_mfcc = 0, nnz = 0;
+};
+
+struct sonar_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::map<std::string, DevBuf> bufs;
+  std::map<std::string, FpTables> fp_tables;
+  struct ChromaT { void* win; void* trig; void* map; };
+  std::map<std::string, ChromaT> chroma_tables;
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;   // spare pair (kept for ABI simplicity)
+  // one event pair per timed launch since the last sonar_last_kernel_ms query
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  size_t ev_used = 0;
+  double last_ms = 0.0;
+};
+
+struct sonar_result {
+  struct Arr {
+    std::string name;
+    std::vector<double> v;
+    int64_t rows = 0, cols = 0;
+  };
+  std::vector<Arr> arrays;
+  void put(const std::string& name, std::vector<double> v, int64_t rows, int64_t cols) {
+    for (auto& a : arrays)
+      if (a.name == name) { a.v = std::move(v); a.rows = rows; a.cols = cols; return; }
+    arrays.push_back({name, std::move(v), rows, cols});
+  }
+  void scalar(const std::string& name, double x) { put(name, {x}, 1, 1); }
+  void vec(const std::string& name, const std::vector<double>& v) { put(name, v, (int64_t)v.size(), 1); }
+};
+
+namespace sonar {
+namespace detail {
+int fail(sonar_ctx* c, int code, const std::string& msg);
+void* dbuf(sonar_ctx* c, const std::string& name, size_t bytes);
+hipEvent_t timed_begin(sonar_ctx* c, hipStream_t s);
+void timed_end(sonar_ctx* c, hipStream_t s, hipEvent_t end);
+}  // namespace detail
+}  // namespace sonar
+
+#define HIP_TRY(ctx, call)                                                                   \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return ::sonar::detail::fail(ctx, SONAR_ERR_DEVICE, std::string(#call ": ") + hipGetErrorString(e_)); \
+  } while (0)

@@ -1,15 +1,480 @@
-// go_api.cpp -- C++ restatement of the Go orchestration above the kernels
-// (placeholder; filled in below the first GPU milestone).
-#include "../../include/sonar_gpu.h"
+// go_api.cpp -- C++ restatement of the Go orchestration above the GPU seams.
+//
+//   sonar_generate_fingerprint      FingerprintGenerator.GenerateFingerprint
+//                                   (fingerprint/fingerprint.go:137-236) with the
+//                                   ContentAwareConfigManager tables (content_config.go:54-278)
+//   sonar_extract_speech_features   SpeechFeatureExtractor.ExtractFeatures
+//                                   (fingerprint/extractors/speech.go:135-550)
+//   sonar_align_features            AlignmentExtractor.ExtractAlignmentFeatures
+//                                   (fingerprint/extractors/alignment.go:139-476)
+//
+// Every per-frame / per-cell array is produced by a HIP kernel (sonar_fingerprint,
+// YIN, NCC, DTW, energy, tilt, stats); this file only runs what the Go code runs
+// sequentially on O(frames) data: YIN temporal tracking, percentile thresholds,
+// onset peak picking, scorer formulas.  Not produced (outside the GPU hot path,
+// SURVEY.md section 2): formant / voice-quality heuristics (format.go, voice_quality.go),
+// content detection (content_detector.go), fingerprint ID/timestamp metadata.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
 #include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "ctx.h"
+#include "host_dsp.h"
+#include "kernels.h"
+
+using sonar::detail::dbuf;
+using sonar::detail::fail;
+
+namespace {
+
+enum ContentType { CT_MUSIC = 0, CT_NEWS, CT_SPORTS, CT_TALK, CT_MIXED, CT_UNKNOWN };
+
+int to_content_type(const char* s) {   // config.ToContentType (fingerprint/config/config.go:50-65)
+  if (!s) return CT_UNKNOWN;
+  const std::string v(s);
+  if (v == "music") return CT_MUSIC;
+  if (v == "news") return CT_NEWS;
+  if (v == "sports") return CT_SPORTS;
+  if (v == "talk") return CT_TALK;
+  if (v == "mixed") return CT_MIXED;
+  return CT_UNKNOWN;
+}
+
+struct Settings { bool mfcc, speech, temporal; };
+// content_config.go:104-278 (sports has no entry -> unknown settings, :68-72)
+Settings settings_for(int ct) {
+  switch (ct) {
+    case CT_MUSIC: return {true, false, false};
+    case CT_NEWS: return {true, true, true};
+    case CT_TALK: return {true, true, true};
+    case CT_MIXED: return {true, true, true};
+    default: return {true, false, true};
+  }
+}
+
+template <typename T>
+int d2h(sonar_ctx* c, std::vector<T>& v, const void* d, size_t n) {
+  v.resize(n);
+  if (n) HIP_TRY(c, hipMemcpyAsync(v.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+  return SONAR_OK;
+}
+
+double percentile10_threshold(std::vector<double> e) {            // speech.go:594-604 (bubble sort)
+  std::sort(e.begin(), e.end());
+  return e[e.size() / 10];
+}
+
+// speech_analysis.go:165-202 on the first 1024 samples
+bool check_periodicity(const std::vector<double>& fr) {
+  if (fr.size() < 1024) return false;
+  double mc = 0.0;
+  for (int lag = 20; lag < 400 && lag < 512; lag++) {
+    double corr = 0.0; int cnt = 0;
+    for (int i = 0; i < 1024 - lag; i++) { corr += fr[i] * fr[i + lag]; cnt++; }
+    if (cnt > 0) { corr /= (double)cnt; if (corr > mc) mc = corr; }
+  }
+  double en = 0.0;
+  for (int i = 0; i < 1024; i++) en += fr[i] * fr[i];
+  en /= 1024.0;
+  if (en > 0) mc /= en;
+  return mc > 0.1;
+}
+
+}  // namespace
+
 extern "C" {
-void sonar_fingerprint_config_default(sonar_fingerprint_config* c) {
+
+void sonar_fingerprint_config_default(sonar_fingerprint_config* c) {   // fingerprint.go:70-98
   std::memset(c, 0, sizeof(*c));
-  c->window_size = 2048; c->hop_size = 512; c->enable_content_detect = 1; c->window_type = SONAR_WIN_HANN;
+  c->window_size = 2048;
+  c->hop_size = 512;
+  c->feature_window_size = 0;    // FeatureConfig.WindowSize is unset in the default config (F13)
+  c->feature_hop_size = 0;
+  c->enable_content_detect = 1;
+  c->window_type = SONAR_WIN_HANN;
+  c->precision = SONAR_F64;
 }
-int sonar_generate_fingerprint(sonar_ctx*, const double*, int64_t, int32_t, const char*, const sonar_fingerprint_config*,
-                               sonar_result** out) { if (out) *out = nullptr; return SONAR_ERR_UNSUPPORTED; }
-int sonar_align_features(sonar_ctx*, const double*, int64_t, const double*, int64_t, const double*, int64_t,
-                         const double*, int64_t, int64_t, int64_t, int32_t, int32_t, int32_t, int32_t, double,
-                         sonar_result** out) { if (out) *out = nullptr; return SONAR_ERR_UNSUPPORTED; }
+
+void sonar_feature_config_default(sonar_feature_config* c) {
+  std::memset(c, 0, sizeof(*c));
+  c->stft_window_size = 1024;
+  c->stft_hop_size = 256;
+  c->window_type = SONAR_WIN_HANN;
+  c->enable_mfcc = 1;
+  c->mfcc_coefficients = 13;
+  c->is_news = 1;
+  c->precision = SONAR_F64;
 }
+
+// ------------------------------------------------ SpeechFeatureExtractor ----
+int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, int32_t sample_rate,
+                                  const sonar_feature_config* fc, sonar_result** out) {
+  if (!c || !fc || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (n <= 0 || !pcm) return fail(c, SONAR_ERR_EMPTY, "PCM data cannot be empty");
+  if (sample_rate <= 0) return fail(c, SONAR_ERR_INVALID, "sample rate must be positive");
+  const int W = fc->stft_window_size, H = fc->stft_hop_size;
+  const int64_t F = sonar_stft_frames(n, W, H);
+  if (F == SONAR_ERR_EMPTY) return fail(c, SONAR_ERR_EMPTY, "empty signal");
+  if (F == SONAR_ERR_INVALID) return fail(c, SONAR_ERR_INVALID, W <= 0 ? "window size must be positive" : "hop size must be positive");
+  if (F < 0) return fail(c, SONAR_ERR_TOO_SHORT, "signal too short for given window size and hop size");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const int csr = fc->sample_rate;                                // FeatureConfig.SampleRate (0 under F1)
+  const int K = W / 2 + 1;
+  const int nm = fc->mfcc_coefficients > 0 ? fc->mfcc_coefficients : 13;
+  const int64_t Fe = sonar_energy_frames(n, fc->window_size, fc->hop_size);
+  const int64_t Fp = sonar_pitch_frames(n);
+  (void)K;
+
+  // ---- device inputs -------------------------------------------------------
+  double* dpcm = (double*)dbuf(c, "sx.pcm", n * 8);
+  double* dy = (double*)dbuf(c, "sx.pre", n * 8);
+  if (!dpcm || !dy) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (pcm)");
+  HIP_TRY(c, hipMemcpyAsync(dpcm, pcm, n * 8, hipMemcpyHostToDevice, s));
+  // preprocessForSpeech: PreEmphasis("speech") alpha 0.97, fresh state (speech.go:238-245)
+  if (sonar::launch_preemph(dpcm, 1, n, 0.97, dy, s) != 0) return fail(c, SONAR_ERR_DEVICE, "preemph launch failed");
+
+  // ---- fused STFT kernel: MFCC + descriptors, ZCR and short-time energy ---------
+  const size_t fsz = (size_t)std::max<int64_t>(F, 1);
+  double* dmfcc = (double*)dbuf(c, "sx.mfcc", fsz * nm * 8);
+  double* dspec = (double*)dbuf(c, "sx.spec", fsz * 9 * 8);
+  double* dzcr = (double*)dbuf(c, "sx.zcr", fsz * 8);
+  double* den = (double*)dbuf(c, "sx.energy", std::max<int64_t>(Fe, 1) * 8);
+  if (!dmfcc || !dspec || !dzcr || !den) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (features)");
+  sonar_fp_cfg cfg;
+  sonar_fp_cfg_default(&cfg);
+  cfg.window_size = W; cfg.hop_size = H; cfg.window_type = fc->window_type;
+  cfg.sample_rate = csr;                                          // NewMFCC(config.SampleRate, ...) etc.
+  cfg.n_mfcc = nm; cfg.n_filters = 26; cfg.use_lifter = 1; cfg.lifter = 22.0;   // NewMFCC defaults (mfcc.go:44-54)
+  cfg.low_freq = 0.0; cfg.high_freq = (double)csr / 2.0;
+  cfg.energy_window = fc->window_size; cfg.energy_hop = fc->hop_size;
+  cfg.preemph_alpha = 0.97;
+  cfg.flags = SONAR_FP_SPECTRAL | SONAR_FP_ZCR | SONAR_FP_ENERGY | (fc->enable_mfcc ? SONAR_FP_MFCC : 0);
+  cfg.precision = fc->precision; cfg.pcm_dtype = SONAR_F64; cfg.out_dtype = SONAR_F64; cfg.device_ptrs = 1;
+  sonar_fp_out fo;
+  std::memset(&fo, 0, sizeof(fo));
+  fo.mfcc = dmfcc;
+  const size_t Fz = (size_t)F;
+  fo.centroid = dspec; fo.rolloff = dspec + Fz; fo.bandwidth = dspec + 2 * Fz; fo.flatness = dspec + 3 * Fz;
+  fo.crest = dspec + 4 * Fz; fo.slope = dspec + 5 * Fz; fo.flux = dspec + 6 * Fz; fo.low_ratio = dspec + 7 * Fz;
+  fo.high_ratio = dspec + 8 * Fz; fo.zcr = dzcr; fo.energy = Fe > 0 ? den : nullptr;
+  int rc = sonar_fingerprint(c, dpcm, n, &cfg, &fo);
+  if (rc != SONAR_OK) return rc;
+
+  // ---- YIN raw results on the pre-emphasised PCM (extractHarmonicFeatures :464) ---
+  double* dpit = (double*)dbuf(c, "sx.pitch", std::max<int64_t>(Fp, 1) * 8);
+  double* dcon = (double*)dbuf(c, "sx.conf", std::max<int64_t>(Fp, 1) * 8);
+  if (!dpit || !dcon) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (pitch)");
+  if (sonar::launch_yin(dy, n, Fp, csr, dpit, dcon, nullptr, s) != 0) return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
+  // whole-signal statistics of the pre-emphasised PCM
+  const int SB = 256;
+  double* dpart = (double*)dbuf(c, "sx.stats", SB * 4 * 8);
+  if (sonar::launch_stats(dy, n, dpart, SB, s) != 0) return fail(c, SONAR_ERR_DEVICE, "stats launch failed");
+  // extractSimpleEnvelope (speech.go:752-777): RMS 512/256 of the pre-emphasised PCM
+  const int64_t Fenv = sonar_energy_frames(n, 512, 256);
+  double* denv = (double*)dbuf(c, "sx.env", std::max<int64_t>(Fenv, 1) * 8);
+  if (Fenv > 0 && sonar::launch_energy(dpcm, 1, n, Fenv, 512, 256, 0.97, denv, 1, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "envelope launch failed");
+  // ComputeLoudnessRange (energy.go:145-178): 400 ms / 100 ms RMS frames when sr > 0
+  const int lw = (int)(0.4 * (double)csr);
+  const int lh = std::max(1, lw / 4);
+  const int64_t Fl = csr > 0 ? sonar_energy_frames(n, lw, lh) : 0;
+  double* dld = (double*)dbuf(c, "sx.loud", std::max<int64_t>(Fl, 1) * 8);
+  if (Fl > 0 && sonar::launch_energy(dpcm, 1, n, Fl, lw, lh, 0.97, dld, 1, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "loudness launch failed");
+  double* dtilt = (double*)dbuf(c, "sx.tilt", std::max<int64_t>(Fp, 1) * 8);
+  if (fc->enable_speech_features && sonar::launch_tilt(dy, n, Fp, dtilt, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "tilt launch failed");
+
+  std::vector<double> mfcc, spec, zcr, energy, praw, craw, part, env, loud, tilt, head;
+  if (d2h(c, mfcc, dmfcc, fc->enable_mfcc ? Fz * nm : 0) || d2h(c, spec, dspec, Fz * 9) || d2h(c, zcr, dzcr, Fz) ||
+      d2h(c, energy, den, (size_t)Fe) || d2h(c, praw, dpit, (size_t)Fp) || d2h(c, craw, dcon, (size_t)Fp) ||
+      d2h(c, part, dpart, SB * 4) || d2h(c, env, denv, (size_t)std::max<int64_t>(Fenv, 0)) ||
+      d2h(c, loud, dld, (size_t)Fl) || d2h(c, tilt, dtilt, fc->enable_speech_features ? (size_t)Fp : 0) ||
+      d2h(c, head, dy, (size_t)std::min<int64_t>(n, 1024)))
+    return SONAR_ERR_DEVICE;
+  HIP_TRY(c, hipStreamSynchronize(s));
+
+  auto* res = new sonar_result();
+  if (fc->enable_mfcc) res->put("mfcc", mfcc, F, nm);
+  static const char* spec_names[9] = {"spectral_centroid", "spectral_rolloff", "spectral_bandwidth",
+                                      "spectral_flatness", "spectral_crest", "spectral_slope", "spectral_flux",
+                                      "", ""};
+  for (int d = 0; d < 7; d++) {
+    const int64_t cnt = d == 6 ? (F > 1 ? F - 1 : 0) : F;
+    if (d == 6 && F <= 1) continue;                               // flux only when TimeFrames > 1 (:362-365)
+    res->put(spec_names[d], std::vector<double>(spec.begin() + d * Fz, spec.begin() + d * Fz + cnt), cnt, 1);
+  }
+  res->vec("zero_crossing_rate", zcr);
+
+  // whole-signal stats: partials reduced in block order
+  double peak = 0, sabs = 0, ssq = 0, cross = 0;
+  for (int b = 0; b < SB; b++) {
+    peak = std::max(peak, part[4 * b]); sabs += part[4 * b + 1]; ssq += part[4 * b + 2]; cross += part[4 * b + 3];
+  }
+  // cross-block sign changes at block boundaries are counted inside each block (i > 0 uses y[i-1])
+
+  // ---- speech features (extractSpeechFeatures :272-313) -------------------------
+  sonar::host::YinTracker tracker;
+  bool is_speech = false;
+  if (fc->enable_speech_features) {
+    // detectSpeech (speech_analysis.go:105-132), sample rate = FeatureConfig.SampleRate
+    bool sp = !(n < (int64_t)(csr / 4));
+    const double z = n <= 1 ? 0.0 : cross / (double)(n - 1);
+    if (sp && (z < 0.01 || z > 0.3)) sp = false;
+    if (sp && std::sqrt(ssq / (double)n) < 0.001) sp = false;
+    if (sp) sp = check_periodicity(head);
+    is_speech = sp;
+    res->scalar("is_speech", sp ? 1.0 : 0.0);
+    if (sp) {
+      std::vector<double> voicing(Fp);                             // extractVoicingProbability (:530-550)
+      for (int64_t i = 0; i < Fp; i++) {
+        double p = praw[i], q = craw[i], v = 0;
+        if (i * 512 + 1024 <= n) { tracker.step(p, q, v); voicing[i] = v; }
+      }
+      res->vec("voicing_probability", voicing);
+      res->vec("spectral_tilt", tilt);
+      // extractPauseDurations (:587-637)
+      std::vector<double> pauses;
+      if (!energy.empty()) {
+        const double thr = percentile10_threshold(energy);
+        const double fts = (double)fc->hop_size / (double)csr;
+        bool in = false; int64_t st = 0;
+        for (int64_t i = 0; i < (int64_t)energy.size(); i++) {
+          if (energy[i] <= thr) { if (!in) { in = true; st = i; } }
+          else if (in) { const double d = (double)(i - st) * fts; if (d > 0.1) pauses.push_back(d); in = false; }
+        }
+        if (in) { const double d = (double)((int64_t)energy.size() - st) * fts; if (d > 0.1) pauses.push_back(d); }
+      }
+      res->vec("pause_duration", pauses);
+    }
+  }
+
+  // ---- temporal features (extractTemporalFeatures :370-409) ---------------------
+  const double lrange = csr > 0 ? sonar::host::loudness_range_from_rms(loud) : 0.0;
+  if (fc->enable_temporal_features) {
+    res->vec("rms_energy", energy);
+    res->scalar("dynamic_range", lrange);
+    double sil = 0.0;
+    if (!energy.empty()) {                                        // calculateSilenceRatio (:639-665)
+      const double thr = percentile10_threshold(energy);
+      int64_t k = 0;
+      for (double e : energy) if (e <= thr) k++;
+      sil = (double)k / (double)energy.size();
+    }
+    res->scalar("silence_ratio", sil);
+    res->scalar("peak_amplitude", peak);
+    res->scalar("average_amplitude", n > 0 ? sabs / (double)n : 0.0);
+    // detectOnsets (:668-693) + calculateAdaptiveThreshold (:695-716)
+    std::vector<int64_t> onsets;
+    if (energy.size() >= 3) {
+      std::vector<double> der(energy.size() - 1);
+      for (size_t i = 0; i + 1 < energy.size(); i++) der[i] = energy[i + 1] - energy[i];
+      double sum = 0; for (double v : der) sum += v;
+      const double mean = sum / (double)der.size();
+      double var = 0; for (double v : der) { const double d = v - mean; var += d * d; }
+      const double thr = mean + 2 * std::sqrt(var / (double)der.size());
+      for (size_t i = 1; i + 1 < der.size(); i++)
+        if (der[i] > der[i - 1] && der[i] > der[i + 1] && der[i] > thr) onsets.push_back((int64_t)i);
+    }
+    res->scalar("onset_density", (double)onsets.size() / ((double)n / (double)sample_rate));
+    std::vector<double> att(onsets.size());                       // calculateAttackTimes (:718-749)
+    const double fts = (double)fc->hop_size / (double)csr;
+    for (size_t i = 0; i < onsets.size(); i++) {
+      const int64_t on = onsets[i];
+      const double pk = energy[on];
+      int64_t st = on;
+      for (int64_t j = on - 1; j >= 0 && j > on - 10; j--) if (energy[j] < 0.1 * pk) { st = j; break; }
+      att[i] = (double)(on - st) * fts;
+      if (att[i] > 0.1) att[i] = 0.1;
+    }
+    res->vec("attack_time", att);
+    res->vec("envelope_shape", env);
+  }
+
+  // ---- energy features (extractEnergyFeatures :411-461) -------------------------
+  res->vec("short_time_energy", energy);
+  res->scalar("energy_variance", sonar::host::energy_variance(energy));
+  res->scalar("loudness_range", lrange);
+  {
+    const size_t ne = energy.size();
+    std::vector<double> ent(ne, 0.0), lo(ne, 0.0), hi(ne, 0.0);
+    for (size_t i = 0; i < ne; i++) {
+      if (energy[i] > 0) ent[i] = -energy[i] * std::log(energy[i] + 1e-10);
+      if ((int64_t)i < F) { lo[i] = spec[7 * Fz + i]; hi[i] = spec[8 * Fz + i]; }
+    }
+    res->vec("energy_entropy", ent);
+    res->vec("low_energy_ratio", lo);
+    res->vec("high_energy_ratio", hi);
+  }
+
+  // ---- harmonic features (extractHarmonicFeatures :464-509) --------------------
+  {
+    std::vector<double> pe(Fp, 0.0), pc(Fp, 0.0), vs(Fp, 0.0), hr(Fp), ih(Fp), tcen(Fp, 0.0);
+    for (int64_t i = 0; i < Fp; i++) {
+      if (i * 512 + 1024 <= n) {                                  // DetectPitch size check (pitch_detection.go:226)
+        double p = praw[i], q = craw[i], v = 0;
+        tracker.step(p, q, v);
+        pe[i] = p; pc[i] = q; vs[i] = v;
+      }
+      hr[i] = vs[i] * 10.0;
+      ih[i] = 1.0 - vs[i];
+      if (pe[i] > 0) tcen[i] = pe[i];
+    }
+    res->vec("pitch_estimate", pe);
+    res->vec("pitch_confidence", pc);
+    res->vec("voicing_strength", vs);
+    res->vec("harmonic_ratio", hr);
+    res->vec("inharmonicity_ratio", ih);
+    res->vec("tonal_centroid", tcen);
+  }
+  (void)is_speech;
+  *out = res;
+  return SONAR_OK;
+}
+
+// ------------------------------------------ FingerprintGenerator ------------
+int sonar_generate_fingerprint(sonar_ctx* c, const double* pcm, int64_t n, int32_t sample_rate, const char* content_type,
+                               const sonar_fingerprint_config* cfg, sonar_result** out) {
+  if (!c || !cfg || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  const int ct = to_content_type(content_type);                   // fingerprint.go:155
+  if (ct == CT_UNKNOWN && cfg->enable_content_detect)
+    return fail(c, SONAR_ERR_UNSUPPORTED,
+                "content type is unknown and content detection (ContentDetector.DetectContentType) is not on "
+                "the GPU path: pass music/news/sports/talk/mixed or disable content detection");
+  const Settings st = settings_for(ct);                           // GetGenerationConfig -> buildFeatureConfig
+  sonar_feature_config fc;
+  sonar_feature_config_default(&fc);
+  fc.sample_rate = 0;                                             // F1: SampleRate is never copied (content_config.go:87-103)
+  fc.window_size = cfg->feature_window_size;                      // base FeatureConfig.WindowSize/HopSize
+  fc.hop_size = cfg->feature_hop_size;
+  fc.stft_window_size = cfg->window_size;                         // generationConfig.WindowSize/HopSize (:174-179)
+  fc.stft_hop_size = cfg->hop_size;
+  fc.window_type = cfg->window_type;
+  fc.enable_mfcc = st.mfcc; fc.enable_speech_features = st.speech; fc.enable_temporal_features = st.temporal;
+  fc.mfcc_coefficients = 13;
+  fc.is_news = ct != CT_TALK;                                     // CreateExtractor (feature_extractor.go:38-62)
+  fc.precision = cfg->precision;
+  const int rc = sonar_extract_speech_features(c, pcm, n, sample_rate, &fc, out);
+  if (rc != SONAR_OK) return rc;
+  (*out)->scalar("content_type", (double)ct);
+  (*out)->scalar("sample_rate", (double)sample_rate);
+  (*out)->scalar("hop_size", (double)cfg->feature_hop_size);       // AudioFingerprint.HopSize (fingerprint.go:215)
+  (*out)->scalar("duration_seconds", (double)n / (double)sample_rate);
+  return SONAR_OK;
+}
+
+// ------------------------------------------ AlignmentExtractor --------------
+int sonar_align_features(sonar_ctx* c, const double* qe, int64_t nqe, const double* re, int64_t nre, const double* qc,
+                         int64_t nqc, const double* rc_, int64_t nrc, int64_t q_pcm_len, int64_t r_pcm_len,
+                         int32_t sample_rate, int32_t feature_sample_rate, int32_t hop, int32_t win,
+                         double max_lag_seconds, sonar_result** out) {
+  if (!c || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (hop <= 0) return fail(c, SONAR_ERR_INVALID, "hop size must be positive (NewAlignmentExtractor divides by it)");
+  (void)win;
+  const int64_t max_lag_samples = (int64_t)(max_lag_seconds * (double)feature_sample_rate);   // alignment.go:104
+  auto* res = new sonar_result();
+  const double qlen = (double)q_pcm_len / (double)sample_rate, rlen = (double)r_pcm_len / (double)sample_rate;
+  res->scalar("query_length", qlen);
+  res->scalar("reference_length", rlen);
+
+  struct Cand { bool ok = false; int type = 0; sonar::host::AlignScores s; bool dtw = false;
+                int64_t p0q = 0, p0r = 0, p1q = 0, p1r = 0, plen = 0; };
+  Cand corr, chroma;
+  // 2. energy cross-correlation (performMultiFeatureAlignment :320-333 -> alignWithFeatures :357-410)
+  if (qe && re && nqe > 0 && nre > 0) {
+    const int64_t minf = std::min(nqe, nre);
+    int64_t mlf = max_lag_samples / hop;
+    mlf = std::min(mlf, minf - 1);
+    const int64_t L = std::max<int64_t>(0, std::min({mlf, nqe - 1, nre - 1}));
+    std::vector<double> cr(2 * L + 1), met(10);
+    const int rc = sonar_ncc(c, qe, nqe, re, nre, (int32_t)mlf, cr.data(), met.data(), 0);
+    if (rc != SONAR_OK) { delete res; return rc; }
+    sonar::host::NccMetrics m;
+    m.peak_corr = met[0]; m.peak_lag = (int64_t)met[1]; m.peak_index = (int64_t)met[2]; m.p_value = met[3];
+    m.snr = met[4]; m.sharpness = met[5]; m.second_peak = met[6]; m.psl = met[7]; m.overlap = (int64_t)met[8];
+    m.num_lags = (int64_t)met[9];
+    corr.ok = true; corr.type = 1;
+    corr.s = sonar::host::xcorr_scores(m, hop, sample_rate, (int)mlf);
+    res->vec("correlations", cr);
+    res->scalar("peak_lag", (double)m.peak_lag);
+    res->scalar("peak_correlation", m.peak_corr);
+    res->scalar("corr_snr", m.snr);
+    res->scalar("corr_sharpness", m.sharpness);
+    res->scalar("corr_peak_to_sidelobe", m.psl);
+    res->scalar("corr_offset", (double)corr.s.offset);
+    res->scalar("corr_offset_seconds", corr.s.offset_seconds);
+    res->scalar("corr_similarity", corr.s.similarity);
+    res->scalar("corr_confidence", corr.s.confidence);
+    res->scalar("corr_quality", corr.s.quality);
+    res->scalar("corr_noise_level", corr.s.noise_level);
+  }
+  // 4. chroma DTW (:346-351)
+  if (qc && rc_ && nqc > 0 && nrc > 0) {
+    const int64_t cap = nqc + nrc + 1;
+    std::vector<int32_t> pq(cap), pr(cap);
+    std::vector<double> pc(cap);
+    int64_t P = 0; double dist = 0;
+    const int rc = sonar_dtw(c, qc, nqc, rc_, nrc, 12, -1, &dist, pq.data(), pr.data(), pc.data(), &P, nullptr, 0);
+    if (rc != SONAR_OK) { delete res; return rc; }
+    chroma.ok = true; chroma.type = 2; chroma.dtw = true;
+    chroma.s = sonar::host::dtw_scores(pq.data(), pr.data(), pc.data(), P, nqc, nrc, dist, sample_rate);
+    chroma.plen = P;
+    if (P > 0) { chroma.p0q = pq[0]; chroma.p0r = pr[0]; chroma.p1q = pq[P - 1]; chroma.p1r = pr[P - 1]; }
+    std::vector<double> vq(P), vr(P), vc(P);
+    for (int64_t i = 0; i < P; i++) { vq[i] = pq[i]; vr[i] = pr[i]; vc[i] = pc[i]; }
+    res->scalar("dtw_distance", dist);
+    res->vec("dtw_path_query", vq);
+    res->vec("dtw_path_reference", vr);
+    res->vec("dtw_path_cost", vc);
+    res->scalar("dtw_offset", (double)chroma.s.offset);
+    res->scalar("dtw_offset_seconds", chroma.s.offset_seconds);
+    res->scalar("dtw_similarity", chroma.s.similarity);
+    res->scalar("dtw_confidence", chroma.s.confidence);
+    res->scalar("dtw_quality", chroma.s.quality);
+    res->scalar("dtw_stability", chroma.s.stability);
+  }
+  // selectBestAlignment (:412-446); Go iterates a map (random order) with strict >:
+  // here corr_energy is visited first, so exact ties go to it deterministically
+  const Cand* best = nullptr;
+  double best_score = 0.0;
+  for (const Cand* cd : {&corr, &chroma}) {
+    if (!cd->ok) continue;
+    const double w = cd->type == 1 ? 1.0 : 0.7;
+    const double sc = w * (0.4 * cd->s.confidence + 0.4 * cd->s.similarity + 0.2 * cd->s.quality);
+    if (sc > best_score) { best_score = sc; best = cd; }
+  }
+  double stretch = 1.0;                                           // estimateTimeStretch (:448-476)
+  if (best) {
+    res->scalar("temporal_offset", best->s.offset_seconds);
+    res->scalar("offset_confidence", best->s.confidence);
+    res->scalar("alignment_similarity", best->s.similarity);
+    res->scalar("alignment_quality", best->s.quality);
+    res->scalar("method", (double)best->type);
+    if (qlen > 0 && rlen > 0) {
+      const double lr = qlen / rlen;
+      stretch = lr;
+      if (best->dtw && best->plen > 1) {
+        const double qs = (double)(best->p1q - best->p0q + 1), rs = (double)(best->p1r - best->p0r + 1);
+        if (rs > 0) stretch = 0.7 * (qs / rs) + 0.3 * lr;
+      }
+    }
+  } else {
+    res->scalar("method", 0.0);
+  }
+  if (corr.ok) res->scalar("feature_similarity_corr_energy", corr.s.similarity);
+  if (chroma.ok) res->scalar("feature_similarity_dtw_chroma", chroma.s.similarity);
+  res->scalar("time_stretch", stretch);
+  *out = res;
+  return SONAR_OK;
+}
+
+}  // extern "C"

@@ -65,6 +65,10 @@ int launch_yin(const double* pcm, int64_t n, int64_t frames, int sample_rate, do
 int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, const double* window,
                   const double* trig, const int* chroma_map, double* out, hipStream_t s);
 int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, hipStream_t s);
+// speech-extractor helpers (misc_kernels.hip)
+int launch_preemph(const void* pcm, int pcm_f64, int64_t n, double alpha, double* y, hipStream_t s);
+int launch_stats(const double* y, int64_t n, double* part, int blocks, hipStream_t s);
+int launch_tilt(const double* y, int64_t n, int64_t frames, double* tilt, hipStream_t s);
 // NCC (align_kernels.hip)
 int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t L, double* norm_a,
                double* norm_b, double* stats, double* corr, hipStream_t s);

@@ -246,4 +246,66 @@ int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// ---- speech-extractor helpers -------------------------------------------
+// y = PreEmphasis.ProcessBuffer(x) (pre_emphasis.go:184-190), float64 output
+__global__ void preemph_kernel(const void* pcm, int pcm_f64, int64_t n, double alpha, double* y) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = preemph(pcm, pcm_f64, i, alpha);
+}
+
+// per-block partials over y: {max|y|, sum|y|, sum y^2, sign changes}, reduced on the host
+// in block order (speech.go:383-393 peak/average amplitude; speech_analysis.go:135-162 ZCR/RMS)
+__global__ __launch_bounds__(256) void stats_kernel(const double* y, int64_t n, double* part) {
+  __shared__ double sm[4][256];
+  double mx = 0, sa = 0, s2 = 0, cr = 0;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t b0 = (int64_t)blockIdx.x * per, b1 = min(n, b0 + per);
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
+    const double v = y[i], a = fabs(v);
+    mx = a > mx ? a : mx; sa += a; s2 += v * v;
+    if (i > 0) { const double u = y[i - 1]; cr += ((u >= 0 && v < 0) || (u < 0 && v >= 0)) ? 1.0 : 0.0; }
+  }
+  sm[0][threadIdx.x] = mx; sm[1][threadIdx.x] = sa; sm[2][threadIdx.x] = s2; sm[3][threadIdx.x] = cr;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      sm[0][threadIdx.x] = sm[0][threadIdx.x] > sm[0][threadIdx.x + o] ? sm[0][threadIdx.x] : sm[0][threadIdx.x + o];
+      for (int q = 1; q < 4; q++) sm[q][threadIdx.x] += sm[q][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) for (int q = 0; q < 4; q++) part[4 * blockIdx.x + q] = sm[q][0];
+}
+
+// SpeechFeatureExtractor.extractSpectralTilt (speech.go:552-585): frames of 1024 at hop 512
+__global__ void tilt_kernel(const double* y, int64_t n, int64_t frames, double* tilt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= frames) return;
+  const int64_t s = i * 512;
+  int64_t e = s + 1024; if (e > n) e = n;
+  double hi = 0.0, lo = 0.0;
+  for (int64_t j = s + 1; j < e; ++j) {
+    const double d = __dsub_rn(y[j], y[j - 1]);
+    hi = __dadd_rn(hi, __dmul_rn(d, d));
+    lo = __dadd_rn(lo, __dmul_rn(y[j], y[j]));
+  }
+  tilt[i] = lo > 0 ? -10.0 * log10(hi / lo) : 0.0;
+}
+
+int launch_preemph(const void* pcm, int pcm_f64, int64_t n, double alpha, double* y, hipStream_t s) {
+  if (n <= 0) return 0;
+  int64_t blocks = (n + 255) / 256; if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(preemph_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pcm, pcm_f64, n, alpha, y);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+int launch_stats(const double* y, int64_t n, double* part, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(stats_kernel, dim3(blocks), dim3(256), 0, s, y, n, part);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+int launch_tilt(const double* y, int64_t n, int64_t frames, double* tilt, hipStream_t s) {
+  if (frames <= 0) return 0;
+  hipLaunchKernelGGL(tilt_kernel, dim3((unsigned)((frames + 255) / 256)), dim3(256), 0, s, y, n, frames, tilt);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 }  // namespace sonar

@@ -22,66 +22,17 @@
 #include <string>
 #include <vector>
 
+#include "ctx.h"
 #include "host_dsp.h"
 #include "kernels.h"
 
-struct DevBuf {
-  void* ptr = nullptr;
-  size_t cap = 0;
-};
-
-struct FpTables {
-  void* window = nullptr;
-  int *mel_lo = nullptr, *mel_hi = nullptr, *mel_woff = nullptr, *grp_off = nullptr, *grp_mels = nullptr;
-  void *mel_w = nullptr, *dct = nullptr, *lift = nullptr;
-  int n_mels = 0, n_mfcc = 0, nnz = 0;
-};
-
-struct sonar_ctx {
-  int device = 0;
-  hipStream_t own = nullptr;
-  hipStream_t stream = nullptr;
-  std::string err;
-  std::map<std::string, DevBuf> bufs;
-  std::map<std::string, FpTables> fp_tables;
-  struct ChromaT { void* win; void* trig; void* map; };
-  std::map<std::string, ChromaT> chroma_tables;
-  bool timing = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;   // spare pair (kept for ABI simplicity)
-  // one event pair per timed launch since the last sonar_last_kernel_ms query
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
-  size_t ev_used = 0;
-  double last_ms = 0.0;
-};
-
-struct sonar_result {
-  struct Arr {
-    std::string name;
-    std::vector<double> v;
-    int64_t rows = 0, cols = 0;
-  };
-  std::vector<Arr> arrays;
-  void put(const std::string& name, std::vector<double> v, int64_t rows, int64_t cols) {
-    for (auto& a : arrays)
-      if (a.name == name) { a.v = std::move(v); a.rows = rows; a.cols = cols; return; }
-    arrays.push_back({name, std::move(v), rows, cols});
-  }
-  void scalar(const std::string& name, double x) { put(name, {x}, 1, 1); }
-  void vec(const std::string& name, const std::vector<double>& v) { put(name, v, (int64_t)v.size(), 1); }
-};
-
-namespace {
+namespace sonar {
+namespace detail {
 
 int fail(sonar_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
 }
-
-#define HIP_TRY(ctx, call)                                                                   \
-  do {                                                                                       \
-    hipError_t e_ = (call);                                                                  \
-    if (e_ != hipSuccess) return fail(ctx, SONAR_ERR_DEVICE, std::string(#call ": ") + hipGetErrorString(e_)); \
-  } while (0)
 
 void* dbuf(sonar_ctx* c, const std::string& name, size_t bytes) {
   if (bytes == 0) bytes = 16;
@@ -93,23 +44,6 @@ void* dbuf(sonar_ctx* c, const std::string& name, size_t bytes) {
   }
   return b.ptr;
 }
-
-template <typename T>
-void* upload(const std::vector<T>& v) {
-  void* p = nullptr;
-  size_t bytes = std::max<size_t>(16, v.size() * sizeof(T));
-  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-  if (!v.empty()) hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
-  return p;
-}
-void* upload_real(const std::vector<double>& v, bool f64) {
-  if (f64) return upload(v);
-  std::vector<float> f(v.begin(), v.end());
-  return upload(f);
-}
-
-int64_t go_frames(int64_t n, int W, int H) { return (n - W) / H + 1; }
-
 
 // brackets the dominant kernel of a call with a HIP event pair on its stream
 hipEvent_t timed_begin(sonar_ctx* c, hipStream_t s) {
@@ -128,6 +62,29 @@ void timed_end(sonar_ctx* c, hipStream_t s, hipEvent_t end) {
   hipEventRecord(end, s);
   c->ev_used++;
 }
+
+}  // namespace detail
+}  // namespace sonar
+
+namespace {
+using namespace sonar::detail;
+
+template <typename T>
+void* upload(const std::vector<T>& v) {
+  void* p = nullptr;
+  size_t bytes = std::max<size_t>(16, v.size() * sizeof(T));
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  if (!v.empty()) hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+  return p;
+}
+void* upload_real(const std::vector<double>& v, bool f64) {
+  if (f64) return upload(v);
+  std::vector<float> f(v.begin(), v.end());
+  return upload(f);
+}
+
+int64_t go_frames(int64_t n, int W, int H) { return (n - W) / H + 1; }
+
 
 }  // namespace
 

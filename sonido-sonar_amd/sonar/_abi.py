@@ -61,6 +61,12 @@ class FingerprintConfig(C.Structure):
                 ("window_type", C.c_int32), ("precision", C.c_int32)]
 
 
+class FeatureConfig(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ["sample_rate", "window_size", "hop_size", "stft_window_size",
+                                         "stft_hop_size", "window_type", "enable_mfcc", "enable_speech_features",
+                                         "enable_temporal_features", "mfcc_coefficients", "is_news", "precision"]]
+
+
 _lib = None
 _vp, _d, _i32p, _i64p = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
 
@@ -104,6 +110,10 @@ def lib():
     L.sonar_fingerprint_config_default.restype = None
     L.sonar_generate_fingerprint.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_char_p,
                                              C.POINTER(FingerprintConfig), C.POINTER(_vp)]
+    L.sonar_feature_config_default.argtypes = [C.POINTER(FeatureConfig)]
+    L.sonar_feature_config_default.restype = None
+    L.sonar_extract_speech_features.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(FeatureConfig),
+                                                C.POINTER(_vp)]
     L.sonar_align_features.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, _vp, C.c_int64, _vp, C.c_int64,
                                        C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                        C.c_double, C.POINTER(_vp)]
@@ -306,6 +316,22 @@ class Context:
         self._check(self._L.sonar_generate_fingerprint(self._h, _ptr(pcm) if len(pcm) else None, len(pcm),
                                                        sample_rate, content_type.encode(), C.byref(cfg),
                                                        C.byref(h)))
+        return self._result(h)
+
+    @staticmethod
+    def feature_config(**kw):
+        cfg = FeatureConfig()
+        lib().sonar_feature_config_default(C.byref(cfg))
+        for k, v in kw.items():
+            setattr(cfg, k, v)
+        return cfg
+
+    def extract_speech_features(self, pcm, sample_rate, cfg: FeatureConfig = None):
+        pcm = _f64(pcm)
+        cfg = cfg or self.feature_config()
+        h = C.c_void_p()
+        self._check(self._L.sonar_extract_speech_features(self._h, _ptr(pcm) if len(pcm) else None, len(pcm),
+                                                          sample_rate, C.byref(cfg), C.byref(h)))
         return self._result(h)
 
     def align_features(self, q_energy, r_energy, q_chroma=None, r_chroma=None, q_pcm_len=0, r_pcm_len=0,

@@ -1,0 +1,107 @@
+"""The C++ mirror of the Go orchestration (GenerateFingerprint -> speech extractor,
+AlignmentExtractor) against the oracle composition of the same Go code.
+Integer/decision outputs (is_speech, peak lag, DTW path, pitch frames) are exact;
+float features use the 1e-4-relative north-star tolerance (F64 kernels: 1e-6, device log/exp are not correctly rounded)."""
+import numpy as np
+import pytest
+
+import oracle as O
+import sonar
+from sonar import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rtol, name):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    if a.size == 1 and b.size == 1:
+        a, b = a.reshape(()), b.reshape(())
+    assert a.shape == b.shape, (name, a.shape, b.shape)
+    if a.size == 0:
+        return
+    scale = max(np.max(np.abs(b)), 1e-30)
+    err = np.max(np.abs(a - b)) / scale
+    assert err < rtol, (name, err)
+
+
+def _cmp(got, ref, rtol):
+    for k, v in ref.items():
+        assert k in got, k
+        if k == "spectral_rolloff":
+            assert np.mean(np.abs(got[k] - v) > 1e-6 * (1 + np.abs(v))) < 0.01
+            continue
+        if k == "spectral_slope":
+            _close(got[k], v, max(rtol, 1e-6), k)
+            continue
+        _close(got[k], v, rtol, k)
+
+
+def test_generate_fingerprint_music_c1(ctx):
+    """C1: GenerateFingerprint on the 10 s sweep, ContentType=music, 1024/256 (F1: SampleRate = 0)."""
+    x = synth.sweep(10.0)
+    cfg = ctx.fingerprint_config(window_size=1024, hop_size=256, feature_window_size=1024, feature_hop_size=256,
+                                 precision=sonar.F64)
+    got = ctx.generate_fingerprint(x, 44100, "music", cfg)
+    ref = O.speech_features_reference(x, 44100, dict(sample_rate=0, window_size=1024, hop_size=256,
+                                                     stft_window_size=1024, stft_hop_size=256, enable_mfcc=1,
+                                                     enable_speech_features=0, enable_temporal_features=0,
+                                                     mfcc_coefficients=13))
+    assert got["mfcc"].shape == (1719, 13)
+    assert np.allclose(got["mfcc"][:, 0], np.sqrt(26) * np.log(1e-10))    # F2 constant
+    assert np.all(got["spectral_centroid"] == 0) and np.all(got["zero_crossing_rate"] == 0)   # F3
+    assert np.all(got["pitch_estimate"] == 0)
+    _cmp(got, ref, 1e-6)
+
+
+def test_generate_fingerprint_talk_and_errors(ctx):
+    x = synth.c4_speech(seconds=4.0, sr=16000)
+    cfg = ctx.fingerprint_config(window_size=512, hop_size=128, feature_window_size=512, feature_hop_size=128,
+                                 precision=sonar.F64)
+    got = ctx.generate_fingerprint(x, 16000, "talk", cfg)
+    ref = O.speech_features_reference(x, 16000, dict(sample_rate=0, window_size=512, hop_size=128,
+                                                     stft_window_size=512, stft_hop_size=128, enable_mfcc=1,
+                                                     enable_speech_features=1, enable_temporal_features=1,
+                                                     mfcc_coefficients=13))
+    assert got["is_speech"] == ref["is_speech"]
+    _cmp(got, ref, 1e-6)
+    with pytest.raises(sonar.SonarError, match="content detection"):
+        ctx.generate_fingerprint(x, 16000, "speech", cfg)           # F12: "speech" is not a content type
+    with pytest.raises(sonar.SonarError, match="signal too short"):
+        ctx.generate_fingerprint(x[:300], 16000, "news", cfg)
+
+
+@pytest.mark.parametrize("prec,rtol", [(sonar.F64, 1e-6), (sonar.F32, 1e-4)])
+def test_speech_extractor_real_sample_rate_c4(ctx, prec, rtol):
+    """C4 arithmetic: direct speech extractor with FeatureConfig.SampleRate = 16000, W=512 H=128."""
+    x = synth.c4_speech(seconds=20.0, sr=16000)
+    fc = dict(sample_rate=16000, window_size=512, hop_size=128, stft_window_size=512, stft_hop_size=128,
+              enable_mfcc=1, enable_speech_features=1, enable_temporal_features=1, mfcc_coefficients=13)
+    got = ctx.extract_speech_features(x, 16000, ctx.feature_config(is_news=0, precision=prec, **fc))
+    ref = O.speech_features_reference(x, 16000, fc)
+    for k in ("pitch_estimate", "pitch_confidence", "voicing_strength", "zero_crossing_rate", "short_time_energy"):
+        assert np.array_equal(got[k], ref[k]), k            # YIN tau/tracking and ZCR counts are exact
+    if prec == sonar.F32:
+        ref = {k: v for k, v in ref.items() if k not in ("spectral_slope",)}
+    _cmp(got, ref, rtol)
+
+
+def test_align_features_c3_lag(ctx):
+    """C3-style: energy NCC + chroma DTW of two streams with an injected lag (60 s, scaled down from 5 min)."""
+    q, r = synth.c3_pair(seconds=60.0, lag_s=12.34)
+    fq = ctx.extract_speech_features(q, 44100, ctx.feature_config(sample_rate=44100, window_size=1024, hop_size=256))
+    fr = ctx.extract_speech_features(r, 44100, ctx.feature_config(sample_rate=44100, window_size=1024, hop_size=256))
+    F = sonar.stft_frames(len(q), 1024, 256)
+    cq = ctx.chroma_stft(q, F, 256, 44100)
+    cr = ctx.chroma_stft(r, F, 256, 44100)
+    got = ctx.align_features(fq["short_time_energy"], fr["short_time_energy"], cq, cr, len(q), len(r),
+                             sample_rate=44100, feature_sample_rate=44100, hop_size=256, window_size=1024,
+                             max_lag_seconds=20.0)
+    ref = O.align_features_reference(fq["short_time_energy"], fr["short_time_energy"], cq, cr, len(q), len(r),
+                                     44100, 44100, 256, 20.0)
+    assert got["peak_lag"] == ref["peak_lag"]
+    assert abs(got["peak_lag"] - (-12.34 * 44100 / 256)) <= 1.5 or abs(got["peak_lag"] - 12.34 * 44100 / 256) <= 1.5
+    assert np.array_equal(got["correlations"], ref["correlations"])
+    assert np.array_equal(got["dtw_path_query"], ref["dtw_path_query"])
+    assert got["method"] == ref["method"]
+    for k in ("temporal_offset", "offset_confidence", "alignment_similarity", "alignment_quality"):
+        assert got[k] == pytest.approx(ref[k], rel=1e-9, abs=1e-12), k
