@@ -96,7 +96,7 @@ def load_traffic():
         return None
     with open(files[-1]) as f:
         d = json.load(f)
-    return d.get("fp_tile_kernel_hbm_bytes_per_launch")
+    return d.get("fp_wave_kernel_hbm_bytes_per_launch")
 
 
 def cpu_baseline(seconds_hint):
@@ -212,7 +212,7 @@ def main():
                    "parallelism": f"frame-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS,
-                     "traffic": traffic, "kernel": "fp_tile_kernel<float,8>", "kernel_ms": kernel_ms,
+                     "traffic": traffic, "kernel": "fp_wave_kernel<float,float,8,false>", "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_frame": BYTES_PER_FRAME,
                      "valu_tflops": F * FLOPS_PER_FRAME / (kernel_ms * 1e-3) / 1e12,
                      "valu_frac": F * FLOPS_PER_FRAME / (kernel_ms * 1e-3) / 1e12 / FP32_PEAK_TFS},

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round profile on the GPU box: kernel-trace stats of the default bench command,
+# separate FETCH_SIZE / WRITE_SIZE PMC passes (never combined with trace domains),
+# then the plain bench line.  Usage: bash tools/profile_round.sh <tag>
+set -o pipefail
+TAG=${1:-r01}
+R="$GRAFT_REPO_ROOT"; [ -z "$R" ] && R=/root/repo
+OUT="$R/gpurun_out/prof_$TAG"; mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+    python3 "$R/bench.py" > "$OUT/bench_traced.log" 2>&1 || { echo "trace pass failed"; exit 1; }
+echo "trace done"
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/$c" -o run -- \
+      python3 "$R/bench.py" --no-cpu-baseline --dtw-len 0 --steps 5 --warmup 1 > "$OUT/$c.log" 2>&1 \
+      || { echo "pmc $c failed"; exit 1; }
+  echo "$c done"
+done
+timeout -k 10 420 python3 "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; exit 1; }
+cat "$OUT/bench.json"
