@@ -1,0 +1,376 @@
+// Package sonargpu is the cgo shim between the Go library (RyanBlaney/sonido-sonar)
+// and libsonar_gpu.so, the MI355X implementation of its per-frame DSP and
+// alignment hot path.  It is the "reference-side binding" INTEGRATION.md
+// describes: a maintainer drops this directory into the Go module (for
+// example as internal/sonargpu) and calls it from the two seams named below.
+//
+//	GenerateFingerprint   <- fingerprint/fingerprint.go:137 (FingerprintGenerator.GenerateFingerprint)
+//	ExtractSpeech         <- fingerprint/extractors/speech.go:135 (SpeechFeatureExtractor.ExtractFeatures)
+//	AlignFeatures         <- fingerprint/extractors/alignment.go:139 (AlignmentExtractor.ExtractAlignmentFeatures)
+//	Fingerprint / DTW / NCC are the lower seams: analyzers/spectral.go:385 + spectral/mfcc.go:167,
+//	stats/dtw.go:55, stats/correlation.go:131.
+//
+// Ownership follows the cgo rules: Go allocates every host slice and passes &s[0];
+// the C side owns device memory and its HIP stream inside the Context and keeps
+// no Go pointer after a call returns.  A Context is not goroutine-safe (neither are
+// the Go objects it replaces); use one per goroutine.
+//
+// No Go toolchain exists in the build container of this repository, so this file is
+// written against include/sonar_gpu.h and has not been compiled there.
+package sonargpu
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../lib -lsonar_gpu -Wl,-rpath,${SRCDIR}/../../lib
+#include <stdlib.h>
+#include "sonar_gpu.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"unsafe"
+)
+
+// Error codes of include/sonar_gpu.h.
+var (
+	ErrInvalid     = errors.New("sonargpu: invalid argument")
+	ErrTooShort    = errors.New("sonargpu: signal too short")
+	ErrEmpty       = errors.New("sonargpu: empty input")
+	ErrUnsupported = errors.New("sonargpu: unsupported configuration")
+	ErrDevice      = errors.New("sonargpu: HIP runtime error")
+	ErrNoMem       = errors.New("sonargpu: device allocation failed")
+)
+
+// Precision of the device arithmetic.
+const (
+	F32 = int(C.SONAR_F32) // throughput mode (1e-4 relative to the fp64 Go path)
+	F64 = int(C.SONAR_F64) // parity mode
+)
+
+// Context owns a device, a HIP stream and cached device tables.
+type Context struct{ c *C.sonar_ctx }
+
+// NewContext opens device `device` (HIP ordinal).
+func NewContext(device int) (*Context, error) {
+	var c *C.sonar_ctx
+	if rc := C.sonar_create(C.int(device), &c); rc != C.SONAR_OK {
+		return nil, fmt.Errorf("sonargpu: sonar_create(%d) failed (%d)", device, int(rc))
+	}
+	return &Context{c: c}, nil
+}
+
+// Close releases the device resources.
+func (x *Context) Close() {
+	if x.c != nil {
+		C.sonar_destroy(x.c)
+		x.c = nil
+	}
+}
+
+// err maps a return code to a Go error carrying the C side's message, which uses
+// the reference's own error text ("empty signal", "signal too short for given
+// window size and hop size", "empty sequences provided", ...).
+func (x *Context) err(rc C.int) error {
+	if rc == C.SONAR_OK {
+		return nil
+	}
+	msg := C.GoString(C.sonar_last_error(x.c))
+	var base error
+	switch rc {
+	case C.SONAR_ERR_TOO_SHORT:
+		base = ErrTooShort
+	case C.SONAR_ERR_EMPTY:
+		base = ErrEmpty
+	case C.SONAR_ERR_UNSUPPORTED:
+		base = ErrUnsupported
+	case C.SONAR_ERR_DEVICE:
+		base = ErrDevice
+	case C.SONAR_ERR_NOMEM:
+		base = ErrNoMem
+	default:
+		base = ErrInvalid
+	}
+	return fmt.Errorf("%s: %w", msg, base)
+}
+
+func f64p(s []float64) *C.double {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.double)(unsafe.Pointer(&s[0]))
+}
+
+// rows2 flattens a [][]float64 into one contiguous row-major slice (the one copy
+// SURVEY.md section 8(b) budgets for the [][] <-> contiguous conversion).
+func rows2(m [][]float64) ([]float64, int) {
+	if len(m) == 0 {
+		return nil, 0
+	}
+	d := len(m[0])
+	out := make([]float64, 0, len(m)*d)
+	for _, r := range m {
+		out = append(out, r...)
+	}
+	return out, d
+}
+
+func split(flat []float64, rows, cols int) [][]float64 {
+	out := make([][]float64, rows)
+	for i := range out {
+		out[i] = flat[i*cols : (i+1)*cols : (i+1)*cols]
+	}
+	return out
+}
+
+// Result is a set of named float64 arrays returned by the Go-API mirror entries.
+type Result struct {
+	Arrays  map[string][]float64
+	Shapes  map[string][2]int
+	Scalars map[string]float64
+}
+
+// Matrix returns a named 2-D result as [][]float64 (e.g. "mfcc").
+func (r *Result) Matrix(name string) [][]float64 {
+	a, ok := r.Arrays[name]
+	if !ok {
+		return nil
+	}
+	s := r.Shapes[name]
+	return split(a, s[0], s[1])
+}
+
+func (x *Context) collect(res *C.sonar_result) *Result {
+	defer C.sonar_result_free(res)
+	out := &Result{Arrays: map[string][]float64{}, Shapes: map[string][2]int{}, Scalars: map[string]float64{}}
+	n := int(C.sonar_result_count(res))
+	for i := 0; i < n; i++ {
+		cname := C.sonar_result_name(res, C.int(i))
+		name := C.GoString(cname)
+		var data *C.double
+		var rows, cols C.int64_t
+		if C.sonar_result_get(res, cname, &data, &rows, &cols) != C.SONAR_OK {
+			continue
+		}
+		cnt := int(rows) * int(cols)
+		vals := make([]float64, cnt)
+		if cnt > 0 {
+			copy(vals, unsafe.Slice((*float64)(unsafe.Pointer(data)), cnt))
+		}
+		out.Arrays[name] = vals
+		out.Shapes[name] = [2]int{int(rows), int(cols)}
+		if cnt == 1 {
+			out.Scalars[name] = vals[0]
+		}
+	}
+	return out
+}
+
+// FingerprintConfig mirrors fingerprint.FingerprintConfig (fingerprint.go:29-35).
+type FingerprintConfig struct {
+	WindowSize, HopSize               int
+	FeatureWindowSize, FeatureHopSize int // FingerprintConfig.FeatureConfig.{WindowSize,HopSize}
+	EnableContentDetect               bool
+	Precision                         int
+}
+
+// DefaultFingerprintConfig mirrors DefaultFingerprintConfig (fingerprint.go:70-98).
+func DefaultFingerprintConfig() FingerprintConfig {
+	var c C.sonar_fingerprint_config
+	C.sonar_fingerprint_config_default(&c)
+	return FingerprintConfig{int(c.window_size), int(c.hop_size), int(c.feature_window_size),
+		int(c.feature_hop_size), c.enable_content_detect != 0, int(c.precision)}
+}
+
+// GenerateFingerprint runs FingerprintGenerator.GenerateFingerprint's feature path
+// (content-type resolution, F1 SampleRate=0 extractor, STFT, features) on the GPU.
+// contentType is audioData.Metadata.ContentType.
+func (x *Context) GenerateFingerprint(pcm []float64, sampleRate int, contentType string,
+	cfg FingerprintConfig) (*Result, error) {
+	if len(pcm) == 0 {
+		return nil, fmt.Errorf("empty signal: %w", ErrEmpty)
+	}
+	cc := C.sonar_fingerprint_config{}
+	C.sonar_fingerprint_config_default(&cc)
+	cc.window_size, cc.hop_size = C.int32_t(cfg.WindowSize), C.int32_t(cfg.HopSize)
+	cc.feature_window_size, cc.feature_hop_size = C.int32_t(cfg.FeatureWindowSize), C.int32_t(cfg.FeatureHopSize)
+	cc.enable_content_detect = 0
+	if cfg.EnableContentDetect {
+		cc.enable_content_detect = 1
+	}
+	cc.precision = C.int32_t(cfg.Precision)
+	ct := C.CString(contentType)
+	defer C.free(unsafe.Pointer(ct))
+	var res *C.sonar_result
+	if rc := C.sonar_generate_fingerprint(x.c, f64p(pcm), C.int64_t(len(pcm)), C.int32_t(sampleRate), ct,
+		&cc, &res); rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	return x.collect(res), nil
+}
+
+// FeatureConfig mirrors the config.FeatureConfig fields the speech extractor reads.
+type FeatureConfig struct {
+	SampleRate, WindowSize, HopSize                          int
+	EnableMFCC, EnableSpeechFeatures, EnableTemporalFeatures bool
+	MFCCCoefficients                                         int
+	Precision                                                int
+}
+
+func b2i(b bool) C.int32_t {
+	if b {
+		return 1
+	}
+	return 0
+}
+
+// ExtractSpeech = NewSpeechFeatureExtractor(&cfg, isNews).ExtractFeatures(STFT(pcm, W, H), pcm, sampleRate).
+func (x *Context) ExtractSpeech(pcm []float64, sampleRate, stftWindow, stftHop int, cfg FeatureConfig,
+	isNews bool) (*Result, error) {
+	var fc C.sonar_feature_config
+	C.sonar_feature_config_default(&fc)
+	fc.sample_rate, fc.window_size, fc.hop_size = C.int32_t(cfg.SampleRate), C.int32_t(cfg.WindowSize), C.int32_t(cfg.HopSize)
+	fc.stft_window_size, fc.stft_hop_size = C.int32_t(stftWindow), C.int32_t(stftHop)
+	fc.enable_mfcc, fc.enable_speech_features = b2i(cfg.EnableMFCC), b2i(cfg.EnableSpeechFeatures)
+	fc.enable_temporal_features = b2i(cfg.EnableTemporalFeatures)
+	fc.mfcc_coefficients, fc.is_news, fc.precision = C.int32_t(cfg.MFCCCoefficients), b2i(isNews), C.int32_t(cfg.Precision)
+	var res *C.sonar_result
+	if rc := C.sonar_extract_speech_features(x.c, f64p(pcm), C.int64_t(len(pcm)), C.int32_t(sampleRate),
+		&fc, &res); rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	return x.collect(res), nil
+}
+
+// AlignFeatures = AlignmentExtractor.ExtractAlignmentFeatures on the energy envelopes
+// (EnergyFeatures.ShortTimeEnergy) and optional chroma of two fingerprints.
+func (x *Context) AlignFeatures(qEnergy, rEnergy []float64, qChroma, rChroma [][]float64,
+	qPCMLen, rPCMLen, sampleRate int, featureSampleRate, hop, window int, maxLagSeconds float64) (*Result, error) {
+	qc, _ := rows2(qChroma)
+	rc2, _ := rows2(rChroma)
+	var res *C.sonar_result
+	rc := C.sonar_align_features(x.c, f64p(qEnergy), C.int64_t(len(qEnergy)), f64p(rEnergy), C.int64_t(len(rEnergy)),
+		f64p(qc), C.int64_t(len(qChroma)), f64p(rc2), C.int64_t(len(rChroma)),
+		C.int64_t(qPCMLen), C.int64_t(rPCMLen), C.int32_t(sampleRate), C.int32_t(featureSampleRate),
+		C.int32_t(hop), C.int32_t(window), C.double(maxLagSeconds), &res)
+	if rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	return x.collect(res), nil
+}
+
+// MFCCParams mirrors spectral.MFCCParams (algorithms/spectral/mfcc.go:27-34).
+type MFCCParams struct {
+	NumCoefficients, NumFilters int
+	LowFreq, HighFreq           float64
+	UseLiftering                bool
+	LifterCoeff                 float64
+}
+
+// Fingerprint is the fused lower seam: SpectralAnalyzer.ComputeSTFTWithWindow(pcm, W, H, Hann)
+// followed by NewMFCCWithParams(sampleRate, p).ComputeFrames(|X|) — one kernel, the STFT is
+// never materialised.  Returns F x NumCoefficients.
+func (x *Context) Fingerprint(pcm []float64, windowSize, hopSize, sampleRate int, p MFCCParams,
+	precision int) ([][]float64, error) {
+	var cfg C.sonar_fp_cfg
+	C.sonar_fp_cfg_default(&cfg)
+	cfg.window_size, cfg.hop_size, cfg.sample_rate = C.int32_t(windowSize), C.int32_t(hopSize), C.int32_t(sampleRate)
+	cfg.n_mfcc, cfg.n_filters = C.int32_t(p.NumCoefficients), C.int32_t(p.NumFilters)
+	cfg.low_freq, cfg.high_freq, cfg.lifter = C.double(p.LowFreq), C.double(p.HighFreq), C.double(p.LifterCoeff)
+	cfg.use_lifter = b2i(p.UseLiftering)
+	cfg.flags = C.SONAR_FP_MFCC
+	cfg.precision, cfg.pcm_dtype, cfg.out_dtype = C.int32_t(precision), C.SONAR_F64, C.SONAR_F64
+	frames := int(C.sonar_stft_frames(C.int64_t(len(pcm)), C.int32_t(windowSize), C.int32_t(hopSize)))
+	if frames <= 0 {
+		return nil, fmt.Errorf("signal too short for given window size and hop size: %w", ErrTooShort)
+	}
+	nc := p.NumCoefficients
+	if nc <= 0 {
+		nc = 13
+	}
+	flat := make([]float64, frames*nc)
+	out := C.sonar_fp_out{mfcc: unsafe.Pointer(&flat[0])}
+	if rc := C.sonar_fingerprint(x.c, unsafe.Pointer(&pcm[0]), C.int64_t(len(pcm)), &cfg, &out); rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	return split(flat, frames, nc), nil
+}
+
+// DTWResult mirrors stats.DTWResult + AlignPoint (algorithms/stats/dtw.go:17-34).
+type DTWResult struct {
+	Distance   float64
+	PathQuery  []int
+	PathRef    []int
+	PathCost   []float64
+	CostMatrix [][]float64 // nil unless wantCost (costMatrix[1:], dtw.go:96)
+}
+
+// DTW = NewDTWAlignment().Align(q, r) with the Euclidean distance and symmetric2 step;
+// band < 0 disables the Sakoe-Chiba window.
+func (x *Context) DTW(q, r [][]float64, band int, wantCost bool) (*DTWResult, error) {
+	if len(q) == 0 || len(r) == 0 {
+		return nil, fmt.Errorf("empty sequences provided: %w", ErrEmpty)
+	}
+	qf, d := rows2(q)
+	rf, _ := rows2(r)
+	cap := len(q) + len(r)
+	pq, pr := make([]C.int32_t, cap), make([]C.int32_t, cap)
+	pc := make([]float64, cap)
+	var dist C.double
+	var plen C.int64_t
+	var cost []float64
+	var costp *C.double
+	if wantCost {
+		cost = make([]float64, len(q)*(len(r)+1))
+		costp = f64p(cost)
+	}
+	rc := C.sonar_dtw(x.c, f64p(qf), C.int64_t(len(q)), f64p(rf), C.int64_t(len(r)), C.int32_t(d), C.int32_t(band),
+		&dist, &pq[0], &pr[0], f64p(pc), &plen, costp, 0)
+	if rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	res := &DTWResult{Distance: float64(dist), PathQuery: make([]int, plen), PathRef: make([]int, plen),
+		PathCost: pc[:plen]}
+	for i := 0; i < int(plen); i++ {
+		res.PathQuery[i], res.PathRef[i] = int(pq[i]), int(pr[i])
+	}
+	if wantCost {
+		res.CostMatrix = split(cost, len(q), len(r)+1)
+	}
+	return res, nil
+}
+
+// CorrelationResult mirrors the fields of stats.CorrelationResult (correlation.go:44-70) the alignment code reads.
+type CorrelationResult struct {
+	Correlations                                  []float64
+	PeakCorrelation                               float64
+	PeakLag, PeakIndex                            int
+	PValue, SNR, Sharpness, SecondPeak, PSL       float64
+	OverlapLength                                 int
+}
+
+// NCC = CrossCorrelation{NormalizedCrossCorrelation, TimeDomain, maxLag}.Compute(s1, s2).
+func (x *Context) NCC(s1, s2 []float64, maxLag int) (*CorrelationResult, error) {
+	if len(s1) == 0 || len(s2) == 0 {
+		return nil, fmt.Errorf("empty signals provided: %w", ErrEmpty)
+	}
+	L := maxLag
+	if len(s1)-1 < L {
+		L = len(s1) - 1
+	}
+	if len(s2)-1 < L {
+		L = len(s2) - 1
+	}
+	if L < 0 {
+		L = 0
+	}
+	corr := make([]float64, 2*L+1)
+	var m [10]float64
+	if rc := C.sonar_ncc(x.c, f64p(s1), C.int64_t(len(s1)), f64p(s2), C.int64_t(len(s2)), C.int32_t(maxLag),
+		f64p(corr), (*C.double)(unsafe.Pointer(&m[0])), 0); rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	return &CorrelationResult{Correlations: corr, PeakCorrelation: m[0], PeakLag: int(m[1]), PeakIndex: int(m[2]),
+		PValue: m[3], SNR: m[4], Sharpness: m[5], SecondPeak: m[6], PSL: m[7], OverlapLength: int(m[8])}, nil
+}
