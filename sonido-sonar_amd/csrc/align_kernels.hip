@@ -9,14 +9,12 @@
 //       bit-identical to a sequential float64 evaluation.
 //  DTW  DTWAlignment.Align / fillCostMatrix / findPreviousStep / backtrack
 //       (algorithms/stats/dtw.go:55-217) with EuclideanDistanceFunc (distance.go:29-36).
-//       dtw_dist_kernel   : C[i][j] = ||q_{i-1} - r_{j-1}||, C[0][*] = C[*][0] = +Inf, C[0][0] = 0
-//                           (fully parallel, the matrix lives in HBM: 288 GB fits 51,676^2 doubles)
-//       dtw_wave_kernel   : one launch per anti-diagonal of 64 x 64 tiles; one wave per tile
-//                           sweeps its tile anti-diagonally (lane = row), neighbours through
-//                           DPP shuffles, and records Go's backtrack choice (vertical <=
-//                           horizontal <= diagonal, strict <) as a direction byte per cell.
-//       dtw_backtrack_kernel: one wave walks the direction bytes from (N, M) through
-//                           64 x 64 LDS-cached blocks.
+//       dtw_band_kernel   : ONE persistent launch; 64-row bands pipelined through an sc1
+//                           edge hand-off, lane = row, DPP neighbours, distance inline
+//                           (see the DTW section below for the layout)
+//       dtw_walk_kernel   : one wave walks the 2-bit direction codes from (N, M)
+#include <type_traits>
+
 #include "kernels.h"
 
 #pragma clang fp contract(off)
@@ -103,151 +101,466 @@ int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t
 }
 
 // ---------------------------------------------------------------- DTW ----
-constexpr int DTW_T = 64;   // tile rows (= lanes) and columns
+// Forward sweep (fillCostMatrix + applyStepPattern "symmetric2", dtw.go:106-135,138-143)
+// as ONE persistent launch.  Rows are cut into bands of 64; one wave owns a band
+// (lane l = row 64b+1+l) and sweeps it in S = nr + 63 skewed steps: at step s lane
+// l relaxes column j = s - l + 1, so C[i-1][j] (lane l-1, previous step) and
+// C[i-1][j-1] (what this lane received one step earlier) arrive through one
+// DPP wave_shr:1 per step and C[i][j-1] is the lane's own register.  Bands are
+// handed out by an atomic ticket in order, so a wave only ever waits for an
+// earlier, already running band: band b's last row goes to band b+1 through the
+// edge buffer E as 8-byte sc1 stores that ARE the flag (the buffer is pre-filled
+// with a signalling-NaN sentinel no arithmetic can produce; MI355X_MICROARCH.md
+// "Valid forms", R2).  The local distance (EuclideanDistanceFunc, distance.go:29-36,
+// unfused, Go's summation order) is computed inline from the lane's query row in
+// registers and a 128-row LDS ring of reference rows (row s-l for lane l).
+//   Cn[b][s][l]  C[64b+1+l][s-l+1]    one coalesced 512-B store per step (8 B/cell)
+//   Dn[b][w][l]  2-bit findPreviousStep codes (dtw.go:191-217) of steps 16w..16w+15
+// The walk (backtrack, dtw.go:165-188) is one wave reading Dn through 16-word
+// register windows (readlane), s = j-1+l strictly decreases along the path.
+constexpr int DTW_RING = 128;                       // reference rows held in LDS
+constexpr int DTW_ECH = 8;                          // edge values polled per chunk
+#ifndef DTW_G
+#define DTW_G 4                                     // steps per scheduling group in the sweep
+#endif
+constexpr uint64_t DTW_SENT = 0x7FF000017FF00001ull;  // signalling NaN: never an arithmetic result
+constexpr int DTW_SPIN_LIMIT = 1 << 22;
 
-__global__ __launch_bounds__(256) void dtw_dist_kernel(const double* q, int64_t nq, const double* r, int64_t nr,
-                                                       int dim, int band, double* C) {
-  const int64_t pitch = nr + 1;
-  const int64_t total = (nq + 1) * pitch;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = idx / pitch, j = idx - i * pitch;
-    double v;
-    if (i == 0 || j == 0) {
-      v = (i == 0 && j == 0) ? 0.0 : __builtin_inf();
-    } else if (band > 0 && (i - j > band || j - i > band)) {
-      v = __builtin_inf();                       // outside Sakoe-Chiba band: never filled (dtw.go:115-119)
-    } else {
-      const double* a = q + (i - 1) * dim;
-      const double* b = r + (j - 1) * dim;
-      double s = 0.0;
-      for (int d = 0; d < dim; ++d) { const double df = __dsub_rn(a[d], b[d]); s = __dadd_rn(s, __dmul_rn(df, df)); }
-      v = sqrt(s);
-    }
-    C[idx] = v;
-  }
+struct DtwArgs {
+  const double* q;
+  const double* r;
+  int dim, band;
+  int64_t nq, nr, nb, S, SW;
+  double* Cn;
+  uint32_t* Dn;
+  uint64_t* E;
+  int32_t* sync;   // [0] band ticket, [1] error flag
+  uint64_t* trace; // optional [nb][4]: t_start, t_first_edge, t_end, spins (s_memrealtime, 100 MHz)
+};
+
+namespace {
+__device__ __forceinline__ double shr1(double v, double lane0) {
+  const int2 a = __builtin_bit_cast(int2, v), o = __builtin_bit_cast(int2, lane0);
+  const int lo = __builtin_amdgcn_update_dpp(o.x, a.x, 0x138, 0xf, 0xf, false);   // wave_shr:1
+  const int hi = __builtin_amdgcn_update_dpp(o.y, a.y, 0x138, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, make_int2(lo, hi));
 }
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int2 a = __builtin_bit_cast(int2, v);
+  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readlane(a.x, l), __builtin_amdgcn_readlane(a.y, l)));
+}
+}  // namespace
 
-// One wave per 64x64 tile on anti-diagonal `diag` of the tile grid.
-__global__ __launch_bounds__(64) void dtw_wave_kernel(double* C, uint8_t* dir, int64_t nq, int64_t nr, int band,
-                                                      int64_t diag, int64_t ntr, int64_t ntc) {
-  __shared__ double above[DTW_T + 1];            // C[i0-1][j0-1 .. j0+63]
-  const int lane = threadIdx.x;
-  const int64_t tr_lo = diag - (ntc - 1) > 0 ? diag - (ntc - 1) : 0;
-  const int64_t tr = tr_lo + blockIdx.x;
-  const int64_t tc = diag - tr;
-  if (tr >= ntr || tc < 0) return;
-  const int64_t pitch = nr + 1;
-  const int64_t i0 = 1 + tr * DTW_T, j0 = 1 + tc * DTW_T;
-  const int64_t i = i0 + lane;
-  const bool row_ok = i <= nq;
-  for (int k = lane; k <= DTW_T; k += 64) {
-    const int64_t j = j0 - 1 + k;
-    above[k] = (j <= nr) ? C[(i0 - 1) * pitch + j] : __builtin_inf();
+// Block = 2 waves.  Wave 0 sweeps the band and touches global memory only with
+// stores (a gfx9 vmcnt wait would also drain its Cn stores, ~0.5 us per step);
+// wave 1 feeds it through LDS: the reference-row ring (256 rows, refilled 64 at a
+// time once wave 0's published progress shows the slots dead) and the edge ring
+// (C[64b][j] polled from E with sc1 loads).  LDS words rdy/efill/prog carry the
+// counts; a wave reads data only after it has read the count that covers it.
+constexpr int DTW_RROWS = 256;    // reference rows in the LDS ring (4 blocks of 64)
+constexpr int DTW_EQ = 256;       // edge values in the LDS ring
+constexpr int DTW_EAHEAD = 128;   // wave 1 fetches edge columns up to prog + EAHEAD
+
+template <int D, bool FAST, bool BANDED>
+__global__ __launch_bounds__(128) void dtw_band_kernel(DtwArgs a) {
+  constexpr int DR = D > 0 ? D : 1;
+  __shared__ __attribute__((aligned(16))) double ring[DTW_RROWS * DR];
+  __shared__ double eq[DTW_EQ];
+  __shared__ int64_t shb;
+  __shared__ int prog, rdy, efill;   // wave 0 steps done; blocks in ring; edge columns in eq
+#define SONAR_LDS_LD(x) __hip_atomic_load(&(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#define SONAR_LDS_ST(x, v) __hip_atomic_store(&(x), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    shb = atomicAdd(&a.sync[0], 1);
+    prog = 0; rdy = -1; efill = 0;
   }
-  if (lane == 0 && j0 + DTW_T - 1 <= nr) above[DTW_T] = C[(i0 - 1) * pitch + j0 + DTW_T - 1];
-  const double left0 = row_ok ? C[i * pitch + (j0 - 1)] : __builtin_inf();
   __syncthreads();
-  double diag0 = __shfl_up(left0, 1, 64);
-  if (lane == 0) diag0 = above[0];
+  const int64_t b = shb;
+  if (b >= a.nb) return;
+  const int64_t nq = a.nq, nr = a.nr, S = a.S;
+  const int dim = D > 0 ? D : a.dim;
+  const double inf = __builtin_inf();
+  constexpr uint64_t INF_BITS = 0x7FF0000000000000ull;
+  const uint64_t* Ein = b > 0 ? a.E + (b - 1) * (nr + 1) : nullptr;       // C[64b][j] at index j
+  const int64_t nblk = (nr + 63) >> 6;
 
-  double out = left0;      // my value at the previous column
-  double up_prev = 0.0;    // value received from the lane above at the previous step
-  for (int s = 0; s < DTW_T + 63; ++s) {
-    double up = __shfl_up(out, 1, 64);
-    const int cj = s - lane;
-    if (lane == 0) up = above[(s + 1) <= DTW_T ? (s + 1) : DTW_T];
-    const int64_t j = j0 + cj;
-    const bool act = row_ok && cj >= 0 && cj < DTW_T && j <= nr;
-    if (act) {
-      const double left = (cj == 0) ? left0 : out;
-      const double dg = (cj == 0) ? diag0 : up_prev;
-      const int64_t o = i * pitch + j;
-      const double d = C[o];
-      const bool inband = !(band > 0 && (i - j > band || j - i > band));
-      double v = d;
-      if (inband) v = __dadd_rn(d, go_min(go_min(up, left), dg));
-      // findPreviousStep (dtw.go:191-217): vertical, horizontal, diagonal; strict <
-      uint8_t code = 0; double best = up;
-      if (left < best) { code = 1; best = left; }
-      if (dg < best) code = 2;
-      C[o] = v;
-      dir[(i - 1) * nr + (j - 1)] = code;
-      out = v;
+  if (wave == 1) {
+    // ------------------------------------------------------------ feeder wave
+    int64_t nextblk = 0, have = 0;
+    uint64_t spins = 0;
+    const int64_t ecols = Ein ? nr : 0;
+    while (true) {
+      const int64_t p = SONAR_LDS_LD(prog);
+      bool work = false;
+      if constexpr (D > 0) {
+        // block m overwrites block m-4, whose last row 64m-193 is read by lane 63 for step
+        // 64m-130 (computed one step early): wait until wave 0 has done 64(m-2) steps
+        if (nextblk < nblk && (nextblk < 4 || p >= 64 * (nextblk - 2))) {
+          const int64_t row = 64 * nextblk + lane;
+          double* dst = ring + ((64 * nextblk + lane) & (DTW_RROWS - 1)) * D;
+#pragma unroll
+          for (int k = 0; k < DR; ++k) dst[k] = row < nr ? a.r[row * D + k] : 0.0;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) SONAR_LDS_ST(rdy, (int)nextblk);
+          ++nextblk;
+          work = true;
+        }
+      }
+      if (have < ecols) {
+        const int64_t want = p + DTW_EAHEAD < ecols ? p + DTW_EAHEAD : ecols;
+        if (have < want) {
+          const int64_t jj = have + 1 + lane;
+          uint64_t v = INF_BITS;
+          if (jj <= want) v = __hip_atomic_load(Ein + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t bad = __builtin_amdgcn_ballot_w64(jj <= want && v == DTW_SENT);
+          const int64_t lim = want - have < 64 ? want - have : 64;
+          const int64_t got = bad ? (int64_t)__builtin_ctzll(bad) : lim;   // contiguous ready prefix
+          if (lane < got) eq[jj & (DTW_EQ - 1)] = __builtin_bit_cast(double, v);
+          if (got > 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            have += got;
+            if (lane == 0) SONAR_LDS_ST(efill, (int)have);
+            work = true;
+          }
+        }
+      }
+      const bool done = (D == 0 || nextblk >= nblk) && have >= ecols;
+      if (done) break;
+      if (!work) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (uint64_t)DTW_SPIN_LIMIT * 4) {   // producer band never arrived: flag, release wave 0
+          if (lane == 0) { atomicOr(&a.sync[1], 1); SONAR_LDS_ST(efill, (int)ecols); SONAR_LDS_ST(rdy, (int)nblk); }
+          break;
+        }
+      }
     }
+    return;
+  }
+
+  // ---------------------------------------------------------------- sweep wave
+  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint64_t t_first = 0, spins_total = 0;
+  const int64_t i = 64 * b + 1 + lane;
+  const bool row_ok = i <= nq;
+  const int64_t qrow = row_ok ? i - 1 : 0;
+  double qv[DR];
+  if constexpr (D > 0) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) qv[k] = a.q[qrow * D + k];
+  }
+  // local distance of the lane's cell at step t (EuclideanDistanceFunc order, unfused)
+  auto dist = [&](int64_t t) -> double {
+    if constexpr (D > 0) {
+      const double* rw = ring + ((t - lane) & (DTW_RROWS - 1)) * D;
+      double df = qv[0] - rw[0];
+      double sum = df * df;                            // 0.0 + x == x for x >= +0 or NaN
+#pragma unroll
+      for (int k = 1; k < D; ++k) {
+        df = qv[k] - rw[k];
+        sum = sum + df * df;
+      }
+      return sqrt(sum);
+    } else {
+      double sum = 0.0;
+      const int64_t jj = t - lane + 1;
+      if (row_ok && jj >= 1 && jj <= nr) {
+        const double* qa = a.q + qrow * dim;
+        const double* rb = a.r + (jj - 1) * dim;
+        for (int k = 0; k < dim; ++k) {
+          const double df = qa[k] - rb[k];
+          sum = sum + df * df;
+        }
+      }
+      return sqrt(sum);
+    }
+  };
+  // spin (LDS only) until a feeder count reaches `need`
+#define SONAR_WAIT_COUNT(word, need)                                                  \
+  do {                                                                                \
+    uint64_t sp_ = 0;                                                                 \
+    while (SONAR_LDS_LD(word) < (need)) {                                             \
+      __builtin_amdgcn_s_sleep(1);                                                    \
+      if (++sp_ > (uint64_t)DTW_SPIN_LIMIT * 4) { if (lane == 0) atomicOr(&a.sync[1], 2); break; } \
+    }                                                                                 \
+    spins_total += sp_;                                                               \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
+  } while (0)
+
+  uint64_t* Eout = (b + 1 < a.nb) ? a.E + b * (nr + 1) : nullptr;         // C[64b+64][j]
+  double out = inf;                                   // C[i][j-1]; C[i][0] = +Inf
+  double up_prev = (lane == 0 && b == 0) ? 0.0 : inf; // C[i-1][j-1]; C[0][0] = 0
+  uint32_t dacc = 0;
+  const int64_t band = a.band;
+  double* Cb = a.Cn + ((b * S) << 6) + lane;
+  uint32_t* Db = a.Dn + ((b * a.SW) << 6) + lane;
+  // one sweep step: lane l relaxes C[i][s-l+1] with local distance d; l0up = C[64b][s+1]
+  // for lane 0.  FULL: every lane's column is in [1, nr] (s in [63, nr-1]), so no
+  // per-lane predicate is needed (rows past nq compute values nobody reads).
+  auto step = [&](auto full_tag, int s, double l0up, double d, double* cs) -> uint32_t {
+    constexpr bool FULL = decltype(full_tag)::value;
+    const double up = shr1(out, l0up);               // C[i-1][j]
+    const int j = s - lane + 1;
+    const double left = out, dg = up_prev;
+    // findPreviousStep: vertical, horizontal, diagonal; strict < (NaN compares false)
+    uint32_t code = 0;
+    double best = up;
+    if (left < best) { code = 1; best = left; }
+    if (dg < best) { code = 2; best = dg; }
+    if constexpr (!FAST) best = go_min(go_min(up, left), dg);   // math.Min: NaN / -Inf / -0 rules
+    double v = d + best;
+    if constexpr (BANDED) {
+      if (i - j > band || j - i > band) v = inf;      // outside the Sakoe-Chiba band: never filled
+    }
+    if constexpr (FULL) {
+      out = v;
+    } else {
+      if (row_ok && j >= 1 && j <= nr) out = v;
+    }
+    *cs = out;
     up_prev = up;
+    return code;
+  };
+
+  // distances of chunk c+1 are computed while chunk c runs its min-chains: 8
+  // independent f64 chains give the ILP one wave per SIMD cannot get otherwise
+  double dc[DTW_ECH], dn[DTW_ECH];
+  if constexpr (D > 0) SONAR_WAIT_COUNT(rdy, 0);
+#pragma unroll
+  for (int u = 0; u < DTW_ECH; ++u) {
+    dc[u] = u < S ? dist(u) : 0.0;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  for (int s0 = 0; s0 < S; s0 += DTW_ECH) {
+    if (lane == 0) SONAR_LDS_ST(prog, s0);             // steps < s0 are done
+    const bool more = s0 + DTW_ECH < S;
+    if constexpr (D > 0) {
+      const int need = (s0 + 2 * DTW_ECH - 1) >> 6;    // next chunk's dist() reads rows up to s0 + 15
+      if (more && need < nblk) SONAR_WAIT_COUNT(rdy, need);
+    }
+    double ech = inf;
+    if (Ein) {
+      const int need = (int)(s0 + DTW_ECH < nr ? s0 + DTW_ECH : nr);
+      SONAR_WAIT_COUNT(efill, need);
+      if (a.trace && s0 == 0) t_first = __builtin_amdgcn_s_memrealtime();
+      const int64_t jj = s0 + 1 + lane;
+      if (lane < DTW_ECH && jj <= nr) ech = eq[jj & (DTW_EQ - 1)];
+    }
+    double* cs = Cb + ((int64_t)s0 << 6);
+    double eacc = inf;                                 // lane u <- C[64b+64][s0+u-62] (lane 63's value)
+    const bool full = s0 >= 63 && s0 + DTW_ECH <= nr;
+    if (full) {
+      // groups of DTW_G steps, each interleaved with DTW_G of the next chunk's distances;
+      // the sched_barrier keeps the scheduler from hoisting every ring read (VGPRs)
+#pragma unroll
+      for (int g0 = 0; g0 < DTW_ECH; g0 += DTW_G) {
+#pragma unroll
+        for (int u = g0; u < g0 + DTW_G; ++u) dn[u] = dist(s0 + DTW_ECH + u);
+#pragma unroll
+        for (int u = g0; u < g0 + DTW_G; ++u) {
+          const uint32_t code =
+              step(std::true_type{}, s0 + u, Ein ? readlane_f64(ech, u) : inf, dc[u], cs + (u << 6));
+          dacc |= code << (2 * ((s0 & 8) + u));
+          if (Eout) { const double e = readlane_f64(out, 63); eacc = lane == u ? e : eacc; }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int g0 = 0; g0 < DTW_ECH; g0 += DTW_G) {
+#pragma unroll
+        for (int u = g0; u < g0 + DTW_G; ++u) dn[u] = s0 + DTW_ECH + u < S ? dist(s0 + DTW_ECH + u) : 0.0;
+#pragma unroll
+        for (int u = g0; u < g0 + DTW_G; ++u) {
+          if (s0 + u < S) {
+            const uint32_t code = step(std::false_type{}, s0 + u, Ein ? readlane_f64(ech, u) : inf, dc[u],
+                                       cs + (u << 6));
+            dacc |= code << (2 * ((s0 & 8) + u));
+            if (Eout) { const double e = readlane_f64(out, 63); eacc = lane == u ? e : eacc; }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (Eout) {                                        // one sc1 store of the chunk's 8 edge values
+      const int64_t je = (int64_t)s0 + lane - 62;
+      if (lane < DTW_ECH && je >= 1 && je <= nr)
+        __hip_atomic_store(Eout + je, __builtin_bit_cast(uint64_t, eacc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if ((s0 & 8) || !more) {                           // steps 16w .. 16w+15 complete (or the last one)
+      Db[(int64_t)(s0 >> 4) << 6] = dacc;
+      dacc = 0;
+    }
+#pragma unroll
+    for (int u = 0; u < DTW_ECH; ++u) dc[u] = dn[u];
+  }
+  if (lane == 0) SONAR_LDS_ST(prog, (int)S);
+#undef SONAR_WAIT_COUNT
+#undef SONAR_LDS_LD
+#undef SONAR_LDS_ST
+  if (a.trace && lane == 0) {
+    a.trace[4 * b + 0] = t_start;
+    a.trace[4 * b + 1] = t_first;
+    a.trace[4 * b + 2] = __builtin_amdgcn_s_memrealtime();
+    a.trace[4 * b + 3] = spins_total;
   }
 }
 
-// Single wave: backtrack (dtw.go:165-188) through 64x64 LDS-cached blocks.
-// Records points in reverse order: rev_q[k] = i-1, rev_r[k] = j-1.
-__global__ __launch_bounds__(64) void dtw_backtrack_kernel(const uint8_t* dir, int64_t nq, int64_t nr, int32_t* rev_q,
-                                                           int32_t* rev_r, int64_t* plen) {
-  __shared__ uint8_t blk[64][64];
+// Single wave: backtrack (dtw.go:165-188) over the 2-bit codes.  Points are
+// recorded in reverse order (rev_q[k] = i-1, rev_r[k] = j-1), 64 at a time.
+// Interior steps read lane l's code word of band (i-1)/64 from a 16-word
+// register window (s = j-1+l only decreases inside a band, so only the lower
+// bound is checked); the borders (i == 0 or j == 0) are straight runs.
+__global__ __launch_bounds__(64) void dtw_walk_kernel(const uint32_t* Dn, int64_t nq, int64_t nr, int64_t SW,
+                                                      int32_t* rev_q, int32_t* rev_r, int64_t* plen) {
   const int lane = threadIdx.x;
-  int64_t i = nq, j = nr, P = 0;
-  int64_t r0 = 1 << 30, c0 = 1 << 30;   // block rows [r0, r0+63], cols [c0, c0+63]
-  while (i > 0 || j > 0) {
-    if (lane == 0) { rev_q[P] = (int32_t)(i - 1); rev_r[P] = (int32_t)(j - 1); }
+  uint32_t win[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) win[k] = 0u;
+  int i = (int)nq, j = (int)nr, P = 0;
+  int wb = -1, wlo = 0;
+  const int sw = (int)SW;
+  int32_t aq = 0, ar = 0;
+  auto record = [&](int qi, int ri) {
+    if (lane == (P & 63)) { aq = qi; ar = ri; }
+    if ((P & 63) == 63) { rev_q[P - 63 + lane] = aq; rev_r[P - 63 + lane] = ar; }
     ++P;
-    if (i == 0) { --j; continue; }
-    if (j == 0) { --i; continue; }
-    if (i < r0 || i > r0 + 63 || j < c0 || j > c0 + 63) {
-      __syncthreads();
-      r0 = i - 63 > 1 ? i - 63 : 1;
-      c0 = j - 63 > 1 ? j - 63 : 1;
-      const int64_t row = r0 + lane;
-      if (row <= nq) {
-        const uint8_t* src = dir + (row - 1) * nr + (c0 - 1);
-        const int64_t ncols = (nr - (c0 - 1)) < 64 ? (nr - (c0 - 1)) : 64;
-        for (int k = 0; k < ncols; ++k) blk[lane][k] = src[k];
-      }
-      __syncthreads();
+  };
+  while (i > 0 && j > 0) {
+    record(i - 1, j - 1);
+    const int l = (i - 1) & 63, bnd = (i - 1) >> 6;
+    const int s = j - 1 + l, w = s >> 4;
+    if (bnd != wb || w < wlo) {
+      wb = bnd;
+      wlo = w - 15 > 0 ? w - 15 : 0;
+      const uint32_t* src = Dn + (((int64_t)bnd * sw + wlo) << 6) + lane;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) win[k] = (wlo + k < sw) ? src[k << 6] : 0u;
     }
-    const uint8_t code = blk[i - r0][j - c0];
-    if (code == 0) --i;
-    else if (code == 1) --j;
-    else { --i; --j; }
+    const uint32_t word = __builtin_amdgcn_readlane(win[w - wlo], l);
+    const uint32_t code = (word >> ((s & 15) << 1)) & 3u;
+    i -= code != 1u;          // vertical (0) or diagonal (2)
+    j -= code != 0u;          // horizontal (1) or diagonal (2)
   }
+  while (i > 0 || j > 0) {    // findPreviousStep on the borders: i == 0 -> left, j == 0 -> up
+    record(i - 1, j - 1);
+    if (i == 0) --j; else --i;
+  }
+  const int rem = P & 63;
+  if (rem && lane < rem) { rev_q[P - rem + lane] = aq; rev_r[P - rem + lane] = ar; }
   if (lane == 0) *plen = P;
 }
 
-// path cost C[i][j] - C[i-1][j-1] (0 on the borders), forward order
-__global__ void dtw_path_cost_kernel(const double* C, int64_t nr, const int32_t* rev_q, const int32_t* rev_r,
+namespace {
+__device__ __forceinline__ double cn_at(const double* Cn, int64_t S, int64_t i, int64_t j) {
+  if (i == 0) return j == 0 ? 0.0 : __builtin_inf();
+  if (j == 0) return __builtin_inf();
+  const int64_t b = (i - 1) >> 6, l = (i - 1) & 63;
+  return Cn[((b * S + (j - 1 + l)) << 6) + l];
+}
+}  // namespace
+
+// path cost C[i][j] - C[i-1][j-1] (0 on the borders), forward order (dtw.go:170-173)
+__global__ void dtw_path_cost_kernel(const double* Cn, int64_t S, const int32_t* rev_q, const int32_t* rev_r,
                                      int64_t P, int32_t* pq, int32_t* pr, double* pc) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= P) return;
   const int64_t src = P - 1 - k;
   const int64_t qi = rev_q[src], ri = rev_r[src];   // i-1, j-1
-  const int64_t pitch = nr + 1;
   double c = 0.0;
-  if (qi >= 0 && ri >= 0) c = __dsub_rn(C[(qi + 1) * pitch + (ri + 1)], C[qi * pitch + ri]);
+  if (qi >= 0 && ri >= 0) c = __dsub_rn(cn_at(Cn, S, qi + 1, ri + 1), cn_at(Cn, S, qi, ri));
   pq[k] = (int32_t)qi; pr[k] = (int32_t)ri; pc[k] = c;
 }
 
-int launch_dtw(const double* q, int64_t nq, const double* r, int64_t nr, int dim, int band, double* C, uint8_t* dir,
-               int32_t* rev_q, int32_t* rev_r, int64_t* plen, hipStream_t s) {
-  const int64_t total = (nq + 1) * (nr + 1);
-  int64_t blocks = (total + 255) / 256;
-  if (blocks > 256 * 64) blocks = 256 * 64;
-  hipLaunchKernelGGL(dtw_dist_kernel, dim3((unsigned)blocks), dim3(256), 0, s, q, nq, r, nr, dim, band, C);
-  const int64_t ntr = (nq + DTW_T - 1) / DTW_T, ntc = (nr + DTW_T - 1) / DTW_T;
-  for (int64_t d = 0; d < ntr + ntc - 1; ++d) {
-    const int64_t lo = d - (ntc - 1) > 0 ? d - (ntc - 1) : 0;
-    const int64_t hi = d < ntr - 1 ? d : ntr - 1;
-    const int64_t cnt = hi - lo + 1;
-    hipLaunchKernelGGL(dtw_wave_kernel, dim3((unsigned)cnt), dim3(64), 0, s, C, dir, nq, nr, band, d, ntr, ntc);
+// costMatrix[1:] row-major: block = one band x 64 columns, staged through LDS so
+// both the skewed reads and the row-major writes are coalesced.
+__global__ __launch_bounds__(256) void dtw_cost_rowmajor_kernel(const double* Cn, int64_t nq, int64_t nr, int64_t S,
+                                                                double* out) {
+  __shared__ double tile[64][65];
+  const int64_t b = blockIdx.y, j0 = 1 + (int64_t)blockIdx.x * 64;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int u = wv; u < 127; u += 4) {             // steps s = j0-1+u cover columns j0..j0+63 of every row
+    const int64_t s = j0 - 1 + u;
+    const int64_t col = u - lane;                  // j - j0
+    if (s < S && col >= 0 && col < 64) tile[lane][col] = Cn[((b * S + s) << 6) + lane];
   }
-  hipLaunchKernelGGL(dtw_backtrack_kernel, dim3(1), dim3(64), 0, s, dir, nq, nr, rev_q, rev_r, plen);
+  __syncthreads();
+  const int64_t pitch = nr + 1;
+  for (int rr = wv; rr < 64; rr += 4) {
+    const int64_t i = 64 * b + 1 + rr;
+    const int64_t j = j0 + lane;
+    if (i <= nq && j <= nr) out[(i - 1) * pitch + j] = tile[rr][lane];
+    if (i <= nq && blockIdx.x == 0 && lane == 0) out[(i - 1) * pitch] = __builtin_inf();
+  }
+}
+
+__global__ void nonfinite_kernel(const double* x, int64_t n, int32_t* flag) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+    if (!__builtin_isfinite(x[k])) *flag = 1;
+}
+
+DtwGeom dtw_geom(int64_t nq, int64_t nr) {
+  DtwGeom g;
+  g.nq = nq; g.nr = nr;
+  g.nb = (nq + 63) / 64;
+  g.S = nr + 63;
+  g.SW = (g.S + 15) / 16;
+  return g;
+}
+size_t dtw_cn_bytes(const DtwGeom& g) { return (size_t)g.nb * g.S * 64 * 8; }
+size_t dtw_dn_bytes(const DtwGeom& g) { return (size_t)g.nb * g.SW * 64 * 4; }
+size_t dtw_edge_bytes(const DtwGeom& g) { return (size_t)(g.nb > 1 ? g.nb - 1 : 1) * (g.nr + 1) * 8; }
+int64_t dtw_cn_index(const DtwGeom& g, int64_t i, int64_t j) {
+  const int64_t b = (i - 1) >> 6, l = (i - 1) & 63;
+  return ((b * g.S + (j - 1 + l)) << 6) + l;
+}
+
+int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, const DtwGeom& g, double* Cn,
+               uint32_t* Dn, uint64_t* E, int32_t* sync_words, int32_t* rev_q, int32_t* rev_r, int64_t* plen,
+               uint64_t* trace, hipStream_t s) {
+  if (hipMemsetAsync(sync_words, 0, 2 * sizeof(int32_t), s) != hipSuccess) return -5;
+  if (g.nb > 1 && hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, dtw_edge_bytes(g) / 4, s) != hipSuccess) return -5;
+  DtwArgs a{q, r, dim, band, g.nq, g.nr, g.nb, g.S, g.SW, Cn, Dn, reinterpret_cast<uint64_t*>(E), sync_words,
+            trace};
+  const dim3 grid((unsigned)g.nb), block(128);
+#define SONAR_DTW_LAUNCH(DD)                                                                          \
+  do {                                                                                                \
+    if (band > 0) {                                                                                   \
+      if (fast) hipLaunchKernelGGL((dtw_band_kernel<DD, true, true>), grid, block, 0, s, a);          \
+      else hipLaunchKernelGGL((dtw_band_kernel<DD, false, true>), grid, block, 0, s, a);              \
+    } else {                                                                                          \
+      if (fast) hipLaunchKernelGGL((dtw_band_kernel<DD, true, false>), grid, block, 0, s, a);         \
+      else hipLaunchKernelGGL((dtw_band_kernel<DD, false, false>), grid, block, 0, s, a);             \
+    }                                                                                                 \
+  } while (0)
+  if (dim == 12) SONAR_DTW_LAUNCH(12);
+  else if (dim == 1) SONAR_DTW_LAUNCH(1);
+  else SONAR_DTW_LAUNCH(0);
+#undef SONAR_DTW_LAUNCH
+  hipLaunchKernelGGL(dtw_walk_kernel, dim3(1), dim3(64), 0, s, Dn, g.nq, g.nr, g.SW, rev_q, rev_r, plen);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int launch_dtw_path_cost(const double* C, int64_t nr, const int32_t* rev_q, const int32_t* rev_r,
-                         const int64_t* /*plen_dev*/, int64_t P, int32_t* pq, int32_t* pr, double* pc,
-                         hipStream_t s) {
+int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const int32_t* rev_q, const int32_t* rev_r, int64_t P,
+                         int32_t* pq, int32_t* pr, double* pc, hipStream_t s) {
   if (P <= 0) return 0;
-  hipLaunchKernelGGL(dtw_path_cost_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, C, nr, rev_q, rev_r,
+  hipLaunchKernelGGL(dtw_path_cost_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, Cn, g.S, rev_q, rev_r,
                      P, pq, pr, pc);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_dtw_cost_rowmajor(const double* Cn, const DtwGeom& g, double* out, hipStream_t s) {
+  const dim3 grid((unsigned)((g.nr + 63) / 64), (unsigned)g.nb);
+  hipLaunchKernelGGL(dtw_cost_rowmajor_kernel, grid, dim3(256), 0, s, Cn, g.nq, g.nr, g.S, out);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s) {
+  if (n <= 0) return 0;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, n, flag);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -72,11 +72,30 @@ int launch_tilt(const double* y, int64_t n, int64_t frames, double* tilt, hipStr
 // NCC (align_kernels.hip)
 int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t L, double* norm_a,
                double* norm_b, double* stats, double* corr, hipStream_t s);
-// DTW (align_kernels.hip): cost holds (nq+1) x (nr+1) doubles
-int launch_dtw(const double* q, int64_t nq, const double* r, int64_t nr, int dim, int band, double* cost,
-               uint8_t* dir, int32_t* rev_q, int32_t* rev_r, int64_t* plen, hipStream_t s);
-int launch_dtw_path_cost(const double* cost, int64_t nr, const int32_t* rev_q, const int32_t* rev_r,
-                         const int64_t* plen_dev, int64_t plen, int32_t* pq, int32_t* pr, double* pc,
-                         hipStream_t s);
+// DTW (dtw.go:55-217).  Band-pipelined persistent kernel; see align_kernels.hip.
+struct DtwGeom {
+  int64_t nq, nr;   // sequence lengths
+  int64_t nb;       // 64-row bands = ceil(nq / 64)
+  int64_t S;        // sweep steps per band = nr + 63
+  int64_t SW;       // 16-step direction words per band = ceil(S / 16)
+};
+DtwGeom dtw_geom(int64_t nq, int64_t nr);
+// bytes of the band-skewed cost store Cn, direction store Dn and edge buffer E
+size_t dtw_cn_bytes(const DtwGeom& g);
+size_t dtw_dn_bytes(const DtwGeom& g);
+size_t dtw_edge_bytes(const DtwGeom& g);
+// offset (elements) of C[i][j] (1-based, i,j >= 1) inside Cn
+int64_t dtw_cn_index(const DtwGeom& g, int64_t i, int64_t j);
+// forward sweep + backtrack; `fast` = every input finite (no NaN path in math.Min)
+int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, const DtwGeom& g, double* Cn,
+               uint32_t* Dn, uint64_t* E, int32_t* sync_words /* [0] ticket, [1] error */, int32_t* rev_q,
+               int32_t* rev_r, int64_t* plen, uint64_t* trace /* nullable, [nb][4] diagnostics */,
+               hipStream_t s);
+int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const int32_t* rev_q, const int32_t* rev_r, int64_t P,
+                         int32_t* pq, int32_t* pr, double* pc, hipStream_t s);
+// costMatrix[1:] (nq x (nr+1), column 0 = +Inf) from the band-skewed store
+int launch_dtw_cost_rowmajor(const double* Cn, const DtwGeom& g, double* out, hipStream_t s);
+// sets *flag = 1 if any of the n values is not finite
+int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 
 }  // namespace sonar

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -496,21 +497,50 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
     HIP_TRY(c, hipMemcpyAsync(pr, r, nr * dim * 8, hipMemcpyHostToDevice, s));
     dq = pq; dr = pr;
   }
-  const size_t cells = (size_t)(nq + 1) * (size_t)(nr + 1);
-  double* C = (double*)dbuf(c, "dtw.C", cells * 8);
-  uint8_t* dir = (uint8_t*)dbuf(c, "dtw.dir", (size_t)nq * nr);
+  const sonar::DtwGeom g = sonar::dtw_geom(nq, nr);
+  double* Cn = (double*)dbuf(c, "dtw.Cn", sonar::dtw_cn_bytes(g));
+  uint32_t* Dn = (uint32_t*)dbuf(c, "dtw.Dn", sonar::dtw_dn_bytes(g));
+  uint64_t* E = (uint64_t*)dbuf(c, "dtw.E", sonar::dtw_edge_bytes(g));
+  int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", 16);
   const int64_t cap = nq + nr + 1;
   int32_t* rq = (int32_t*)dbuf(c, "dtw.rq", cap * 4);
   int32_t* rr = (int32_t*)dbuf(c, "dtw.rr", cap * 4);
   int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
-  if (!C || !dir || !rq || !rr || !pl) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (cost matrix)");
+  if (!Cn || !Dn || !E || !sync || !rq || !rr || !pl)
+    return fail(c, SONAR_ERR_NOMEM, "device allocation failed (cost matrix)");
+  // math.Min's NaN / -Inf / -0 rules only matter when an input is not finite
+  bool fast = true;
+  if (!device_ptrs) {
+    for (int64_t k = 0; k < nq * dim && fast; ++k) fast = std::isfinite(q[k]);
+    for (int64_t k = 0; k < nr * dim && fast; ++k) fast = std::isfinite(r[k]);
+  } else {
+    HIP_TRY(c, hipMemsetAsync(sync + 2, 0, 4, s));
+    if (sonar::launch_nonfinite(dq, nq * dim, sync + 2, s) || sonar::launch_nonfinite(dr, nr * dim, sync + 2, s))
+      return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
+    int32_t nf = 0;
+    HIP_TRY(c, hipMemcpyAsync(&nf, sync + 2, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    fast = nf == 0;
+  }
+  // SONAR_DTW_TRACE=<file>: per-band timestamps of the sweep (diagnostics only)
+  const char* trace_path = std::getenv("SONAR_DTW_TRACE");
+  uint64_t* trace = trace_path ? (uint64_t*)dbuf(c, "dtw.trace", (size_t)g.nb * 32) : nullptr;
   hipEvent_t tend = timed_begin(c, s);
-  if (sonar::launch_dtw(dq, nq, dr, nr, dim, band, C, dir, rq, rr, pl, s) != 0)
+  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, rq, rr, pl, trace, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
   timed_end(c, s, tend);
+  if (trace) {
+    std::vector<uint64_t> t((size_t)g.nb * 4);
+    HIP_TRY(c, hipMemcpyAsync(t.data(), trace, t.size() * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if (FILE* f = std::fopen(trace_path, "wb")) { std::fwrite(t.data(), 8, t.size(), f); std::fclose(f); }
+  }
   int64_t P = 0;
+  int32_t flags[2] = {0, 0};
   HIP_TRY(c, hipMemcpyAsync(&P, pl, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(flags, sync, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
+  if (flags[1]) return fail(c, SONAR_ERR_DEVICE, "dtw band pipeline timed out");
   int32_t* oq = path_q; int32_t* orr = path_r; double* oc = path_cost;
   if (!device_ptrs) {
     oq = (int32_t*)dbuf(c, "dtw.pq", cap * 4);
@@ -518,17 +548,22 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
     oc = (double*)dbuf(c, "dtw.pc", cap * 8);
     if (!oq || !orr || !oc) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (path)");
   }
-  if (sonar::launch_dtw_path_cost(C, nr, rq, rr, pl, P, oq, orr, oc, s) != 0)
+  if (sonar::launch_dtw_path_cost(Cn, g, rq, rr, P, oq, orr, oc, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw path launch failed");
   double cNM = 0;
-  HIP_TRY(c, hipMemcpyAsync(&cNM, C + (size_t)nq * (nr + 1) + nr, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(&cNM, Cn + sonar::dtw_cn_index(g, nq, nr), 8, hipMemcpyDeviceToHost, s));
+  double* cost_dev = cost;
+  if (cost && !device_ptrs) {
+    cost_dev = (double*)dbuf(c, "dtw.cost", (size_t)nq * (nr + 1) * 8);
+    if (!cost_dev) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (cost output)");
+  }
+  if (cost && sonar::launch_dtw_cost_rowmajor(Cn, g, cost_dev, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "dtw cost launch failed");
   if (!device_ptrs) {
     if (path_q) HIP_TRY(c, hipMemcpyAsync(path_q, oq, P * 4, hipMemcpyDeviceToHost, s));
     if (path_r) HIP_TRY(c, hipMemcpyAsync(path_r, orr, P * 4, hipMemcpyDeviceToHost, s));
     if (path_cost) HIP_TRY(c, hipMemcpyAsync(path_cost, oc, P * 8, hipMemcpyDeviceToHost, s));
-    if (cost) HIP_TRY(c, hipMemcpyAsync(cost, C + (nr + 1), (size_t)nq * (nr + 1) * 8, hipMemcpyDeviceToHost, s));
-  } else if (cost) {
-    HIP_TRY(c, hipMemcpyAsync(cost, C + (nr + 1), (size_t)nq * (nr + 1) * 8, hipMemcpyDeviceToDevice, s));
+    if (cost) HIP_TRY(c, hipMemcpyAsync(cost, cost_dev, (size_t)nq * (nr + 1) * 8, hipMemcpyDeviceToHost, s));
   }
   HIP_TRY(c, hipStreamSynchronize(s));
   if (path_len) *path_len = P;

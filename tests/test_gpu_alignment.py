@@ -34,7 +34,8 @@ def test_ncc_errors(ctx):
 
 @pytest.mark.parametrize("nq,nr,dim,band", [(100, 120, 12, -1), (257, 130, 1, -1), (64, 64, 12, -1),
                                            (300, 280, 3, 40), (1, 1, 2, -1), (1, 70, 1, -1), (130, 1, 4, -1),
-                                           (500, 499, 12, 5)])
+                                           (500, 499, 12, 5), (2000, 1500, 12, -1), (193, 2500, 12, 300),
+                                           (700, 650, 5, -1), (129, 128, 1, 2)])
 def test_dtw_matches_oracle(ctx, nq, nr, dim, band):
     rng = np.random.default_rng(nq * 7 + nr)
     q = rng.random((nq, dim))
@@ -43,7 +44,7 @@ def test_dtw_matches_oracle(ctx, nq, nr, dim, band):
     ref = O.dtw(q, r, band=band, want_cost=True)
     assert np.array_equal(got["path_q"], ref["path_q"]) and np.array_equal(got["path_r"], ref["path_r"])
     assert np.array_equal(got["cost"], ref["cost"])
-    assert np.array_equal(got["path_cost"], ref["path_cost"])
+    assert np.array_equal(got["path_cost"], ref["path_cost"], equal_nan=True)   # Inf - Inf off the band
     assert got["distance"] == ref["distance"]
 
 
@@ -58,3 +59,31 @@ def test_dtw_ties_identical_sequences(ctx):
 def test_dtw_errors(ctx):
     with pytest.raises(sonar.SonarError, match="empty sequences provided"):
         ctx.dtw(np.zeros((0, 2)), np.ones((3, 2)))
+
+
+def test_dtw_nonfinite_inputs(ctx):
+    """NaN / Inf inputs take the math.Min path with Go's NaN / -Inf / -0 rules."""
+    rng = np.random.default_rng(5)
+    q = rng.random((150, 12))
+    r = rng.random((140, 12))
+    q[20, 3] = np.nan
+    r[77, 0] = np.inf
+    q[90, 5] = -np.inf
+    got = ctx.dtw(q, r, want_cost=True)
+    ref = O.dtw(q, r, want_cost=True)
+    assert np.array_equal(got["path_q"], ref["path_q"]) and np.array_equal(got["path_r"], ref["path_r"])
+    assert np.array_equal(got["cost"], ref["cost"], equal_nan=True)
+    assert np.array_equal(got["path_cost"], ref["path_cost"], equal_nan=True)
+
+
+def test_dtw_large_band_pipeline(ctx):
+    """126 bands in flight: the sc1 edge hand-off between bands under full occupancy."""
+    rng = np.random.default_rng(11)
+    n = 8000
+    q = rng.random((n, 12))
+    r = np.roll(q, 23, axis=0) + 0.05 * rng.random((n, 12))
+    got = ctx.dtw(q, r)
+    ref = O.dtw(q, r)
+    assert np.array_equal(got["path_q"], ref["path_q"]) and np.array_equal(got["path_r"], ref["path_r"])
+    assert np.array_equal(got["path_cost"], ref["path_cost"])
+    assert got["distance"] == ref["distance"]
