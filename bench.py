@@ -4,10 +4,11 @@
 Headline: audio frames/sec of the fused STFT -> mel(40) -> MFCC(13) kernel
 (W=1024, H=256, 44.1 kHz, float32) on 1 h of synthetic PCM per GPU, PCM
 resident in HBM when timing starts.  Multi-GPU (torchrun, one process per
-GPU): every rank fingerprints its own 1 h stream (frames shard with no
-data-path collective -> "scaling": "weak"); the RCCL all-gather that
-reassembles the feature timeline runs once after the timed region and is
-reported separately.  Extra fields: DTW cells/sec (C3 size, float64, cost
+GPU): one stream of N hours is sharded by STFT frames (sonar/shard.py) --
+rank g holds its frames' samples plus the 768-sample halo, generated on its
+own device by sample index -- with no data-path collective ("scaling":
+"weak", 1 h per GPU); the RCCL all-gather that reassembles the feature
+timeline runs once after the timed region and is reported separately.  Extra fields: DTW cells/sec (C3 size, float64, cost
 matrix in HBM), roofline of the dominant kernel, CPU baseline (the oracle,
 a float64 C restatement of the Go path, on a bounded sample).
 
@@ -30,7 +31,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import sonar  # noqa: E402
-from sonar import synth  # noqa: E402
+from sonar import shard  # noqa: E402
 
 W, H, SR, N_MELS, N_MFCC = 1024, 256, 44100, 40, 13
 BYTES_PER_FRAME = 4 * H + 4 * N_MFCC            # PCM in (hop, f32) + MFCC out (f32)
@@ -77,16 +78,15 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def make_pcm(seconds, rank, device):
-    """C2 recipe on the device: the 10 s sweep tiled + 0.05 N(0,1), float32."""
-    n = int(round(seconds * SR))
-    base = torch.tensor(synth.sweep(10.0), dtype=torch.float32, device=device)
-    reps = math.ceil(n / base.numel())
-    pcm = base.repeat(reps)[:n].contiguous()
-    g = torch.Generator(device=device)
-    g.manual_seed(1234 + rank)
-    pcm.add_(0.05 * torch.randn(n, generator=g, device=device, dtype=torch.float32))
-    return pcm
+def make_shard(seconds, world, rank, device):
+    """This rank's frames of the world x `seconds` stream and the samples they read."""
+    n_total = world * int(round(seconds * SR))
+    F_total = shard.stft_frames(n_total, W, H)
+    f0, f1 = shard.frame_range(F_total, world, rank)
+    s0, s1 = shard.sample_span(f0, f1, W, H)
+    pcm = shard.stream_pcm(s0, s1, device=device)
+    counts = [b - a for a, b in (shard.frame_range(F_total, world, g) for g in range(world))]
+    return pcm, F_total, f1 - f0, counts
 
 
 def load_traffic():
@@ -105,19 +105,19 @@ def cpu_baseline(seconds_hint):
     threads = os.cpu_count() or 1
     threads = min(threads, 16)      # the GPU box shares its CPUs: 16 is this job's share
     probe = 60.0
-    x = synth.c2_hour(seconds=probe).astype(np.float64)
+    x = shard.stream_pcm(0, int(probe * SR)).double().numpy()
     t0 = time.perf_counter()
     m = O.stft_mag(x, W, H, nthreads=threads)
     O.mfcc_frames(m, SR, n_coef=N_MFCC, n_mels=N_MELS)
     dt = time.perf_counter() - t0
     secs = seconds_hint or min(3600.0, max(probe, probe * 15.0 / max(dt, 1e-6)))   # ~15 s of CPU work
-    x = synth.c2_hour(seconds=secs).astype(np.float64)
+    x = shard.stream_pcm(0, int(secs * SR)).double().numpy()
     t0 = time.perf_counter()
     m = O.stft_mag(x, W, H, nthreads=threads)
     O.mfcc_frames(m, SR, n_coef=N_MFCC, n_mels=N_MELS)
     dt = time.perf_counter() - t0
     return {"value": len(m) / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{secs:.0f} s of the C2 signal ({len(m)} frames), float64: STFT over {threads} threads "
+            "sample": f"{secs:.0f} s of the bench stream ({len(m)} frames), float64: STFT over {threads} threads "
                       "(Go worker-pool shape), MFCC.ComputeFrames single-threaded, as in the Go path"}
 
 
@@ -140,9 +140,9 @@ def main():
     args = parse()
     world, rank, local = dist_setup()
     dev = torch.device("cuda", local)
-    pcm = make_pcm(args.seconds, rank, dev)
+    pcm, F_total, F, counts = make_shard(args.seconds, world, rank, dev)
     n = pcm.numel()
-    F = sonar.stft_frames(n, W, H)
+    assert sonar.stft_frames(n, W, H) == F
     out = torch.empty((F, N_MFCC), dtype=torch.float32, device=dev)
     ctx = sonar.Context(local)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
@@ -169,20 +169,21 @@ def main():
     kernel_ms = ctx.last_kernel_ms()
     elapsed = max_over_ranks(elapsed, world)
     ms_per_step = elapsed / args.steps * 1e3
-    value = F * world / (elapsed / args.steps)
+    value = F_total / (elapsed / args.steps)
 
-    # RCCL all-gather of the MFCC timeline (reassembly of the N-stream feature
-    # timeline over xGMI), once, outside the timed region
+    # RCCL all-gather of the MFCC timeline (reassembly of the frame-sharded stream
+    # over xGMI), once, outside the timed region
     gather_ms = None
     if world > 1:
-        parts = [torch.empty_like(out) for _ in range(world)]
         torch.cuda.synchronize()
         barrier(world)
         tg = time.perf_counter()
-        torch.distributed.all_gather(parts, out)
+        timeline = shard.gather_rows(out, world, counts)
         torch.cuda.synchronize()
         gather_ms = max_over_ranks((time.perf_counter() - tg) * 1e3, world)
-        assert torch.equal(parts[rank], out)
+        assert timeline.shape == (F_total, N_MFCC)
+        f0 = sum(counts[:rank])
+        assert torch.equal(timeline[f0:f0 + F], out)
 
     extra = {}
     if args.dtw_len > 0:
@@ -206,10 +207,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (C2: 10 s 100 Hz-10 kHz sweep tiled + 0.05 N(0,1), seeded per rank)",
+        "data": "synthetic C2-shaped stream (10 s 100 Hz-10 kHz sweep repeated + 0.05 N(0,1) from a "
+                "counter hash), N x 1 h, frame-sharded with halo",
         "config": {"workload": "STFT(W=1024,H=256,Hann)->mel(40)->ln->DCT-II(13)->lifter(22) on 1 h of "
-                               "44.1 kHz float32 PCM per GPU", "frames_per_gpu": F, "samples_per_gpu": n,
-                   "parallelism": f"frame-shard x{world}"},
+                               "44.1 kHz float32 PCM per GPU", "frames_total": F_total, "frames_rank0": F,
+                   "samples_rank0": n, "parallelism": f"frame-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS,
                      "traffic": traffic, "kernel": "fp_wave_kernel<float,float,8,false>", "kernel_ms": kernel_ms,
@@ -220,7 +222,7 @@ def main():
     }
     if gather_ms is not None:
         line["allgather_ms"] = gather_ms
-        line["allgather_bytes_per_rank"] = out.numel() * 4 * world
+        line["allgather_bytes"] = F_total * N_MFCC * 4
     line.update(extra)
     if rank == 0:
         print(json.dumps(line), flush=True)

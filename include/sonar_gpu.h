@@ -23,6 +23,9 @@
  *   sonar_ncc                  <- CrossCorrelation.Compute, NormalizedCrossCorrelation /
  *                                 TimeDomain (algorithms/stats/correlation.go:131)
  *   sonar_dtw                  <- DTWAlignment.Align (algorithms/stats/dtw.go:55)
+ *   sonar_formants             <- FormantAnalyzer.AnalyzeMultipleFrames / AnalyzeFormants
+ *                                 (algorithms/speech/format.go:85-449) over LPCAnalyzer.Analyze
+ *                                 (algorithms/speech/lpc.go:44-265)
  *   sonar_generate_fingerprint <- FingerprintGenerator.GenerateFingerprint
  *                                 (fingerprint/fingerprint.go:137)
  *   sonar_extract_speech_features <- SpeechFeatureExtractor.ExtractFeatures
@@ -179,6 +182,34 @@ int sonar_ncc(sonar_ctx* ctx, const double* a, int64_t na, const double* b, int6
 int sonar_dtw(sonar_ctx* ctx, const double* q, int64_t nq, const double* r, int64_t nr, int32_t dim,
               int32_t band, double* distance, int32_t* path_q, int32_t* path_r, double* path_cost,
               int64_t* path_len, double* cost, int32_t device_ptrs);
+
+/* ---- LPC formants: FormantAnalyzer.AnalyzeMultipleFrames (algorithms/speech/format.go:427-449)
+ * over FormantAnalyzer.AnalyzeFormants (:85-124) + LPCAnalyzer.Analyze (lpc.go:44-82).
+ * Analysis window W = 2048 if sample_rate >= 16000 else 1024, LPC order 12 + sr/1000,
+ * pre-emphasis 0.97, symmetric Hamming (format.go:48-69).  Frames start at 0, hop, ...
+ * while start < n - frame_size (frame_size <= 0 -> W, hop <= 0 -> frame_size/2).  Every
+ * attempted frame gets a record; status != 0 marks the frames Go skips. ------------ */
+typedef struct {
+  int32_t status;          /* 0 ok; 1 frame shorter than W; 3 "zero energy signal";
+                              4 "prediction error energy became zero" (lpc.go:93-113)   */
+  int32_t n_formants;      /* validated formants, <= 4 (ascending frequency)            */
+  double frequency[4];
+  double bandwidth[4];
+  double amplitude[4];
+  double confidence[4];
+  double vocal_tract_length;   /* cm, 17.5 when no formant qualifies                    */
+  double quality;              /* calculateAnalysisQuality                               */
+  double gain;                 /* sqrt(residual energy)                                  */
+  double residual_energy;
+  int32_t stable;              /* checkStability: every |a_i| < 1                        */
+  int32_t lpc_order;
+} sonar_formant_frame;
+
+int64_t sonar_formant_frame_count(int64_t n, int32_t sample_rate, int32_t frame_size, int32_t hop_size);
+/* lpc_coeffs (nullable): frames x (order+1) a[0..p], a[0] = 1; reflection (nullable): frames x order */
+int sonar_formants(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate, int32_t frame_size,
+                   int32_t hop_size, sonar_formant_frame* out, double* lpc_coeffs, double* reflection,
+                   int32_t device_ptrs);
 
 /* ---- host mirror of the Go API (C++ above the kernels) ------------------ */
 typedef struct sonar_result sonar_result;   /* named float64 arrays + scalars */

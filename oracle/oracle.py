@@ -62,6 +62,10 @@ def lib():
         L.or_dtw.argtypes = [_d, C.c_int64, _d, C.c_int64, C.c_int, C.c_int, _d, _i32, _i32, _d, _i64, _d]
         L.or_align_dtw_metrics.argtypes = [_i32, _i32, _d, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_int, _d]
         L.or_align_xcorr_metrics.argtypes = [_d, C.c_int, C.c_int, C.c_int, _d]
+        L.or_autocorr_fft.argtypes = [_d, C.c_int, C.c_int, _d]
+        L.or_formant_frame.argtypes = [_d, C.c_int64, C.c_int, _d, _d, _d]
+        L.or_formant_frames.argtypes = [_d, C.c_int64, C.c_int, C.c_int, C.c_int, _d, _d, _d]
+        L.or_formant_frames.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -348,6 +352,26 @@ def speech_features_reference(pcm, sample_rate, fc):
                 mc /= en
             sp = mc > 0.1 and len(pre) >= 1024
         out["is_speech"] = 1.0 if sp else 0.0
+        fq, vtl = np.zeros((0, 0)), 17.5                     # speech.go:279-303
+        if sp:
+            fm = formant_frame(pre, csr)
+            if fm["status"][0] == 0:
+                nv = int(fm["n_formants"][0])
+                fq = fm["frequency"][0][:nv].reshape(1, nv) if nv else np.zeros((0, 0))
+                vtl = float(fm["vocal_tract_length"][0])
+        out["formant_frequencies"], out["vocal_tract_length"] = fq, vtl
+        if sp:                                               # estimateSpeechRate (speech.go:779-797)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                dur = np.float64(len(pre)) / np.float64(csr)     # IEEE like Go: sr 0 -> +Inf
+            sil = 0.0
+            if len(ste):
+                thr = np.sort(ste)[len(ste) // 10]
+                sil = np.count_nonzero(ste <= thr) / len(ste)
+            with np.errstate(invalid="ignore"):
+                st = dur * (1.0 - sil)
+                out["speech_rate"] = float(4.0 * st / dur) if st > 0 else 3.0
+        else:
+            out["speech_rate"] = 0.0
         if sp:
             vo = np.zeros(Fp)
             for i, r in enumerate(raw):
@@ -401,4 +425,56 @@ def align_features_reference(qe, re_, qc, rc, q_pcm_len, r_pcm_len, sample_rate,
         out["offset_confidence"] = best[2]["confidence"]
         out["alignment_similarity"] = best[2]["similarity"]
         out["alignment_quality"] = best[2]["quality"]
+    return out
+
+
+FORMANT_KEYS = ("status", "n_formants", "frequency", "bandwidth", "amplitude", "confidence",
+                "vocal_tract_length", "quality", "gain", "residual_energy", "stable")
+
+
+def _formant_recs(recs):
+    recs = np.atleast_2d(recs)
+    return {"status": recs[:, 0].astype(np.int32), "n_formants": recs[:, 1].astype(np.int32),
+            "frequency": recs[:, 2:6], "bandwidth": recs[:, 6:10], "amplitude": recs[:, 10:14],
+            "confidence": recs[:, 14:18], "vocal_tract_length": recs[:, 18], "quality": recs[:, 19],
+            "gain": recs[:, 20], "residual_energy": recs[:, 21], "stable": recs[:, 22].astype(np.int32)}
+
+
+def formant_frames(pcm, sample_rate, frame_size=0, hop_size=0, want_lpc=False):
+    """FormantAnalyzer.AnalyzeMultipleFrames (format.go:427-449): one record per attempted frame."""
+    pcm = _f64(pcm)
+    W = 2048 if sample_rate >= 16000 else 1024
+    p = 12 + sample_rate // 1000
+    fs = frame_size if frame_size > 0 else W
+    hp = hop_size if hop_size > 0 else fs // 2
+    F = (len(pcm) - fs - 1) // hp + 1 if len(pcm) > fs else 0
+    recs = np.zeros((max(F, 1), 24))
+    co = np.zeros((max(F, 1), p + 1))
+    rf = np.zeros((max(F, 1), p))
+    lib().or_formant_frames(_p(pcm), len(pcm), sample_rate, frame_size, hop_size, _p(recs), _p(co), _p(rf))
+    out = _formant_recs(recs[:F])
+    if want_lpc:
+        out["lpc_coeffs"], out["reflection"] = co[:F], rf[:F]
+    return out
+
+
+def formant_frame(sig, sample_rate):
+    """FormantAnalyzer.AnalyzeFormants on one signal (format.go:85-124)."""
+    sig = _f64(sig)
+    p = 12 + sample_rate // 1000
+    rec = np.zeros(24)
+    co = np.zeros(p + 1)
+    rf = np.zeros(p)
+    lib().or_formant_frame(_p(sig), len(sig), sample_rate, _p(rec), _p(co), _p(rf))
+    out = _formant_recs(rec)
+    out["lpc_coeffs"], out["reflection"] = co, rf
+    return out
+
+
+def autocorr_fft(x, max_lag):
+    """AutoCorrelation(maxLag).Compute correlations on the FFT path (lags -L..L)."""
+    x = _f64(x)
+    L = max(0, min(max_lag, len(x) - 1))
+    out = np.zeros(2 * L + 1)
+    lib().or_autocorr_fft(_p(x), len(x), max_lag, _p(out))
     return out

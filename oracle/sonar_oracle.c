@@ -870,3 +870,209 @@ void or_align_xcorr_metrics(const double* m, int hop, int sr, int max_lag, doubl
     out[0] = (double)off; out[1] = (double)off / (double)sr; out[2] = sim; out[3] = conf;
     out[4] = qual; out[5] = 1.0 - snr / 20.0;
 }
+
+/* ======================================================== LPC / formants ====
+ * FormantAnalyzer.AnalyzeFormants (algorithms/speech/format.go:85-124) with
+ * LPCAnalyzer.Analyze (algorithms/speech/lpc.go:44-82).  The autocorrelation
+ * is AutoCorrelation(1024) = CrossCorrelation{maxLag 1024, useFFT, threshold
+ * 1000}.Compute(x, x) (stats/correlation.go:103-114, 131-200, 231-297): the
+ * z-scored frame, nextPowerOf2(2n-1)-point recursive radix-2 FFT (:726-774),
+ * |X|^2 via Go's complex multiply, conj-FFT-conj inverse.  R = Correlations[:p+1]
+ * i.e. lags -L .. -L+p (F11). */
+
+static void go_rec_fft(double* re, double* im, int n) {           /* correlation.go:727-755 */
+  if (n <= 1) return;
+  const int h = n / 2;
+  double* er = (double*)malloc(sizeof(double) * 4 * h);
+  double *ei = er + h, *odr = er + 2 * h, *odi = er + 3 * h;
+  for (int i = 0; i < h; i++) { er[i] = re[2 * i]; ei[i] = im[2 * i]; odr[i] = re[2 * i + 1]; odi[i] = im[2 * i + 1]; }
+  go_rec_fft(er, ei, h);
+  go_rec_fft(odr, odi, h);
+  for (int i = 0; i < h; i++) {
+    const double th = -2.0 * M_PI * (double)i / (double)n;
+    const double c = cos(th), s = sin(th);                        /* cmplx.Exp(0 + i*th) = (cos, sin) */
+    const double tr = c * odr[i] - s * odi[i], ti = c * odi[i] + s * odr[i];
+    re[i] = er[i] + tr; im[i] = ei[i] + ti;
+    re[i + h] = er[i] - tr; im[i + h] = ei[i] - ti;
+  }
+  free(er);
+}
+
+/* Correlations of AutoCorrelation(maxLag).Compute on the FFT path; fills corr[0..2L] */
+int or_autocorr_fft(const double* x, int n, int max_lag, double* corr) {
+  double mean = 0.0;                                               /* normalize :464-501 */
+  for (int i = 0; i < n; i++) mean += x[i];
+  mean /= (double)n;
+  double var = 0.0;
+  for (int i = 0; i < n; i++) { const double d = x[i] - mean; var += d * d; }
+  var /= (double)n;
+  const double sd = sqrt(var);
+  int N = 1;
+  while (N < 2 * n - 1) N <<= 1;                                   /* nextPowerOf2 */
+  double* re = (double*)calloc((size_t)4 * N, sizeof(double));
+  double *im = re + N, *re2 = re + 2 * N, *im2 = re + 3 * N;
+  for (int i = 0; i < n; i++) re[i] = sd < 1e-10 ? x[i] - mean : (x[i] - mean) / sd;
+  memcpy(re2, re, sizeof(double) * N);
+  go_rec_fft(re, im, N);
+  go_rec_fft(re2, im2, N);
+  for (int i = 0; i < N; i++) {                                    /* fft1 * conj(fft2), then conj for ifft */
+    const double a = re[i], b = im[i], c = re2[i], d = -im2[i];
+    re[i] = a * c - b * d;
+    im[i] = -(a * d + b * c);
+  }
+  go_rec_fft(re, im, N);
+  int L = max_lag < n - 1 ? max_lag : n - 1;
+  if (L < 0) L = 0;
+  for (int k = 0; k <= 2 * L; k++) {
+    const int lag = k - L;
+    const int idx = lag >= 0 ? lag : N + lag;
+    corr[k] = re[idx] / (double)N;                                 /* real(conj(y) / N) */
+  }
+  free(re);
+  return L;
+}
+
+static void go_envelope(const double* a, int p, int nfft, double* env) {   /* lpc.go:233-265 */
+  for (int k = 0; k <= nfft / 2; k++) {
+    const double w = 2.0 * M_PI * (double)k / (double)nfft;
+    double rp = 1.0, ip = 0.0;
+    for (int i = 1; i <= p; i++) {
+      const double ang = -(double)i * w;
+      rp += a[i] * cos(ang);
+      ip += a[i] * sin(ang);
+    }
+    const double m = sqrt(rp * rp + ip * ip);
+    env[k] = m > 0 ? 1.0 / m : 0.0;
+  }
+}
+
+/* rec[24]: status, n_formants, freq[4], bw[4], amp[4], conf[4], vtl, quality, gain,
+ * residual_energy, stable, order.  status: 0 ok, 1 too short, 2 LPC too short,
+ * 3 zero energy, 4 prediction error became zero. */
+int or_formant_frame(const double* sig, int64_t len, int sr, double* rec, double* coeffs, double* refl) {
+  const int W = sr >= 16000 ? 2048 : 1024;                         /* NewFormantAnalyzer format.go:48-69 */
+  const int p = 12 + sr / 1000;
+  memset(rec, 0, sizeof(double) * 24);
+  rec[23] = p;
+  if (len < W) { rec[0] = 1; return 1; }
+  double* x = (double*)malloc(sizeof(double) * W);                 /* preprocessSignal :127-146 */
+  x[0] = sig[0];
+  for (int i = 1; i < W; i++) x[i] = sig[i] - 0.97 * sig[i - 1];
+  for (int i = 0; i < W; i++) x[i] *= 0.54 - 0.46 * cos(2.0 * M_PI * (double)i / (double)(W - 1));
+  if (W < 2 * p) { free(x); rec[0] = 2; return 2; }                /* lpc.go:45-47 */
+  double* corr = (double*)malloc(sizeof(double) * (2 * 1024 + 1));
+  or_autocorr_fft(x, W, 1024, corr);
+  double R[128];
+  for (int i = 0; i <= p; i++) R[i] = corr[i];                     /* F11 */
+  free(corr);
+  free(x);
+  if (R[0] == 0) { rec[0] = 3; return 3; }
+  double a[128] = {0}, k[128] = {0};                               /* levinsonDurbin lpc.go:85-135 */
+  double E = R[0];
+  a[0] = 1.0;
+  for (int i = 1; i <= p; i++) {
+    double num = R[i];
+    for (int j = 1; j < i; j++) num -= a[j] * R[i - j];
+    if (E == 0) { rec[0] = 4; return 4; }
+    k[i - 1] = num / E;
+    a[i] = k[i - 1];
+    for (int j = 1; j < i; j++) a[j] = a[j] - k[i - 1] * a[i - j];   /* in place, as written */
+    E *= (1 - k[i - 1] * k[i - 1]);
+    if (E <= 0) break;
+  }
+  const double gain = sqrt(E);
+  int stable = 1;                                                  /* checkStability :155-166 */
+  for (int i = 1; i <= p; i++) if (fabs(a[i]) >= 1.0) stable = 0;
+  if (coeffs) memcpy(coeffs, a, sizeof(double) * (p + 1));
+  if (refl) memcpy(refl, k, sizeof(double) * p);
+
+  double env[513];                                                 /* findFormantsFromLPC format.go:148-190 */
+  go_envelope(a, p, 1024, env);
+  const double res = (double)sr / 1024.0;
+  double maxv = 0.0;
+  for (int i = 0; i < 513; i++) if (env[i] > maxv) maxv = env[i];
+  double fq[513], bw[513], am[513], cf[513];
+  int nf = 0;
+  if (maxv != 0) {
+    for (int i = 1; i < 512; i++) {                                /* findSpectralPeaks :193-222 */
+      if (!(env[i] > env[i - 1] && env[i] > env[i + 1])) continue;
+      if (!(env[i] / maxv > 0.1)) continue;
+      const double f = (double)i * res;
+      if (f < 50.0 || f > (double)sr / 2.0) continue;
+      const double hh = env[i] / 2.0;                              /* estimateFormantBandwidth :225-262 */
+      int li = i, ri = i;
+      for (int t = i - 1; t >= 0; t--) if (env[t] <= hh) { li = t; break; }
+      for (int t = i + 1; t < 513; t++) if (env[t] <= hh) { ri = t; break; }
+      double b = (double)(ri - li) * res;
+      if (b < 50.0) b = 50.0; else if (b > 500.0) b = 500.0;
+      double c = 1.0;                                              /* calculateFormantConfidence :265-289 */
+      if (f >= 300 && f <= 3500) c *= 1.0;
+      else if (f >= 100 && f <= 5000) c *= 0.7;
+      else c *= 0.3;
+      c *= go_min(env[i], 1.0);
+      if (b >= 50 && b <= 300) c *= 1.0;
+      else if (b >= 30 && b <= 500) c *= 0.8;
+      else c *= 0.5;
+      c = go_max(0.0, go_min(1.0, c));
+      fq[nf] = f; bw[nf] = b; am[nf] = env[i]; cf[nf] = c; nf++;
+    }
+  }
+  if (nf > 4) nf = 4;                                              /* already ascending; maxFormants */
+  double vf[4], vb[4], va[4], vc[4];                               /* validateFormants :292-315 */
+  int nv = 0;
+  for (int i = 0; i < nf; i++) {
+    if (fq[i] < 50.0 || fq[i] > (double)sr / 2.0) continue;
+    if (cf[i] < 0.2) continue;
+    if (bw[i] <= 0 || bw[i] > 1000) continue;
+    vf[nv] = fq[i]; vb[nv] = bw[i]; va[nv] = am[i]; vc[nv] = cf[i]; nv++;
+  }
+  if (nv > 1) {                                                    /* ensureProperSpacing :318-343 */
+    int ns = 1;
+    for (int i = 1; i < nv; i++) {
+      if (vf[i] - vf[ns - 1] >= 200.0) { vf[ns] = vf[i]; vb[ns] = vb[i]; va[ns] = va[i]; vc[ns] = vc[i]; ns++; }
+      else if (vc[i] > vc[ns - 1]) { vf[ns - 1] = vf[i]; vb[ns - 1] = vb[i]; va[ns - 1] = va[i]; vc[ns - 1] = vc[i]; }
+    }
+    nv = ns;
+  }
+  double vtl = 17.5;                                               /* estimateVocalTractLength :346-377 */
+  if (nv > 0) {
+    double tot = 0.0;
+    int cnt = 0;
+    for (int i = 0; i < nv; i++) {
+      if (vf[i] > 0 && vc[i] > 0.3) {
+        const double v = (2.0 * (i + 1) - 1.0) * 35000.0 / (4.0 * vf[i]);
+        if (v >= 10.0 && v <= 25.0) { tot += v; cnt++; }
+      }
+    }
+    if (cnt > 0) vtl = tot / (double)cnt;
+  }
+  double quality = 0.0;                                            /* calculateAnalysisQuality :380-411 */
+  if (nv > 0) {
+    const double q1 = go_min((double)nv / 3.0, 1.0);
+    double ac = 0.0;
+    for (int i = 0; i < nv; i++) ac += vc[i];
+    ac /= (double)nv;
+    double lq = 1.0;
+    if (E > 0) lq = go_max(0.0, 1.0 - go_min(1.0, E));
+    quality = (q1 + ac + lq + (stable ? 1.0 : 0.0)) / 4.0;
+  }
+  rec[0] = 0; rec[1] = nv;
+  for (int i = 0; i < nv; i++) { rec[2 + i] = vf[i]; rec[6 + i] = vb[i]; rec[10 + i] = va[i]; rec[14 + i] = vc[i]; }
+  rec[18] = vtl; rec[19] = quality; rec[20] = gain; rec[21] = E; rec[22] = stable;
+  return 0;
+}
+
+/* AnalyzeMultipleFrames (format.go:427-449): frames i = 0, hop, ... while i < n - frame_size;
+ * every attempted frame gets a record (status != 0 frames are the ones Go skips). */
+int64_t or_formant_frames(const double* sig, int64_t n, int sr, int frame_size, int hop, double* recs,
+                          double* coeffs, double* refl) {
+  const int W = sr >= 16000 ? 2048 : 1024;
+  const int p = 12 + sr / 1000;
+  if (frame_size <= 0) frame_size = W;
+  if (hop <= 0) hop = frame_size / 2;
+  int64_t f = 0;
+  for (int64_t i = 0; i < n - frame_size; i += hop, f++)
+    or_formant_frame(sig + i, frame_size, sr, recs + 24 * f, coeffs ? coeffs + (p + 1) * f : NULL,
+                     refl ? refl + p * f : NULL);
+  return f;
+}

@@ -57,6 +57,10 @@ int    or_dtw(const double* q, int64_t nq, const double* r, int64_t nr, int dim,
 void   or_align_dtw_metrics(const int32_t* pq, const int32_t* pr, const double* pc, int64_t P,
                             int64_t nq, int64_t nr, double dist, int sample_rate, double* out);
 void   or_align_xcorr_metrics(const double* metrics, int hop, int sample_rate, int max_lag, double* out);
+int    or_autocorr_fft(const double* x, int n, int max_lag, double* corr);
+int    or_formant_frame(const double* sig, int64_t len, int sample_rate, double* rec24, double* coeffs, double* refl);
+int64_t or_formant_frames(const double* sig, int64_t n, int sample_rate, int frame_size, int hop, double* recs,
+                          double* coeffs, double* refl);
 
 #ifdef __cplusplus
 }

@@ -118,7 +118,6 @@ int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t
 //   Dn[b][w][l]  2-bit findPreviousStep codes (dtw.go:191-217) of steps 16w..16w+15
 // The walk (backtrack, dtw.go:165-188) is one wave reading Dn through 16-word
 // register windows (readlane), s = j-1+l strictly decreases along the path.
-constexpr int DTW_RING = 128;                       // reference rows held in LDS
 constexpr int DTW_ECH = 8;                          // edge values polled per chunk
 #ifndef DTW_G
 #define DTW_G 4                                     // steps per scheduling group in the sweep

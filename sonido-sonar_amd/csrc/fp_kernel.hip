@@ -239,7 +239,6 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
   for (int64_t ui = 0; ui < nunits; ++ui) {
     T nxt_e[FR][R], nxt_o[FR][R];
     if (ui + 1 < nunits) load_unit(unit_frame(ui + 1), nxt_e, nxt_o);
-    const int64_t uf = unit_frame(ui);
     const int rb = unit_row(ui);
     T* S = rows + (int64_t)rb * K;              // scratch = the unit's own rows
 

@@ -232,6 +232,45 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     if (sp) sp = check_periodicity(head);
     is_speech = sp;
     res->scalar("is_speech", sp ? 1.0 : 0.0);
+    // AnalyzeSpeech -> FormantAnalyzer.AnalyzeFormants(preprocessed PCM) (speech_analysis.go:70-74,
+    // format.go:85-124); a failed analysis leaves FormantResult nil (speech.go:297-303)
+    std::vector<double> formants;
+    double vtl = 17.5;
+    if (sp) {
+      const int W = csr >= 16000 ? 2048 : 1024, p = 12 + csr / 1000;
+      sonar_formant_frame* dfm = (sonar_formant_frame*)dbuf(c, "sx.formant", sizeof(sonar_formant_frame));
+      double* dham = (double*)dbuf(c, "sx.ham", W * 8);
+      if (!dfm || !dham) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+      std::vector<double> ham(W);
+      for (int i = 0; i < W; i++) ham[i] = 0.54 - 0.46 * std::cos(2.0 * M_PI * (double)i / (double)(W - 1));
+      HIP_TRY(c, hipMemcpyAsync(dham, ham.data(), W * 8, hipMemcpyHostToDevice, s));
+      if (p > 64 || sonar::launch_formants(dy, 1, 0, W, p, csr, n >= W ? 1 : 0, dham, dfm, nullptr, nullptr, s) != 0)
+        return fail(c, SONAR_ERR_DEVICE, "formant launch failed");
+      sonar_formant_frame fm;
+      HIP_TRY(c, hipMemcpyAsync(&fm, dfm, sizeof(fm), hipMemcpyDeviceToHost, s));
+      HIP_TRY(c, hipStreamSynchronize(s));
+      if (fm.status == 0) {
+        formants.assign(fm.frequency, fm.frequency + fm.n_formants);
+        vtl = fm.vocal_tract_length;
+      }
+    }
+    res->put("formant_frequencies", formants, formants.empty() ? 0 : 1, (int64_t)formants.size());   // convertFormantData
+    res->scalar("vocal_tract_length", vtl);
+    if (sp) {
+      // estimateSpeechRate (speech.go:779-797) on the energy frames of the pre-emphasised PCM
+      const double dur = (double)n / (double)csr;
+      double sil = 0.0;
+      if (!energy.empty()) {
+        const double thr = percentile10_threshold(energy);
+        int64_t k = 0;
+        for (double e : energy) if (e <= thr) k++;
+        sil = (double)k / (double)energy.size();
+      }
+      const double speech_time = dur * (1.0 - sil);
+      res->scalar("speech_rate", speech_time > 0 ? 4.0 * speech_time / dur : 3.0);
+    } else {
+      res->scalar("speech_rate", 0.0);
+    }
     if (sp) {
       std::vector<double> voicing(Fp);                             // extractVoicingProbability (:530-550)
       for (int64_t i = 0; i < Fp; i++) {

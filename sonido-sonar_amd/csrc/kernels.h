@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "../../include/sonar_gpu.h"
+
 namespace sonar {
 
 // Fused per-frame kernel (fp_kernel.hip).  Every wave owns a contiguous range
@@ -97,5 +99,9 @@ int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const int32_t* rev_
 int launch_dtw_cost_rowmajor(const double* Cn, const DtwGeom& g, double* out, hipStream_t s);
 // sets *flag = 1 if any of the n values is not finite
 int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
+
+// LPC formants (lpc_kernels.hip): one block per frame; out is sonar_formant_frame[frames]
+int launch_formants(const double* pcm, int64_t frames, int64_t hop, int W, int p, int sr, int frame_ok_len,
+                    const double* ham, sonar_formant_frame* out, double* coeffs, double* refl, hipStream_t s);
 
 }  // namespace sonar

@@ -571,6 +571,87 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
   return SONAR_OK;
 }
 
+// ========================================================= formants ====
+namespace {
+int formant_geometry(int sr, int* W, int* p) {
+  *W = sr >= 16000 ? 2048 : 1024;                    // NewFormantAnalyzer (format.go:48-69)
+  *p = 12 + sr / 1000;
+  return 0;
+}
+int run_formants(sonar_ctx* c, const double* pcm, int64_t n, int sr, int64_t frames, int64_t hop, bool ok_len,
+                 sonar_formant_frame* out, double* coeffs, double* refl, int device_ptrs) {
+  int W, p;
+  formant_geometry(sr, &W, &p);
+  if (p > 64) return fail(c, SONAR_ERR_UNSUPPORTED, "LPC order above 64 (sample rate > 52 kHz)");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  std::vector<double> ham(W);
+  for (int i = 0; i < W; ++i) ham[i] = 0.54 - 0.46 * std::cos(2.0 * M_PI * (double)i / (double)(W - 1));
+  double* dham = (double*)dbuf(c, "lpc.ham", W * 8);
+  if (!dham) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+  HIP_TRY(c, hipMemcpyAsync(dham, ham.data(), W * 8, hipMemcpyHostToDevice, s));
+  const double* dp = pcm;
+  sonar_formant_frame* dout = out;
+  double *dco = coeffs, *dre = refl;
+  if (!device_ptrs) {
+    double* b = (double*)dbuf(c, "lpc.pcm", std::max<int64_t>(n, 1) * 8);
+    dout = (sonar_formant_frame*)dbuf(c, "lpc.out", std::max<int64_t>(frames, 1) * sizeof(sonar_formant_frame));
+    dco = coeffs ? (double*)dbuf(c, "lpc.coeffs", std::max<int64_t>(frames, 1) * (p + 1) * 8) : nullptr;
+    dre = refl ? (double*)dbuf(c, "lpc.refl", std::max<int64_t>(frames, 1) * p * 8) : nullptr;
+    if (!b || !dout || (coeffs && !dco) || (refl && !dre)) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+    HIP_TRY(c, hipMemcpyAsync(b, pcm, n * 8, hipMemcpyHostToDevice, s));
+    dp = b;
+  }
+  hipEvent_t tend = timed_begin(c, s);
+  if (sonar::launch_formants(dp, frames, hop, W, p, sr, ok_len ? 1 : 0, dham, dout, dco, dre, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "formant launch failed");
+  timed_end(c, s, tend);
+  if (!device_ptrs) {
+    HIP_TRY(c, hipMemcpyAsync(out, dout, frames * sizeof(sonar_formant_frame), hipMemcpyDeviceToHost, s));
+    if (coeffs) HIP_TRY(c, hipMemcpyAsync(coeffs, dco, frames * (p + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (refl) HIP_TRY(c, hipMemcpyAsync(refl, dre, frames * p * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SONAR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t sonar_formant_frame_count(int64_t n, int32_t sample_rate, int32_t frame_size, int32_t hop_size) {
+  int W, p;
+  formant_geometry(sample_rate, &W, &p);
+  if (frame_size <= 0) frame_size = W;
+  if (hop_size <= 0) hop_size = frame_size / 2;
+  if (hop_size <= 0) return 0;
+  return n > frame_size ? (n - frame_size - 1) / hop_size + 1 : 0;   // for i := 0; i < n-frameSize; i += hop
+}
+
+int sonar_formants(sonar_ctx* c, const double* pcm, int64_t n, int32_t sample_rate, int32_t frame_size,
+                   int32_t hop_size, sonar_formant_frame* out, double* lpc_coeffs, double* reflection,
+                   int32_t device_ptrs) {
+  if (!c) return SONAR_ERR_INVALID;
+  if (sample_rate <= 0) return fail(c, SONAR_ERR_INVALID, "sample rate must be positive");
+  int W, p;
+  formant_geometry(sample_rate, &W, &p);
+  if (frame_size <= 0) frame_size = W;
+  if (hop_size <= 0) hop_size = frame_size / 2;
+  if (hop_size <= 0) return fail(c, SONAR_ERR_INVALID, "hop size must be positive");
+  const int64_t frames = sonar_formant_frame_count(n, sample_rate, frame_size, hop_size);
+  if (frames == 0) return SONAR_OK;
+  if (!pcm || !out) return fail(c, SONAR_ERR_INVALID, "null buffer");
+  return run_formants(c, pcm, n, sample_rate, frames, hop_size, frame_size >= W, out, lpc_coeffs, reflection,
+                      device_ptrs);
+}
+
+}  // extern "C"
+
+int sonar_analyze_formants_host(sonar_ctx* c, const double* pcm, int64_t n, int sample_rate, sonar_formant_frame* out) {
+  int W, p;
+  formant_geometry(sample_rate, &W, &p);
+  return run_formants(c, pcm, n, sample_rate, 1, 0, n >= W, out, nullptr, nullptr, 0);
+}
+
 // ====================================================== result object ====
 int sonar_result_get(const sonar_result* r, const char* name, const double** data, int64_t* rows, int64_t* cols) {
   if (!r || !name) return SONAR_ERR_INVALID;

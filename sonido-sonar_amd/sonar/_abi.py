@@ -67,6 +67,13 @@ class FeatureConfig(C.Structure):
                                          "enable_temporal_features", "mfcc_coefficients", "is_news", "precision"]]
 
 
+class FormantFrame(C.Structure):
+    _fields_ = [("status", C.c_int32), ("n_formants", C.c_int32), ("frequency", C.c_double * 4),
+                ("bandwidth", C.c_double * 4), ("amplitude", C.c_double * 4), ("confidence", C.c_double * 4),
+                ("vocal_tract_length", C.c_double), ("quality", C.c_double), ("gain", C.c_double),
+                ("residual_energy", C.c_double), ("stable", C.c_int32), ("lpc_order", C.c_int32)]
+
+
 _lib = None
 _vp, _d, _i32p, _i64p = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
 
@@ -117,6 +124,9 @@ def lib():
     L.sonar_align_features.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, _vp, C.c_int64, _vp, C.c_int64,
                                        C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                        C.c_double, C.POINTER(_vp)]
+    L.sonar_formant_frame_count.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32]
+    L.sonar_formant_frame_count.restype = C.c_int64
+    L.sonar_formants.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, C.c_int32]
     L.sonar_result_get.argtypes = [_vp, C.c_char_p, C.POINTER(_d), _i64p, _i64p]
     L.sonar_result_count.argtypes = [_vp]
     L.sonar_result_name.argtypes = [_vp, C.c_int]
@@ -125,6 +135,12 @@ def lib():
     L.sonar_result_free.restype = None
     _lib = L
     return L
+
+
+def _formant_dict(recs, F):
+    a = np.ctypeslib.as_array(recs)[:F] if F else np.zeros(0, dtype=np.dtype(FormantFrame))
+    return {k: np.array(a[k]) for k in ("status", "n_formants", "frequency", "bandwidth", "amplitude", "confidence",
+                                        "vocal_tract_length", "quality", "gain", "residual_energy", "stable")}
 
 
 def abi_version():
@@ -266,6 +282,22 @@ class Context:
         self._check(self._L.sonar_ncc(self._h, _ptr(a) if len(a) else None, len(a), _ptr(b) if len(b) else None,
                                       len(b), max_lag, _ptr(corr), _ptr(met), 0))
         return corr, dict(zip(NCC_KEYS, met.tolist()))
+
+    def formants(self, pcm, sample_rate, frame_size=0, hop_size=0, want_lpc=False):
+        """FormantAnalyzer.AnalyzeMultipleFrames; every attempted frame, `status` != 0 where Go skips."""
+        pcm = _f64(pcm)
+        L = lib()
+        F = int(L.sonar_formant_frame_count(len(pcm), sample_rate, frame_size, hop_size))
+        recs = (FormantFrame * max(F, 1))()
+        p = 12 + sample_rate // 1000
+        co = np.zeros((F, p + 1)) if want_lpc else None
+        rf = np.zeros((F, p)) if want_lpc else None
+        self._check(L.sonar_formants(self._h, _ptr(pcm), len(pcm), sample_rate, frame_size, hop_size, recs,
+                                     _ptr(co) if want_lpc else None, _ptr(rf) if want_lpc else None, 0))
+        out = _formant_dict(recs, F)
+        if want_lpc:
+            out["lpc_coeffs"], out["reflection"] = co, rf
+        return out
 
     def dtw(self, q, r, band=-1, want_cost=False):
         q, r = _f64(q), _f64(r)

@@ -1,0 +1,50 @@
+"""Row a13: LPC formant analysis (FormantAnalyzer.AnalyzeMultipleFrames / AnalyzeFormants,
+algorithms/speech/format.go:85-449; LPCAnalyzer, lpc.go:44-265) on the GPU vs the oracle.
+
+The reference obtains R through an FFT cross-correlation; the device sums the same lags
+directly, so R agrees to ~1e-13 relative and every downstream value to a tolerance:
+frame status, formant count and formant frequencies (bin index x sr/1024) must match
+exactly; LPC coefficients, amplitudes, confidences, gain and quality to 1e-6 relative."""
+import numpy as np
+import pytest
+
+import oracle as O
+from sonar import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _cmp(got, ref):
+    assert np.array_equal(got["status"], ref["status"])
+    ok = ref["status"] == 0
+    assert np.array_equal(got["n_formants"][ok], ref["n_formants"][ok])
+    assert np.array_equal(got["frequency"][ok], ref["frequency"][ok])
+    assert np.array_equal(got["bandwidth"][ok], ref["bandwidth"][ok])
+    assert np.array_equal(got["stable"][ok], ref["stable"][ok])
+    for k in ("amplitude", "confidence", "vocal_tract_length", "quality", "gain", "residual_energy"):
+        a, b = got[k][ok], ref[k][ok]
+        assert np.allclose(a, b, rtol=1e-6, atol=1e-9, equal_nan=True), k
+
+
+@pytest.mark.parametrize("sr,seconds", [(16000, 30.0), (8000, 10.0), (44100, 5.0)])
+def test_formant_frames_match_oracle(ctx, sr, seconds):
+    x = synth.c4_speech(seconds=seconds, sr=sr)
+    got = ctx.formants(x, sr, want_lpc=True)
+    ref = O.formant_frames(x, sr, want_lpc=True)
+    assert len(got["status"]) == len(ref["status"]) > 0
+    _cmp(got, ref)
+    ok = ref["status"] == 0
+    scale = np.max(np.abs(ref["lpc_coeffs"][ok]), axis=1, keepdims=True)
+    assert np.max(np.abs(got["lpc_coeffs"][ok] - ref["lpc_coeffs"][ok]) / scale) < 1e-6
+
+
+def test_formant_frames_custom_geometry_and_edges(ctx):
+    x = synth.c4_speech(seconds=6.0, sr=16000)
+    for fs, hop in [(4096, 1000), (2048, 512), (1500, 700)]:          # 1500 < W: every frame rejected
+        got = ctx.formants(x, 16000, frame_size=fs, hop_size=hop)
+        ref = O.formant_frames(x, 16000, frame_size=fs, hop_size=hop)
+        _cmp(got, ref)
+    z = np.zeros(3 * 2048)
+    got = ctx.formants(z, 16000)
+    assert np.all(got["status"] == 3)                                  # zero energy signal
+    assert len(ctx.formants(x[:2048], 16000)["status"]) == 0           # i < n - frameSize: no frame

@@ -82,3 +82,36 @@ def test_yin_finds_220hz():
     t = np.arange(1024) / sr
     p, c, tau = O.yin_raw(np.sin(2 * np.pi * 220 * t), sr)
     assert abs(p - 220) < 2 and c > 0.5
+
+
+def test_autocorr_fft_matches_direct_sums():
+    """The oracle's restatement of CrossCorrelation.computeFFT (recursive radix-2, z-scored,
+    stats/correlation.go:231-297, 726-774) equals the direct lag sums it stands for."""
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal(2048) * np.hanning(2048) + 0.3
+    z = (x - x.mean()) / x.std()
+    got = O.autocorr_fft(x, 1024)
+    full = np.correlate(z, z, mode="full")                    # lags -(n-1) .. n-1
+    ref = full[2047 - 1024: 2047 + 1025]
+    assert got.shape == (2049,)
+    assert np.max(np.abs(got - ref)) < 1e-10 * np.max(np.abs(ref))
+
+
+def test_formant_frame_structure():
+    """AnalyzeFormants invariants: <= 4 ascending formants >= 200 Hz apart inside [50, sr/2],
+    bandwidth clamp [50, 500], VTL default 17.5, too-short frames rejected (format.go:85-411)."""
+    from sonar import synth
+    x = synth.c4_speech(seconds=4.0, sr=16000)
+    r = O.formant_frames(x, 16000)
+    assert len(r["status"]) == (len(x) - 2048 - 1) // 1024 + 1
+    for k in range(len(r["status"])):
+        n = r["n_formants"][k]
+        f = r["frequency"][k][:n]
+        assert n <= 4 and np.all(np.diff(f) >= 200.0) and np.all((f >= 50) & (f <= 8000))
+        assert np.all((r["bandwidth"][k][:n] >= 50) & (r["bandwidth"][k][:n] <= 500))
+        if n == 0 and r["status"][k] == 0:
+            assert r["vocal_tract_length"][k] == 17.5 and r["quality"][k] == 0.0
+    short = O.formant_frame(x[:2000], 16000)
+    assert short["status"][0] == 1
+    silent = O.formant_frame(np.zeros(4096), 16000)
+    assert silent["status"][0] == 3                               # "zero energy signal"
