@@ -1,0 +1,78 @@
+"""Generate the committed fixtures under tests/golden/ from the oracle.
+
+The Go reference cannot run here (no Go toolchain, no go-dsp/gonum sources) and holds no
+tests or vectors of its own, so these fixtures are produced by
+the oracle -- the float64 C restatement of the Go path -- on seeded synthetic inputs.  They
+pin the oracle against regressions (tests/test_golden_cpu.py) and give the GPU tests fixed
+vectors (tests/test_gpu_golden.py).  Inputs are stored with the outputs (float32 PCM,
+float64 features), so the fixtures do not depend on the generators staying unchanged.
+
+    python tools/make_golden.py      # rewrites tests/golden/*.npz
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "sonido-sonar_amd")]
+import oracle as O  # noqa: E402
+from sonar import shard, synth  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print(f"{path}: {os.path.getsize(path) / 1024:.0f} KiB")
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    # path A: 1 s of the bench stream, W=1024 H=256, 40-mel/13 MFCC at 44.1 kHz + descriptors
+    pcm = shard.stream_pcm(0, 44100).numpy()
+    x = pcm.astype(np.float64)
+    mag = O.stft_mag(x, 1024, 256)
+    d = O.spectral_descriptors(mag, 44100)
+    save("stft_mfcc_44k", pcm=pcm, mfcc40=O.mfcc_frames(mag, 44100, n_coef=13, n_mels=40),
+         mfcc26=O.mfcc_frames(mag, 44100, n_coef=13, n_mels=26), mag_head=mag[:4],
+         **{"desc_" + k: v for k, v in d.items()},
+         zcr=O.zcr_frames(O.preemphasis(x, 0.97), len(mag), 1024, 256, 44100),
+         energy=O.short_time_energy(O.preemphasis(x, 0.97), 1024, 256))
+    # GenerateFingerprint semantics (F1: sample rate 0) on 2 s of the C1 sweep, music
+    sw = synth.sweep(10.0)[:88200].astype(np.float32)
+    fc = dict(sample_rate=0, window_size=1024, hop_size=256, stft_window_size=1024, stft_hop_size=256,
+              enable_mfcc=1, enable_speech_features=0, enable_temporal_features=0, mfcc_coefficients=13)
+    ref = O.speech_features_reference(sw.astype(np.float64), 44100, fc)
+    save("generate_fingerprint_music_c1", pcm=sw, **{k: np.asarray(v, dtype=np.float64) for k, v in ref.items()})
+    # speech config (C4 arithmetic): 3 s at 16 kHz, W=512 H=128, real sample rate
+    sp = synth.c4_speech(seconds=3.0, sr=16000).astype(np.float32)
+    fc = dict(sample_rate=16000, window_size=512, hop_size=128, stft_window_size=512, stft_hop_size=128,
+              enable_mfcc=1, enable_speech_features=1, enable_temporal_features=1, mfcc_coefficients=13)
+    ref = O.speech_features_reference(sp.astype(np.float64), 16000, fc)
+    fm = O.formant_frames(sp.astype(np.float64), 16000, want_lpc=True)
+    p, c, t = zip(*[O.yin_raw(sp[i * 512:i * 512 + 1024].astype(np.float64), 16000)
+                    for i in range(O.lib().or_pitch_frames(len(sp))) if i * 512 + 1024 <= len(sp)])
+    save("speech_c4_16k", pcm=sp, **{"sx_" + k: np.asarray(v, dtype=np.float64) for k, v in ref.items()},
+         **{"fm_" + k: np.asarray(v) for k, v in fm.items()},
+         yin_pitch=np.array(p), yin_conf=np.array(c), yin_tau=np.array(t, dtype=np.int32))
+    # chroma (music extractor): 1 s of the bench stream, F = 169 frames at hop 256
+    F = O.stft_frames(len(x), 1024, 256)
+    save("chroma_44k", pcm=pcm, chroma=O.chroma_music(x, F, 256, 44100), n_frames=np.int64(F))
+    # alignment: NCC of two energy-like envelopes, DTW of chroma-like sequences
+    rng = np.random.Generator(np.random.PCG64(2024))
+    e = np.abs(np.convolve(rng.standard_normal(3400), np.ones(20) / 20, mode="same"))
+    ea, eb = e[137:137 + 3000], e[:3000]
+    corr, met = O.ncc(ea, eb, 500)
+    q = rng.random((150, 12))
+    r = np.roll(q, 9, axis=0) + 0.02 * rng.random((150, 12))
+    r = r[:140]
+    dres = O.dtw(q, r, want_cost=True)
+    save("alignment", ncc_a=ea, ncc_b=eb, ncc_corr=corr, ncc_metrics=np.array([met[k] for k in O.NCC_KEYS]),
+         dtw_q=q, dtw_r=r, dtw_path_q=dres["path_q"], dtw_path_r=dres["path_r"], dtw_path_cost=dres["path_cost"],
+         dtw_distance=np.float64(dres["distance"]), dtw_cost=dres["cost"])
+
+
+if __name__ == "__main__":
+    main()
