@@ -150,29 +150,44 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 }
 }  // namespace
 
-// Block = 2 waves.  Wave 0 sweeps the band and touches global memory only with
-// stores (a gfx9 vmcnt wait would also drain its Cn stores, ~0.5 us per step);
-// wave 1 feeds it through LDS: the reference-row ring (256 rows, refilled 64 at a
-// time once wave 0's published progress shows the slots dead) and the edge ring
-// (C[64b][j] polled from E with sc1 loads).  LDS words rdy/efill/prog carry the
-// counts; a wave reads data only after it has read the count that covers it.
-constexpr int DTW_RROWS = 256;    // reference rows in the LDS ring (4 blocks of 64)
+// Block = 2 + DTW_NDW waves, all coupled through LDS counters (a wave reads data
+// only after it has read the count that covers it):
+//  wave 0  sweep: the min-chain of every cell, the C / direction / edge stores.  It
+//          never loads from global memory (on gfx9 a vmcnt wait would also drain
+//          its own Cn stores, ~0.5 us per step), reading distances and the band's
+//          top edge from LDS.
+//  wave 1  feeder: reference rows into a 256-row LDS ring (32-row blocks, written
+//          once the sweep's progress shows the overwritten rows dead) and C[64b][j]
+//          polled from E with sc1 loads into an edge ring.
+//  wave 2+ distance: 8-step chunks round-robin; the unfused Euclidean distance
+//          of every lane's cell into a DTW_DQ-step LDS distance ring.
+// The sweep's critical path is then ~20 VALU ops per step instead of ~70, and the
+// distance work runs on other SIMDs in parallel.
+constexpr int DTW_RROWS = 256;    // reference rows in the LDS ring
+constexpr int DTW_RBLK = 32;      // rows per ring refill
+constexpr int DTW_DQ = 16;        // steps of distances held in LDS
 constexpr int DTW_EQ = 256;       // edge values in the LDS ring
-constexpr int DTW_EAHEAD = 128;   // wave 1 fetches edge columns up to prog + EAHEAD
+constexpr int DTW_EAHEAD = 128;   // the feeder fetches edge columns up to prog + EAHEAD
+#ifndef DTW_NDW
+#define DTW_NDW 2                 // distance waves per block
+#endif
 
 template <int D, bool FAST, bool BANDED>
-__global__ __launch_bounds__(128) void dtw_band_kernel(DtwArgs a) {
+__global__ __launch_bounds__(64 * (2 + DTW_NDW)) void dtw_band_kernel(DtwArgs a) {
   constexpr int DR = D > 0 ? D : 1;
   __shared__ __attribute__((aligned(16))) double ring[DTW_RROWS * DR];
+  __shared__ double dring[DTW_DQ][64];
   __shared__ double eq[DTW_EQ];
   __shared__ int64_t shb;
-  __shared__ int prog, rdy, efill;   // wave 0 steps done; blocks in ring; edge columns in eq
+  __shared__ int prog, rdy, efill;          // sweep steps done; highest ring block ready; edge columns in eq
+  __shared__ int dchunk[DTW_NDW];           // per distance wave: 1 + index of its last finished chunk
 #define SONAR_LDS_LD(x) __hip_atomic_load(&(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
 #define SONAR_LDS_ST(x, v) __hip_atomic_store(&(x), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
     shb = atomicAdd(&a.sync[0], 1);
     prog = 0; rdy = -1; efill = 0;
+    for (int w = 0; w < DTW_NDW; ++w) dchunk[w] = 0;
   }
   __syncthreads();
   const int64_t b = shb;
@@ -182,24 +197,41 @@ __global__ __launch_bounds__(128) void dtw_band_kernel(DtwArgs a) {
   const double inf = __builtin_inf();
   constexpr uint64_t INF_BITS = 0x7FF0000000000000ull;
   const uint64_t* Ein = b > 0 ? a.E + (b - 1) * (nr + 1) : nullptr;       // C[64b][j] at index j
-  const int64_t nblk = (nr + 63) >> 6;
+  const int64_t nblk = (nr + DTW_RBLK - 1) / DTW_RBLK;
+  const int64_t i = 64 * b + 1 + lane;
+  const bool row_ok = i <= nq;
+  const int64_t qrow = row_ok ? i - 1 : 0;
+  uint64_t spins_total = 0;
+  // spin (LDS only) until `cond` holds; bounded, flags the error word instead of hanging
+#define SONAR_SPIN_UNTIL(cond)                                                        \
+  do {                                                                                \
+    uint64_t sp_ = 0;                                                                 \
+    while (!(cond)) {                                                                 \
+      __builtin_amdgcn_s_sleep(1);                                                    \
+      if (++sp_ > (uint64_t)DTW_SPIN_LIMIT * 4) { if (lane == 0) atomicOr(&a.sync[1], 2); break; } \
+    }                                                                                 \
+    spins_total += sp_;                                                               \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
+  } while (0)
 
   if (wave == 1) {
     // ------------------------------------------------------------ feeder wave
     int64_t nextblk = 0, have = 0;
-    uint64_t spins = 0;
+    uint64_t idle = 0;
     const int64_t ecols = Ein ? nr : 0;
     while (true) {
       const int64_t p = SONAR_LDS_LD(prog);
       bool work = false;
       if constexpr (D > 0) {
-        // block m overwrites block m-4, whose last row 64m-193 is read by lane 63 for step
-        // 64m-130 (computed one step early): wait until wave 0 has done 64(m-2) steps
-        if (nextblk < nblk && (nextblk < 4 || p >= 64 * (nextblk - 2))) {
-          const int64_t row = 64 * nextblk + lane;
-          double* dst = ring + ((64 * nextblk + lane) & (DTW_RROWS - 1)) * D;
+        // block m overwrites block m-8; its last row 32m-225 is read for step 32m-162,
+        // which the sweep has consumed once prog >= 32m-161
+        if (nextblk < nblk && (nextblk < DTW_RROWS / DTW_RBLK || p >= DTW_RBLK * nextblk - 161)) {
+          if (lane < DTW_RBLK) {
+            const int64_t row = DTW_RBLK * nextblk + lane;
+            double* dst = ring + (row & (DTW_RROWS - 1)) * D;
 #pragma unroll
-          for (int k = 0; k < DR; ++k) dst[k] = row < nr ? a.r[row * D + k] : 0.0;
+            for (int k = 0; k < DR; ++k) dst[k] = row < nr ? a.r[row * D + k] : 0.0;
+          }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           if (lane == 0) SONAR_LDS_ST(rdy, (int)nextblk);
           ++nextblk;
@@ -224,11 +256,10 @@ __global__ __launch_bounds__(128) void dtw_band_kernel(DtwArgs a) {
           }
         }
       }
-      const bool done = (D == 0 || nextblk >= nblk) && have >= ecols;
-      if (done) break;
+      if ((D == 0 || nextblk >= nblk) && have >= ecols) break;
       if (!work) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (uint64_t)DTW_SPIN_LIMIT * 4) {   // producer band never arrived: flag, release wave 0
+        if (++idle > (uint64_t)DTW_SPIN_LIMIT * 4) {   // producer band never arrived: flag, release the rest
           if (lane == 0) { atomicOr(&a.sync[1], 1); SONAR_LDS_ST(efill, (int)ecols); SONAR_LDS_ST(rdy, (int)nblk); }
           break;
         }
@@ -237,12 +268,6 @@ __global__ __launch_bounds__(128) void dtw_band_kernel(DtwArgs a) {
     return;
   }
 
-  // ---------------------------------------------------------------- sweep wave
-  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-  uint64_t t_first = 0, spins_total = 0;
-  const int64_t i = 64 * b + 1 + lane;
-  const bool row_ok = i <= nq;
-  const int64_t qrow = row_ok ? i - 1 : 0;
   double qv[DR];
   if constexpr (D > 0) {
 #pragma unroll
@@ -274,18 +299,37 @@ __global__ __launch_bounds__(128) void dtw_band_kernel(DtwArgs a) {
       return sqrt(sum);
     }
   };
-  // spin (LDS only) until a feeder count reaches `need`
-#define SONAR_WAIT_COUNT(word, need)                                                  \
-  do {                                                                                \
-    uint64_t sp_ = 0;                                                                 \
-    while (SONAR_LDS_LD(word) < (need)) {                                             \
-      __builtin_amdgcn_s_sleep(1);                                                    \
-      if (++sp_ > (uint64_t)DTW_SPIN_LIMIT * 4) { if (lane == 0) atomicOr(&a.sync[1], 2); break; } \
-    }                                                                                 \
-    spins_total += sp_;                                                               \
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
-  } while (0)
 
+  if (wave >= 2) {
+    // ---------------------------------------------------------- distance waves
+    const int w = wave - 2;
+    for (int64_t c = w; DTW_ECH * c < S; c += DTW_NDW) {
+      const int64_t t0 = DTW_ECH * c;
+      // ring slots of steps t0..t0+7 were last read by the sweep for steps t0-DQ..t0-DQ+7
+      SONAR_SPIN_UNTIL(SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW_DQ);
+      if constexpr (D > 0) {
+        const int64_t need = (t0 + DTW_ECH - 1) / DTW_RBLK;             // rows up to t0+7
+        const int64_t needc = need < nblk - 1 ? need : nblk - 1;
+        SONAR_SPIN_UNTIL(SONAR_LDS_LD(rdy) >= needc);
+      }
+#pragma unroll
+      for (int g0 = 0; g0 < DTW_ECH; g0 += DTW_G) {
+        double dv[DTW_G];
+#pragma unroll
+        for (int u = 0; u < DTW_G; ++u) dv[u] = t0 + g0 + u < S ? dist(t0 + g0 + u) : 0.0;
+#pragma unroll
+        for (int u = 0; u < DTW_G; ++u) dring[(t0 + g0 + u) & (DTW_DQ - 1)][lane] = dv[u];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) SONAR_LDS_ST(dchunk[w], (int)(c + 1));
+    }
+    return;
+  }
+
+  // ---------------------------------------------------------------- sweep wave
+  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint64_t t_first = 0;
   uint64_t* Eout = (b + 1 < a.nb) ? a.E + b * (nr + 1) : nullptr;         // C[64b+64][j]
   double out = inf;                                   // C[i][j-1]; C[i][0] = +Inf
   double up_prev = (lane == 0 && b == 0) ? 0.0 : inf; // C[i-1][j-1]; C[0][0] = 0
@@ -293,6 +337,7 @@ __global__ __launch_bounds__(128) void dtw_band_kernel(DtwArgs a) {
   const int64_t band = a.band;
   double* Cb = a.Cn + ((b * S) << 6) + lane;
   uint32_t* Db = a.Dn + ((b * a.SW) << 6) + lane;
+
   // one sweep step: lane l relaxes C[i][s-l+1] with local distance d; l0up = C[64b][s+1]
   // for lane 0.  FULL: every lane's column is in [1, nr] (s in [63, nr-1]), so no
   // per-lane predicate is needed (rows past nq compute values nobody reads).
@@ -321,65 +366,39 @@ __global__ __launch_bounds__(128) void dtw_band_kernel(DtwArgs a) {
     return code;
   };
 
-  // distances of chunk c+1 are computed while chunk c runs its min-chains: 8
-  // independent f64 chains give the ILP one wave per SIMD cannot get otherwise
-  double dc[DTW_ECH], dn[DTW_ECH];
-  if constexpr (D > 0) SONAR_WAIT_COUNT(rdy, 0);
-#pragma unroll
-  for (int u = 0; u < DTW_ECH; ++u) {
-    dc[u] = u < S ? dist(u) : 0.0;
-    __builtin_amdgcn_sched_barrier(0);
-  }
-
   for (int s0 = 0; s0 < S; s0 += DTW_ECH) {
     if (lane == 0) SONAR_LDS_ST(prog, s0);             // steps < s0 are done
-    const bool more = s0 + DTW_ECH < S;
-    if constexpr (D > 0) {
-      const int need = (s0 + 2 * DTW_ECH - 1) >> 6;    // next chunk's dist() reads rows up to s0 + 15
-      if (more && need < nblk) SONAR_WAIT_COUNT(rdy, need);
-    }
+    const int64_t c = s0 / DTW_ECH;
+    SONAR_SPIN_UNTIL(SONAR_LDS_LD(dchunk[c % DTW_NDW]) > c);
     double ech = inf;
     if (Ein) {
       const int need = (int)(s0 + DTW_ECH < nr ? s0 + DTW_ECH : nr);
-      SONAR_WAIT_COUNT(efill, need);
+      SONAR_SPIN_UNTIL(SONAR_LDS_LD(efill) >= need);
       if (a.trace && s0 == 0) t_first = __builtin_amdgcn_s_memrealtime();
       const int64_t jj = s0 + 1 + lane;
       if (lane < DTW_ECH && jj <= nr) ech = eq[jj & (DTW_EQ - 1)];
     }
+    double dc[DTW_ECH];
+#pragma unroll
+    for (int u = 0; u < DTW_ECH; ++u) dc[u] = dring[(s0 + u) & (DTW_DQ - 1)][lane];
     double* cs = Cb + ((int64_t)s0 << 6);
     double eacc = inf;                                 // lane u <- C[64b+64][s0+u-62] (lane 63's value)
-    const bool full = s0 >= 63 && s0 + DTW_ECH <= nr;
-    if (full) {
-      // groups of DTW_G steps, each interleaved with DTW_G of the next chunk's distances;
-      // the sched_barrier keeps the scheduler from hoisting every ring read (VGPRs)
+    if (s0 >= 63 && s0 + DTW_ECH <= nr) {
 #pragma unroll
-      for (int g0 = 0; g0 < DTW_ECH; g0 += DTW_G) {
-#pragma unroll
-        for (int u = g0; u < g0 + DTW_G; ++u) dn[u] = dist(s0 + DTW_ECH + u);
-#pragma unroll
-        for (int u = g0; u < g0 + DTW_G; ++u) {
-          const uint32_t code =
-              step(std::true_type{}, s0 + u, Ein ? readlane_f64(ech, u) : inf, dc[u], cs + (u << 6));
-          dacc |= code << (2 * ((s0 & 8) + u));
-          if (Eout) { const double e = readlane_f64(out, 63); eacc = lane == u ? e : eacc; }
-        }
-        __builtin_amdgcn_sched_barrier(0);
+      for (int u = 0; u < DTW_ECH; ++u) {
+        const uint32_t code = step(std::true_type{}, s0 + u, Ein ? readlane_f64(ech, u) : inf, dc[u], cs + (u << 6));
+        dacc |= code << (2 * ((s0 & 8) + u));
+        if (Eout) { const double e = readlane_f64(out, 63); eacc = lane == u ? e : eacc; }
       }
     } else {
 #pragma unroll
-      for (int g0 = 0; g0 < DTW_ECH; g0 += DTW_G) {
-#pragma unroll
-        for (int u = g0; u < g0 + DTW_G; ++u) dn[u] = s0 + DTW_ECH + u < S ? dist(s0 + DTW_ECH + u) : 0.0;
-#pragma unroll
-        for (int u = g0; u < g0 + DTW_G; ++u) {
-          if (s0 + u < S) {
-            const uint32_t code = step(std::false_type{}, s0 + u, Ein ? readlane_f64(ech, u) : inf, dc[u],
-                                       cs + (u << 6));
-            dacc |= code << (2 * ((s0 & 8) + u));
-            if (Eout) { const double e = readlane_f64(out, 63); eacc = lane == u ? e : eacc; }
-          }
+      for (int u = 0; u < DTW_ECH; ++u) {
+        if (s0 + u < S) {
+          const uint32_t code = step(std::false_type{}, s0 + u, Ein ? readlane_f64(ech, u) : inf, dc[u],
+                                     cs + (u << 6));
+          dacc |= code << (2 * ((s0 & 8) + u));
+          if (Eout) { const double e = readlane_f64(out, 63); eacc = lane == u ? e : eacc; }
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
     }
     if (Eout) {                                        // one sc1 store of the chunk's 8 edge values
@@ -387,15 +406,13 @@ __global__ __launch_bounds__(128) void dtw_band_kernel(DtwArgs a) {
       if (lane < DTW_ECH && je >= 1 && je <= nr)
         __hip_atomic_store(Eout + je, __builtin_bit_cast(uint64_t, eacc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if ((s0 & 8) || !more) {                           // steps 16w .. 16w+15 complete (or the last one)
+    if ((s0 & 8) || s0 + DTW_ECH >= S) {               // steps 16w .. 16w+15 complete (or the last one)
       Db[(int64_t)(s0 >> 4) << 6] = dacc;
       dacc = 0;
     }
-#pragma unroll
-    for (int u = 0; u < DTW_ECH; ++u) dc[u] = dn[u];
   }
   if (lane == 0) SONAR_LDS_ST(prog, (int)S);
-#undef SONAR_WAIT_COUNT
+#undef SONAR_SPIN_UNTIL
 #undef SONAR_LDS_LD
 #undef SONAR_LDS_ST
   if (a.trace && lane == 0) {
@@ -522,7 +539,7 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
   if (g.nb > 1 && hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, dtw_edge_bytes(g) / 4, s) != hipSuccess) return -5;
   DtwArgs a{q, r, dim, band, g.nq, g.nr, g.nb, g.S, g.SW, Cn, Dn, reinterpret_cast<uint64_t*>(E), sync_words,
             trace};
-  const dim3 grid((unsigned)g.nb), block(128);
+  const dim3 grid((unsigned)g.nb), block(64 * (2 + DTW_NDW));
 #define SONAR_DTW_LAUNCH(DD)                                                                          \
   do {                                                                                                \
     if (band > 0) {                                                                                   \

@@ -23,6 +23,16 @@ namespace sonar {
 constexpr int LPC_MAXP = 64;
 
 namespace {
+// a rejected frame still gets a complete record (the output buffer is reused across calls)
+__device__ void clear_record(sonar_formant_frame* o, int status, int p) {
+  o->status = status;
+  o->n_formants = 0;
+  for (int i = 0; i < 4; ++i) o->frequency[i] = o->bandwidth[i] = o->amplitude[i] = o->confidence[i] = 0.0;
+  o->vocal_tract_length = 0.0;
+  o->quality = 0.0;
+  o->stable = 0;
+  o->lpc_order = p;
+}
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }   // finite operands only
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
 
@@ -54,7 +64,7 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
   sonar_formant_frame* o = out + f;
 
   if (!frame_ok_len) {                              // len(frame) < windowSize (format.go:86-88)
-    if (tid == 0) { o->status = 1; o->n_formants = 0; o->lpc_order = p; }
+    if (tid == 0) { clear_record(o, 1, p); o->gain = 0.0; o->residual_energy = 0.0; }
     return;
   }
   for (int i = tid; i < W; i += 256) {
@@ -114,7 +124,7 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
   const int status = (int)red[0];
   const double E = red[1];
   if (status != 0) {
-    if (tid == 0) o->n_formants = 0;
+    if (tid == 0) clear_record(o, status, p);
     return;
   }
   if (coeffs) for (int i = tid; i <= p; i += 256) coeffs[f * (p + 1) + i] = a[i];
