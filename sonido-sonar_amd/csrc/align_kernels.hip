@@ -134,7 +134,7 @@ struct DtwArgs {
   uint32_t* Dn;
   uint64_t* E;
   int32_t* sync;   // [0] band ticket, [1] error flag
-  uint64_t* trace; // optional [nb][4]: t_start, t_first_edge, t_end, spins (s_memrealtime, 100 MHz)
+  uint64_t* trace; // optional [nb][4]: t_start, t_first_edge, t_end, sweep wait ticks (s_memrealtime, 100 MHz)
 };
 
 namespace {
@@ -142,6 +142,12 @@ __device__ __forceinline__ double shr1(double v, double lane0) {
   const int2 a = __builtin_bit_cast(int2, v), o = __builtin_bit_cast(int2, lane0);
   const int lo = __builtin_amdgcn_update_dpp(o.x, a.x, 0x138, 0xf, 0xf, false);   // wave_shr:1
   const int hi = __builtin_amdgcn_update_dpp(o.y, a.y, 0x138, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, make_int2(lo, hi));
+}
+__device__ __forceinline__ double shl1(double v) {      // lane l <- lane l+1 (lane 63 <- +Inf)
+  const int2 a = __builtin_bit_cast(int2, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, a.x, 0x130, 0xf, 0xf, false);   // wave_shl:1
+  const int hi = __builtin_amdgcn_update_dpp(0x7FF00000, a.y, 0x130, 0xf, 0xf, false);
   return __builtin_bit_cast(double, make_int2(lo, hi));
 }
 __device__ __forceinline__ double readlane_f64(double v, int l) {
@@ -163,13 +169,19 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 //          of every lane's cell into a DTW_DQ-step LDS distance ring.
 // The sweep's critical path is then ~20 VALU ops per step instead of ~70, and the
 // distance work runs on other SIMDs in parallel.
-constexpr int DTW_RROWS = 256;    // reference rows in the LDS ring
-constexpr int DTW_RBLK = 32;      // rows per ring refill
-constexpr int DTW_DQ = 16;        // steps of distances held in LDS
+#ifndef DTW_RROWS_CFG
+#define DTW_RROWS_CFG 128
+#endif
+#ifndef DTW_DQ_CFG
+#define DTW_DQ_CFG 32
+#endif
+constexpr int DTW_RROWS = DTW_RROWS_CFG;   // reference rows in the LDS ring
+constexpr int DTW_RBLK = 32;               // rows per ring refill
+constexpr int DTW_DQ = DTW_DQ_CFG;         // steps of distances held in LDS
 constexpr int DTW_EQ = 256;       // edge values in the LDS ring
 constexpr int DTW_EAHEAD = 128;   // the feeder fetches edge columns up to prog + EAHEAD
 #ifndef DTW_NDW
-#define DTW_NDW 2                 // distance waves per block
+#define DTW_NDW 3                 // distance waves per block
 #endif
 
 template <int D, bool FAST, bool BANDED>
@@ -178,6 +190,7 @@ __global__ __launch_bounds__(64 * (2 + DTW_NDW)) void dtw_band_kernel(DtwArgs a)
   __shared__ __attribute__((aligned(16))) double ring[DTW_RROWS * DR];
   __shared__ double dring[DTW_DQ][64];
   __shared__ double eq[DTW_EQ];
+  __shared__ double erow[DTW_ECH][64];      // the sweep's last 8 rows of C (lane 63 = the band's edge)
   __shared__ int64_t shb;
   __shared__ int prog, rdy, efill;          // sweep steps done; highest ring block ready; edge columns in eq
   __shared__ int dchunk[DTW_NDW];           // per distance wave: 1 + index of its last finished chunk
@@ -206,11 +219,14 @@ __global__ __launch_bounds__(64 * (2 + DTW_NDW)) void dtw_band_kernel(DtwArgs a)
 #define SONAR_SPIN_UNTIL(cond)                                                        \
   do {                                                                                \
     uint64_t sp_ = 0;                                                                 \
-    while (!(cond)) {                                                                 \
-      __builtin_amdgcn_s_sleep(1);                                                    \
-      if (++sp_ > (uint64_t)DTW_SPIN_LIMIT * 4) { if (lane == 0) atomicOr(&a.sync[1], 2); break; } \
+    if (!(cond)) {                                                                    \
+      const uint64_t w0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;            \
+      while (!(cond)) {                                                               \
+        __builtin_amdgcn_s_sleep(1);                                                  \
+        if (++sp_ > (uint64_t)DTW_SPIN_LIMIT * 4) { if (lane == 0) atomicOr(&a.sync[1], 2); break; } \
+      }                                                                               \
+      if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - w0_;             \
     }                                                                                 \
-    spins_total += sp_;                                                               \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
   } while (0)
 
@@ -223,9 +239,10 @@ __global__ __launch_bounds__(64 * (2 + DTW_NDW)) void dtw_band_kernel(DtwArgs a)
       const int64_t p = SONAR_LDS_LD(prog);
       bool work = false;
       if constexpr (D > 0) {
-        // block m overwrites block m-8; its last row 32m-225 is read for step 32m-162,
-        // which the sweep has consumed once prog >= 32m-161
-        if (nextblk < nblk && (nextblk < DTW_RROWS / DTW_RBLK || p >= DTW_RBLK * nextblk - 161)) {
+        // block m overwrites block m - RROWS/RBLK, whose last row RBLK*m - RROWS + RBLK - 1 is
+        // read (by lane 63) for step row + 63: the sweep has consumed it once prog >= row + 64
+        if (nextblk < nblk &&
+            (nextblk < DTW_RROWS / DTW_RBLK || p >= DTW_RBLK * nextblk - DTW_RROWS + DTW_RBLK + 63)) {
           if (lane < DTW_RBLK) {
             const int64_t row = DTW_RBLK * nextblk + lane;
             double* dst = ring + (row & (DTW_RROWS - 1)) * D;
@@ -343,7 +360,7 @@ __global__ __launch_bounds__(64 * (2 + DTW_NDW)) void dtw_band_kernel(DtwArgs a)
   // per-lane predicate is needed (rows past nq compute values nobody reads).
   auto step = [&](auto full_tag, int s, double l0up, double d, double* cs) -> uint32_t {
     constexpr bool FULL = decltype(full_tag)::value;
-    const double up = shr1(out, l0up);               // C[i-1][j]
+    const double up = shr1(out, l0up);               // C[i-1][j]; lane 0 takes l0up's lane 0
     const int j = s - lane + 1;
     const double left = out, dg = up_prev;
     // findPreviousStep: vertical, horizontal, diagonal; strict < (NaN compares false)
@@ -366,50 +383,56 @@ __global__ __launch_bounds__(64 * (2 + DTW_NDW)) void dtw_band_kernel(DtwArgs a)
     return code;
   };
 
-  for (int s0 = 0; s0 < S; s0 += DTW_ECH) {
-    if (lane == 0) SONAR_LDS_ST(prog, s0);             // steps < s0 are done
-    const int64_t c = s0 / DTW_ECH;
-    SONAR_SPIN_UNTIL(SONAR_LDS_LD(dchunk[c % DTW_NDW]) > c);
-    double ech = inf;
-    if (Ein) {
-      const int need = (int)(s0 + DTW_ECH < nr ? s0 + DTW_ECH : nr);
-      SONAR_SPIN_UNTIL(SONAR_LDS_LD(efill) >= need);
-      if (a.trace && s0 == 0) t_first = __builtin_amdgcn_s_memrealtime();
-      const int64_t jj = s0 + 1 + lane;
-      if (lane < DTW_ECH && jj <= nr) ech = eq[jj & (DTW_EQ - 1)];
-    }
-    double dc[DTW_ECH];
-#pragma unroll
-    for (int u = 0; u < DTW_ECH; ++u) dc[u] = dring[(s0 + u) & (DTW_DQ - 1)][lane];
-    double* cs = Cb + ((int64_t)s0 << 6);
-    double eacc = inf;                                 // lane u <- C[64b+64][s0+u-62] (lane 63's value)
-    if (s0 >= 63 && s0 + DTW_ECH <= nr) {
-#pragma unroll
-      for (int u = 0; u < DTW_ECH; ++u) {
-        const uint32_t code = step(std::true_type{}, s0 + u, Ein ? readlane_f64(ech, u) : inf, dc[u], cs + (u << 6));
-        dacc |= code << (2 * ((s0 & 8) + u));
-        if (Eout) { const double e = readlane_f64(out, 63); eacc = lane == u ? e : eacc; }
+  // the band's sweep, specialised on whether it has a band above (edge in) and below (edge out)
+  auto sweep = [&](auto ein_tag, auto eout_tag) {
+    constexpr bool EIN = decltype(ein_tag)::value, EOUT = decltype(eout_tag)::value;
+    for (int s0 = 0; s0 < S; s0 += DTW_ECH) {
+      if (lane == 0) SONAR_LDS_ST(prog, s0);           // steps < s0 are done
+      const int64_t c = s0 / DTW_ECH;
+      SONAR_SPIN_UNTIL(SONAR_LDS_LD(dchunk[c % DTW_NDW]) > c);
+      double ech = inf;                                // lane k: C[64b][s0+1+k]; shifted down one lane per step
+      if constexpr (EIN) {
+        const int need = (int)(s0 + DTW_ECH < nr ? s0 + DTW_ECH : nr);
+        SONAR_SPIN_UNTIL(SONAR_LDS_LD(efill) >= need);
+        if (a.trace && s0 == 0) t_first = __builtin_amdgcn_s_memrealtime();
+        const int64_t jj = s0 + 1 + lane;
+        if (lane < DTW_ECH && jj <= nr) ech = eq[jj & (DTW_EQ - 1)];
       }
-    } else {
+      double dc[DTW_ECH];
 #pragma unroll
-      for (int u = 0; u < DTW_ECH; ++u) {
-        if (s0 + u < S) {
-          const uint32_t code = step(std::false_type{}, s0 + u, Ein ? readlane_f64(ech, u) : inf, dc[u],
-                                     cs + (u << 6));
-          dacc |= code << (2 * ((s0 & 8) + u));
-          if (Eout) { const double e = readlane_f64(out, 63); eacc = lane == u ? e : eacc; }
+      for (int u = 0; u < DTW_ECH; ++u) dc[u] = dring[(s0 + u) & (DTW_DQ - 1)][lane];
+      double* cs = Cb + ((int64_t)s0 << 6);
+      auto body = [&](auto full_tag) {
+#pragma unroll
+        for (int u = 0; u < DTW_ECH; ++u) {
+          if (decltype(full_tag)::value || s0 + u < S) {
+            const uint32_t code = step(full_tag, s0 + u, ech, dc[u], cs + (u << 6));
+            dacc |= code << (2 * ((s0 & 8) + u));
+            if constexpr (EOUT) erow[u][lane] = out;   // lane 63's value is this band's edge
+            if constexpr (EIN) ech = shl1(ech);
+          }
         }
+      };
+      if (s0 >= 63 && s0 + DTW_ECH <= nr) body(std::true_type{});
+      else body(std::false_type{});
+      if constexpr (EOUT) {                            // one sc1 store of the chunk's 8 edge values
+        const int64_t je = (int64_t)s0 + lane - 62;
+        if (lane < DTW_ECH && je >= 1 && je <= nr)
+          __hip_atomic_store(Eout + je, __builtin_bit_cast(uint64_t, erow[lane & (DTW_ECH - 1)][63]),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if ((s0 & 8) || s0 + DTW_ECH >= S) {             // steps 16w .. 16w+15 complete (or the last one)
+        Db[(int64_t)(s0 >> 4) << 6] = dacc;
+        dacc = 0;
       }
     }
-    if (Eout) {                                        // one sc1 store of the chunk's 8 edge values
-      const int64_t je = (int64_t)s0 + lane - 62;
-      if (lane < DTW_ECH && je >= 1 && je <= nr)
-        __hip_atomic_store(Eout + je, __builtin_bit_cast(uint64_t, eacc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if ((s0 & 8) || s0 + DTW_ECH >= S) {               // steps 16w .. 16w+15 complete (or the last one)
-      Db[(int64_t)(s0 >> 4) << 6] = dacc;
-      dacc = 0;
-    }
+  };
+  if (Ein) {
+    if (Eout) sweep(std::true_type{}, std::true_type{});
+    else sweep(std::true_type{}, std::false_type{});
+  } else {
+    if (Eout) sweep(std::false_type{}, std::true_type{});
+    else sweep(std::false_type{}, std::false_type{});
   }
   if (lane == 0) SONAR_LDS_ST(prog, (int)S);
 #undef SONAR_SPIN_UNTIL

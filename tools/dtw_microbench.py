@@ -29,6 +29,6 @@ if tp and os.path.exists(tp):
     st, fe, en, sp = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0, (t[:, 2] - t0) / 100.0, t[:, 3]
     print("bands", len(t), "end max us", en.max(), "start us [0,1,2,100,400,807]:", st[[0, 1, 2, 100, 400, -1]])
     print("first-edge us:", fe[[1, 2, 100, 400, -1]], "dur us (end-start):", (en - st)[[0, 1, 100, 400, -1]])
-    print("spins:", sp[[1, 2, 100, 400, -1]], "mean", sp[1:].mean())
+    print("sweep wait us:", sp[[0, 1, 2, 100, 400, -1]] / 100.0, "mean", sp.mean() / 100.0)
     d = np.diff(st)
     print("start gaps us: median", np.median(d), "max", d.max())
