@@ -446,48 +446,76 @@ __global__ __launch_bounds__(64 * (2 + DTW_NDW)) void dtw_band_kernel(DtwArgs a)
   }
 }
 
-// Single wave: backtrack (dtw.go:165-188) over the 2-bit codes.  Points are
-// recorded in reverse order (rev_q[k] = i-1, rev_r[k] = j-1), 64 at a time.
-// Interior steps read lane l's code word of band (i-1)/64 from a 16-word
-// register window (s = j-1+l only decreases inside a band, so only the lower
-// bound is checked); the borders (i == 0 or j == 0) are straight runs.
+// Single wave: backtrack (dtw.go:165-188) over the 2-bit direction codes.  The walk
+// is inherently sequential, so it only emits its own moves (2 bits per step, 16 per
+// word, stored 64 words at a time); dtw_path_decode_kernel turns them into points and
+// costs in parallel.  Interior steps read lane l's code word of band (i-1)/64 from a
+// 16-word register window (s = j-1+l only decreases inside a band, so only the
+// lower bound is checked); the next band's window is prefetched on band entry.
+// Moves: 0 = vertical (i-1), 1 = horizontal (j-1), 2 = diagonal.
 __global__ __launch_bounds__(64) void dtw_walk_kernel(const uint32_t* Dn, int64_t nq, int64_t nr, int64_t SW,
-                                                      int32_t* rev_q, int32_t* rev_r, int64_t* plen) {
+                                                      uint32_t* codes, int64_t* plen) {
   const int lane = threadIdx.x;
-  uint32_t win[16];
+  uint32_t win[16], nxt[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) win[k] = 0u;
+  for (int k = 0; k < 16; ++k) { win[k] = 0u; nxt[k] = 0u; }
   int i = (int)nq, j = (int)nr, P = 0;
-  int wb = -1, wlo = 0;
+  int wb = -1, wlo = 0, pb = -1, plo = 0;
   const int sw = (int)SW;
-  int32_t aq = 0, ar = 0;
-  auto record = [&](int qi, int ri) {
-    if (lane == (P & 63)) { aq = qi; ar = ri; }
-    if ((P & 63) == 63) { rev_q[P - 63 + lane] = aq; rev_r[P - 63 + lane] = ar; }
+  uint32_t cacc = 0, vacc = 0;
+  auto emit = [&](uint32_t code) {
+    cacc |= code << (2 * (P & 15));
     ++P;
+    if ((P & 15) == 0) {
+      const int wi = (P >> 4) - 1;
+      vacc = lane == (wi & 63) ? cacc : vacc;
+      cacc = 0;
+      if ((wi & 63) == 63) codes[wi - 63 + lane] = vacc;
+    }
+  };
+  auto load_win = [&](uint32_t (&dst)[16], int bnd, int lo) {
+    const uint32_t* src = Dn + (((int64_t)bnd * sw + lo) << 6) + lane;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[k] = (lo + k < sw) ? src[k << 6] : 0u;
   };
   while (i > 0 && j > 0) {
-    record(i - 1, j - 1);
     const int l = (i - 1) & 63, bnd = (i - 1) >> 6;
     const int s = j - 1 + l, w = s >> 4;
     if (bnd != wb || w < wlo) {
-      wb = bnd;
-      wlo = w - 15 > 0 ? w - 15 : 0;
-      const uint32_t* src = Dn + (((int64_t)bnd * sw + wlo) << 6) + lane;
+      if (bnd == pb && w >= plo && w < plo + 16) {     // prefetched on entry to the band below
 #pragma unroll
-      for (int k = 0; k < 16; ++k) win[k] = (wlo + k < sw) ? src[k << 6] : 0u;
+        for (int k = 0; k < 16; ++k) win[k] = nxt[k];
+        wlo = plo;
+      } else {
+        wlo = w - 15 > 0 ? w - 15 : 0;
+        load_win(win, bnd, wlo);
+        __builtin_amdgcn_s_waitcnt(0x0F70);             // vmcnt(0) here, before the prefetch is issued
+      }
+      if (bnd != wb && bnd > 0) {                       // the walk enters band bnd-1 at a column <= j
+        pb = bnd - 1;
+        const int wt = (j - 1 + 63) >> 4;
+        plo = wt - 15 > 0 ? wt - 15 : 0;
+        load_win(nxt, pb, plo);
+      }
+      wb = bnd;
     }
-    const uint32_t word = __builtin_amdgcn_readlane(win[w - wlo], l);
+    const int kw = __builtin_amdgcn_readfirstlane(w - wlo);      // uniform: keeps the index scalar
+    const uint32_t word = __builtin_amdgcn_readlane(win[kw], __builtin_amdgcn_readfirstlane(l));
     const uint32_t code = (word >> ((s & 15) << 1)) & 3u;
-    i -= code != 1u;          // vertical (0) or diagonal (2)
-    j -= code != 0u;          // horizontal (1) or diagonal (2)
+    emit(code);
+    i -= code != 1u;
+    j -= code != 0u;
   }
   while (i > 0 || j > 0) {    // findPreviousStep on the borders: i == 0 -> left, j == 0 -> up
-    record(i - 1, j - 1);
+    emit(i == 0 ? 1u : 0u);
     if (i == 0) --j; else --i;
   }
-  const int rem = P & 63;
-  if (rem && lane < rem) { rev_q[P - rem + lane] = aq; rev_r[P - rem + lane] = ar; }
+  const int nw = (P + 15) >> 4;
+  if (P & 15) vacc = lane == ((nw - 1) & 63) ? cacc : vacc;
+  if (nw > 0 && (nw & 63) != 0) {
+    const int base = (nw - 1) & ~63;
+    if (lane < nw - base) codes[base + lane] = vacc;
+  }
   if (lane == 0) *plen = P;
 }
 
@@ -500,16 +528,44 @@ __device__ __forceinline__ double cn_at(const double* Cn, int64_t S, int64_t i, 
 }
 }  // namespace
 
-// path cost C[i][j] - C[i-1][j-1] (0 on the borders), forward order (dtw.go:170-173)
-__global__ void dtw_path_cost_kernel(const double* Cn, int64_t S, const int32_t* rev_q, const int32_t* rev_r,
-                                     int64_t P, int32_t* pq, int32_t* pr, double* pc) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= P) return;
-  const int64_t src = P - 1 - k;
-  const int64_t qi = rev_q[src], ri = rev_r[src];   // i-1, j-1
-  double c = 0.0;
-  if (qi >= 0 && ri >= 0) c = __dsub_rn(cn_at(Cn, S, qi + 1, ri + 1), cn_at(Cn, S, qi, ri));
-  pq[k] = (int32_t)qi; pr[k] = (int32_t)ri; pc[k] = c;
+// Path points and costs from the walk's moves (dtw.go:165-188): one block; each
+// thread replays a contiguous run of moves from the exclusive prefix sum of the
+// earlier runs' (di, dj).  Point k of the walk is (i_k - 1, j_k - 1) with cost
+// C[i][j] - C[i-1][j-1] (0 on the borders); output is in forward order (index P-1-k).
+__global__ __launch_bounds__(1024) void dtw_path_decode_kernel(const uint32_t* codes, int64_t P, int64_t nq,
+                                                               int64_t nr, const double* Cn, int64_t S, int32_t* pq,
+                                                               int32_t* pr, double* pc) {
+  __shared__ int64_t wsum[2][16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t seg = (P + 1023) / 1024;
+  const int64_t k0 = t * seg < P ? t * seg : P, k1 = (t + 1) * seg < P ? (t + 1) * seg : P;
+  auto code_at = [&](int64_t k) -> uint32_t { return (codes[k >> 4] >> ((k & 15) << 1)) & 3u; };
+  int64_t di = 0, dj = 0;
+  for (int64_t k = k0; k < k1; ++k) {
+    const uint32_t c = code_at(k);
+    di += c != 1u;
+    dj += c != 0u;
+  }
+  // block exclusive scan of (di, dj)
+  int64_t si = di, sj = dj;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t ui = __shfl_up(si, o, 64), uj = __shfl_up(sj, o, 64);
+    if (lane >= o) { si += ui; sj += uj; }
+  }
+  if (lane == 63) { wsum[0][wv] = si; wsum[1][wv] = sj; }
+  __syncthreads();
+  int64_t oi = 0, oj = 0;
+  for (int w = 0; w < wv; ++w) { oi += wsum[0][w]; oj += wsum[1][w]; }
+  int64_t i = nq - (oi + si - di), j = nr - (oj + sj - dj);
+  for (int64_t k = k0; k < k1; ++k) {
+    const int64_t f = P - 1 - k;
+    double c = 0.0;
+    if (i > 0 && j > 0) c = __dsub_rn(cn_at(Cn, S, i, j), cn_at(Cn, S, i - 1, j - 1));
+    pq[f] = (int32_t)(i - 1); pr[f] = (int32_t)(j - 1); pc[f] = c;
+    const uint32_t m = code_at(k);
+    i -= m != 1u;
+    j -= m != 0u;
+  }
 }
 
 // costMatrix[1:] row-major: block = one band x 64 columns, staged through LDS so
@@ -556,8 +612,8 @@ int64_t dtw_cn_index(const DtwGeom& g, int64_t i, int64_t j) {
 }
 
 int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, const DtwGeom& g, double* Cn,
-               uint32_t* Dn, uint64_t* E, int32_t* sync_words, int32_t* rev_q, int32_t* rev_r, int64_t* plen,
-               uint64_t* trace, hipStream_t s) {
+               uint32_t* Dn, uint64_t* E, int32_t* sync_words, uint32_t* codes, int64_t* plen, uint64_t* trace,
+               hipStream_t s) {
   if (hipMemsetAsync(sync_words, 0, 2 * sizeof(int32_t), s) != hipSuccess) return -5;
   if (g.nb > 1 && hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, dtw_edge_bytes(g) / 4, s) != hipSuccess) return -5;
   DtwArgs a{q, r, dim, band, g.nq, g.nr, g.nb, g.S, g.SW, Cn, Dn, reinterpret_cast<uint64_t*>(E), sync_words,
@@ -577,15 +633,14 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
   else if (dim == 1) SONAR_DTW_LAUNCH(1);
   else SONAR_DTW_LAUNCH(0);
 #undef SONAR_DTW_LAUNCH
-  hipLaunchKernelGGL(dtw_walk_kernel, dim3(1), dim3(64), 0, s, Dn, g.nq, g.nr, g.SW, rev_q, rev_r, plen);
+  hipLaunchKernelGGL(dtw_walk_kernel, dim3(1), dim3(64), 0, s, Dn, g.nq, g.nr, g.SW, codes, plen);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const int32_t* rev_q, const int32_t* rev_r, int64_t P,
-                         int32_t* pq, int32_t* pr, double* pc, hipStream_t s) {
+int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const uint32_t* codes, int64_t P, int32_t* pq,
+                         int32_t* pr, double* pc, hipStream_t s) {
   if (P <= 0) return 0;
-  hipLaunchKernelGGL(dtw_path_cost_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, Cn, g.S, rev_q, rev_r,
-                     P, pq, pr, pc);
+  hipLaunchKernelGGL(dtw_path_decode_kernel, dim3(1), dim3(1024), 0, s, codes, P, g.nq, g.nr, Cn, g.S, pq, pr, pc);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

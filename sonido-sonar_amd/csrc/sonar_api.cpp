@@ -503,10 +503,9 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
   uint64_t* E = (uint64_t*)dbuf(c, "dtw.E", sonar::dtw_edge_bytes(g));
   int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", 16);
   const int64_t cap = nq + nr + 1;
-  int32_t* rq = (int32_t*)dbuf(c, "dtw.rq", cap * 4);
-  int32_t* rr = (int32_t*)dbuf(c, "dtw.rr", cap * 4);
+  uint32_t* codes = (uint32_t*)dbuf(c, "dtw.codes", ((cap + 1023) / 1024) * 64 * 4);
   int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
-  if (!Cn || !Dn || !E || !sync || !rq || !rr || !pl)
+  if (!Cn || !Dn || !E || !sync || !codes || !pl)
     return fail(c, SONAR_ERR_NOMEM, "device allocation failed (cost matrix)");
   // math.Min's NaN / -Inf / -0 rules only matter when an input is not finite
   bool fast = true;
@@ -526,7 +525,7 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
   const char* trace_path = std::getenv("SONAR_DTW_TRACE");
   uint64_t* trace = trace_path ? (uint64_t*)dbuf(c, "dtw.trace", (size_t)g.nb * 32) : nullptr;
   hipEvent_t tend = timed_begin(c, s);
-  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, rq, rr, pl, trace, s) != 0)
+  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, codes, pl, trace, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
   timed_end(c, s, tend);
   if (trace) {
@@ -548,7 +547,7 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
     oc = (double*)dbuf(c, "dtw.pc", cap * 8);
     if (!oq || !orr || !oc) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (path)");
   }
-  if (sonar::launch_dtw_path_cost(Cn, g, rq, rr, P, oq, orr, oc, s) != 0)
+  if (sonar::launch_dtw_path_cost(Cn, g, codes, P, oq, orr, oc, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw path launch failed");
   double cNM = 0;
   HIP_TRY(c, hipMemcpyAsync(&cNM, Cn + sonar::dtw_cn_index(g, nq, nr), 8, hipMemcpyDeviceToHost, s));
