@@ -167,6 +167,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.enable_kernel_timing(False)
     kernel_ms = ctx.last_kernel_ms()
+    kernel_name = ctx.last_fp_kernel()
     elapsed = max_over_ranks(elapsed, world)
     ms_per_step = elapsed / args.steps * 1e3
     value = F_total / (elapsed / args.steps)
@@ -214,7 +215,7 @@ def main():
                    "samples_rank0": n, "parallelism": f"frame-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS,
-                     "traffic": traffic, "kernel": "fp_wave_kernel<float,float,8,false>", "kernel_ms": kernel_ms,
+                     "traffic": traffic, "kernel": kernel_name, "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_frame": BYTES_PER_FRAME,
                      "valu_tflops": F * FLOPS_PER_FRAME / (kernel_ms * 1e-3) / 1e12,
                      "valu_frac": F * FLOPS_PER_FRAME / (kernel_ms * 1e-3) / 1e12 / FP32_PEAK_TFS},

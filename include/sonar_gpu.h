@@ -81,7 +81,8 @@ enum {
   SONAR_FP_MAGNITUDE = 1u << 1, /* out->magnitude  F x (W/2+1)  (SpectrogramResult)  */
   SONAR_FP_SPECTRAL = 1u << 2,  /* centroid..slope, flux (F-1), low/high energy ratio */
   SONAR_FP_ZCR = 1u << 3,       /* out->zcr        F, on the pre-emphasised PCM       */
-  SONAR_FP_ENERGY = 1u << 4     /* out->energy     sonar_energy_frames(), pre-emphasised */
+  SONAR_FP_ENERGY = 1u << 4,    /* out->energy     sonar_energy_frames(), pre-emphasised */
+  SONAR_FP_GENERIC = 1u << 30   /* force the general fused kernel (A/B checks of the f32 MFCC path) */
 };
 
 typedef struct sonar_ctx sonar_ctx;
@@ -99,6 +100,9 @@ int sonar_synchronize(sonar_ctx* ctx);
  * the last call, measured with HIP events on the stream it ran on (bench). */
 int sonar_last_kernel_ms(sonar_ctx* ctx, double* ms);
 int sonar_enable_kernel_timing(sonar_ctx* ctx, int on);
+/* Name of the fused path-A kernel the last sonar_fingerprint call launched
+ * ("mfcc_pair_kernel" or "fp_wave_kernel"; "" if none) -- diagnostics. */
+const char* sonar_last_fp_kernel(sonar_ctx* ctx);
 
 /* ---- sizes (same integer rules as the Go code) ------------------------ */
 /* (n - W)/H + 1, Go truncating division; <= 0 -> SONAR_ERR_TOO_SHORT

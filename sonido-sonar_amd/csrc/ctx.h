@@ -22,6 +22,17 @@ struct FpTables {
   int n_mels = 0, n_mfcc = 0, nnz = 0;
 };
 
+// tables of the headline kernel (mfcc_pair.hip); ok = false -> configuration unsupported there
+struct PairTables {
+  bool ok = false;
+  float* window = nullptr;
+  void *tw1 = nullptr, *tw2 = nullptr, *chunk_w = nullptr;
+  int* chunk_ks = nullptr;
+  uint16_t* mel_src = nullptr;
+  float* dct = nullptr;
+  int J = 0, NMP = 0, n_mels = 0, n_mfcc = 0, max_src = 0;
+};
+
 struct sonar_ctx {
   int device = 0;
   hipStream_t own = nullptr;
@@ -29,6 +40,7 @@ struct sonar_ctx {
   std::string err;
   std::map<std::string, DevBuf> bufs;
   std::map<std::string, FpTables> fp_tables;
+  std::map<std::string, PairTables> pair_tables;
   struct ChromaT { void* win; void* trig; void* map; };
   std::map<std::string, ChromaT> chroma_tables;
   bool timing = false;
@@ -37,6 +49,7 @@ struct sonar_ctx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   size_t ev_used = 0;
   double last_ms = 0.0;
+  const char* last_fp_kernel = "";
 };
 
 struct sonar_result {

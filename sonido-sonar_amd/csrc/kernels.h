@@ -51,6 +51,33 @@ struct FpParams {
 };
 
 int launch_fingerprint(const FpParams& p, int precision_f64, hipStream_t s);
+
+// Headline fused kernel (mfcc_pair.hip): float32, W = 1024, MFCC output only.
+// One wave transforms two consecutive frames as one 1024-point complex FFT.
+struct MfccPairParams {
+  const float* pcm;     // device f32
+  int64_t n;            // samples
+  int64_t F;            // STFT frames
+  int H;                // hop
+  int64_t pairs_per_wave;
+  const float* window;  // [1024]
+  const float2* tw1;    // [64][16]  w_1024^{b k1}
+  const float2* tw2;    // [8][8]    w_64^{b0 c0}
+  const int* chunk_ks;  // [64] first bin of each lane's filterbank chunk
+  const float2* chunk_w;   // [64][J] (weight of slot a, weight of slot b), 1/4 (or 1/16) folded
+  const uint16_t* mel_src; // [64][16] partial-sum float2 index (2 lane + slot), bit 15 = unused
+  const float* dct;     // [16][NMP] DCT-II rows with the lifter folded in
+  int J;                // bins per chunk (<= 16)
+  int max_src;          // most partial sums of one filter (<= 16)
+  int NMP;              // n_mels padded to a multiple of 8 (<= 64)
+  int n_mels, n_mfcc;   // n_mfcc <= 16
+  int pow2;             // F5: MFCC.Compute fed |X|^2 -> filterbank of |X|^4
+  float* out;           // [F][n_mfcc]
+  int lds_src, lds_dct, lds_wave0, lds_bytes;
+};
+int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s);
+int mfcc_pair_wave_bytes();
+int mfcc_pair_rows();
 bool fingerprint_supported(int W);
 int fp_batch_frames(int W);
 int fp_pre_rows(int W, int spec);

@@ -86,6 +86,105 @@ void* upload_real(const std::vector<double>& v, bool f64) {
 
 int64_t go_frames(int64_t n, int W, int H) { return (n - W) / H + 1; }
 
+// Tables of the headline kernel (mfcc_pair.hip).  The filterbank is cut into
+// per-lane chunks: a run of consecutive bins whose nonzero filters are the same
+// pair (a, b) (a triangle bank has exactly the rising edge of filter j and the
+// falling edge of filter j-1 over [p_j, p_{j+1}), mel_scale.go:65-83), split
+// into pieces of at most J bins; every filter then sums the partials of its
+// chunks in ascending-bin order.  Returns false when the bank does not fit
+// (more than 2 filters on one bin, > 64 chunks at J = 16, > 8 chunks per filter).
+bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
+  const int W = 1024, K = W / 2 + 1;
+  std::vector<double> win;
+  if (!sonar::host::make_window(cfg->window_type, W, true, true, 8.6, 0.5, win)) return false;
+  sonar::host::MfccTables mt;
+  if (!sonar::host::make_mfcc_tables(cfg->sample_rate, cfg->n_mfcc, cfg->n_filters, cfg->filterbank, cfg->low_freq,
+                                     cfg->high_freq, cfg->use_lifter != 0, cfg->lifter, W, mt))
+    return false;
+  if (mt.n_mfcc > 16 || mt.n_mels > 64) return false;
+  auto weight = [&](int m, int k) -> double {
+    return (k >= mt.lo[m] && k < mt.hi[m]) ? mt.w[mt.woff[m] + (k - mt.lo[m])] : 0.0;
+  };
+  // runs of bins whose nonzero filters fit in one pair {a, b}: a run may grow from one filter
+  // to two (the zero-weight rising start k = l of a triangle opens the run of [l, c)), never
+  // shrink (a one-filter tail after a two-filter run starts a run of its own)
+  struct Seg { int k0, k1, a, b; };
+  std::vector<Seg> segs;
+  for (int k = 0; k < K; k++) {
+    int act[3], na = 0;
+    for (int m = 0; m < mt.n_mels; m++)
+      if (k >= mt.lo[m] && k < mt.hi[m]) { if (na == 2) return false; act[na++] = m; }
+    if (na == 0) continue;
+    if (!segs.empty() && segs.back().k1 == k) {
+      Seg& g = segs.back();
+      int u[2] = {g.a, g.b}, nu = g.b >= 0 ? 2 : 1;
+      bool fits = true;
+      if (na < nu) fits = false;
+      for (int i = 0; i < na && fits; i++) {
+        bool in = false;
+        for (int j = 0; j < nu; j++) in |= (u[j] == act[i]);
+        if (!in) { if (nu == 2) { fits = false; break; } u[nu++] = act[i]; }
+      }
+      if (fits) {
+        g.k1 = k + 1;
+        if (nu == 2) { g.a = std::min(u[0], u[1]); g.b = std::max(u[0], u[1]); }
+        continue;
+      }
+    }
+    segs.push_back({k, k + 1, act[0], na > 1 ? act[1] : -1});
+  }
+  int J = 1;
+  for (;; J++) {
+    if (J > 16) return false;
+    size_t n = 0;
+    for (auto& g : segs) n += (g.k1 - g.k0 + J - 1) / J;
+    if (n <= 64) break;
+  }
+  const double scale = cfg->mfcc_input_power ? 1.0 / 16.0 : 0.25;   // |2X|^2 or |2X|^4 from the pair split
+  std::vector<int> ks(64, 0);
+  std::vector<float> cw(64 * 2 * J, 0.f);
+  std::vector<std::vector<int>> src(64);
+  int lane = 0;
+  for (auto& g : segs)
+    for (int k0 = g.k0; k0 < g.k1; k0 += J, lane++) {
+      ks[lane] = k0;
+      for (int i = 0; i < J && k0 + i < g.k1; i++) {
+        cw[(lane * J + i) * 2] = (float)(weight(g.a, k0 + i) * scale);
+        cw[(lane * J + i) * 2 + 1] = g.b >= 0 ? (float)(weight(g.b, k0 + i) * scale) : 0.f;
+      }
+      src[g.a].push_back(2 * lane);
+      if (g.b >= 0) src[g.b].push_back(2 * lane + 1);
+    }
+  std::vector<uint16_t> msrc(64 * 16, 0x8000);
+  int max_src = 1;
+  for (int m = 0; m < mt.n_mels; m++) {
+    if (src[m].size() > 16) return false;
+    max_src = std::max(max_src, (int)src[m].size());
+    for (size_t i = 0; i < src[m].size(); i++) msrc[m * 16 + i] = (uint16_t)src[m][i];
+  }
+  const int NMP = (mt.n_mels + 7) / 8 * 8;
+  std::vector<float> dct(16 * NMP, 0.f);
+  for (int q = 0; q < mt.n_mfcc; q++)
+    for (int m = 0; m < mt.n_mels; m++) dct[q * NMP + m] = (float)(mt.dct[(size_t)q * mt.n_mels + m] * mt.lift[q]);
+  std::vector<float> tw1(64 * 16 * 2), tw2(64 * 2), wf(win.begin(), win.end());
+  for (int b = 0; b < 64; b++)
+    for (int k = 0; k < 16; k++) {
+      const double a = -2.0 * M_PI * (double)((b * k) % 1024) / 1024.0;
+      tw1[(b * 16 + k) * 2] = (float)std::cos(a); tw1[(b * 16 + k) * 2 + 1] = (float)std::sin(a);
+    }
+  for (int b = 0; b < 8; b++)
+    for (int c = 0; c < 8; c++) {
+      const double a = -2.0 * M_PI * (double)(b * c) / 64.0;
+      tw2[(b * 8 + c) * 2] = (float)std::cos(a); tw2[(b * 8 + c) * 2 + 1] = (float)std::sin(a);
+    }
+  t.window = (float*)upload(wf); t.tw1 = upload(tw1); t.tw2 = upload(tw2);
+  t.chunk_ks = (int*)upload(ks); t.chunk_w = upload(cw); t.mel_src = (uint16_t*)upload(msrc);
+  t.dct = (float*)upload(dct);
+  t.J = J; t.NMP = NMP; t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc; t.max_src = max_src;
+  t.ok = t.window && t.tw1 && t.tw2 && t.chunk_ks && t.chunk_w && t.mel_src && t.dct;
+  return t.ok;
+}
+
 
 }  // namespace
 
@@ -152,6 +251,8 @@ int sonar_enable_kernel_timing(sonar_ctx* c, int on) {
   c->timing = on != 0;
   return SONAR_OK;
 }
+
+const char* sonar_last_fp_kernel(sonar_ctx* c) { return c ? c->last_fp_kernel : ""; }
 
 int sonar_last_kernel_ms(sonar_ctx* c, double* ms) {
   if (!c || !ms) return SONAR_ERR_INVALID;
@@ -261,7 +362,48 @@ int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_c
     }
   }
 
-  if (need_fft) {
+  // headline path: float32 MFCC only at W = 1024 (mfcc_pair.hip); SONAR_FP_GENERIC forces fp_kernel.hip
+  const bool pair_ok = need_fft && !f64 && !pcm64 && !o64 && W == 1024 && (flags & SONAR_FP_MFCC) &&
+                       !(flags & (SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_GENERIC | 0x80000000u));
+  bool pair_done = false;
+  c->last_fp_kernel = "";
+  if (pair_ok) {
+    char key[512];
+    std::snprintf(key, sizeof(key), "%d|%d|%d|%d|%.17g|%.17g|%d|%.17g|%d|%d", cfg->window_type, cfg->sample_rate,
+                  cfg->n_mfcc, cfg->n_filters, cfg->low_freq, cfg->high_freq, cfg->use_lifter, cfg->lifter,
+                  cfg->filterbank, cfg->mfcc_input_power);
+    auto it = c->pair_tables.find(key);
+    if (it == c->pair_tables.end()) {
+      PairTables t;
+      build_pair_tables(cfg, t);
+      it = c->pair_tables.emplace(key, t).first;
+    }
+    const PairTables& t = it->second;
+    if (t.ok) {
+      sonar::MfccPairParams q{};
+      q.pcm = (const float*)dpcm; q.n = n; q.F = F; q.H = H;
+      q.window = t.window; q.tw1 = (const float2*)t.tw1; q.tw2 = (const float2*)t.tw2;
+      q.chunk_ks = t.chunk_ks; q.chunk_w = (const float2*)t.chunk_w; q.mel_src = t.mel_src; q.dct = t.dct;
+      q.J = t.J; q.max_src = t.max_src; q.NMP = t.NMP; q.n_mels = t.n_mels; q.n_mfcc = t.n_mfcc; q.pow2 = cfg->mfcc_input_power != 0;
+      q.out = (float*)d_mfcc;
+      auto al = [](int x) { return (x + 15) & ~15; };
+      q.lds_src = al(64 * t.J * 8);
+      q.lds_dct = q.lds_src + 64 * 16 * 2;
+      q.lds_wave0 = q.lds_dct + al(16 * t.NMP * 4);
+      q.lds_bytes = q.lds_wave0 + 4 * sonar::mfcc_pair_wave_bytes();
+      int dev_cus = 256;
+      hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
+      const int64_t NP = (F + 1) / 2, target_waves = (int64_t)dev_cus * 12;
+      q.pairs_per_wave = std::max<int64_t>(1, (NP + target_waves - 1) / target_waves);
+      hipEvent_t tend = timed_begin(c, s);
+      if (sonar::launch_mfcc_pair(q, s) != 0)
+        return fail(c, SONAR_ERR_DEVICE, std::string("mfcc kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+      timed_end(c, s, tend);
+      pair_done = true;
+      c->last_fp_kernel = "mfcc_pair_kernel";
+    }
+  }
+  if (need_fft && !pair_done) {
     const bool spec = (flags & SONAR_FP_SPECTRAL) != 0;
     const int NB = sonar::fp_batch_frames(W);
     const int PRE = sonar::fp_pre_rows(W, spec);
@@ -332,6 +474,7 @@ int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_c
     p.frames_per_wave = fpw;
     hipEvent_t tend = timed_begin(c, s);
     const int rc = sonar::launch_fingerprint(p, f64, s);
+    c->last_fp_kernel = "fp_wave_kernel";
     if (rc != 0) return fail(c, SONAR_ERR_DEVICE, std::string("fingerprint kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     timed_end(c, s, tend);
   }

@@ -28,6 +28,7 @@ from ._abi import (  # noqa: F401
     FP_SPECTRAL,
     FP_ZCR,
     FP_ENERGY,
+    FP_GENERIC,
     F32,
     F64,
     EXPORTED_SYMBOLS,

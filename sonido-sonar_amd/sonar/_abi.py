@@ -15,6 +15,7 @@ HEADER = os.path.join(_REPO, "include", "sonar_gpu.h")
 
 OK, ERR_INVALID, ERR_TOO_SHORT, ERR_EMPTY, ERR_UNSUPPORTED, ERR_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4, -5, -6
 FP_MFCC, FP_MAGNITUDE, FP_SPECTRAL, FP_ZCR, FP_ENERGY = 1, 2, 4, 8, 16
+FP_GENERIC = 1 << 30   # force the general fused kernel (A/B checks of the f32 MFCC path)
 F32, F64 = 0, 1
 WINDOWS = {"hann": 0, "hamming": 1, "blackman": 2, "blackman_harris": 3, "kaiser": 4,
            "tukey": 5, "rectangular": 6, "bartlett": 7, "welch": 8}
@@ -100,6 +101,8 @@ def lib():
     L.sonar_synchronize.argtypes = [_vp]
     L.sonar_last_kernel_ms.argtypes = [_vp, _d]
     L.sonar_enable_kernel_timing.argtypes = [_vp, C.c_int]
+    L.sonar_last_fp_kernel.argtypes = [_vp]
+    L.sonar_last_fp_kernel.restype = C.c_char_p
     for f in ("sonar_stft_frames", "sonar_energy_frames"):
         getattr(L, f).argtypes = [C.c_int64, C.c_int32, C.c_int32]
         getattr(L, f).restype = C.c_int64
@@ -208,6 +211,10 @@ class Context:
         v = C.c_double()
         self._check(self._L.sonar_last_kernel_ms(self._h, C.byref(v)))
         return v.value
+
+    def last_fp_kernel(self):
+        """Name of the fused kernel the last fingerprint call launched (diagnostics)."""
+        return self._L.sonar_last_fp_kernel(self._h).decode()
 
     # -- path A ------------------------------------------------------------
     @staticmethod

@@ -1,0 +1,108 @@
+"""Headline kernel (mfcc_pair.hip): float32 STFT(1024) -> mel -> ln -> DCT-II -> lifter,
+two frames per 1024-point complex FFT.  Parity against the fp64 oracle (the C restatement
+of analyzers/spectral.go:385-545 + spectral/mfcc.go:113-245) on the configurations that
+route to it (f32 PCM, f32 output, MFCC only, W = 1024), and against the general fused
+kernel (SONAR_FP_GENERIC) on the same input.
+
+Tolerance (north_star: float features within 1e-4 relative): 1e-4 of the frame's MFCC
+L2 norm -- the near-zero coefficients c1..c12 carry rounding of the large c0, so a
+per-coefficient relative bound is not meaningful in f32."""
+import numpy as np
+import pytest
+
+import oracle as O
+import sonar
+from sonar import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(ctx, **kw):
+    base = dict(window_size=1024, hop_size=256, sample_rate=44100, n_filters=40, n_mfcc=13,
+                precision=sonar.F32, pcm_dtype=sonar.F32, out_dtype=sonar.F32)
+    base.update(kw)
+    return ctx.config(**base)
+
+
+def _ref(x, H=256, sr=44100, nm=40, nc=13, power=False, win="hann"):
+    mag = O.stft_mag(x.astype(np.float64), 1024, H, window_type=win, nthreads=8)
+    return O.mfcc_frames(mag ** 2 if power else mag, sr, n_coef=nc, n_mels=nm)
+
+
+def _fp(ctx, x, cfg, kernel="mfcc_pair_kernel"):
+    out = ctx.fingerprint(x, cfg)["mfcc"]
+    assert ctx.last_fp_kernel() == kernel
+    return out
+
+
+def _err(got, ref):
+    return np.max(np.abs(got.astype(np.float64) - ref) / np.maximum(np.linalg.norm(ref, axis=1), 1e-30)[:, None])
+
+
+@pytest.mark.parametrize("seconds", [0.1, 1.0, 7.3])
+@pytest.mark.parametrize("H", [256, 100, 1000, 512])
+def test_pair_kernel_matches_oracle(ctx, seconds, H):
+    x = synth.c2_hour(seconds=seconds)
+    got = _fp(ctx, x, _cfg(ctx, hop_size=H))
+    ref = _ref(x, H=H)
+    assert got.shape == ref.shape
+    assert _err(got, ref) < 1e-4
+
+
+@pytest.mark.parametrize("n_extra", [0, 1, 255, 256, 257, 511])
+def test_odd_even_frame_counts(ctx, n_extra):
+    """F odd -> the last pair carries one frame; every frame count around a pair boundary."""
+    x = synth.c2_hour(seconds=0.5)[: 1024 + 256 * 40 + n_extra]
+    got = _fp(ctx, x, _cfg(ctx))
+    ref = _ref(x)
+    assert got.shape == ref.shape == (sonar.stft_frames(len(x), 1024, 256), 13)
+    assert _err(got, ref) < 1e-4
+
+
+@pytest.mark.parametrize("sr,nm,nc", [(44100, 26, 13), (44100, 40, 13), (22050, 32, 16), (48000, 64, 13),
+                                      (16000, 26, 12), (44100, 20, 1)])
+def test_filterbank_shapes(ctx, sr, nm, nc):
+    x = synth.c2_hour(seconds=2.0)
+    # 64 mels at 48 kHz needs > 64 filterbank chunks: served by the general kernel
+    got = _fp(ctx, x, _cfg(ctx, sample_rate=sr, n_filters=nm, n_mfcc=nc),
+              "fp_wave_kernel" if nm == 64 else "mfcc_pair_kernel")
+    ref = _ref(x, sr=sr, nm=nm, nc=nc)
+    assert _err(got, ref) < 1e-4
+
+
+def test_music_power_input_F5(ctx):
+    x = synth.c2_hour(seconds=2.0)
+    got = _fp(ctx, x, _cfg(ctx, mfcc_input_power=1))
+    assert _err(got, _ref(x, power=True)) < 1e-4
+
+
+@pytest.mark.parametrize("win", ["hamming", "blackman", "rectangular"])
+def test_window_types(ctx, win):
+    x = synth.c2_hour(seconds=1.0)
+    got = _fp(ctx, x, _cfg(ctx, window_type=win))
+    assert _err(got, _ref(x, win=win)) < 1e-4
+
+
+def test_sample_rate_zero_constant(ctx):
+    """F1/F2: all-zero filterbank -> every filter ln(1e-10) -> c0 = sqrt(n_mels) ln(1e-10)."""
+    x = synth.sweep(1.0).astype(np.float32)
+    got = _fp(ctx, x, _cfg(ctx, sample_rate=0, n_filters=26))
+    assert np.allclose(got[:, 0], np.sqrt(26) * np.log(1e-10), rtol=0, atol=117.41e-5)
+    assert np.abs(got[:, 1:]).max() < 117.41e-5
+
+
+def test_single_short_frame(ctx):
+    """n in (W-H, W): Go yields one all-zero frame (spectral.go:409, :524-534)."""
+    x = synth.c2_hour(seconds=0.1)[:1000]
+    got = _fp(ctx, x, _cfg(ctx, n_filters=26))
+    assert got.shape == (1, 13)
+    assert abs(got[0, 0] - np.sqrt(26) * np.log(1e-10)) < 1e-3 and np.abs(got[0, 1:]).max() < 1e-3
+
+
+def test_pair_vs_generic_kernel_long(ctx):
+    """60 s (10,332 frames): many pairs per wave; the two device kernels agree."""
+    x = synth.c2_hour(seconds=60.0)
+    a = _fp(ctx, x, _cfg(ctx)).astype(np.float64)
+    b = _fp(ctx, x, _cfg(ctx, flags=sonar.FP_MFCC | sonar.FP_GENERIC), "fp_wave_kernel").astype(np.float64)
+    assert a.shape == b.shape
+    assert _err(a, b) < 1e-4

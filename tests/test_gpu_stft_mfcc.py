@@ -82,6 +82,7 @@ def test_mfcc_f32_headline_config(ctx):
     cfg = ctx.config(window_size=1024, hop_size=256, sample_rate=44100, n_filters=40, n_mfcc=13,
                      precision=sonar.F32, pcm_dtype=sonar.F32, out_dtype=sonar.F32)
     got = ctx.fingerprint(x, cfg)["mfcc"].astype(np.float64)
+    assert ctx.last_fp_kernel() == "mfcc_pair_kernel"
     ref = O.mfcc_frames(O.stft_mag(x.astype(np.float64), 1024, 256, nthreads=8), 44100, n_coef=13, n_mels=40)
     assert got.shape == ref.shape == (3442, 13)
     assert _rel_rows(got, ref, np.linalg.norm(ref, axis=1)) < 1e-4

@@ -4,14 +4,15 @@ import os, sys, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "sonido-sonar_amd"), ROOT]
 import torch, sonar
-from bench import make_pcm
+from sonar import shard
 dev = torch.device("cuda", 0)
-pcm = make_pcm(float(os.environ.get("SECONDS", "3600")), 0, dev)
+pcm = shard.stream_pcm(0, int(float(os.environ.get("SECONDS", "3600")) * 44100), device=dev)
 n = pcm.numel()
 ctx = sonar.Context(0)
 ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
 variants = {
     "mfcc": dict(flags=sonar.FP_MFCC),
+    "mfcc_generic": dict(flags=sonar.FP_MFCC | sonar.FP_GENERIC),
     "fft_only": dict(flags=sonar.FP_MFCC | (1 << 31)),
     "mfcc+spectral": dict(flags=sonar.FP_MFCC | sonar.FP_SPECTRAL),
     "mfcc_w2048": dict(flags=sonar.FP_MFCC, window_size=2048, hop_size=512),
@@ -40,4 +41,4 @@ for name in sel:
     torch.cuda.synchronize()
     ctx.enable_kernel_timing(False)
     ms = ctx.last_kernel_ms()
-    print(json.dumps({"variant": name, "frames": F, "kernel_ms": round(ms, 4), "Mframes_per_s": round(F / ms / 1e3, 1)}), flush=True)
+    print(json.dumps({"variant": name, "kernel": ctx.last_fp_kernel(), "frames": F, "kernel_ms": round(ms, 4), "Mframes_per_s": round(F / ms / 1e3, 1)}), flush=True)
