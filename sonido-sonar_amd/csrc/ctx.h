@@ -30,7 +30,7 @@ struct PairTables {
   int* chunk_ks = nullptr;
   uint16_t* mel_src = nullptr;
   float* dct = nullptr;
-  int J = 0, NMP = 0, n_mels = 0, n_mfcc = 0, max_src = 0;
+  int J = 0, JS = 0, NMP = 0, n_mels = 0, n_mfcc = 0, max_src = 0;
 };
 
 struct sonar_ctx {

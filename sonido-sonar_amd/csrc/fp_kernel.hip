@@ -79,9 +79,11 @@ __device__ __forceinline__ void dft_reg(T (&re)[N], T (&im)[N]) {
   }
 }
 
-// orders LDS traffic of one wave (cross-lane exchange through LDS)
+// orders LDS traffic of one wave (cross-lane exchange through LDS): fence + wave barrier pin
+// the DS ops in place; the explicit lgkmcnt(0) retires them before the next phase (defensive).
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 }
 

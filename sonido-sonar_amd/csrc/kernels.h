@@ -64,10 +64,11 @@ struct MfccPairParams {
   const float2* tw1;    // [64][16]  w_1024^{b k1}
   const float2* tw2;    // [8][8]    w_64^{b0 c0}
   const int* chunk_ks;  // [64] first bin of each lane's filterbank chunk
-  const float2* chunk_w;   // [64][J] (weight of slot a, weight of slot b), 1/4 (or 1/16) folded
-  const uint16_t* mel_src; // [64][16] partial-sum float2 index (2 lane + slot), bit 15 = unused
-  const float* dct;     // [16][NMP] DCT-II rows with the lifter folded in
+  const float2* chunk_w;   // [64][JS] (weight of slot a, weight of slot b), 1/4 (or 1/16) folded
+  const uint16_t* mel_src; // [16][64] partial-sum float2 index (2 lane + slot), bit 15 = unused
+  const float* dct;     // [16][NMP + 4] DCT-II rows with the lifter folded in
   int J;                // bins per chunk (<= 16)
+  int JS;               // chunk_w row stride = J | 1 (odd: conflict-free b64 reads)
   int max_src;          // most partial sums of one filter (<= 16)
   int NMP;              // n_mels padded to a multiple of 8 (<= 64)
   int n_mels, n_mfcc;   // n_mfcc <= 16

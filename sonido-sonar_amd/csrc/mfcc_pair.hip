@@ -110,10 +110,23 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
 }
 // register bit <-> lane bit 3 (lane ^ 8 = row_ror:8 inside each 16-lane row) for 4 pairs:
 // a' = bit3 ? ror8(b) : a,  b' = bit3 ? b : ror8(a), as v_cndmask_b32 with a DPP source
-// (VOP2 reads its mask from VCC, set here; s_nop 1 covers the VALU-write -> DPP-read hazard)
+// (VOP2 reads its mask from VCC, set here; s_nop 1 covers the VALU-write -> DPP-read hazard).
+// The leading s_nop 4 keeps any in-flight VALU write of VCC from before the block off the mask.
 __device__ __forceinline__ void swap8x4(float (&a)[4], float (&b)[4], uint64_t m_lo, uint64_t m_hi) {
+#ifdef SONAR_SWAP8_BUILTIN   // compiler-managed form (4 VALU per pair and plane instead of 2)
+  const bool hi = (__lane_id() & 8) != 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const float ra = f_of((uint32_t)__builtin_amdgcn_update_dpp(0, (int)u_of(a[i]), 0x128, 0xf, 0xf, false));
+    const float rb = f_of((uint32_t)__builtin_amdgcn_update_dpp(0, (int)u_of(b[i]), 0x128, 0xf, 0xf, false));
+    const float na = hi ? rb : a[i], nb = hi ? b[i] : ra;
+    a[i] = na; b[i] = nb;
+  }
+  return;
+#endif
   float na[4], nb[4];
   asm volatile(
+      "s_nop 4\n\t"
       "s_mov_b64 vcc, %[mlo]\n\t"
       "s_nop 1\n\t"
       "v_cndmask_b32_dpp %[na0], %[b0], %[a0], vcc row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
@@ -134,8 +147,12 @@ __device__ __forceinline__ void swap8x4(float (&a)[4], float (&b)[4], uint64_t m
   for (int i = 0; i < 4; i++) { a[i] = na[i]; b[i] = nb[i]; }
 }
 
+// Phase boundary of the wave-private LDS exchanges: the fence and wave barrier keep the
+// compiler from moving DS ops across it; the explicit lgkmcnt(0) retires every DS op of the
+// phase before the next phase reads other lanes' words (defensive; costs < 2 % here).
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -147,7 +164,11 @@ constexpr int kT2Irreg[2][8] = {
 
 constexpr int kT2Stride = 136;          // bytes per lane row of the T2 buffer (17 float2)
 constexpr int kWaveBytes = 64 * kT2Stride;
-constexpr int kPRows = 528;             // power rows [bin][2 frames]: 513 + chunk over-read padding
+// power rows [bin][2 frames]: bin k at row k + 2 (k >> 4) -- two pad rows per 16 bins make the
+// split's stores (bins k1 + 16 c0 across a lane group) conflict-free; rows cover the chunk
+// over-read up to bin 527; the pad rows take the dummy bin-512 stores of lanes != 63
+__host__ __device__ constexpr int prow(int k) { return k + 2 * (k >> 4); }
+constexpr int kPRows = 600;
 constexpr int kPartOff = kPRows * 8;    // partial sums [64 lanes][a0 a1 b0 b1]
 constexpr int kLogOff = kPartOff + 64 * 16;   // logmel [2][NMP]
 
@@ -160,13 +181,19 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // ---- shared tables -> LDS ---------------------------------------------------
   float2* s_cw = reinterpret_cast<float2*>(smem);                                  // [64][J] (wa, wb)
-  uint16_t* s_src = reinterpret_cast<uint16_t*>(smem + p.lds_src);                 // [64][16] partial float2 idx
-  float* s_dct = reinterpret_cast<float*>(smem + p.lds_dct);                       // [16][NMP], lifter folded
-  for (int i = threadIdx.x; i < 64 * p.J; i += blockDim.x) s_cw[i] = p.chunk_w[i];
+  uint16_t* s_src = reinterpret_cast<uint16_t*>(smem + p.lds_src);                 // [16][64] partial float2 idx
+  float* s_dct = reinterpret_cast<float*>(smem + p.lds_dct);                       // [16][NMP + 4], lifter folded
+  for (int i = threadIdx.x; i < 64 * p.JS; i += blockDim.x) s_cw[i] = p.chunk_w[i];
   for (int i = threadIdx.x; i < 64 * 16; i += blockDim.x) s_src[i] = p.mel_src[i];
-  for (int i = threadIdx.x; i < 16 * p.NMP; i += blockDim.x) s_dct[i] = p.dct[i];
-  __syncthreads();
+  for (int i = threadIdx.x; i < 16 * (p.NMP + 4); i += blockDim.x) s_dct[i] = p.dct[i];
   unsigned char* wb = smem + p.lds_wave0 + wave * kWaveBytes;
+  // Zero the wave's region once: the filterbank chunks read up to 11 rows past bin 512 with
+  // zero weight, and some of those bytes (the unused 17th float2 of T2 lane rows 33/34) are
+  // never written by this kernel -- stale LDS from an earlier launch can hold NaN/Inf, and
+  // 0 * NaN would turn the last filter into ln(1e-10) (seen in tools/pair_stress2.py).
+  for (int i = lane; i < kWaveBytes / 16; i += 64)
+    *reinterpret_cast<float4*>(wb + 16 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
 
   // ---- per-lane constants ---------------------------------------------------------
   float win[16];
@@ -192,8 +219,8 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   else rA = 0;
   const int rB = (lane == 63) ? 64 : 128 - rA;
   const bool self = (lane == 63);
-  const int pA = rA * 8, pB = rB * 8;                         // power row byte offsets
-  const int p8 = self ? 512 * 8 : (kPRows - 1) * 8;          // slot 8 (bin 512) or a dummy row
+  const int pA = prow(rA) * 8, pB = prow(rB) * 8;             // power row byte offsets (+1152 per 128 bins)
+  const int p8 = 8 * (self ? prow(512) : 18 * (lane & 31) + 16 + (lane >> 5));   // bin 512, or a pad row
   const int ks = p.chunk_ks[lane];                           // mel chunk start bin
   const int nmp = p.NMP;
 
@@ -299,13 +326,13 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       const cf sec = self ? v[(8 - c) & 7] : v[15 - c];        // B[7 - c], or A[(8 - c) & 7] on lane 63
-      pw(v[c], sec, pA + 1024 * c);
+      pw(v[c], sec, pA + 1152 * c);
     }
-    pw(self ? v[12] : v[4], v[11], pB + 3072);                 // (A4, B3) / lane 63: (B4, B3)
+    pw(self ? v[12] : v[4], v[11], pB + 3456);                 // (A4, B3) / lane 63: (B4, B3)
 #pragma unroll
     for (int c = 5; c < 8; c++) {
       const cf fst = self ? v[8 + c] : v[c];                   // lane 63: (B5, B2), (B6, B1), (B7, B0)
-      pw(fst, v[15 - c], pB + 1024 * (7 - c));
+      pw(fst, v[15 - c], pB + 1152 * (7 - c));
     }
     {                                                           // bin 512 (lane 63: (A4, A4))
       const float p0 = v[4].x * v[4].x * 4.f, p1 = v[4].y * v[4].y * 4.f;   // |2 a|^2 -> 4 a^2
@@ -315,11 +342,12 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     // ---- filterbank: lane chunk [ks, ks + J) of one filter pair ----------------------
     {
       float a0 = 0.f, a1 = 0.f, c0 = 0.f, c1 = 0.f;
-      const unsigned char* prow = wb + ks * 8;
-      const float2* cw = s_cw + lane * p.J;
+      const unsigned char* pr = wb + prow(ks) * 8;
+      const int ib = 16 - (ks & 15);                          // first i past a pad pair
+      const float2* cw = s_cw + lane * p.JS;
 #pragma unroll 4
       for (int i = 0; i < p.J; i++) {
-        const float2 pp = *reinterpret_cast<const float2*>(prow + 8 * i);
+        const float2 pp = *reinterpret_cast<const float2*>(pr + 8 * i + (i >= ib ? 16 : 0));
         const float2 w = cw[i];
         a0 += w.x * pp.x; a1 += w.x * pp.y;
         c0 += w.y * pp.x; c1 += w.y * pp.y;
@@ -330,9 +358,8 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     // ---- ln of the filter sums (lane = filter) ----------------------------------------
     if (lane < nmp) {
       float m0 = 0.f, m1 = 0.f;
-      const uint16_t* sl = s_src + 16 * lane;
       for (int i = 0; i < p.max_src; i++) {
-        const uint32_t idx = sl[i];
+        const uint32_t idx = s_src[64 * i + lane];
         const float2 q = *reinterpret_cast<const float2*>(wb + kPartOff + 8 * (idx & 0x7fff));
         const bool use = (idx & 0x8000u) == 0;
         m0 += use ? q.x : 0.f;
@@ -350,7 +377,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       const int q = lane & 15, f = (lane >> 4) & 1, hh = lane >> 5;
       const int half = nmp >> 1;
       const float* lm = reinterpret_cast<const float*>(wb + kLogOff) + f * nmp + hh * half;
-      const float* d = s_dct + q * nmp + hh * half;
+      const float* d = s_dct + q * (nmp + 4) + hh * half;     // row stride NMP + 4: 11 x 16 B slots
       float s = 0.f;
       for (int m = 0; m < half; m += 4) {
         const float4 x = *reinterpret_cast<const float4*>(lm + m);

@@ -141,16 +141,17 @@ bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
     if (n <= 64) break;
   }
   const double scale = cfg->mfcc_input_power ? 1.0 / 16.0 : 0.25;   // |2X|^2 or |2X|^4 from the pair split
+  const int JS = J | 1;
   std::vector<int> ks(64, 0);
-  std::vector<float> cw(64 * 2 * J, 0.f);
+  std::vector<float> cw(64 * 2 * JS, 0.f);
   std::vector<std::vector<int>> src(64);
   int lane = 0;
   for (auto& g : segs)
     for (int k0 = g.k0; k0 < g.k1; k0 += J, lane++) {
       ks[lane] = k0;
       for (int i = 0; i < J && k0 + i < g.k1; i++) {
-        cw[(lane * J + i) * 2] = (float)(weight(g.a, k0 + i) * scale);
-        cw[(lane * J + i) * 2 + 1] = g.b >= 0 ? (float)(weight(g.b, k0 + i) * scale) : 0.f;
+        cw[(lane * JS + i) * 2] = (float)(weight(g.a, k0 + i) * scale);
+        cw[(lane * JS + i) * 2 + 1] = g.b >= 0 ? (float)(weight(g.b, k0 + i) * scale) : 0.f;
       }
       src[g.a].push_back(2 * lane);
       if (g.b >= 0) src[g.b].push_back(2 * lane + 1);
@@ -160,12 +161,13 @@ bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
   for (int m = 0; m < mt.n_mels; m++) {
     if (src[m].size() > 16) return false;
     max_src = std::max(max_src, (int)src[m].size());
-    for (size_t i = 0; i < src[m].size(); i++) msrc[m * 16 + i] = (uint16_t)src[m][i];
+    for (size_t i = 0; i < src[m].size(); i++) msrc[i * 64 + m] = (uint16_t)src[m][i];
   }
   const int NMP = (mt.n_mels + 7) / 8 * 8;
-  std::vector<float> dct(16 * NMP, 0.f);
+  std::vector<float> dct(16 * (NMP + 4), 0.f);
   for (int q = 0; q < mt.n_mfcc; q++)
-    for (int m = 0; m < mt.n_mels; m++) dct[q * NMP + m] = (float)(mt.dct[(size_t)q * mt.n_mels + m] * mt.lift[q]);
+    for (int m = 0; m < mt.n_mels; m++)
+      dct[q * (NMP + 4) + m] = (float)(mt.dct[(size_t)q * mt.n_mels + m] * mt.lift[q]);
   std::vector<float> tw1(64 * 16 * 2), tw2(64 * 2), wf(win.begin(), win.end());
   for (int b = 0; b < 64; b++)
     for (int k = 0; k < 16; k++) {
@@ -180,7 +182,7 @@ bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
   t.window = (float*)upload(wf); t.tw1 = upload(tw1); t.tw2 = upload(tw2);
   t.chunk_ks = (int*)upload(ks); t.chunk_w = upload(cw); t.mel_src = (uint16_t*)upload(msrc);
   t.dct = (float*)upload(dct);
-  t.J = J; t.NMP = NMP; t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc; t.max_src = max_src;
+  t.J = J; t.JS = JS; t.NMP = NMP; t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc; t.max_src = max_src;
   t.ok = t.window && t.tw1 && t.tw2 && t.chunk_ks && t.chunk_w && t.mel_src && t.dct;
   return t.ok;
 }
@@ -384,17 +386,18 @@ int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_c
       q.pcm = (const float*)dpcm; q.n = n; q.F = F; q.H = H;
       q.window = t.window; q.tw1 = (const float2*)t.tw1; q.tw2 = (const float2*)t.tw2;
       q.chunk_ks = t.chunk_ks; q.chunk_w = (const float2*)t.chunk_w; q.mel_src = t.mel_src; q.dct = t.dct;
-      q.J = t.J; q.max_src = t.max_src; q.NMP = t.NMP; q.n_mels = t.n_mels; q.n_mfcc = t.n_mfcc; q.pow2 = cfg->mfcc_input_power != 0;
+      q.J = t.J; q.JS = t.JS; q.max_src = t.max_src; q.NMP = t.NMP; q.n_mels = t.n_mels; q.n_mfcc = t.n_mfcc; q.pow2 = cfg->mfcc_input_power != 0;
       q.out = (float*)d_mfcc;
       auto al = [](int x) { return (x + 15) & ~15; };
-      q.lds_src = al(64 * t.J * 8);
+      q.lds_src = al(64 * t.JS * 8);
       q.lds_dct = q.lds_src + 64 * 16 * 2;
-      q.lds_wave0 = q.lds_dct + al(16 * t.NMP * 4);
+      q.lds_wave0 = q.lds_dct + al(16 * (t.NMP + 4) * 4);
       q.lds_bytes = q.lds_wave0 + 4 * sonar::mfcc_pair_wave_bytes();
       int dev_cus = 256;
       hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
       const int64_t NP = (F + 1) / 2, target_waves = (int64_t)dev_cus * 12;
       q.pairs_per_wave = std::max<int64_t>(1, (NP + target_waves - 1) / target_waves);
+      if (std::getenv("SONAR_DEBUG_SYNC")) hipDeviceSynchronize();
       hipEvent_t tend = timed_begin(c, s);
       if (sonar::launch_mfcc_pair(q, s) != 0)
         return fail(c, SONAR_ERR_DEVICE, std::string("mfcc kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -494,6 +497,7 @@ int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_c
     }
   }
   if (!dev) {
+    if (std::getenv("SONAR_DEBUG_SYNC")) hipDeviceSynchronize();
     for (auto& m : copies) HIP_TRY(c, hipMemcpyAsync(m.host, m.devp, m.bytes, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
   }

@@ -32,11 +32,27 @@ def _ref(x, H=256, sr=44100, nm=40, nc=13, power=False, win="hann"):
 def _fp(ctx, x, cfg, kernel="mfcc_pair_kernel"):
     out = ctx.fingerprint(x, cfg)["mfcc"]
     assert ctx.last_fp_kernel() == kernel
+    again = ctx.fingerprint(x, cfg)["mfcc"]
+    assert np.array_equal(out, again, equal_nan=True), "nondeterministic: " + str(
+        np.nonzero(np.any(out != again, axis=1))[0][:16].tolist())
     return out
 
 
+class _Err(float):
+    """max row-relative error; repr names the worst frames (diagnostics on failure)"""
+    def __new__(cls, got, ref):
+        e = np.max(np.abs(got.astype(np.float64) - ref), axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-30)
+        obj = super().__new__(cls, float(np.max(e)) if not np.isnan(e).any() else float("nan"))
+        bad = np.nonzero(~(e < 1e-4))[0]
+        obj.info = f"{len(bad)} bad of {len(e)} frames: {bad[:16].tolist()} nan={int(np.isnan(got).sum())}"
+        return obj
+
+    def __repr__(self):
+        return f"{float(self)!r} ({self.info})"
+
+
 def _err(got, ref):
-    return np.max(np.abs(got.astype(np.float64) - ref) / np.maximum(np.linalg.norm(ref, axis=1), 1e-30)[:, None])
+    return _Err(got, ref)
 
 
 @pytest.mark.parametrize("seconds", [0.1, 1.0, 7.3])

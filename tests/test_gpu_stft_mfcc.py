@@ -85,7 +85,8 @@ def test_mfcc_f32_headline_config(ctx):
     assert ctx.last_fp_kernel() == "mfcc_pair_kernel"
     ref = O.mfcc_frames(O.stft_mag(x.astype(np.float64), 1024, 256, nthreads=8), 44100, n_coef=13, n_mels=40)
     assert got.shape == ref.shape == (3442, 13)
-    assert _rel_rows(got, ref, np.linalg.norm(ref, axis=1)) < 1e-4
+    e = np.max(np.abs(got - ref), axis=1) / np.linalg.norm(ref, axis=1)
+    assert e.max() < 1e-4, (np.nonzero(~(e < 1e-4))[0][:16].tolist(), int((~(e < 1e-4)).sum()))
 
 
 def test_mfcc_sample_rate_zero_constant(ctx):
