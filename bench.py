@@ -89,14 +89,15 @@ def make_shard(seconds, world, rank, device):
     return pcm, F_total, f1 - f0, counts
 
 
-def load_traffic():
-    """Per-launch HBM bytes of the fused kernel from the committed rocprofv3 PMC summary."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return d.get("fp_wave_kernel_hbm_bytes_per_launch")
+def load_traffic(kernel_name):
+    """Per-launch HBM bytes of `kernel_name` from the newest committed rocprofv3 PMC summary
+    (profiles/<round>_traffic.json, FETCH_SIZE x2 + WRITE_SIZE; tools/traffic_summary.py)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if kernel_name and kernel_name in d.get("kernel", ""):
+            return d.get("hbm_bytes_per_launch")
+    return None
 
 
 def cpu_baseline(seconds_hint):
@@ -195,7 +196,7 @@ def main():
         cpu = cpu_baseline(args.cpu_seconds)
 
     achieved_gbs = F * BYTES_PER_FRAME / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic()
+    traffic = load_traffic(kernel_name)
     line = {
         "metric": "audio frames/sec (STFT->MFCC, 1024/256)",
         "value": value,

@@ -16,5 +16,9 @@ for c in FETCH_SIZE WRITE_SIZE; do
       || { echo "pmc $c failed"; exit 1; }
   echo "$c done"
 done
+# per-launch HBM bytes -> profiles/<tag>_traffic.json (read by bench.py's roofline.traffic)
+(cd "$R" && python3 tools/traffic_summary.py "$OUT" "$TAG" mfcc_pair_kernel > "$OUT/traffic_summary.log") \
+    || { echo "traffic summary failed"; exit 1; }
 timeout -k 10 420 python3 "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; exit 1; }
 cat "$OUT/bench.json"
+cp "$OUT/bench.json" "$R/profiles/${TAG}_bench.json"

@@ -7,7 +7,7 @@ reports half the bytes of wide coalesced streaming reads, so it is doubled."""
 import csv, glob, json, os, shutil, sys, collections
 
 src, tag = sys.argv[1], sys.argv[2]
-pat = sys.argv[3] if len(sys.argv) > 3 else "fp_wave_kernel"
+pat = sys.argv[3] if len(sys.argv) > 3 else "mfcc_pair_kernel"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles")
 os.makedirs(dst, exist_ok=True)
@@ -37,7 +37,7 @@ kname = next(k for k in durs if pat in k)
 out = {"tag": tag, "kernel": kname,
        "kernel_trace_avg_ms": sum(durs[kname]) / len(durs[kname]), "kernel_trace_launches": len(durs[kname]),
        "fetch_bytes_per_launch_corrected": fetch, "write_bytes_per_launch": write,
-       "fp_wave_kernel_hbm_bytes_per_launch": fetch + write,
+       "hbm_bytes_per_launch": fetch + write,
        "raw": per,
        "note": "FETCH_SIZE x2 (gfx950 wide-read half count), KiB -> bytes; separate --pmc passes"}
 json.dump(out, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
