@@ -174,7 +174,9 @@ constexpr int kLogOff = kPartOff + 64 * 16;   // logmel [2][NMP]
 
 }  // namespace
 
-template <bool POW2>
+// JT / MS / NH: compile-time chunk length, sources per filter and DCT half-length for the
+// headline bank (40 mels at 44.1 kHz: 12 / 8 / 20); 0 = read from p (runtime loops).
+template <bool POW2, int JT, int MS, int NH>
 __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
@@ -345,8 +347,9 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       const unsigned char* pr = wb + prow(ks) * 8;
       const int ib = 16 - (ks & 15);                          // first i past a pad pair
       const float2* cw = s_cw + lane * p.JS;
-#pragma unroll 4
-      for (int i = 0; i < p.J; i++) {
+      const int J = JT ? JT : p.J;
+#pragma unroll
+      for (int i = 0; i < J; i++) {
         const float2 pp = *reinterpret_cast<const float2*>(pr + 8 * i + (i >= ib ? 16 : 0));
         const float2 w = cw[i];
         a0 += w.x * pp.x; a1 += w.x * pp.y;
@@ -358,7 +361,9 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     // ---- ln of the filter sums (lane = filter) ----------------------------------------
     if (lane < nmp) {
       float m0 = 0.f, m1 = 0.f;
-      for (int i = 0; i < p.max_src; i++) {
+      const int ms = MS ? MS : p.max_src;
+#pragma unroll
+      for (int i = 0; i < ms; i++) {
         const uint32_t idx = s_src[64 * i + lane];
         const float2 q = *reinterpret_cast<const float2*>(wb + kPartOff + 8 * (idx & 0x7fff));
         const bool use = (idx & 0x8000u) == 0;
@@ -375,10 +380,11 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     // ---- DCT-II (+ lifter): lane = q + 16 f + 32 h, half h of the filters ----------------
     {
       const int q = lane & 15, f = (lane >> 4) & 1, hh = lane >> 5;
-      const int half = nmp >> 1;
+      const int half = NH ? NH : (nmp >> 1);
       const float* lm = reinterpret_cast<const float*>(wb + kLogOff) + f * nmp + hh * half;
       const float* d = s_dct + q * (nmp + 4) + hh * half;     // row stride NMP + 4: 11 x 16 B slots
       float s = 0.f;
+#pragma unroll
       for (int m = 0; m < half; m += 4) {
         const float4 x = *reinterpret_cast<const float4*>(lm + m);
         const float4 y = *reinterpret_cast<const float4*>(d + m);
@@ -396,7 +402,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   load_pair(pb, ar, ai);
   for (int64_t pi = pb; pi < pe; ++pi) {
     float nr[16], ni[16];
-    if (pi + 1 < pe) load_pair(pi + 1, nr, ni);
+    if (pi + 1 < pe) load_pair(pi + 1, nr, ni);     // next pair's PCM in flight during this one
     process(pi, ar, ai);
 #pragma unroll
     for (int a = 0; a < 16; a++) { ar[a] = nr[a]; ai[a] = ni[a]; }
@@ -407,7 +413,9 @@ int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   const int64_t NP = (p.F + 1) >> 1;
   const int64_t waves = (NP + p.pairs_per_wave - 1) / p.pairs_per_wave;
   const int64_t grid = (waves + 3) / 4;
-  auto kern = p.pow2 ? mfcc_pair_kernel<true> : mfcc_pair_kernel<false>;
+  const bool head = p.J == 12 && p.max_src <= 8 && p.NMP == 40;
+  auto kern = p.pow2 ? (head ? mfcc_pair_kernel<true, 12, 8, 20> : mfcc_pair_kernel<true, 0, 0, 0>)
+                     : (head ? mfcc_pair_kernel<false, 12, 8, 20> : mfcc_pair_kernel<false, 0, 0, 0>);
   if (p.lds_bytes > 64 * 1024)
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), p.lds_bytes, s, p);
