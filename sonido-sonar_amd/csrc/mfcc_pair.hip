@@ -152,7 +152,9 @@ __device__ __forceinline__ void swap8x4(float (&a)[4], float (&b)[4], uint64_t m
 // phase before the next phase reads other lanes' words (defensive; costs < 2 % here).
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#ifndef SONAR_NO_LGKM_SYNC
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -163,7 +165,7 @@ constexpr int kT2Irreg[2][8] = {
     {56 * 136, 57 * 136, 58 * 136, 59 * 136, 59 * 136 + 64, 58 * 136 + 64, 57 * 136 + 64, 56 * 136 + 64}};
 
 constexpr int kT2Stride = 136;          // bytes per lane row of the T2 buffer (17 float2)
-constexpr int kWaveBytes = 64 * kT2Stride;
+constexpr int kWaveBytes = 64 * kT2Stride + 16;   // + a float2 that stays zero (unused filter sources)
 // power rows [bin][2 frames]: bin k at row k + 2 (k >> 4) -- two pad rows per 16 bins make the
 // split's stores (bins k1 + 16 c0 across a lane group) conflict-free; rows cover the chunk
 // over-read up to bin 527; the pad rows take the dummy bin-512 stores of lanes != 63
@@ -364,11 +366,11 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       const int ms = MS ? MS : p.max_src;
 #pragma unroll
       for (int i = 0; i < ms; i++) {
-        const uint32_t idx = s_src[64 * i + lane];
-        const float2 q = *reinterpret_cast<const float2*>(wb + kPartOff + 8 * (idx & 0x7fff));
-        const bool use = (idx & 0x8000u) == 0;
-        m0 += use ? q.x : 0.f;
-        m1 += use ? q.y : 0.f;
+        const uint32_t idx = s_src[64 * i + lane];               // 0x8000: unused -> the zero float2
+        const int off = (idx & 0x8000u) ? 64 * kT2Stride : kPartOff + 8 * (int)idx;
+        const float2 q = *reinterpret_cast<const float2*>(wb + off);
+        m0 += q.x;
+        m1 += q.y;
       }
       const float lf = -23.025850929940457f;                    // ln(1e-10)
       float l0 = m0 > 0.f ? __logf(m0) : lf, l1 = m1 > 0.f ? __logf(m1) : lf;

@@ -10,7 +10,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))       # sonido-sonar_amd/
 _REPO = os.path.dirname(_PKG)
-LIB_PATH = os.path.join(_PKG, "lib", "libsonar_gpu.so")
+LIB_PATH = os.environ.get("SONAR_LIB") or os.path.join(_PKG, "lib", "libsonar_gpu.so")   # override: A/B builds
 HEADER = os.path.join(_REPO, "include", "sonar_gpu.h")
 
 OK, ERR_INVALID, ERR_TOO_SHORT, ERR_EMPTY, ERR_UNSUPPORTED, ERR_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4, -5, -6

@@ -36,7 +36,7 @@ for name in sel:
         ctx.fingerprint_device(pcm.data_ptr(), n, cfg, **ptrs)
     torch.cuda.synchronize(); ctx.last_kernel_ms()
     ctx.enable_kernel_timing(True)
-    for _ in range(int(os.environ.get("ITERS", "20"))):
+    for _ in range(int(os.environ.get("ITERS", "100"))):
         ctx.fingerprint_device(pcm.data_ptr(), n, cfg, **ptrs)
     torch.cuda.synchronize()
     ctx.enable_kernel_timing(False)
