@@ -31,7 +31,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import sonar  # noqa: E402
-from sonar import shard  # noqa: E402
+from sonar import pairs, shard  # noqa: E402
 
 W, H, SR, N_MELS, N_MFCC = 1024, 256, 44100, 40, 13
 BYTES_PER_FRAME = 4 * H + 4 * N_MFCC            # PCM in (hop, f32) + MFCC out (f32)
@@ -48,6 +48,10 @@ def parse():
     ap.add_argument("--seconds", type=float, default=3600.0, help="audio seconds per GPU (1 h config)")
     ap.add_argument("--dtw-len", type=int, default=51676, help="DTW sequence length (0 = skip); C3 = 51,676")
     ap.add_argument("--dtw-steps", type=int, default=3)
+    ap.add_argument("--c5-pairs", type=int, default=1000, help="C5 stream pairs in total (0 = skip)")
+    ap.add_argument("--c5-seconds", type=float, default=60.0)
+    ap.add_argument("--c5-max-lag", type=float, default=20.0, help="maxOffsetSeconds (lags are drawn in [0, 20) s)")
+    ap.add_argument("--c5-workers", type=int, default=8, help="concurrent contexts (HIP streams) per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=0.0, help="force CPU-baseline sample length")
     return ap.parse_args()
@@ -137,6 +141,35 @@ def bench_dtw(ctx, n, steps):
             "dtw_path_len": int(len(res["path_q"]))}
 
 
+def bench_c5(args, world, rank, dev):
+    """BASELINE config C5 (path B): P stream pairs sharded over the ranks by contiguous pair ranges
+    (sonar/pairs.py), each pair through the music-extractor energy + chroma and
+    ExtractAlignmentFeatures (NCC + chroma DTW); no data-path collective, the per-pair records
+    are all-gathered over RCCL after the timed region.  Pairs are generated on the device
+    before timing ("inputs resident in HBM")."""
+    P = args.c5_pairs
+    a, b = pairs.pair_range(P, world, rank)
+    counts = [pairs.pair_range(P, world, g)[1] - pairs.pair_range(P, world, g)[0] for g in range(world)]
+    data = {k: pairs.c5_pair_device(k, args.c5_seconds, device=dev) for k in range(a, b)}
+    # warm-up on one pair: tables, buffers, kernel code objects
+    pairs.align_pairs([a], lambda k: data[k], max_lag_seconds=args.c5_max_lag, workers=1, device=dev.index)
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    recs = pairs.align_pairs(range(a, b), lambda k: data[k], max_lag_seconds=args.c5_max_lag,
+                             workers=args.c5_workers, device=dev.index)
+    torch.cuda.synchronize()
+    barrier(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    allrec = pairs.gather_records(torch.tensor(recs, dtype=torch.float64, device=dev), world, counts).cpu().numpy()
+    ipl, itrue = pairs.RECORD_FIELDS.index("peak_lag"), pairs.RECORD_FIELDS.index("lag_seconds_true")
+    lag_frames = allrec[:, itrue] * SR / H
+    ok = np.minimum(np.abs(allrec[:, ipl] - lag_frames), np.abs(allrec[:, ipl] + lag_frames)) <= 1.5
+    return {"c5_pairs_per_s": P / dt, "c5_ms": dt * 1e3, "c5_pairs": P, "c5_seconds_per_stream": args.c5_seconds,
+            "c5_max_lag_s": args.c5_max_lag, "c5_workers_per_rank": args.c5_workers,
+            "c5_lag_recovered": float(ok.mean()), "c5_dtw_cells_per_pair": int((args.c5_seconds * SR - W) // H + 1) ** 2}
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup()
@@ -190,6 +223,8 @@ def main():
     extra = {}
     if args.dtw_len > 0:
         extra = bench_dtw(ctx, args.dtw_len, args.dtw_steps)
+    if args.c5_pairs > 0:
+        extra.update(bench_c5(args, world, rank, dev))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

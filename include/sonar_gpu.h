@@ -276,6 +276,17 @@ int sonar_align_features(sonar_ctx* ctx,
                          int32_t feature_sample_rate, int32_t hop_size, int32_t window_size,
                          double max_lag_seconds, sonar_result** out);
 
+/* The two MusicFeatureExtractor.ExtractFeatures outputs that the alignment extractor consumes
+ * (fingerprint/extractors/music.go:178-245): preprocessAudio (DC removal R = 0.995, then
+ * pre-emphasis 0.95, :245-259) -> extractEnergyFeatures' ShortTimeEnergy with the extractor's
+ * FeatureConfig WindowSize/HopSize (:460-466, temporal/energy.go:25-50) and
+ * extractChromaFeatures (:327-376): spectrogram frames F = sonar_stft_frames(n, stft_window,
+ * stft_hop), frame length n / F, hop = FeatureConfig.HopSize.  energy has
+ * sonar_energy_frames(n, feature_window, feature_hop) entries, chroma F x 12.  float64. */
+int sonar_music_alignment_features(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate,
+                                   int32_t stft_window, int32_t stft_hop, int32_t feature_window,
+                                   int32_t feature_hop, double* energy, double* chroma, int32_t device_ptrs);
+
 /* result accessors: rows*cols float64 values, row-major; scalars are 1x1 */
 int sonar_result_get(const sonar_result* res, const char* name, const double** data, int64_t* rows,
                      int64_t* cols);

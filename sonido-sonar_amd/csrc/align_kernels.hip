@@ -39,11 +39,41 @@ __global__ void ncc_stats_kernel(const double* a, int64_t na, const double* b, i
   if (w > 1) return;
   const double* s = w ? b : a;
   const int64_t n = w ? nb : na;
+  // sequential sums in Go's index order (bit-exact); loads run 16 ahead of the add chain
+  constexpr int B = 16;
   double mean = 0.0;
-  for (int64_t i = 0; i < n; ++i) mean = __dadd_rn(mean, s[i]);
+  {
+    double cur[B], nxt[B];
+    int64_t i = 0;
+#pragma unroll
+    for (int j = 0; j < B; j++) cur[j] = j < n ? s[j] : 0.0;
+    for (; i + B <= n; i += B) {
+#pragma unroll
+      for (int j = 0; j < B; j++) nxt[j] = i + B + j < n ? s[i + B + j] : 0.0;
+#pragma unroll
+      for (int j = 0; j < B; j++) mean = __dadd_rn(mean, cur[j]);
+#pragma unroll
+      for (int j = 0; j < B; j++) cur[j] = nxt[j];
+    }
+    for (int j = 0; i + j < n; j++) mean = __dadd_rn(mean, cur[j]);
+  }
   mean = __ddiv_rn(mean, (double)n);
   double var = 0.0;
-  for (int64_t i = 0; i < n; ++i) { const double d = __dsub_rn(s[i], mean); var = __dadd_rn(var, __dmul_rn(d, d)); }
+  {
+    double cur[B], nxt[B];
+    int64_t i = 0;
+#pragma unroll
+    for (int j = 0; j < B; j++) cur[j] = j < n ? s[j] : 0.0;
+    for (; i + B <= n; i += B) {
+#pragma unroll
+      for (int j = 0; j < B; j++) nxt[j] = i + B + j < n ? s[i + B + j] : 0.0;
+#pragma unroll
+      for (int j = 0; j < B; j++) { const double d = __dsub_rn(cur[j], mean); var = __dadd_rn(var, __dmul_rn(d, d)); }
+#pragma unroll
+      for (int j = 0; j < B; j++) cur[j] = nxt[j];
+    }
+    for (int j = 0; i + j < n; j++) { const double d = __dsub_rn(cur[j], mean); var = __dadd_rn(var, __dmul_rn(d, d)); }
+  }
   var = __ddiv_rn(var, (double)n);
   stats[2 * w] = mean;
   stats[2 * w + 1] = sqrt(var);
@@ -77,11 +107,31 @@ __global__ __launch_bounds__(256) void ncc_lag_kernel(const double* x, int64_t n
     double sm = 0.0, q1 = 0.0, q2 = 0.0;
     const double* px = x + s1;
     const double* py = y + s2;
-    for (int64_t k = 0; k < ov; ++k) {
-      const double v1 = px[k], v2 = py[k];
-      sm = __dadd_rn(sm, __dmul_rn(v1, v2));
-      q1 = __dadd_rn(q1, __dmul_rn(v1, v1));
-      q2 = __dadd_rn(q2, __dmul_rn(v2, v2));
+    // Go's index order per lag (bit-exact); the next 8 pairs load while these 8 accumulate
+    constexpr int B = 8;
+    double c1[B], c2[B], n1[B], n2[B];
+#pragma unroll
+    for (int j = 0; j < B; j++) { c1[j] = j < ov ? px[j] : 0.0; c2[j] = j < ov ? py[j] : 0.0; }
+    int64_t k = 0;
+    for (; k + B <= ov; k += B) {
+#pragma unroll
+      for (int j = 0; j < B; j++) {
+        const bool in = k + B + j < ov;
+        n1[j] = in ? px[k + B + j] : 0.0; n2[j] = in ? py[k + B + j] : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < B; j++) {
+        sm = __dadd_rn(sm, __dmul_rn(c1[j], c2[j]));
+        q1 = __dadd_rn(q1, __dmul_rn(c1[j], c1[j]));
+        q2 = __dadd_rn(q2, __dmul_rn(c2[j], c2[j]));
+      }
+#pragma unroll
+      for (int j = 0; j < B; j++) { c1[j] = n1[j]; c2[j] = n2[j]; }
+    }
+    for (int j = 0; k + j < ov; j++) {
+      sm = __dadd_rn(sm, __dmul_rn(c1[j], c2[j]));
+      q1 = __dadd_rn(q1, __dmul_rn(c1[j], c1[j]));
+      q2 = __dadd_rn(q2, __dmul_rn(c2[j], c2[j]));
     }
     const double dn = sqrt(__dmul_rn(q1, q2));
     c = dn < 1e-10 ? 0.0 : __ddiv_rn(sm, dn);

@@ -411,6 +411,46 @@ int sonar_generate_fingerprint(sonar_ctx* c, const double* pcm, int64_t n, int32
 }
 
 // ------------------------------------------ AlignmentExtractor --------------
+// MusicFeatureExtractor energy + chroma (music.go:245-259, :327-376, :460-466)
+int sonar_music_alignment_features(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, int32_t stft_w,
+                                   int32_t stft_h, int32_t fw, int32_t fh, double* energy, double* chroma,
+                                   int32_t device_ptrs) {
+  if (!c) return SONAR_ERR_INVALID;
+  if (!pcm || n <= 0) return fail(c, SONAR_ERR_INVALID, "invalid input data");        // music.go:179-181
+  if (stft_w <= 0 || stft_h <= 0) return fail(c, SONAR_ERR_INVALID, "window and hop size must be positive");
+  const int64_t F = sonar_stft_frames(n, stft_w, stft_h);
+  if (F <= 0) return fail(c, SONAR_ERR_TOO_SHORT, "signal too short for given window size and hop size");
+  if (fh <= 0) return fail(c, SONAR_ERR_INVALID, "hop size must be positive");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const double* dp = pcm;
+  if (!device_ptrs) {
+    void* b = dbuf(c, "mf.pcm", n * 8);
+    if (!b) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+    HIP_TRY(c, hipMemcpyAsync(b, pcm, n * 8, hipMemcpyHostToDevice, s));
+    dp = (const double*)b;
+  }
+  double* y = (double*)dbuf(c, "mf.pre", n * 8);                 // processedPCM
+  if (!y) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+  if (sonar::launch_dc_preemph(dp, n, 0.995, 0.95, y, s) != 0) return fail(c, SONAR_ERR_DEVICE, "dc launch failed");
+  const int64_t Fe = sonar_energy_frames(n, fw, fh);
+  double* de = device_ptrs ? energy : (double*)dbuf(c, "mf.energy", std::max<int64_t>(Fe, 1) * 8);
+  // ShortTimeEnergy of the already pre-emphasised signal: alpha 0 makes the kernel's
+  // pre-emphasis the identity (x - 0 * x[n-1] == x exactly)
+  if (Fe > 0 && sonar::launch_energy(y, 1, n, Fe, fw, fh, 0.0, de, 1, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "energy launch failed");
+  double* dc = device_ptrs ? chroma : (double*)dbuf(c, "mf.chroma", F * 12 * 8);
+  if (!de || !dc) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+  const int rc = sonar_chroma_stft(c, y, n, F, fh, sr, 0, dc, 1);
+  if (rc != SONAR_OK) return rc;
+  if (!device_ptrs) {
+    if (Fe > 0) HIP_TRY(c, hipMemcpyAsync(energy, de, Fe * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(chroma, dc, F * 12 * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SONAR_OK;
+}
+
 int sonar_align_features(sonar_ctx* c, const double* qe, int64_t nqe, const double* re, int64_t nre, const double* qc,
                          int64_t nqc, const double* rc_, int64_t nrc, int64_t q_pcm_len, int64_t r_pcm_len,
                          int32_t sample_rate, int32_t feature_sample_rate, int32_t hop, int32_t win,

@@ -186,12 +186,26 @@ __global__ __launch_bounds__(256) void dcpre_kernel(const double* x, int64_t n, 
   double x1 = 0.0, y1 = 0.0;
   if (i > 0) x1 = x[i - 1];
   double yprev = 0.0;
-  for (; i < e; ++i) {
-    const double xv = x[i];
-    const double yv = __dadd_rn(__dsub_rn(xv, x1), __dmul_rn(R, y1));
-    x1 = xv; y1 = yv;
-    if (i >= s) z[i] = __dsub_rn(yv, __dmul_rn(alpha, yprev));
-    yprev = yv;
+  // the recurrence is serial; the next 16 samples load while these 16 advance it
+  constexpr int B = 16;
+  double cur[B], nxt[B];
+#pragma unroll
+  for (int j = 0; j < B; j++) cur[j] = i + j < e ? x[i + j] : 0.0;
+  for (; i < e; i += B) {
+#pragma unroll
+    for (int j = 0; j < B; j++) nxt[j] = i + B + j < e ? x[i + B + j] : 0.0;
+#pragma unroll
+    for (int j = 0; j < B; j++) {
+      if (i + j < e) {
+        const double xv = cur[j];
+        const double yv = __dadd_rn(__dsub_rn(xv, x1), __dmul_rn(R, y1));
+        x1 = xv; y1 = yv;
+        if (i + j >= s) z[i + j] = __dsub_rn(yv, __dmul_rn(alpha, yprev));
+        yprev = yv;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < B; j++) cur[j] = nxt[j];
   }
 }
 

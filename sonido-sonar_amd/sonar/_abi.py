@@ -114,6 +114,8 @@ def lib():
     L.sonar_pitch_yin.argtypes = [_vp, _vp, C.c_int64, C.c_int32, _vp, _vp, _vp, C.c_int32]
     L.sonar_chroma_stft.argtypes = [_vp, _vp, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, C.c_int32]
     L.sonar_ncc.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, _vp, _vp, C.c_int32]
+    L.sonar_music_alignment_features.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                                 C.c_int32, _vp, _vp, C.c_int32]
     L.sonar_dtw.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, _d, _vp, _vp, _vp, _i64p,
                             _vp, C.c_int32]
     L.sonar_fingerprint_config_default.argtypes = [C.POINTER(FingerprintConfig)]
@@ -279,6 +281,26 @@ class Context:
         self._check(self._L.sonar_chroma_stft(self._h, _ptr(pcm), len(pcm), n_frames, hop, sample_rate,
                                               int(preprocess), _ptr(out), 0))
         return out
+
+    def music_alignment_features(self, pcm, sample_rate, stft_window=1024, stft_hop=256, feature_window=1024,
+                                 feature_hop=256):
+        """MusicFeatureExtractor's ShortTimeEnergy + ChromaFeatures (host arrays) -> (energy, chroma)."""
+        pcm = _f64(pcm)
+        n = len(pcm)
+        F = stft_frames(n, stft_window, stft_hop) if n > 0 else 0
+        energy = np.zeros(max(energy_frames(n, feature_window, feature_hop), 0))
+        chroma = np.zeros((max(F, 0), 12))
+        self._check(self._L.sonar_music_alignment_features(
+            self._h, _ptr(pcm) if n else None, n, sample_rate, stft_window, stft_hop, feature_window, feature_hop,
+            _ptr(energy) if len(energy) else None, _ptr(chroma) if len(chroma) else None, 0))
+        return energy, chroma
+
+    def music_alignment_features_device(self, pcm_ptr, n, sample_rate, energy_ptr, chroma_ptr, stft_window=1024,
+                                        stft_hop=256, feature_window=1024, feature_hop=256):
+        """Device-pointer form (float64 buffers, async on the ctx stream)."""
+        self._check(self._L.sonar_music_alignment_features(
+            self._h, C.c_void_p(pcm_ptr), n, sample_rate, stft_window, stft_hop, feature_window, feature_hop,
+            C.c_void_p(energy_ptr), C.c_void_p(chroma_ptr), 1))
 
     # -- path B ------------------------------------------------------------
     def ncc(self, a, b, max_lag):

@@ -1,5 +1,7 @@
 import sys, os, numpy as np
-sys.path[:0] = ["sonido-sonar_amd", "oracle"]
+import os
+_R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(_R, "sonido-sonar_amd"), os.path.join(_R, "oracle")]
 import sonar, oracle as O
 from sonar import synth
 ctx = sonar.Context(0)

@@ -1,7 +1,9 @@
 """Stress check of the headline kernel: random lengths/hops, pair kernel vs the general kernel
 and vs itself (determinism).  Prints one summary line."""
 import sys, time, numpy as np
-sys.path[:0] = ["sonido-sonar_amd"]
+import os
+_R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(_R, "sonido-sonar_amd")]
 import sonar
 from sonar import synth
 ctx = sonar.Context(0)

@@ -1,6 +1,8 @@
 """Failure forensics for the headline kernel: where do bad frames sit and what do they hold."""
 import sys, numpy as np
-sys.path[:0] = ["sonido-sonar_amd"]
+import os
+_R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(_R, "sonido-sonar_amd")]
 import sonar
 from sonar import synth
 ctx = sonar.Context(0)
