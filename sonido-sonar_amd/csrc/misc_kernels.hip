@@ -176,36 +176,85 @@ __global__ __launch_bounds__(256) void chroma_kernel(const double* y, int64_t n,
 // DC blocker y[n] = x[n] - x[n-1] + R y[n-1] followed by pre-emphasis z = y[n] - a y[n-1].
 // Each thread produces a chunk of outputs after a WARM-sample warm-up from zero
 // state; R^WARM < 1e-17, so the result equals the sequential filter to fp64 rounding.
+// One thread per chunk of `chunk` samples (a multiple of 16; chunk starts are 16-aligned).  The
+// DC-removal state at the chunk start is rebuilt by running the recurrence over the preceding
+// `warm` samples from a zero state (0.995^8192 ~ 1.6e-18: the start-up error is below float64
+// rounding of the state).  Samples move as double2 vectors, 16 per step: the warm-up loads and
+// the chunk's stores are whole 128-B lines per lane (scalar per-sample stores to lanes 16 KB
+// apart made this kernel 10x slower).
+// two consecutive samples starting at an even index; callers' buffers may be only 8-B aligned
+// (a torch slice), then the pair is read as two scalars
+__device__ __forceinline__ double2 ld2(const double* x, int64_t i, bool al) {
+  return al ? reinterpret_cast<const double2*>(x)[i >> 1] : make_double2(x[i], x[i + 1]);
+}
+
 __global__ __launch_bounds__(256) void dcpre_kernel(const double* x, int64_t n, double R, double alpha, double* z,
                                                     int chunk, int warm) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t s = c * chunk;
   if (s >= n) return;
   const int64_t e = min(n, s + chunk);
-  int64_t i = s - warm - 1; if (i < 0) i = 0;
-  double x1 = 0.0, y1 = 0.0;
-  if (i > 0) x1 = x[i - 1];
-  double yprev = 0.0;
-  // the recurrence is serial; the next 16 samples load while these 16 advance it
+  const int64_t w0 = s > warm ? s - warm : 0;
+  double x1 = w0 > 0 ? x[w0 - 1] : 0.0, y1 = 0.0;
   constexpr int B = 16;
-  double cur[B], nxt[B];
+  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  // warm-up: [w0, s) in whole 16-sample blocks (w0 and s are multiples of 16)
+  {
+    double2 cur[B / 2], nxt[B / 2];
+    if (w0 < s) {
 #pragma unroll
-  for (int j = 0; j < B; j++) cur[j] = i + j < e ? x[i + j] : 0.0;
-  for (; i < e; i += B) {
-#pragma unroll
-    for (int j = 0; j < B; j++) nxt[j] = i + B + j < e ? x[i + B + j] : 0.0;
-#pragma unroll
-    for (int j = 0; j < B; j++) {
-      if (i + j < e) {
-        const double xv = cur[j];
-        const double yv = __dadd_rn(__dsub_rn(xv, x1), __dmul_rn(R, y1));
-        x1 = xv; y1 = yv;
-        if (i + j >= s) z[i + j] = __dsub_rn(yv, __dmul_rn(alpha, yprev));
-        yprev = yv;
-      }
+      for (int j = 0; j < B / 2; j++) cur[j] = ld2(x, w0 + 2 * j, al);
     }
+    for (int64_t i = w0; i < s; i += B) {
+      if (i + B < s) {
 #pragma unroll
-    for (int j = 0; j < B; j++) cur[j] = nxt[j];
+        for (int j = 0; j < B / 2; j++) nxt[j] = ld2(x, i + B + 2 * j, al);
+      }
+#pragma unroll
+      for (int j = 0; j < B / 2; j++) {
+        const double a = cur[j].x, b = cur[j].y;
+        double yv = __dadd_rn(__dsub_rn(a, x1), __dmul_rn(R, y1)); x1 = a; y1 = yv;
+        yv = __dadd_rn(__dsub_rn(b, x1), __dmul_rn(R, y1)); x1 = b; y1 = yv;
+      }
+#pragma unroll
+      for (int j = 0; j < B / 2; j++) cur[j] = nxt[j];
+    }
+  }
+  double yprev = y1;                                     // y[s-1] (0 at s = 0)
+  // the chunk: full 16-sample blocks as vectors, then a scalar tail (last chunk only)
+  const int64_t ef = s + ((e - s) / B) * B;
+  {
+    double2* zv = reinterpret_cast<double2*>(z);          // z: context buffer, 256-B aligned
+    double2 cur[B / 2], nxt[B / 2], out[B / 2];
+    if (s < ef) {
+#pragma unroll
+      for (int j = 0; j < B / 2; j++) cur[j] = ld2(x, s + 2 * j, al);
+    }
+    for (int64_t i = s; i < ef; i += B) {
+      if (i + B < ef) {
+#pragma unroll
+        for (int j = 0; j < B / 2; j++) nxt[j] = ld2(x, i + B + 2 * j, al);
+      }
+#pragma unroll
+      for (int j = 0; j < B / 2; j++) {
+        const double a = cur[j].x, b = cur[j].y;
+        double yv = __dadd_rn(__dsub_rn(a, x1), __dmul_rn(R, y1)); x1 = a; y1 = yv;
+        out[j].x = __dsub_rn(yv, __dmul_rn(alpha, yprev)); yprev = yv;
+        yv = __dadd_rn(__dsub_rn(b, x1), __dmul_rn(R, y1)); x1 = b; y1 = yv;
+        out[j].y = __dsub_rn(yv, __dmul_rn(alpha, yprev)); yprev = yv;
+      }
+#pragma unroll
+      for (int j = 0; j < B / 2; j++) zv[i / 2 + j] = out[j];
+#pragma unroll
+      for (int j = 0; j < B / 2; j++) cur[j] = nxt[j];
+    }
+  }
+  for (int64_t i = ef; i < e; ++i) {
+    const double xv = x[i];
+    const double yv = __dadd_rn(__dsub_rn(xv, x1), __dmul_rn(R, y1));
+    x1 = xv; y1 = yv;
+    z[i] = __dsub_rn(yv, __dmul_rn(alpha, yprev));
+    yprev = yv;
   }
 }
 
@@ -253,7 +302,7 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
 
 int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, hipStream_t s) {
   if (n <= 0) return 0;
-  const int chunk = 2048, warm = 8192;
+  const int chunk = 1024, warm = 8192;   // multiples of 16 (vector blocks)
   const int64_t nthreads = (n + chunk - 1) / chunk;
   hipLaunchKernelGGL(dcpre_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, s, x, n, R, alpha, y, chunk,
                      warm);
