@@ -287,6 +287,119 @@ int sonar_music_alignment_features(sonar_ctx* ctx, const double* pcm, int64_t n,
                                    int32_t stft_window, int32_t stft_hop, int32_t feature_window,
                                    int32_t feature_hop, double* energy, double* chroma, int32_t device_ptrs);
 
+/* ---- FingerprintComparator (fingerprint/comparison.go) ------------------------------
+ * The comparator's candidate set lives on the device as a gallery of per-fingerprint
+ * summary records (MFCC column mean/std, chroma column means, mean/std of the compared
+ * sequences, the scalars and weights).  Compare() in the reference rebuilds those
+ * statistics from the full feature arrays on every call (comparison.go:344-402,
+ * 646-770, 774-842); they depend on one fingerprint only, so they are reduced once per
+ * fingerprint when it is added, and every comparison reads two records.  Results are the
+ * reference's formulas on the same statistics. */
+
+/* config.ContentType (fingerprint/config/config.go:39-48).  Any other content-type string
+ * is given its own code >= SONAR_CT_UNKNOWN by the caller, so ContentTypeMatch (string
+ * equality, comparison.go:157) keeps distinct unknown strings apart. */
+enum { SONAR_CT_MUSIC = 0, SONAR_CT_NEWS, SONAR_CT_SPORTS, SONAR_CT_TALK, SONAR_CT_MIXED,
+       SONAR_CT_UNKNOWN };
+
+/* sonar_fp_features.present: which members of AudioFingerprint.Features are non-nil */
+enum {
+  SONAR_FEAT_FEATURES = 1u << 0,   /* Features != nil                                    */
+  SONAR_FEAT_MFCC = 1u << 1,       /* Features.MFCC != nil                               */
+  SONAR_FEAT_SPECTRAL = 1u << 2,   /* Features.SpectralFeatures != nil                   */
+  SONAR_FEAT_CHROMA = 1u << 3,     /* Features.ChromaFeatures != nil                     */
+  SONAR_FEAT_TEMPORAL = 1u << 4,   /* Features.TemporalFeatures != nil                   */
+  SONAR_FEAT_SPEECH = 1u << 5,     /* Features.SpeechFeatures != nil                     */
+  SONAR_FEAT_HARMONIC = 1u << 6,   /* Features.HarmonicFeatures != nil                   */
+  SONAR_FEAT_WEIGHTS = 1u << 7     /* Metadata["feature_weights"] is a map[string]float64 */
+};
+
+/* FeatureDistances keys (comparison.go:284-330), bit i of sonar_similarity.distance_mask */
+enum { SONAR_FD_MFCC = 0, SONAR_FD_SPECTRAL, SONAR_FD_CHROMA, SONAR_FD_TEMPORAL, SONAR_FD_SPEECH,
+       SONAR_FD_HARMONIC };
+
+/* One AudioFingerprint as the comparator reads it (fingerprint.go:15-26,
+ * extractors/features.go).  Matrices are row-major float64; MFCC rows are len(mfcc[0])
+ * wide -- a shorter Go row is padded with 0 (the value extractMFCCStatistics uses for a
+ * missing coefficient, comparison.go:784-789).  A sequence with n_* = 0 is empty. */
+typedef struct {
+  int64_t id;                      /* AudioFingerprint.ID, interned (self-skip, comparison.go:218) */
+  uint32_t present;                /* SONAR_FEAT_*                                        */
+  int32_t content_type;            /* SONAR_CT_* (or a distinct code >= SONAR_CT_UNKNOWN)  */
+  double duration_seconds;         /* Duration.Seconds()                                  */
+  const double* mfcc; int64_t mfcc_frames; int32_t mfcc_coeffs;
+  const double* chroma; int64_t chroma_frames; int32_t chroma_bins;
+  const double* spectral_centroid; int64_t n_spectral_centroid;
+  const double* spectral_rolloff; int64_t n_spectral_rolloff;
+  const double* spectral_flux; int64_t n_spectral_flux;
+  double dynamic_range, silence_ratio, onset_density;          /* TemporalFeatures     */
+  const double* rms_energy; int64_t n_rms_energy;
+  double speech_rate, vocal_tract_length;                      /* SpeechFeatures       */
+  const double* voicing_probability; int64_t n_voicing_probability;
+  const double* harmonic_ratio; int64_t n_harmonic_ratio;      /* HarmonicFeatures     */
+  const double* pitch_estimate; int64_t n_pitch_estimate;
+  double feature_weights[6];       /* Metadata weights by SONAR_FD_* (absent key = 0)     */
+} sonar_fp_features;
+
+/* config.ComparisonConfig (fingerprint/config/config.go:68-80) */
+typedef struct {
+  double similarity_threshold;
+  int32_t max_candidates;
+  int32_t enable_detailed_metrics;
+  int32_t enable_content_filter;
+  int32_t method;                  /* 0 auto, 1 fast, 2 precise (Compare ignores it, :133-194) */
+} sonar_compare_cfg;
+
+/* SimilarityResult (comparison.go:28-39) */
+typedef struct {
+  double overall_similarity;
+  double feature_similarity;
+  double confidence;
+  double feature_distances[6];     /* by SONAR_FD_*, where distance_mask has the bit      */
+  double data_availability, feature_coverage, temporal_alignment;   /* QualityMetrics,   */
+  double noise_level, dynamic_range_match, spectral_coherence;      /* when has_quality  */
+  uint32_t distance_mask;
+  int32_t content_type_match;
+  int32_t has_quality;
+  int32_t status;                  /* 0 compared, 1 skipped (same ID), 2 calculateFeatureSimilarity
+                                      returned an error (nil features / nothing comparable) */
+} sonar_similarity;
+
+enum { SONAR_MATCH_EXACT = 0, SONAR_MATCH_VERY_SIMILAR, SONAR_MATCH_SIMILAR,
+       SONAR_MATCH_SOMEWHAT_SIMILAR, SONAR_MATCH_WEAK };   /* classifyMatch, comparison.go:1040-1052 */
+
+typedef struct {                   /* Match (comparison.go:52-58) */
+  int64_t candidate;               /* position in the candidates list of the call          */
+  int32_t rank;                    /* 1-based                                              */
+  int32_t match_type;              /* SONAR_MATCH_*                                        */
+  sonar_similarity similarity;
+} sonar_match;
+
+typedef struct sonar_gallery sonar_gallery;
+int sonar_gallery_create(sonar_ctx* ctx, sonar_gallery** out);
+void sonar_gallery_destroy(sonar_gallery* g);
+int64_t sonar_gallery_size(const sonar_gallery* g);
+/* Append `count` fingerprints: their statistics are reduced on the device and only the
+ * records stay resident.  keep_sequences keeps SpectralCentroid / SpectralRolloff on the
+ * device for EnableDetailedMetrics' spectral coherence (comparison.go:977-1008).
+ * device_ptrs: the feature arrays are device pointers.  Index of the first -> *first. */
+int sonar_gallery_add(sonar_gallery* g, const sonar_fp_features* fps, int32_t count,
+                      int32_t keep_sequences, int32_t device_ptrs, int64_t* first);
+/* FingerprintComparator.Compare / BatchCompare (comparison.go:133-194, 1107-1151) for every
+ * (query, candidate) pair: out[q * nc + c].  candidates NULL -> the whole gallery
+ * (nc = sonar_gallery_size).  A pair with equal IDs gets status 1 (BatchCompare drops it).
+ * Detailed metrics need SpectralCentroid / SpectralRolloff of equal length on both sides
+ * when both are non-empty (gonum stat.Correlation panics otherwise) -> SONAR_ERR_INVALID.
+ * device_ptrs: out is a device pointer. */
+int sonar_compare(sonar_gallery* g, const int64_t* queries, int64_t nq, const int64_t* candidates,
+                  int64_t nc, const sonar_compare_cfg* cfg, sonar_similarity* out, int32_t device_ptrs);
+/* FingerprintComparator.FindBestMatches (comparison.go:197-263) per query: matches with
+ * OverallSimilarity >= threshold, descending, at most max_candidates, ranked from 1.
+ * out[q * max_candidates + k], n_matches[q].  Equal similarities keep candidate order. */
+int sonar_find_best_matches(sonar_gallery* g, const int64_t* queries, int64_t nq,
+                            const int64_t* candidates, int64_t nc, const sonar_compare_cfg* cfg,
+                            sonar_match* out, int64_t* n_matches);
+
 /* result accessors: rows*cols float64 values, row-major; scalars are 1x1 */
 int sonar_result_get(const sonar_result* res, const char* name, const double** data, int64_t* rows,
                      int64_t* cols);

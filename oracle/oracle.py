@@ -66,6 +66,8 @@ def lib():
         L.or_formant_frame.argtypes = [_d, C.c_int64, C.c_int, _d, _d, _d]
         L.or_formant_frames.argtypes = [_d, C.c_int64, C.c_int, C.c_int, C.c_int, _d, _d, _d]
         L.or_formant_frames.restype = C.c_int64
+        L.or_fp_compare.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_find_best_matches.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, _i64]
         _lib = L
     return _lib
 
@@ -478,3 +480,30 @@ def autocorr_fft(x, max_lag):
     out = np.zeros(2 * L + 1)
     lib().or_autocorr_fft(_p(x), len(x), max_lag, _p(out))
     return out
+
+
+# ---- FingerprintComparator (compare_oracle.c) ----------------------------------------
+# The structs are the C ABI's layouts (sonar._abi.FpFeatures / CompareCfg / Similarity /
+# Match); the oracle reads the full feature arrays on every call, like the Go code.
+
+def fp_compare(fa, fb, cfg):
+    """or_fp_compare: Compare(fa, fb) -> Similarity struct (raises on a Go panic case)."""
+    from sonar._abi import Similarity
+    out = Similarity()
+    rc = lib().or_fp_compare(C.addressof(fa), C.addressof(fb), C.addressof(cfg), C.addressof(out))
+    if rc:
+        raise ValueError(f"oracle compare panics in Go (code {rc})")
+    return out
+
+
+def find_best_matches(fq, fcands, cfg):
+    """or_find_best_matches over an array of FpFeatures -> list of Match structs."""
+    from sonar._abi import Match
+    n = len(fcands)
+    out = (Match * max(1, n))()
+    k = C.c_int64()
+    rc = lib().or_find_best_matches(C.addressof(fq), C.addressof(fcands) if n else None, n,
+                                    C.addressof(cfg), C.addressof(out), C.byref(k))
+    if rc:
+        raise ValueError(f"oracle FindBestMatches panics in Go (code {rc})")
+    return [out[i] for i in range(k.value)]

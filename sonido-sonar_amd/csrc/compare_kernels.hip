@@ -1,0 +1,473 @@
+// compare_kernels.hip -- FingerprintComparator (fingerprint/comparison.go) on a device gallery.
+//
+// Three stages, all float64 like the reference:
+//   colstats_*      per-fingerprint statistics (gonum stat.Mean / corrected two-pass
+//                   stat.Variance) of the MFCC columns, chroma columns and the compared
+//                   sequences, reduced over row chunks in a fixed order (deterministic);
+//                   HBM-bound streaming of the feature arrays, once per fingerprint.
+//   coherence       gonum stat.Correlation of SpectralCentroid / SpectralRolloff for each
+//                   pair (EnableDetailedMetrics only, comparison.go:977-1008): one block per
+//                   (pair, sequence) streams both sequences.
+//   compare         one thread per (query, candidate): calculateFeatureSimilarity and the
+//                   scorers over two gallery records (comparison.go:133-194, 266-402,
+//                   646-1037); a few hundred float64 operations per pair.
+// FindBestMatches adds a segmented radix sort (hipCUB) of the per-query keys.
+// Built with -ffp-contract=off: Go on amd64 rounds every product and sum separately.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+
+#include "kernels.h"
+
+namespace sonar {
+namespace {
+
+constexpr int kBlock = 256;
+
+// ---- Go math helpers (NaN behaviour of math.Max / math.Min) ---------------------------
+__device__ __forceinline__ double go_max(double x, double y) {
+  if (isinf(x) && x > 0) return x;
+  if (isinf(y) && y > 0) return y;
+  if (isnan(x) || isnan(y)) return NAN;
+  if (x == 0 && x == y) return signbit(x) ? y : x;
+  return x > y ? x : y;
+}
+__device__ __forceinline__ double go_min(double x, double y) {
+  if (isinf(x) && x < 0) return x;
+  if (isinf(y) && y < 0) return y;
+  if (isnan(x) || isnan(y)) return NAN;
+  if (x == 0 && x == y) return signbit(x) ? x : y;
+  return x < y ? x : y;
+}
+
+// gonum floats.Norm(x, 2) = f64.L2NormUnitary: scaled sum of squares
+__device__ double l2norm(const double* x, int n) {
+  double scale = 0.0, ss = 1.0;
+  for (int i = 0; i < n; i++) {
+    const double v = x[i];
+    if (v == 0.0) continue;
+    const double a = fabs(v);
+    if (isnan(a)) return NAN;
+    if (scale < a) {
+      const double s = scale / a;
+      ss = 1.0 + ss * s * s;
+      scale = a;
+    } else {
+      const double s = a / scale;
+      ss += s * s;
+    }
+  }
+  if (isinf(scale)) return INFINITY;
+  return scale * sqrt(ss);
+}
+
+// cosineSimilarity (comparison.go:858-873)
+__device__ double cosine(const double* a, int na, const double* b, int nb) {
+  if (na != nb || na == 0) return 0.0;
+  double dot = 0.0;
+  for (int i = 0; i < na; i++) dot += a[i] * b[i];
+  const double n1 = l2norm(a, na), n2 = l2norm(b, nb);
+  if (n1 == 0 || n2 == 0) return 0.0;
+  return dot / (n1 * n2);
+}
+
+// compareSequenceStats (:827-842): cosine of (mean, std)
+__device__ double seq_sim(const FpRec& A, const FpRec& B, int s) {
+  const double a[2] = {A.seq_mean[s], A.seq_std[s]}, b[2] = {B.seq_mean[s], B.seq_std[s]};
+  return cosine(a, 2, b, 2);
+}
+
+// compareScalarFeatures (:844-856)
+__device__ double scalar_sim(double v1, double v2) {
+  if (v1 == 0 && v2 == 0) return 1.0;
+  const double mx = go_max(fabs(v1), fabs(v2));
+  if (mx == 0) return 1.0;
+  return go_max(0.0, 1.0 - fabs(v1 - v2) / mx);
+}
+
+__device__ double mean_of(const double* v, int n) {   // stat.Mean(v, nil) = floats.Sum / n
+  double s = 0.0;
+  for (int i = 0; i < n; i++) s += v[i];
+  return s / (double)n;
+}
+
+// ---- column statistics ----------------------------------------------------------------
+// Thread layout for a chunk of a rows x cols matrix: cols <= 256 -> 256/cols rows per step,
+// thread t owns column t % cols (reads of a step are one contiguous run); wider matrices ->
+// thread t owns columns t, t + 256, ... and walks the rows.
+template <int PASS>
+__global__ __launch_bounds__(kBlock) void colstats_kernel(const StatJob* jobs, const int* chunk_job,
+                                                          const int* chunk_k, double* part_sum,
+                                                          double* part_ss, double* part_comp) {
+  __shared__ double s_a[kBlock], s_b[kBlock];
+  const StatJob J = jobs[chunk_job[blockIdx.x]];
+  const int k = chunk_k[blockIdx.x];
+  const int C = J.cols, t = threadIdx.x;
+  const int64_t r0 = (int64_t)k * J.chunk_rows, r1 = min(J.rows, r0 + J.chunk_rows);
+  auto col_mean = [&](int c) {            // the same fixed-order sum as the final pass
+    double s = 0.0;
+    for (int q = 0; q < J.nchunks; q++) s += part_sum[J.part_off + (int64_t)q * C + c];
+    return s / (double)J.rows;
+  };
+  if (C <= kBlock) {
+    const int rpi = kBlock / C, active = rpi * C;
+    double a = 0.0, b = 0.0;
+    if (t < active) {
+      const int c = t % C;
+      const double mu = PASS ? col_mean(c) : 0.0;
+      for (int64_t r = r0 + t / C; r < r1; r += rpi) {
+        const double x = J.src[r * C + c];
+        if (PASS) {
+          const double d = x - mu;
+          a += d * d;
+          b += d;
+        } else {
+          a += x;
+        }
+      }
+    }
+    s_a[t] = a;
+    s_b[t] = b;
+    __syncthreads();
+    if (t < C) {
+      double sa = 0.0, sb = 0.0;
+      for (int q = 0; q < rpi; q++) { sa += s_a[t + q * C]; sb += s_b[t + q * C]; }
+      const int64_t o = J.part_off + (int64_t)k * C + t;
+      if (PASS) { part_ss[o] = sa; part_comp[o] = sb; } else { part_sum[o] = sa; }
+    }
+  } else {
+    for (int c = t; c < C; c += kBlock) {
+      const double mu = PASS ? col_mean(c) : 0.0;
+      double a = 0.0, b = 0.0;
+      for (int64_t r = r0; r < r1; r++) {
+        const double x = J.src[r * C + c];
+        if (PASS) {
+          const double d = x - mu;
+          a += d * d;
+          b += d;
+        } else {
+          a += x;
+        }
+      }
+      const int64_t o = J.part_off + (int64_t)k * C + c;
+      if (PASS) { part_ss[o] = a; part_comp[o] = b; } else { part_sum[o] = a; }
+    }
+  }
+}
+
+// mean = Sum / n; variance = (ss - comp^2 / n) / (n - 1) (gonum corrected two-pass)
+__global__ __launch_bounds__(kBlock) void colstats_final_kernel(const StatJob* jobs, const double* part_sum,
+                                                                const double* part_ss, const double* part_comp) {
+  const StatJob J = jobs[blockIdx.x];
+  for (int c = threadIdx.x; c < J.cols; c += kBlock) {
+    double s = 0.0, ss = 0.0, comp = 0.0;
+    for (int q = 0; q < J.nchunks; q++) {
+      const int64_t o = J.part_off + (int64_t)q * J.cols + c;
+      s += part_sum[o];
+      ss += part_ss[o];
+      comp += part_comp[o];
+    }
+    const double n = (double)J.rows;
+    J.out_mean[c] = s / n;
+    if (J.out_std) J.out_std[c] = sqrt((ss - comp * comp / n) / (n - 1.0));
+  }
+}
+
+// ---- spectral coherence ----------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void coherence_kernel(const FpRec* recs, const int64_t* q_idx,
+                                                           const int64_t* c_idx, int64_t nc, double* coh) {
+  __shared__ double s_v[5][kBlock];
+  const int64_t pair = blockIdx.x >> 1;
+  const int seq = blockIdx.x & 1;             // 0 centroid, 1 rolloff
+  const FpRec& A = recs[q_idx[pair / nc]];
+  const FpRec& B = recs[c_idx ? c_idx[pair % nc] : pair % nc];
+  const int s = seq ? SEQ_ROLLOFF : SEQ_CENTROID;
+  const bool both = (A.present & B.present & SONAR_FEAT_SPECTRAL) && A.seq_len[s] > 0 && B.seq_len[s] > 0;
+  if (!both) {                                // not compared: no coherence entry
+    if (threadIdx.x == 0) coh[2 * pair + seq] = NAN;
+    return;
+  }
+  const double* x = seq ? A.rolloff : A.centroid;
+  const double* y = seq ? B.rolloff : B.centroid;
+  const int64_t n = A.seq_len[s];             // == B.seq_len[s], checked on the host
+  const double xu = A.seq_mean[s], yu = B.seq_mean[s];
+  double sxx = 0.0, syy = 0.0, sxy = 0.0, xc = 0.0, yc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) {
+    const double xd = x[i] - xu, yd = y[i] - yu;
+    sxx += xd * xd;
+    syy += yd * yd;
+    sxy += xd * yd;
+    xc += xd;
+    yc += yd;
+  }
+  s_v[0][threadIdx.x] = sxx; s_v[1][threadIdx.x] = syy; s_v[2][threadIdx.x] = sxy;
+  s_v[3][threadIdx.x] = xc; s_v[4][threadIdx.x] = yc;
+  __syncthreads();
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int v = 0; v < 5; v++) s_v[v][threadIdx.x] += s_v[v][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double nn = (double)n;
+    double a = s_v[0][0], b = s_v[1][0], c = s_v[2][0];
+    const double xcs = s_v[3][0], ycs = s_v[4][0];
+    a -= xcs * xcs / nn;
+    b -= ycs * ycs / nn;
+    c -= xcs * ycs / nn;
+    coh[2 * pair + seq] = c / sqrt(a * b);
+  }
+}
+
+// ---- compare ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void compare_kernel(CompareArgs a) {
+  const int64_t pair = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (pair >= a.nq * a.nc) return;
+  const int64_t qi = a.q_idx[pair / a.nc];
+  const int64_t ci = a.c_idx ? a.c_idx[pair % a.nc] : pair % a.nc;
+  const FpRec& A = a.recs[qi];
+  const FpRec& B = a.recs[ci];
+  sonar_similarity r;
+  r.overall_similarity = 0.0;
+  r.feature_similarity = 0.0;
+  r.confidence = 0.0;
+  for (int i = 0; i < 6; i++) r.feature_distances[i] = 0.0;
+  r.data_availability = r.feature_coverage = r.temporal_alignment = 0.0;
+  r.noise_level = r.dynamic_range_match = r.spectral_coherence = 0.0;
+  r.distance_mask = 0;
+  r.has_quality = 0;
+  r.status = (A.id == B.id) ? 1 : 0;
+  r.content_type_match = A.ct == B.ct;
+  if (a.content_filter && !r.content_type_match) {          // :160-166
+    r.confidence = 0.25;
+    a.out[pair] = r;
+    return;
+  }
+  // calculateFeatureSimilarity (:266-341)
+  double fs = 0.0;
+  if ((A.present & B.present & SONAR_FEAT_FEATURES) == 0) {
+    r.status = r.status ? r.status : 2;                       // "features cannot be nil"
+  } else {
+    double sims[6], ws[6];
+    int n = 0;
+    auto add = [&](int key, double sim) {
+      sims[n] = sim;
+      ws[n] = A.w[key];                                       // weights of fp1 (:282)
+      n++;
+      r.feature_distances[key] = 1.0 - sim;
+      r.distance_mask |= 1u << key;
+    };
+    if (A.mfcc_frames > 0 && B.mfcc_frames > 0) {             // compareMFCC (:344-402)
+      double sim = 0.0;
+      if (A.mfcc_C > 0 && B.mfcc_C > 0)
+        sim = cosine(a.pool + A.mfcc_off, 2 * A.mfcc_C, a.pool + B.mfcc_off, 2 * B.mfcc_C);
+      add(SONAR_FD_MFCC, sim);
+    }
+    if (A.present & B.present & SONAR_FEAT_SPECTRAL) {        // compareSpectralFeatures (:646-671)
+      double v[3];
+      int m = 0;
+      for (int s = SEQ_CENTROID; s <= SEQ_FLUX; s++)
+        if (A.seq_len[s] > 0 && B.seq_len[s] > 0) v[m++] = seq_sim(A, B, s);
+      add(SONAR_FD_SPECTRAL, m ? mean_of(v, m) : 0.0);
+    }
+    if (A.chroma_frames > 0 && B.chroma_frames > 0) {         // compareChromaFeatures (:673-688)
+      double sim = 0.0;
+      if (A.chroma_B > 0 && B.chroma_B > 0)
+        sim = cosine(a.pool + A.chroma_off, A.chroma_B, a.pool + B.chroma_off, B.chroma_B);
+      add(SONAR_FD_CHROMA, sim);
+    }
+    if (A.present & B.present & SONAR_FEAT_TEMPORAL) {        // compareTemporalFeatures (:690-719)
+      double v[4];
+      int m = 0;
+      if (A.dynamic_range > 0 && B.dynamic_range > 0) v[m++] = scalar_sim(A.dynamic_range, B.dynamic_range);
+      v[m++] = scalar_sim(A.silence_ratio, B.silence_ratio);
+      if (A.onset_density > 0 && B.onset_density > 0) v[m++] = scalar_sim(A.onset_density, B.onset_density);
+      if (A.seq_len[SEQ_RMS] > 0 && B.seq_len[SEQ_RMS] > 0) v[m++] = seq_sim(A, B, SEQ_RMS);
+      add(SONAR_FD_TEMPORAL, mean_of(v, m));
+    }
+    if (A.present & B.present & SONAR_FEAT_SPEECH) {          // compareSpeechFeatures (:721-747)
+      double v[3];
+      int m = 0;
+      if (A.speech_rate > 0 && B.speech_rate > 0) v[m++] = scalar_sim(A.speech_rate, B.speech_rate);
+      if (A.vtl > 0 && B.vtl > 0) v[m++] = scalar_sim(A.vtl, B.vtl);
+      if (A.seq_len[SEQ_VOICING] > 0 && B.seq_len[SEQ_VOICING] > 0) v[m++] = seq_sim(A, B, SEQ_VOICING);
+      add(SONAR_FD_SPEECH, m ? mean_of(v, m) : 0.0);
+    }
+    if (A.present & B.present & SONAR_FEAT_HARMONIC) {        // compareHarmonicFeatures (:749-770)
+      double v[2];
+      int m = 0;
+      if (A.seq_len[SEQ_HARMONIC] > 0 && B.seq_len[SEQ_HARMONIC] > 0) v[m++] = seq_sim(A, B, SEQ_HARMONIC);
+      if (A.seq_len[SEQ_PITCH] > 0 && B.seq_len[SEQ_PITCH] > 0) v[m++] = seq_sim(A, B, SEQ_PITCH);
+      add(SONAR_FD_HARMONIC, m ? mean_of(v, m) : 0.0);
+    }
+    if (n == 0) {
+      r.status = r.status ? r.status : 2;                     // "no comparable features found"
+    } else {                                                  // stat.Mean(values, weights)
+      double sv = 0.0, sw = 0.0;
+      for (int i = 0; i < n; i++) { sv += ws[i] * sims[i]; sw += ws[i]; }
+      fs = sv / sw;
+    }
+  }
+  r.feature_similarity = fs;
+  r.overall_similarity = fs;                                  // calculateOverallSimilarity (:886-889)
+  const int nd = __popc(r.distance_mask);
+  if (a.detailed) {                                           // calculateQualityMetrics (:892-936)
+    r.has_quality = 1;
+    const uint32_t both = A.present & B.present;
+    const int avail = ((both & SONAR_FEAT_MFCC) != 0) + ((both & SONAR_FEAT_SPECTRAL) != 0) +
+                      ((both & SONAR_FEAT_CHROMA) != 0) + ((both & SONAR_FEAT_TEMPORAL) != 0) +
+                      ((both & SONAR_FEAT_SPEECH) != 0) + ((both & SONAR_FEAT_HARMONIC) != 0);
+    r.data_availability = (double)avail / 6.0;
+    r.feature_coverage = (double)nd / 6.0;
+    const double dd = fabs(A.duration - B.duration), md = go_max(A.duration, B.duration);
+    r.temporal_alignment = md > 0 ? 1.0 - go_min(1.0, dd / md) : 1.0;
+    // estimateNoiseLevel (:939-958); FeatureDistances in key order (a Go map has none)
+    if (nd == 0) {
+      r.noise_level = 0.5;
+    } else if (nd <= 1) {
+      r.noise_level = 0.0;
+    } else {
+      double v[6];
+      int m = 0;
+      for (int key = 0; key < 6; key++)
+        if (r.distance_mask & (1u << key)) v[m++] = 1.0 - r.feature_distances[key];
+      const double mu = mean_of(v, m);
+      double ss = 0.0, comp = 0.0;
+      for (int i = 0; i < m; i++) {
+        const double d = v[i] - mu;
+        ss += d * d;
+        comp += d;
+      }
+      const double var = (ss - comp * comp / (double)m) / (double)(m - 1);
+      r.noise_level = go_min(1.0, sqrt(var));
+    }
+    // calculateDynamicRangeMatch (:961-974)
+    if (!(both & SONAR_FEAT_TEMPORAL) || A.dynamic_range <= 0 || B.dynamic_range <= 0)
+      r.dynamic_range_match = 0.5;
+    else
+      r.dynamic_range_match = scalar_sim(A.dynamic_range, B.dynamic_range);
+    // calculateSpectralCoherence (:977-1008)
+    if (!(both & SONAR_FEAT_SPECTRAL)) {
+      r.spectral_coherence = 0.5;
+    } else {
+      double v[2];
+      int m = 0;
+      for (int s = 0; s < 2; s++) {
+        const double c = a.coh[2 * pair + s];
+        if (!isnan(c)) v[m++] = fabs(c);
+      }
+      r.spectral_coherence = m ? mean_of(v, m) : 0.5;
+    }
+  }
+  // calculateConfidence (:1011-1037)
+  double conf = 0.5;
+  if (r.overall_similarity > 0.8) conf += 0.3;
+  else if (r.overall_similarity > 0.6) conf += 0.2;
+  if (r.content_type_match) conf += 0.1;
+  conf += (double)nd * 0.05;
+  if (r.has_quality) {
+    conf += r.data_availability * 0.1;
+    conf -= r.noise_level * 0.1;
+  }
+  r.confidence = go_max(0.0, go_min(1.0, conf));
+  a.out[pair] = r;
+}
+
+// ---- FindBestMatches ---------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void match_keys_kernel(const sonar_similarity* sims, int64_t nq, int64_t nc,
+                                                            double thr, double* keys, int64_t* vals,
+                                                            unsigned long long* counts) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nq * nc) return;
+  const sonar_similarity& s = sims[i];
+  const bool pass = s.status != 1 && s.overall_similarity >= thr;   // :218 self skip, :232 threshold
+  keys[i] = pass ? s.overall_similarity : -INFINITY;
+  vals[i] = i % nc;
+  if (pass) atomicAdd(&counts[i / nc], 1ull);
+}
+
+__device__ int classify(double s) {                                  // classifyMatch (:1040-1052)
+  if (s >= 0.95) return SONAR_MATCH_EXACT;
+  if (s >= 0.85) return SONAR_MATCH_VERY_SIMILAR;
+  if (s >= 0.75) return SONAR_MATCH_SIMILAR;
+  if (s >= 0.6) return SONAR_MATCH_SOMEWHAT_SIMILAR;
+  return SONAR_MATCH_WEAK;
+}
+
+__global__ __launch_bounds__(kBlock) void match_gather_kernel(const sonar_similarity* sims, const int64_t* vals,
+                                                              const int64_t* counts, int64_t nq, int64_t nc, int K,
+                                                              sonar_match* out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nq * (int64_t)K) return;
+  const int64_t q = i / K, k = i % K;
+  if (k >= counts[q]) return;
+  const int64_t c = vals[q * nc + k];
+  sonar_match m;
+  m.candidate = c;
+  m.rank = (int32_t)k + 1;
+  m.similarity = sims[q * nc + c];
+  m.match_type = classify(m.similarity.overall_similarity);
+  out[i] = m;
+}
+
+inline unsigned blocks(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+int launch_colstats(const StatJob* jobs, int njobs, const int* chunk_job, const int* chunk_k, int nchunks,
+                    double* part_sum, double* part_ss, double* part_comp, hipStream_t s) {
+  if (njobs == 0) return 0;
+  hipLaunchKernelGGL(colstats_kernel<0>, dim3(nchunks), dim3(kBlock), 0, s, jobs, chunk_job, chunk_k, part_sum,
+                     part_ss, part_comp);
+  hipLaunchKernelGGL(colstats_kernel<1>, dim3(nchunks), dim3(kBlock), 0, s, jobs, chunk_job, chunk_k, part_sum,
+                     part_ss, part_comp);
+  hipLaunchKernelGGL(colstats_final_kernel, dim3(njobs), dim3(kBlock), 0, s, jobs, part_sum, part_ss, part_comp);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_coherence(const FpRec* recs, const int64_t* q_idx, int64_t nq, const int64_t* c_idx, int64_t nc,
+                     double* coh, hipStream_t s) {
+  const int64_t nb = 2 * nq * nc;
+  if (nb == 0) return 0;
+  if (nb > 0x7fffffff) return -1;
+  hipLaunchKernelGGL(coherence_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, recs, q_idx, c_idx, nc, coh);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_compare(const CompareArgs& a, hipStream_t s) {
+  const int64_t n = a.nq * a.nc;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(compare_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_match_keys(const sonar_similarity* sims, int64_t nq, int64_t nc, double threshold, double* keys,
+                      int64_t* vals, int64_t* counts, hipStream_t s) {
+  const int64_t n = nq * nc;
+  if (hipMemsetAsync(counts, 0, nq * sizeof(int64_t), s) != hipSuccess) return -1;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(match_keys_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, sims, nq, nc, threshold, keys, vals,
+                     reinterpret_cast<unsigned long long*>(counts));
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// stable segmented sort, descending by key: equal similarities keep candidate order
+int sort_match_keys(const double* keys_in, double* keys_out, const int64_t* vals_in, int64_t* vals_out,
+                    int64_t nq, int64_t nc, const int64_t* seg_off, void* temp, size_t* temp_bytes, hipStream_t s) {
+  const hipError_t e = hipcub::DeviceSegmentedRadixSort::SortPairsDescending(
+      temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out, (int)(nq * nc), (int)nq, seg_off, seg_off + 1, 0,
+      (int)(sizeof(double) * 8), s);
+  return e == hipSuccess ? 0 : -1;
+}
+
+int launch_match_gather(const sonar_similarity* sims, const int64_t* vals_sorted, const int64_t* counts,
+                        int64_t nq, int64_t nc, int K, sonar_match* out, hipStream_t s) {
+  const int64_t n = nq * (int64_t)K;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(match_gather_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, sims, vals_sorted, counts, nq, nc, K,
+                     out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace sonar

@@ -132,4 +132,60 @@ int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 int launch_formants(const double* pcm, int64_t frames, int64_t hop, int W, int p, int sr, int frame_ok_len,
                     const double* ham, sonar_formant_frame* out, double* coeffs, double* refl, hipStream_t s);
 
+// ---- FingerprintComparator (compare_kernels.hip) -------------------------------------
+// sequences summarised per fingerprint (mean, std), in compare order (comparison.go:646-770)
+enum { SEQ_CENTROID = 0, SEQ_ROLLOFF, SEQ_FLUX, SEQ_RMS, SEQ_VOICING, SEQ_HARMONIC, SEQ_PITCH, SEQ_COUNT };
+// One gallery record: everything Compare reads from one fingerprint.
+struct FpRec {
+  int64_t id;
+  uint32_t present;            // SONAR_FEAT_*
+  int32_t ct;
+  double duration;
+  double w[6];                 // getEffectiveWeights(fp) by SONAR_FD_* (comparison.go:1055-1104)
+  int64_t mfcc_frames, chroma_frames;
+  int32_t mfcc_C, chroma_B;
+  int64_t mfcc_off;            // pool: column means [C] then stds [C] (extractMFCCStatistics order)
+  int64_t chroma_off;          // pool: column means [B]
+  double seq_mean[SEQ_COUNT], seq_std[SEQ_COUNT];
+  int64_t seq_len[SEQ_COUNT];
+  double dynamic_range, silence_ratio, onset_density, speech_rate, vtl;
+  const double* centroid;      // kept sequences (device) for the spectral coherence, or null
+  const double* rolloff;
+};
+// column statistics of one row-major matrix (a sequence is cols = 1): gonum stat.Mean and
+// the corrected two-pass stat.Variance, reduced over row chunks
+struct StatJob {
+  const double* src;
+  int64_t rows;
+  int32_t cols;
+  int32_t nchunks;
+  int64_t chunk_rows;
+  int64_t part_off;            // first partial of this job: part[part_off + k * cols + c]
+  double* out_mean;            // [cols]
+  double* out_std;             // [cols] or null (mean only)
+};
+int launch_colstats(const StatJob* jobs, int njobs, const int* chunk_job, const int* chunk_k, int nchunks,
+                    double* part_sum, double* part_ss, double* part_comp, hipStream_t s);
+// gonum stat.Correlation of SpectralCentroid / SpectralRolloff per pair -> coh[pair][2] (NaN = skip)
+int launch_coherence(const FpRec* recs, const int64_t* q_idx, int64_t nq, const int64_t* c_idx, int64_t nc,
+                     double* coh, hipStream_t s);
+struct CompareArgs {
+  const FpRec* recs;
+  const double* pool;
+  const int64_t* q_idx;        // [nq]
+  const int64_t* c_idx;        // [nc] or null (identity)
+  int64_t nq, nc;
+  const double* coh;           // [nq * nc][2] when detailed
+  int detailed, content_filter;
+  sonar_similarity* out;       // [nq * nc]
+};
+int launch_compare(const CompareArgs& a, hipStream_t s);
+// FindBestMatches: keys (overall or -inf), per-query counts, segmented sort, gather
+int launch_match_keys(const sonar_similarity* sims, int64_t nq, int64_t nc, double threshold, double* keys,
+                      int64_t* vals, int64_t* counts, hipStream_t s);
+int sort_match_keys(const double* keys_in, double* keys_out, const int64_t* vals_in, int64_t* vals_out,
+                    int64_t nq, int64_t nc, const int64_t* seg_off, void* temp, size_t* temp_bytes, hipStream_t s);
+int launch_match_gather(const sonar_similarity* sims, const int64_t* vals_sorted, const int64_t* counts,
+                        int64_t nq, int64_t nc, int K, sonar_match* out, hipStream_t s);
+
 }  // namespace sonar

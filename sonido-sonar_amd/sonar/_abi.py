@@ -75,6 +75,45 @@ class FormantFrame(C.Structure):
                 ("residual_energy", C.c_double), ("stable", C.c_int32), ("lpc_order", C.c_int32)]
 
 
+class FpFeatures(C.Structure):
+    """sonar_fp_features (one AudioFingerprint as FingerprintComparator reads it)."""
+    _fields_ = [("id", C.c_int64), ("present", C.c_uint32), ("content_type", C.c_int32),
+                ("duration_seconds", C.c_double),
+                ("mfcc", C.c_void_p), ("mfcc_frames", C.c_int64), ("mfcc_coeffs", C.c_int32),
+                ("chroma", C.c_void_p), ("chroma_frames", C.c_int64), ("chroma_bins", C.c_int32),
+                ("spectral_centroid", C.c_void_p), ("n_spectral_centroid", C.c_int64),
+                ("spectral_rolloff", C.c_void_p), ("n_spectral_rolloff", C.c_int64),
+                ("spectral_flux", C.c_void_p), ("n_spectral_flux", C.c_int64),
+                ("dynamic_range", C.c_double), ("silence_ratio", C.c_double), ("onset_density", C.c_double),
+                ("rms_energy", C.c_void_p), ("n_rms_energy", C.c_int64),
+                ("speech_rate", C.c_double), ("vocal_tract_length", C.c_double),
+                ("voicing_probability", C.c_void_p), ("n_voicing_probability", C.c_int64),
+                ("harmonic_ratio", C.c_void_p), ("n_harmonic_ratio", C.c_int64),
+                ("pitch_estimate", C.c_void_p), ("n_pitch_estimate", C.c_int64),
+                ("feature_weights", C.c_double * 6)]
+
+
+class CompareCfg(C.Structure):
+    _fields_ = [("similarity_threshold", C.c_double), ("max_candidates", C.c_int32),
+                ("enable_detailed_metrics", C.c_int32), ("enable_content_filter", C.c_int32),
+                ("method", C.c_int32)]
+
+
+class Similarity(C.Structure):
+    _fields_ = [("overall_similarity", C.c_double), ("feature_similarity", C.c_double),
+                ("confidence", C.c_double), ("feature_distances", C.c_double * 6),
+                ("data_availability", C.c_double), ("feature_coverage", C.c_double),
+                ("temporal_alignment", C.c_double), ("noise_level", C.c_double),
+                ("dynamic_range_match", C.c_double), ("spectral_coherence", C.c_double),
+                ("distance_mask", C.c_uint32), ("content_type_match", C.c_int32),
+                ("has_quality", C.c_int32), ("status", C.c_int32)]
+
+
+class Match(C.Structure):
+    _fields_ = [("candidate", C.c_int64), ("rank", C.c_int32), ("match_type", C.c_int32),
+                ("similarity", Similarity)]
+
+
 _lib = None
 _vp, _d, _i32p, _i64p = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
 
@@ -132,6 +171,15 @@ def lib():
     L.sonar_formant_frame_count.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32]
     L.sonar_formant_frame_count.restype = C.c_int64
     L.sonar_formants.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, C.c_int32]
+    L.sonar_gallery_create.argtypes = [_vp, C.POINTER(_vp)]
+    L.sonar_gallery_destroy.argtypes = [_vp]
+    L.sonar_gallery_destroy.restype = None
+    L.sonar_gallery_size.argtypes = [_vp]
+    L.sonar_gallery_size.restype = C.c_int64
+    L.sonar_gallery_add.argtypes = [_vp, C.POINTER(FpFeatures), C.c_int32, C.c_int32, C.c_int32, _i64p]
+    L.sonar_compare.argtypes = [_vp, _i64p, C.c_int64, _i64p, C.c_int64, C.POINTER(CompareCfg), _vp, C.c_int32]
+    L.sonar_find_best_matches.argtypes = [_vp, _i64p, C.c_int64, _i64p, C.c_int64, C.POINTER(CompareCfg),
+                                          C.POINTER(Match), _i64p]
     L.sonar_result_get.argtypes = [_vp, C.c_char_p, C.POINTER(_d), _i64p, _i64p]
     L.sonar_result_count.argtypes = [_vp]
     L.sonar_result_name.argtypes = [_vp, C.c_int]
