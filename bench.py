@@ -52,6 +52,12 @@ def parse():
     ap.add_argument("--c5-seconds", type=float, default=60.0)
     ap.add_argument("--c5-max-lag", type=float, default=20.0, help="maxOffsetSeconds (lags are drawn in [0, 20) s)")
     ap.add_argument("--c5-workers", type=int, default=8, help="concurrent contexts (HIP streams) per rank")
+    ap.add_argument("--c6-gallery", type=int, default=256, help="C3-sized fingerprints added (0 = skip row f1)")
+    ap.add_argument("--c6-frames", type=int, default=51676)
+    ap.add_argument("--c6-compare-gallery", type=int, default=65536)
+    ap.add_argument("--c6-queries", type=int, default=64)
+    ap.add_argument("--c6-reps", type=int, default=3)
+    ap.add_argument("--c6-cpu-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=0.0, help="force CPU-baseline sample length")
     return ap.parse_args()
@@ -170,6 +176,128 @@ def bench_c5(args, world, rank, dev):
             "c5_lag_recovered": float(ok.mean()), "c5_dtw_cells_per_pair": int((args.c5_seconds * SR - W) // H + 1) ** 2}
 
 
+def bench_c6(args, ctx, dev):
+    """Row f1: FingerprintComparator on a device gallery.
+    (1) gallery_add of G C3-sized fingerprints (5 min at 44.1 kHz, 51,676 frames, the speech
+        extractor's arrays) already in HBM: the per-fingerprint statistics kernels stream every
+        feature element once per pass (HBM roofline);
+    (2) BatchCompare of Q queries against a gallery of short fingerprints (one compare thread
+        per pair, pairs/s) and with EnableDetailedMetrics against the C3-sized gallery (the
+        coherence kernel streams both spectral sequences per pair);
+    (3) CPU baseline: the oracle's Compare, which rebuilds the statistics from the full arrays
+        on every call as comparison.go does, on a bounded sample of C3-sized pairs, 1 thread."""
+    from sonar import compare as cmp
+    G, F = args.c6_gallery, args.c6_frames
+    buf, structs, per_bytes = cmp.device_features(G, F, dev, seed=6)
+    torch.cuda.synchronize()
+    g = cmp.Gallery(ctx)
+    g.add_raw(structs, min(G, 4), keep_sequences=False, device_ptrs=True)     # warm-up
+    g.close()
+    res = {}
+    adds = []
+    for rep in range(args.c6_reps):
+        g = cmp.Gallery(ctx)
+        ctx.last_kernel_ms()
+        ctx.enable_kernel_timing(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.add_raw(structs, G, keep_sequences=False, device_ptrs=True)
+        dt = time.perf_counter() - t0
+        ctx.enable_kernel_timing(False)
+        adds.append((dt, ctx.last_kernel_ms()))
+        g.close()
+    dt, kms = min(adds, key=lambda x: x[0])
+    res["c6_gallery_add"] = {"fingerprints": G, "frames_each": F, "feature_bytes_each": per_bytes,
+                             "fingerprints_per_s": G / dt, "ms": dt * 1e3, "colstats_kernel_ms": kms,
+                             "roofline": {"bound": "hbm", "kernel": "colstats_kernel<0>+<1>+final",
+                                          "achieved": G * per_bytes / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                          "unit": "GB/s", "frac": G * per_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                          "algorithmic_bytes": "every feature element read once (8 B)"}}
+    # detailed-metrics compare on the C3-sized gallery (coherence streams the spectral sequences)
+    g = cmp.Gallery(ctx)
+    g.add_raw(structs, G, keep_sequences=True, device_ptrs=True)
+    cfg = cmp.make_cfg({"similarity_threshold": 0.0, "max_candidates": 50, "enable_detailed_metrics": True})
+    q = np.arange(min(8, G))
+    g.compare(q, None, cfg)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.c6_reps):
+        g.compare(q, None, cfg)
+    dt = (time.perf_counter() - t0) / args.c6_reps
+    npair = len(q) * G
+    res["c6_compare_detailed"] = {"queries": len(q), "candidates": G, "pairs_per_s": npair / dt, "ms": dt * 1e3,
+                                  "coherence_stream_gbs": npair * 2 * F * 8 / dt / 1e9}
+    g.close()
+    del buf
+    # plain BatchCompare throughput on a large gallery of short fingerprints
+    G2, Q2 = args.c6_compare_gallery, args.c6_queries
+    buf2, st2, _ = cmp.device_features(G2, 32, dev, seed=7)
+    g = cmp.Gallery(ctx)
+    g.add_raw(st2, G2, keep_sequences=False, device_ptrs=True)
+    cfg = cmp.make_cfg({"similarity_threshold": 0.5, "max_candidates": 50})
+    q = np.arange(Q2)
+    from sonar._abi import Similarity
+    import ctypes
+    dout = torch.empty(Q2 * G2 * ctypes.sizeof(Similarity), dtype=torch.uint8, device=dev)
+    g.compare_device(q, None, cfg, dout.data_ptr())
+    torch.cuda.synchronize()
+    ctx.last_kernel_ms()
+    ctx.enable_kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.c6_reps):
+        g.compare_device(q, None, cfg, dout.data_ptr())
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.c6_reps
+    t2 = time.perf_counter()
+    g.compare(q, None, cfg)
+    dth = time.perf_counter() - t2
+    ctx.enable_kernel_timing(False)
+    kms = ctx.last_kernel_ms()
+    t1 = time.perf_counter()
+    for _ in range(args.c6_reps):
+        g.find_best_matches(q, None, cfg)
+    dtm = (time.perf_counter() - t1) / args.c6_reps
+    res["c6_compare"] = {"queries": Q2, "candidates": G2, "pairs_per_s": Q2 * G2 / dt, "ms": dt * 1e3,
+                         "compare_kernel_ms": kms, "kernel_pairs_per_s": Q2 * G2 / (kms * 1e-3),
+                         "host_results_ms": dth * 1e3, "find_best_matches_ms": dtm * 1e3,
+                         "note": "ms: results left in HBM (device_ptrs); host_results_ms adds the D2H copy of "
+                                 "every SimilarityResult into pageable memory"}
+    del dout
+    g.close()
+    del buf2
+    return res
+
+
+def c6_cpu_baseline(args):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from sonar import compare as cmp
+    F = args.c6_frames
+    rng = np.random.default_rng(6)
+    Fp = F // 2
+
+    def fp(i):
+        d = {"mfcc": np.abs(rng.normal(size=(F, 13))), "spectral": {k: np.abs(rng.normal(size=n)) for k, n in
+                                                                     (("centroid", F), ("rolloff", F), ("flux", F - 1))},
+             "temporal": {"dynamic_range": 20.0, "silence_ratio": 0.1, "onset_density": 1.0,
+                          "rms_energy": np.abs(rng.normal(size=F))},
+             "speech": {"speech_rate": 3.0, "vocal_tract_length": 17.5, "voicing_probability": np.abs(rng.normal(size=F))},
+             "harmonic": {"harmonic_ratio": np.abs(rng.normal(size=Fp)), "pitch_estimate": np.abs(rng.normal(size=Fp))}}
+        return cmp.Fingerprint(f"c{i}", "news", F * 256 / 44100.0, cmp.Features(
+            mfcc=d["mfcc"], spectral=d["spectral"], temporal=d["temporal"], speech=d["speech"], harmonic=d["harmonic"]))
+
+    fps = [cmp.marshal(fp(i)) for i in range(4)]
+    cfg = cmp.make_cfg({"similarity_threshold": 0.0, "max_candidates": 50})
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.c6_cpu_seconds:
+        O.fp_compare(fps[n % 4][0], fps[(n + 1) % 4][0], cfg)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"{n} Compare calls on C3-sized fingerprints ({F} frames), oracle recomputing the "
+                      "statistics per call as comparison.go does, float64, 1 thread"}
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup()
@@ -225,6 +353,10 @@ def main():
         extra = bench_dtw(ctx, args.dtw_len, args.dtw_steps)
     if args.c5_pairs > 0:
         extra.update(bench_c5(args, world, rank, dev))
+    if args.c6_gallery > 0:
+        extra.update(bench_c6(args, ctx, dev))
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            extra["c6_cpu_baseline"] = c6_cpu_baseline(args)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

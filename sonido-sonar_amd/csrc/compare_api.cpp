@@ -30,7 +30,6 @@ struct sonar_gallery {
 namespace {
 
 constexpr double kNaN = std::numeric_limits<double>::quiet_NaN();
-constexpr int64_t kChunkElems = 1 << 16;   // elements per column-statistics block
 
 // getEffectiveWeights (comparison.go:1055-1104), by SONAR_FD_* (mfcc, spectral, chroma,
 // temporal, speech, harmonic); "energy" is never looked up by calculateFeatureSimilarity
@@ -224,7 +223,7 @@ int sonar_gallery_add(sonar_gallery* g, const sonar_fp_features* fps, int32_t co
   int64_t parts = 0;
   for (size_t j = 0; j < jobs.size(); j++) {
     StatJob& J = jobs[j];
-    J.chunk_rows = std::max<int64_t>(1, kChunkElems / J.cols);
+    J.chunk_rows = sonar::colstats_chunk_rows_for(J.cols);
     const int64_t nch = (J.rows + J.chunk_rows - 1) / J.chunk_rows;
     if (nch > 0x7fffffff) return fail(c, SONAR_ERR_UNSUPPORTED, "feature matrix too large");
     J.nchunks = (int32_t)nch;
@@ -235,7 +234,7 @@ int sonar_gallery_add(sonar_gallery* g, const sonar_fp_features* fps, int32_t co
   if (!jobs.empty()) {
     const size_t jb = jobs.size() * sizeof(StatJob), cb = chunk_job.size() * sizeof(int);
     char* meta = static_cast<char*>(dbuf(c, "cmp.jobs", jb + 2 * cb + 64));
-    double* part = static_cast<double*>(dbuf(c, "cmp.part", 3 * parts * sizeof(double)));
+    double* part = static_cast<double*>(dbuf(c, "cmp.part", 2 * parts * sizeof(double)));
     if (!meta || !part) return fail(c, SONAR_ERR_NOMEM, "statistics allocation failed");
     StatJob* djobs = reinterpret_cast<StatJob*>(meta);
     int* dcj = reinterpret_cast<int*>(meta + ((jb + 15) & ~size_t(15)));
@@ -244,8 +243,7 @@ int sonar_gallery_add(sonar_gallery* g, const sonar_fp_features* fps, int32_t co
     HIP_TRY(c, hipMemcpyAsync(dcj, chunk_job.data(), cb, hipMemcpyHostToDevice, s));
     HIP_TRY(c, hipMemcpyAsync(dck, chunk_k.data(), cb, hipMemcpyHostToDevice, s));
     hipEvent_t tend = sonar::detail::timed_begin(c, s);
-    if (sonar::launch_colstats(djobs, (int)jobs.size(), dcj, dck, (int)chunk_job.size(), part, part + parts,
-                               part + 2 * parts, s))
+    if (sonar::launch_colstats(djobs, (int)jobs.size(), dcj, dck, (int)chunk_job.size(), part, part + parts, s))
       return fail(c, SONAR_ERR_DEVICE, "colstats launch failed");
     sonar::detail::timed_end(c, s, tend);
   }
@@ -354,26 +352,26 @@ int sonar_find_best_matches(sonar_gallery* g, const int64_t* queries, int64_t nq
   const int64_t n = nq * nc, K = cfg->max_candidates;
   if (n > 0x7fffffff) return fail(c, SONAR_ERR_UNSUPPORTED, "too many pairs for one call");
   hipStream_t s = c->stream;
-  char* w = static_cast<char*>(dbuf(c, "cmp.match", (size_t)n * 32 + (nq + 1) * 16 + 256));
+  char* w = static_cast<char*>(dbuf(c, "cmp.match", (size_t)n * 49 + nq * 8 + 256));
   if (!w) return fail(c, SONAR_ERR_NOMEM, "allocation failed");
   double* keys = reinterpret_cast<double*>(w);
   double* keys2 = keys + n;
   int64_t* vals = reinterpret_cast<int64_t*>(keys2 + n);
   int64_t* vals2 = vals + n;
-  int64_t* counts = vals2 + n;
-  int64_t* seg = counts + nq;
-  std::vector<int64_t> off(nq + 1);
-  for (int64_t q = 0; q <= nq; q++) off[q] = q * nc;
-  HIP_TRY(c, hipMemcpyAsync(seg, off.data(), (nq + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-  if (sonar::launch_match_keys(sims, nq, nc, cfg->similarity_threshold, keys, vals, counts, s))
+  int64_t* vals3 = vals2 + n;
+  int32_t* qk = reinterpret_cast<int32_t*>(vals3 + n);
+  int32_t* qk2 = qk + n;
+  int64_t* counts = reinterpret_cast<int64_t*>(qk2 + n + (n & 1));
+  uint8_t* pass = reinterpret_cast<uint8_t*>(counts + nq);
+  if (sonar::launch_match_keys(sims, nq, nc, cfg->similarity_threshold, keys, vals, pass, counts, s))
     return fail(c, SONAR_ERR_DEVICE, "match key launch failed");
-  size_t tb = 0;
   if (n > 0) {
-    if (sonar::sort_match_keys(keys, keys2, vals, vals2, nq, nc, seg, nullptr, &tb, s))
+    size_t tb = 0;
+    if (sonar::sort_match_keys(keys, keys2, vals, vals2, vals3, qk, qk2, nq, nc, nullptr, &tb, s))
       return fail(c, SONAR_ERR_DEVICE, "sort sizing failed");
     void* tmp = dbuf(c, "cmp.sorttmp", tb);
     if (!tmp) return fail(c, SONAR_ERR_NOMEM, "allocation failed");
-    if (sonar::sort_match_keys(keys, keys2, vals, vals2, nq, nc, seg, tmp, &tb, s))
+    if (sonar::sort_match_keys(keys, keys2, vals, vals2, vals3, qk, qk2, nq, nc, tmp, &tb, s))
       return fail(c, SONAR_ERR_DEVICE, "sort failed");
   }
   std::vector<int64_t> cnt(nq);
@@ -382,7 +380,7 @@ int sonar_find_best_matches(sonar_gallery* g, const int64_t* queries, int64_t nq
     sonar_match* dm = static_cast<sonar_match*>(dbuf(c, "cmp.matches", (size_t)(nq * K) * sizeof(sonar_match)));
     if (!dm) return fail(c, SONAR_ERR_NOMEM, "allocation failed");
     HIP_TRY(c, hipMemsetAsync(dm, 0, (size_t)(nq * K) * sizeof(sonar_match), s));
-    if (sonar::launch_match_gather(sims, vals2, counts, nq, nc, (int)K, dm, s))
+    if (sonar::launch_match_gather(sims, vals3, counts, nq, nc, (int)K, dm, s))
       return fail(c, SONAR_ERR_DEVICE, "gather launch failed");
     if (!out) return fail(c, SONAR_ERR_INVALID, "out is null");
     HIP_TRY(c, hipMemcpyAsync(out, dm, (size_t)(nq * K) * sizeof(sonar_match), hipMemcpyDeviceToHost, s));

@@ -11,7 +11,7 @@
 //   compare         one thread per (query, candidate): calculateFeatureSimilarity and the
 //                   scorers over two gallery records (comparison.go:133-194, 266-402,
 //                   646-1037); a few hundred float64 operations per pair.
-// FindBestMatches adds a segmented radix sort (hipCUB) of the per-query keys.
+// FindBestMatches adds two stable device-wide radix sorts (hipCUB) of the per-pair keys.
 // Built with -ffp-contract=off: Go on amd64 rounds every product and sum separately.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -93,85 +93,156 @@ __device__ double mean_of(const double* v, int n) {   // stat.Mean(v, nil) = flo
 }
 
 // ---- column statistics ----------------------------------------------------------------
-// Thread layout for a chunk of a rows x cols matrix: cols <= 256 -> 256/cols rows per step,
-// thread t owns column t % cols (reads of a step are one contiguous run); wider matrices ->
-// thread t owns columns t, t + 256, ... and walks the rows.
-template <int PASS>
+// One pass over HBM: a block owns a chunk of rows, holds its kRegs values per thread in
+// registers, and writes the chunk's column sums and its corrected two-pass M2 around the
+// chunk mean (ss - comp^2 / n_k, gonum's form).  The final kernel merges the chunks
+// (Chan et al.: M2 = sum_k M2_k + n_k (mean_k - mean)^2): the same quantity as gonum's
+// corrected two-pass variance over the whole column, rounded differently (~1e-16 rel.).
+// Thread layout for cols <= 256: 256 / cols rows per step, thread t owns column t % cols
+// (each step's reads are one contiguous run); wider matrices: thread t owns columns t,
+// t + 256, ... and reads the chunk's rows twice (L2-resident).
+constexpr int kRegs = 16;
+
+__host__ __device__ inline int64_t colstats_chunk_rows(int cols) {
+  return cols <= kBlock ? (int64_t)(kBlock / cols) * kRegs : kRegs;
+}
+
+__device__ double block_sum(double v, double* s_v) {
+  s_v[threadIdx.x] = v;
+  __syncthreads();
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s_v[threadIdx.x] += s_v[threadIdx.x + w];
+    __syncthreads();
+  }
+  const double r = s_v[0];
+  __syncthreads();
+  return r;
+}
+
+// Chunk merge (own launch, one block per job): mean = Sum / n; variance = M2 / (n - 1)
+// (n = 1 -> 0 / 0 = NaN, as gonum).  All columns at once with the chunk kernel's thread
+// layout; fixed thread assignment + fixed-order sums (deterministic).  A fused "last block
+// merges" variant needs agent-scope release fences, which write back the XCD's L2 per block
+// and measured 20x slower.
+__device__ void colstats_merge(const StatJob& J, const double* part_sum, const double* part_m2, double* s_a) {
+  const int C = J.cols, t = threadIdx.x;
+  const double n = (double)J.rows;
+  auto nk_of = [&](int q) {
+    return (double)(min(J.rows, (int64_t)(q + 1) * J.chunk_rows) - (int64_t)q * J.chunk_rows);
+  };
+  if (C <= kBlock) {
+    const int rpi = kBlock / C, active = rpi * C, c = t % C, g = t / C;
+    double s = 0.0;
+    if (t < active)
+      for (int q = g; q < J.nchunks; q += rpi) s += part_sum[J.part_off + (int64_t)q * C + c];
+    s_a[t] = s;
+    __syncthreads();
+    double tot = 0.0;
+    for (int q = 0; q < rpi; q++) tot += s_a[c + q * C];
+    const double mean = tot / n;
+    __syncthreads();
+    double m2 = 0.0;
+    if (t < active)
+      for (int q = g; q < J.nchunks; q += rpi) {
+        const int64_t o = J.part_off + (int64_t)q * C + c;
+        const double nk = nk_of(q), dm = part_sum[o] / nk - mean;
+        m2 += part_m2[o] + nk * dm * dm;
+      }
+    s_a[t] = m2;
+    __syncthreads();
+    if (t < C) {
+      double mm = 0.0;
+      for (int q = 0; q < rpi; q++) mm += s_a[t + q * C];
+      J.out_mean[t] = mean;
+      if (J.out_std) J.out_std[t] = sqrt(mm / (n - 1.0));
+    }
+  } else {
+    for (int c = 0; c < C; c++) {
+      double s = 0.0;
+      for (int q = t; q < J.nchunks; q += kBlock) s += part_sum[J.part_off + (int64_t)q * C + c];
+      const double mean = block_sum(s, s_a) / n;
+      double m2 = 0.0;
+      for (int q = t; q < J.nchunks; q += kBlock) {
+        const int64_t o = J.part_off + (int64_t)q * C + c;
+        const double nk = nk_of(q), dm = part_sum[o] / nk - mean;
+        m2 += part_m2[o] + nk * dm * dm;
+      }
+      m2 = block_sum(m2, s_a);
+      if (t == 0) {
+        J.out_mean[c] = mean;
+        if (J.out_std) J.out_std[c] = sqrt(m2 / (n - 1.0));
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void colstats_kernel(const StatJob* jobs, const int* chunk_job,
-                                                          const int* chunk_k, double* part_sum,
-                                                          double* part_ss, double* part_comp) {
+                                                          const int* chunk_k, double* part_sum, double* part_m2) {
   __shared__ double s_a[kBlock], s_b[kBlock];
   const StatJob J = jobs[chunk_job[blockIdx.x]];
   const int k = chunk_k[blockIdx.x];
   const int C = J.cols, t = threadIdx.x;
   const int64_t r0 = (int64_t)k * J.chunk_rows, r1 = min(J.rows, r0 + J.chunk_rows);
-  auto col_mean = [&](int c) {            // the same fixed-order sum as the final pass
-    double s = 0.0;
-    for (int q = 0; q < J.nchunks; q++) s += part_sum[J.part_off + (int64_t)q * C + c];
-    return s / (double)J.rows;
-  };
+  const double nk = (double)(r1 - r0);
   if (C <= kBlock) {
-    const int rpi = kBlock / C, active = rpi * C;
-    double a = 0.0, b = 0.0;
-    if (t < active) {
-      const int c = t % C;
-      const double mu = PASS ? col_mean(c) : 0.0;
-      for (int64_t r = r0 + t / C; r < r1; r += rpi) {
-        const double x = J.src[r * C + c];
-        if (PASS) {
-          const double d = x - mu;
-          a += d * d;
-          b += d;
-        } else {
-          a += x;
-        }
+    const int rpi = kBlock / C, active = rpi * C, c = t % C;
+    double v[kRegs];
+    double a = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRegs; i++) {
+      const int64_t r = r0 + t / C + (int64_t)i * rpi;
+      v[i] = (t < active && r < r1) ? J.src[r * C + c] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kRegs; i++) a += v[i];
+    s_a[t] = a;
+    __syncthreads();
+    double sum = 0.0;                                   // chunk column sum, fixed order
+    for (int q = 0; q < rpi; q++) sum += s_a[c + q * C];
+    const double mu = sum / nk;
+    double ss = 0.0, comp = 0.0;
+#pragma unroll
+    for (int i = 0; i < kRegs; i++) {
+      const int64_t r = r0 + t / C + (int64_t)i * rpi;
+      if (t < active && r < r1) {
+        const double d = v[i] - mu;
+        ss += d * d;
+        comp += d;
       }
     }
-    s_a[t] = a;
-    s_b[t] = b;
+    __syncthreads();
+    s_a[t] = ss;
+    s_b[t] = comp;
     __syncthreads();
     if (t < C) {
-      double sa = 0.0, sb = 0.0;
-      for (int q = 0; q < rpi; q++) { sa += s_a[t + q * C]; sb += s_b[t + q * C]; }
+      double sss = 0.0, sc = 0.0;
+      for (int q = 0; q < rpi; q++) { sss += s_a[t + q * C]; sc += s_b[t + q * C]; }
       const int64_t o = J.part_off + (int64_t)k * C + t;
-      if (PASS) { part_ss[o] = sa; part_comp[o] = sb; } else { part_sum[o] = sa; }
+      part_sum[o] = sum;
+      part_m2[o] = sss - sc * sc / nk;
     }
   } else {
     for (int c = t; c < C; c += kBlock) {
-      const double mu = PASS ? col_mean(c) : 0.0;
-      double a = 0.0, b = 0.0;
+      double sum = 0.0;
+      for (int64_t r = r0; r < r1; r++) sum += J.src[r * C + c];
+      const double mu = sum / nk;
+      double ss = 0.0, comp = 0.0;
       for (int64_t r = r0; r < r1; r++) {
-        const double x = J.src[r * C + c];
-        if (PASS) {
-          const double d = x - mu;
-          a += d * d;
-          b += d;
-        } else {
-          a += x;
-        }
+        const double d = J.src[r * C + c] - mu;
+        ss += d * d;
+        comp += d;
       }
       const int64_t o = J.part_off + (int64_t)k * C + c;
-      if (PASS) { part_ss[o] = a; part_comp[o] = b; } else { part_sum[o] = a; }
+      part_sum[o] = sum;
+      part_m2[o] = ss - comp * comp / nk;
     }
   }
 }
 
-// mean = Sum / n; variance = (ss - comp^2 / n) / (n - 1) (gonum corrected two-pass)
 __global__ __launch_bounds__(kBlock) void colstats_final_kernel(const StatJob* jobs, const double* part_sum,
-                                                                const double* part_ss, const double* part_comp) {
-  const StatJob J = jobs[blockIdx.x];
-  for (int c = threadIdx.x; c < J.cols; c += kBlock) {
-    double s = 0.0, ss = 0.0, comp = 0.0;
-    for (int q = 0; q < J.nchunks; q++) {
-      const int64_t o = J.part_off + (int64_t)q * J.cols + c;
-      s += part_sum[o];
-      ss += part_ss[o];
-      comp += part_comp[o];
-    }
-    const double n = (double)J.rows;
-    J.out_mean[c] = s / n;
-    if (J.out_std) J.out_std[c] = sqrt((ss - comp * comp / n) / (n - 1.0));
-  }
+                                                                const double* part_m2) {
+  __shared__ double s_a[kBlock];
+  colstats_merge(jobs[blockIdx.x], part_sum, part_m2, s_a);
 }
 
 // ---- spectral coherence ----------------------------------------------------------------
@@ -377,14 +448,29 @@ __global__ __launch_bounds__(kBlock) void compare_kernel(CompareArgs a) {
 // ---- FindBestMatches ---------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void match_keys_kernel(const sonar_similarity* sims, int64_t nq, int64_t nc,
                                                             double thr, double* keys, int64_t* vals,
-                                                            unsigned long long* counts) {
+                                                            uint8_t* pass_flag) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= nq * nc) return;
   const sonar_similarity& s = sims[i];
   const bool pass = s.status != 1 && s.overall_similarity >= thr;   // :218 self skip, :232 threshold
   keys[i] = pass ? s.overall_similarity : -INFINITY;
-  vals[i] = i % nc;
-  if (pass) atomicAdd(&counts[i / nc], 1ull);
+  vals[i] = i;                                                      // pair index q * nc + c
+  pass_flag[i] = pass;
+}
+
+// matches per query: one block per query, fixed-order tree sum (no atomics)
+__global__ __launch_bounds__(kBlock) void match_count_kernel(const uint8_t* pass_flag, int64_t nc, int64_t* counts) {
+  __shared__ int64_t s_c[kBlock];
+  const uint8_t* f = pass_flag + (int64_t)blockIdx.x * nc;
+  int64_t c = 0;
+  for (int64_t i = threadIdx.x; i < nc; i += kBlock) c += f[i];
+  s_c[threadIdx.x] = c;
+  __syncthreads();
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) s_c[threadIdx.x] += s_c[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) counts[blockIdx.x] = s_c[0];
 }
 
 __device__ int classify(double s) {                                  // classifyMatch (:1040-1052)
@@ -402,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void match_gather_kernel(const sonar_simila
   if (i >= nq * (int64_t)K) return;
   const int64_t q = i / K, k = i % K;
   if (k >= counts[q]) return;
-  const int64_t c = vals[q * nc + k];
+  const int64_t c = vals[q * nc + k] % nc;
   sonar_match m;
   m.candidate = c;
   m.rank = (int32_t)k + 1;
@@ -411,18 +497,23 @@ __global__ __launch_bounds__(kBlock) void match_gather_kernel(const sonar_simila
   out[i] = m;
 }
 
+__global__ __launch_bounds__(kBlock) void pair_query_kernel(const int64_t* pairs, int64_t n, int64_t nc,
+                                                            int32_t* q) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) q[i] = (int32_t)(pairs[i] / nc);
+}
+
 inline unsigned blocks(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 }  // namespace
 
+int64_t colstats_chunk_rows_for(int cols) { return colstats_chunk_rows(cols); }
+
 int launch_colstats(const StatJob* jobs, int njobs, const int* chunk_job, const int* chunk_k, int nchunks,
-                    double* part_sum, double* part_ss, double* part_comp, hipStream_t s) {
+                    double* part_sum, double* part_m2, hipStream_t s) {
   if (njobs == 0) return 0;
-  hipLaunchKernelGGL(colstats_kernel<0>, dim3(nchunks), dim3(kBlock), 0, s, jobs, chunk_job, chunk_k, part_sum,
-                     part_ss, part_comp);
-  hipLaunchKernelGGL(colstats_kernel<1>, dim3(nchunks), dim3(kBlock), 0, s, jobs, chunk_job, chunk_k, part_sum,
-                     part_ss, part_comp);
-  hipLaunchKernelGGL(colstats_final_kernel, dim3(njobs), dim3(kBlock), 0, s, jobs, part_sum, part_ss, part_comp);
+  hipLaunchKernelGGL(colstats_kernel, dim3(nchunks), dim3(kBlock), 0, s, jobs, chunk_job, chunk_k, part_sum, part_m2);
+  hipLaunchKernelGGL(colstats_final_kernel, dim3(njobs), dim3(kBlock), 0, s, jobs, part_sum, part_m2);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -443,22 +534,41 @@ int launch_compare(const CompareArgs& a, hipStream_t s) {
 }
 
 int launch_match_keys(const sonar_similarity* sims, int64_t nq, int64_t nc, double threshold, double* keys,
-                      int64_t* vals, int64_t* counts, hipStream_t s) {
+                      int64_t* vals, uint8_t* pass_flag, int64_t* counts, hipStream_t s) {
   const int64_t n = nq * nc;
-  if (hipMemsetAsync(counts, 0, nq * sizeof(int64_t), s) != hipSuccess) return -1;
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(match_keys_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, sims, nq, nc, threshold, keys, vals,
-                     reinterpret_cast<unsigned long long*>(counts));
+  if (nq == 0) return 0;
+  if (n > 0)
+    hipLaunchKernelGGL(match_keys_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, sims, nq, nc, threshold, keys, vals,
+                       pass_flag);
+  hipLaunchKernelGGL(match_count_kernel, dim3((unsigned)nq), dim3(kBlock), 0, s, pass_flag, nc, counts);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// stable segmented sort, descending by key: equal similarities keep candidate order
-int sort_match_keys(const double* keys_in, double* keys_out, const int64_t* vals_in, int64_t* vals_out,
-                    int64_t nq, int64_t nc, const int64_t* seg_off, void* temp, size_t* temp_bytes, hipStream_t s) {
-  const hipError_t e = hipcub::DeviceSegmentedRadixSort::SortPairsDescending(
-      temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out, (int)(nq * nc), (int)nq, seg_off, seg_off + 1, 0,
-      (int)(sizeof(double) * 8), s);
-  return e == hipSuccess ? 0 : -1;
+// Per-query descending order in two stable device-wide radix sorts (LSD): by similarity
+// (descending), then by query index -- every query keeps its candidates' similarity order and,
+// for equal similarities, candidate order.  (A segmented sort would give each query one block.)
+int sort_match_keys(const double* keys, double* keys2, const int64_t* vals, int64_t* vals2, int64_t* vals3,
+                    int32_t* qk, int32_t* qk2, int64_t nq, int64_t nc, void* temp, size_t* temp_bytes,
+                    hipStream_t s) {
+  const int n = (int)(nq * nc);
+  int qbits = 1;
+  while ((int64_t(1) << qbits) < nq) qbits++;
+  if (!temp) {
+    size_t a = 0, b = 0;
+    if (hipcub::DeviceRadixSort::SortPairsDescending(nullptr, a, keys, keys2, vals, vals2, n, 0, 64, s) !=
+            hipSuccess ||
+        hipcub::DeviceRadixSort::SortPairs(nullptr, b, qk, qk2, vals2, vals3, n, 0, qbits, s) != hipSuccess)
+      return -1;
+    *temp_bytes = a > b ? a : b;
+    return 0;
+  }
+  size_t tb = *temp_bytes;
+  if (hipcub::DeviceRadixSort::SortPairsDescending(temp, tb, keys, keys2, vals, vals2, n, 0, 64, s) != hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(pair_query_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, vals2, (int64_t)n, nc, qk);
+  tb = *temp_bytes;
+  if (hipcub::DeviceRadixSort::SortPairs(temp, tb, qk, qk2, vals2, vals3, n, 0, qbits, s) != hipSuccess) return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_match_gather(const sonar_similarity* sims, const int64_t* vals_sorted, const int64_t* counts,

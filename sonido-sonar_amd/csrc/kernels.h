@@ -153,7 +153,7 @@ struct FpRec {
   const double* rolloff;
 };
 // column statistics of one row-major matrix (a sequence is cols = 1): gonum stat.Mean and
-// the corrected two-pass stat.Variance, reduced over row chunks
+// stat.Variance, one pass over row chunks + a chunk merge
 struct StatJob {
   const double* src;
   int64_t rows;
@@ -164,8 +164,9 @@ struct StatJob {
   double* out_mean;            // [cols]
   double* out_std;             // [cols] or null (mean only)
 };
+int64_t colstats_chunk_rows_for(int cols);   // rows per block (the kernel's register tile)
 int launch_colstats(const StatJob* jobs, int njobs, const int* chunk_job, const int* chunk_k, int nchunks,
-                    double* part_sum, double* part_ss, double* part_comp, hipStream_t s);
+                    double* part_sum, double* part_m2, hipStream_t s);
 // gonum stat.Correlation of SpectralCentroid / SpectralRolloff per pair -> coh[pair][2] (NaN = skip)
 int launch_coherence(const FpRec* recs, const int64_t* q_idx, int64_t nq, const int64_t* c_idx, int64_t nc,
                      double* coh, hipStream_t s);
@@ -180,11 +181,12 @@ struct CompareArgs {
   sonar_similarity* out;       // [nq * nc]
 };
 int launch_compare(const CompareArgs& a, hipStream_t s);
-// FindBestMatches: keys (overall or -inf), per-query counts, segmented sort, gather
+// FindBestMatches: keys (overall or -inf), per-query counts, two stable sorts, gather
 int launch_match_keys(const sonar_similarity* sims, int64_t nq, int64_t nc, double threshold, double* keys,
-                      int64_t* vals, int64_t* counts, hipStream_t s);
-int sort_match_keys(const double* keys_in, double* keys_out, const int64_t* vals_in, int64_t* vals_out,
-                    int64_t nq, int64_t nc, const int64_t* seg_off, void* temp, size_t* temp_bytes, hipStream_t s);
+                      int64_t* vals, uint8_t* pass_flag, int64_t* counts, hipStream_t s);
+int sort_match_keys(const double* keys, double* keys2, const int64_t* vals, int64_t* vals2, int64_t* vals3,
+                    int32_t* qk, int32_t* qk2, int64_t nq, int64_t nc, void* temp, size_t* temp_bytes,
+                    hipStream_t s);
 int launch_match_gather(const sonar_similarity* sims, const int64_t* vals_sorted, const int64_t* counts,
                         int64_t nq, int64_t nc, int K, sonar_match* out, hipStream_t s);
 

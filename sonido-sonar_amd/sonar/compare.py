@@ -242,6 +242,17 @@ class Gallery:
             C.cast(out, C.c_void_p), 0))
         return out, nc
 
+    def compare_device(self, queries, candidates, cfg: CompareCfg, out_ptr: int):
+        """sonar_compare with the results left in device memory at out_ptr (nq x nc records)."""
+        q = np.ascontiguousarray(queries, dtype=np.int64)
+        cand = None if candidates is None else np.ascontiguousarray(candidates, dtype=np.int64)
+        nc = len(self) if cand is None else len(cand)
+        self._ctx._check(self._L.sonar_compare(
+            self._h, q.ctypes.data_as(C.POINTER(C.c_int64)), len(q),
+            None if cand is None else cand.ctypes.data_as(C.POINTER(C.c_int64)), nc, C.byref(cfg),
+            C.c_void_p(out_ptr), 1))
+        return nc
+
     def find_best_matches(self, queries, candidates, cfg: CompareCfg):
         q = np.ascontiguousarray(queries, dtype=np.int64)
         cand = None if candidates is None else np.ascontiguousarray(candidates, dtype=np.int64)
@@ -393,3 +404,37 @@ def get_similarity_statistics(results: List[dict]) -> Dict[str, float]:
     return {"overall_mean": o["mean"], "overall_min": o["min"], "overall_max": o["max"],
             "overall_median": o["median"], "overall_std": o["std"], "hash_mean": h["mean"],
             "feature_mean": f["mean"], "confidence_mean": c["mean"], "total_comparisons": float(len(results))}
+
+
+def device_features(G: int, F: int, device, seed: int = 0, content_types=("news", "music")):
+    """Bench inputs: G speech-extractor-shaped fingerprints of F STFT frames generated on the
+    device (MFCC F x 13, centroid/rolloff F, flux F-1, RMS F, voicing F, harmonic ratio and
+    pitch F/2), as sonar_fp_features with device pointers.  Returns (buffer, structs, bytes
+    of feature data per fingerprint)."""
+    import torch
+    Fp = max(1, F // 2)
+    parts = [("mfcc", F * 13), ("spectral_centroid", F), ("spectral_rolloff", F), ("spectral_flux", F - 1),
+             ("rms_energy", F), ("voicing_probability", F), ("harmonic_ratio", Fp), ("pitch_estimate", Fp)]
+    per = sum(n for _, n in parts)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    buf = torch.randn(G, per, generator=gen, device=device, dtype=torch.float64).abs_()
+    structs = (FpFeatures * G)()
+    base = buf.data_ptr()
+    for i in range(G):
+        f = structs[i]
+        f.id = i
+        f.present = FEAT_FEATURES | FEAT_MFCC | FEAT_SPECTRAL | FEAT_TEMPORAL | FEAT_SPEECH | FEAT_HARMONIC
+        f.content_type = content_code(content_types[i % len(content_types)])
+        f.duration_seconds = F * 256 / 44100.0
+        f.dynamic_range, f.silence_ratio, f.onset_density = 20.0 + i % 7, 0.1, 1.0 + i % 3
+        f.speech_rate, f.vocal_tract_length = 3.0, 17.5
+        off = base + i * per * 8
+        for name, n in parts:
+            if name == "mfcc":
+                f.mfcc, f.mfcc_frames, f.mfcc_coeffs = off, F, 13
+            else:
+                setattr(f, name, off)
+                setattr(f, "n_" + name, n)
+            off += n * 8
+    return buf, structs, per * 8
