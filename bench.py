@@ -209,7 +209,7 @@ def bench_c6(args, ctx, dev):
     dt, kms = min(adds, key=lambda x: x[0])
     res["c6_gallery_add"] = {"fingerprints": G, "frames_each": F, "feature_bytes_each": per_bytes,
                              "fingerprints_per_s": G / dt, "ms": dt * 1e3, "colstats_kernel_ms": kms,
-                             "roofline": {"bound": "hbm", "kernel": "colstats_kernel<0>+<1>+final",
+                             "roofline": {"bound": "hbm", "kernel": "colstats_kernel+colstats_final_kernel",
                                           "achieved": G * per_bytes / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                           "unit": "GB/s", "frac": G * per_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                           "algorithmic_bytes": "every feature element read once (8 B)"}}
@@ -253,6 +253,7 @@ def bench_c6(args, ctx, dev):
     dth = time.perf_counter() - t2
     ctx.enable_kernel_timing(False)
     kms = ctx.last_kernel_ms()
+    g.find_best_matches(q, None, cfg)        # warm-up: sort scratch allocation
     t1 = time.perf_counter()
     for _ in range(args.c6_reps):
         g.find_best_matches(q, None, cfg)

@@ -292,13 +292,8 @@ __global__ __launch_bounds__(kBlock) void coherence_kernel(const FpRec* recs, co
 }
 
 // ---- compare ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void compare_kernel(CompareArgs a) {
-  const int64_t pair = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (pair >= a.nq * a.nc) return;
-  const int64_t qi = a.q_idx[pair / a.nc];
-  const int64_t ci = a.c_idx ? a.c_idx[pair % a.nc] : pair % a.nc;
-  const FpRec& A = a.recs[qi];
-  const FpRec& B = a.recs[ci];
+__device__ __forceinline__ sonar_similarity compare_pair(const CompareArgs& a, const FpRec& A, const FpRec& B,
+                                                         int64_t pair) {
   sonar_similarity r;
   r.overall_similarity = 0.0;
   r.feature_similarity = 0.0;
@@ -312,8 +307,7 @@ __global__ __launch_bounds__(kBlock) void compare_kernel(CompareArgs a) {
   r.content_type_match = A.ct == B.ct;
   if (a.content_filter && !r.content_type_match) {          // :160-166
     r.confidence = 0.25;
-    a.out[pair] = r;
-    return;
+    return r;
   }
   // calculateFeatureSimilarity (:266-341)
   double fs = 0.0;
@@ -442,7 +436,32 @@ __global__ __launch_bounds__(kBlock) void compare_kernel(CompareArgs a) {
     conf -= r.noise_level * 0.1;
   }
   r.confidence = go_max(0.0, go_min(1.0, conf));
-  a.out[pair] = r;
+  return r;
+}
+
+// Thread = pair (q * nc + c).  The records are written through LDS so that a block stores
+// its 256 x 136 B of results as one contiguous run of 16-B stores (a per-thread struct store
+// is 17 scattered 8-B stores, one cache line per lane each).
+__global__ __launch_bounds__(kBlock) void compare_kernel(CompareArgs a) {
+  __shared__ __attribute__((aligned(16))) sonar_similarity s_out[kBlock];
+  const int64_t n = a.nq * a.nc, p0 = (int64_t)blockIdx.x * kBlock, pair = p0 + threadIdx.x;
+  if (pair < n) {
+    const int64_t qi = a.q_idx[pair / a.nc];
+    const int64_t ci = a.c_idx ? a.c_idx[pair % a.nc] : pair % a.nc;
+    s_out[threadIdx.x] = compare_pair(a, a.recs[qi], a.recs[ci], pair);
+  }
+  __syncthreads();
+  const int64_t cnt = min((int64_t)kBlock, n - p0);
+  const int words = (int)(cnt * sizeof(sonar_similarity) / 16);     // 136 B = 8.5 x 16 B
+  const float4* src = reinterpret_cast<const float4*>(s_out);
+  float4* dst = reinterpret_cast<float4*>(a.out + p0);
+  for (int i = threadIdx.x; i < words; i += kBlock) dst[i] = src[i];
+  if ((cnt & 1) && threadIdx.x == 0) {                                // odd count: trailing 8 B
+    const double* s8 = reinterpret_cast<const double*>(s_out);
+    double* d8 = reinterpret_cast<double*>(a.out + p0);
+    const int last = (int)(cnt * sizeof(sonar_similarity) / 8) - 1;
+    d8[last] = s8[last];
+  }
 }
 
 // ---- FindBestMatches ---------------------------------------------------------------------
@@ -529,6 +548,7 @@ int launch_coherence(const FpRec* recs, const int64_t* q_idx, int64_t nq, const 
 int launch_compare(const CompareArgs& a, hipStream_t s) {
   const int64_t n = a.nq * a.nc;
   if (n == 0) return 0;
+  if (blocks(n) > 0x7fffffffu) return -1;
   hipLaunchKernelGGL(compare_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
