@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--c6-queries", type=int, default=64)
     ap.add_argument("--c6-reps", type=int, default=3)
     ap.add_argument("--c6-cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--c7-seconds", type=float, default=600.0, help="DetectFromAudio input length (0 = skip row f2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=0.0, help="force CPU-baseline sample length")
     return ap.parse_args()
@@ -269,6 +270,41 @@ def bench_c6(args, ctx, dev):
     return res
 
 
+def bench_c7(args, ctx):
+    """Row f2: ContentDetector.DetectFromAudio on --c7-seconds of the bench stream
+    (float64 host PCM, as GenerateFingerprint hands it over).  kernel_ms = the device passes (scan,
+    both frame-sum kernels, the 2048-point direct DFT) by HIP events; ms adds the H2D copy and the
+    host reductions.  CPU baseline: the oracle (Go's loops), 1 thread, on the same samples."""
+    x = shard.stream_pcm(0, int(args.c7_seconds * SR)).double().numpy()
+    ctx.detect_from_audio(x[: SR * 5], SR)        # warm-up
+    ctx.last_kernel_ms()
+    ctx.enable_kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.c6_reps):
+        ct, feats = ctx.detect_from_audio(x, SR)
+    dt = (time.perf_counter() - t0) / args.c6_reps
+    ctx.enable_kernel_timing(False)
+    kms = ctx.last_kernel_ms()
+    res = {"samples": len(x), "content_type": ct, "ms": dt * 1e3, "kernel_ms": kms,
+           "samples_per_s": len(x) / dt, "kernel_samples_per_s": len(x) / (kms * 1e-3),
+           "roofline": {"bound": "hbm", "achieved": len(x) * 8 / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": len(x) * 8 / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "algorithmic_bytes": "8 B per PCM sample (read once)"}}
+    out = {"c7_detect_from_audio": res}
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        n = min(len(x), int(SR * 60))
+        t0 = time.perf_counter()
+        oct_, _ = O.detect_from_audio(x[:n], SR)
+        dtc = time.perf_counter() - t0
+        out["c7_cpu_baseline"] = {"value": n / dtc, "unit": "samples/s", "cores": 1, "kind": "port",
+                                  "sample": f"60 s of the bench stream ({n} samples), oracle DetectFromAudio "
+                                            "(Go's loops incl. the O(2048^2) direct DFT), float64, 1 thread"}
+        out["c7_detect_from_audio"]["agrees_with_oracle_on_60s"] = ctx.detect_from_audio(x[:n], SR)[0] == oct_
+    return out
+
+
 def c6_cpu_baseline(args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -358,6 +394,8 @@ def main():
         extra.update(bench_c6(args, ctx, dev))
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             extra["c6_cpu_baseline"] = c6_cpu_baseline(args)
+    if args.c7_seconds > 0:
+        extra.update(bench_c7(args, ctx))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

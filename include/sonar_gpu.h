@@ -33,6 +33,14 @@
  *                                 GenerateFingerprint builds for every content type
  *   sonar_align_features       <- AlignmentExtractor.ExtractAlignmentFeatures
  *                                 (fingerprint/extractors/alignment.go:139)
+ *   sonar_music_alignment_features <- MusicFeatureExtractor energy + chroma
+ *                                 (fingerprint/extractors/music.go:178-376)
+ *   sonar_detect_from_audio / sonar_detect_content_type
+ *                              <- ContentDetector.DetectFromAudio / DetectContentType
+ *                                 (fingerprint/content_detector.go:31-101)
+ *   sonar_gallery_* / sonar_compare / sonar_find_best_matches
+ *                              <- FingerprintComparator.Compare / BatchCompare /
+ *                                 FindBestMatches (fingerprint/comparison.go:133-263, 1107)
  *
  * Conventions
  *  - Every call returns SONAR_OK (0) or a negative SONAR_ERR_*; the message
@@ -54,7 +62,7 @@
 extern "C" {
 #endif
 
-#define SONAR_ABI_VERSION 1
+#define SONAR_ABI_VERSION 2
 
 enum {
   SONAR_OK = 0,
@@ -226,6 +234,15 @@ typedef struct {              /* fingerprint.FingerprintConfig (fingerprint.go:2
   int32_t enable_content_detect;
   int32_t window_type;        /* content settings WindowType (all Hann in the tables) */
   int32_t precision;          /* SONAR_F32 / SONAR_F64                                */
+  /* ContentConfig (config.ContentAwareConfig, config/config.go:5-10) and the rest of
+   * AudioData.Metadata, used by ContentDetector.DetectContentType when the content type
+   * is unknown and enable_content_detect is set (fingerprint.go:155-158) */
+  int32_t acoustic_detection;     /* ContentConfig.EnableContentDetection               */
+  int32_t default_content_type;   /* ContentConfig.DefaultContentType (SONAR_CT_*)      */
+  double auto_detect_threshold;   /* ContentConfig.AutoDetectThreshold                  */
+  const char* genre;              /* Metadata.Genre   (NULL = "")                       */
+  const char* station;            /* Metadata.Station (NULL = "")                       */
+  const char* url;                /* Metadata.URL     (NULL = "")                       */
 } sonar_fingerprint_config;
 
 void sonar_fingerprint_config_default(sonar_fingerprint_config* cfg);  /* fingerprint.go:70-98 */
@@ -286,6 +303,34 @@ int sonar_align_features(sonar_ctx* ctx,
 int sonar_music_alignment_features(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate,
                                    int32_t stft_window, int32_t stft_hop, int32_t feature_window,
                                    int32_t feature_hop, double* energy, double* chroma, int32_t device_ptrs);
+
+/* ---- ContentDetector (fingerprint/content_detector.go) -----------------------------
+ * DetectFromAudio (:72-101): zero-crossing rate, energy variance, silence ratio, dynamic range
+ * and temporal stability over the whole PCM, the spectral centroid / frequency split /
+ * harmonic ratio of a direct DFT of the first min(2048, n) samples, then classifyFromFeatures
+ * (:153-217).  Go picks among equal best scores in map order (random); here the order is
+ * music, news, talk, sports. */
+typedef struct {                     /* AcousticFeatures (:104-115) */
+  double zero_crossing_rate, spectral_centroid, energy_variance, silence_ratio, harmonic_ratio;
+  double low_freq_energy, high_freq_energy, dynamic_range, temporal_stability;
+  double classification_confidence;
+} sonar_acoustic_features;
+
+/* content_type <- SONAR_CT_* (SONAR_CT_UNKNOWN when no score beats the threshold).
+ * sample_rate < 10 -> SONAR_ERR_INVALID (the 100 ms frame loop never ends in Go). */
+int sonar_detect_from_audio(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate,
+                            double auto_detect_threshold, int32_t* content_type,
+                            sonar_acoustic_features* features);
+
+/* DetectContentType (:31-69): metadata first (parseContentType of Metadata.ContentType, else
+ * inferFromGenre, else inferFromStation on station + URL), then DetectFromAudio when
+ * acoustic_detection is set and n > 0, else default_content_type.  has_metadata = 0 is a nil
+ * Metadata; NULL strings are "". */
+int sonar_detect_content_type(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate,
+                              int32_t has_metadata, const char* content_type, const char* genre,
+                              const char* station, const char* url, int32_t acoustic_detection,
+                              int32_t default_content_type, double auto_detect_threshold,
+                              int32_t* out_content_type);
 
 /* ---- FingerprintComparator (fingerprint/comparison.go) ------------------------------
  * The comparator's candidate set lives on the device as a gallery of per-fingerprint

@@ -66,6 +66,7 @@ def lib():
         L.or_formant_frame.argtypes = [_d, C.c_int64, C.c_int, _d, _d, _d]
         L.or_formant_frames.argtypes = [_d, C.c_int64, C.c_int, C.c_int, C.c_int, _d, _d, _d]
         L.or_formant_frames.restype = C.c_int64
+        L.or_detect_from_audio.argtypes = [_d, C.c_int64, C.c_int, C.c_double, _d, C.POINTER(C.c_int)]
         L.or_fp_compare.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.or_find_best_matches.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, _i64]
         _lib = L
@@ -507,3 +508,20 @@ def find_best_matches(fq, fcands, cfg):
     if rc:
         raise ValueError(f"oracle FindBestMatches panics in Go (code {rc})")
     return [out[i] for i in range(k.value)]
+
+
+# ---- ContentDetector.DetectFromAudio (content_oracle.c) ---------------------------------
+ACOUSTIC_KEYS = ["zero_crossing_rate", "spectral_centroid", "energy_variance", "silence_ratio", "harmonic_ratio",
+                 "low_freq_energy", "high_freq_energy", "dynamic_range", "temporal_stability",
+                 "classification_confidence"]
+CONTENT_NAMES = ["music", "news", "sports", "talk", "mixed", "unknown"]
+
+
+def detect_from_audio(pcm, sample_rate, thr=2.0):
+    x = np.ascontiguousarray(pcm, dtype=np.float64)
+    out = np.zeros(10)
+    ct = C.c_int()
+    rc = lib().or_detect_from_audio(_p(x) if len(x) else None, len(x), sample_rate, thr, _p(out), C.byref(ct))
+    if rc:
+        raise ValueError("sample rate < 10: the Go loop never ends")
+    return CONTENT_NAMES[ct.value], dict(zip(ACOUSTIC_KEYS, out.tolist()))

@@ -59,6 +59,7 @@ void   or_align_dtw_metrics(const int32_t* pq, const int32_t* pr, const double* 
 void   or_align_xcorr_metrics(const double* metrics, int hop, int sample_rate, int max_lag, double* out);
 int    or_autocorr_fft(const double* x, int n, int max_lag, double* corr);
 int    or_formant_frame(const double* sig, int64_t len, int sample_rate, double* rec24, double* coeffs, double* refl);
+int    or_detect_from_audio(const double* pcm, int64_t n, int sr, double thr, double* out10, int* content_type);
 int64_t or_formant_frames(const double* sig, int64_t n, int sample_rate, int frame_size, int hop, double* recs,
                           double* coeffs, double* refl);
 

@@ -73,6 +73,12 @@ namespace detail {
 int fail(sonar_ctx* c, int code, const std::string& msg);
 void* dbuf(sonar_ctx* c, const std::string& name, size_t bytes);
 hipEvent_t timed_begin(sonar_ctx* c, hipStream_t s);
+// ContentDetector (content_api.cpp)
+int detect_from_audio(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, double thr, int32_t* out,
+                      sonar_acoustic_features* feat);
+int detect_content_type(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, int32_t has_md, const char* ct,
+                        const char* genre, const char* station, const char* url, int32_t acoustic,
+                        int32_t dflt, double thr, int32_t* out);
 void timed_end(sonar_ctx* c, hipStream_t s, hipEvent_t end);
 }  // namespace detail
 }  // namespace sonar

@@ -98,6 +98,9 @@ void sonar_fingerprint_config_default(sonar_fingerprint_config* c) {   // finger
   c->enable_content_detect = 1;
   c->window_type = SONAR_WIN_HANN;
   c->precision = SONAR_F64;
+  c->acoustic_detection = 1;     // ContentConfig (fingerprint.go:92-96)
+  c->default_content_type = SONAR_CT_UNKNOWN;
+  c->auto_detect_threshold = 2.0;
 }
 
 void sonar_feature_config_default(sonar_feature_config* c) {
@@ -383,11 +386,15 @@ int sonar_generate_fingerprint(sonar_ctx* c, const double* pcm, int64_t n, int32
                                const sonar_fingerprint_config* cfg, sonar_result** out) {
   if (!c || !cfg || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
   *out = nullptr;
-  const int ct = to_content_type(content_type);                   // fingerprint.go:155
-  if (ct == CT_UNKNOWN && cfg->enable_content_detect)
-    return fail(c, SONAR_ERR_UNSUPPORTED,
-                "content type is unknown and content detection (ContentDetector.DetectContentType) is not on "
-                "the GPU path: pass music/news/sports/talk/mixed or disable content detection");
+  int ct = to_content_type(content_type);                         // fingerprint.go:155
+  if (ct == CT_UNKNOWN && cfg->enable_content_detect) {           // fingerprint.go:156-158
+    int32_t d = CT_UNKNOWN;
+    const int rc = sonar::detail::detect_content_type(c, pcm, n, sample_rate, 1, content_type, cfg->genre,
+                                                      cfg->station, cfg->url, cfg->acoustic_detection,
+                                                      cfg->default_content_type, cfg->auto_detect_threshold, &d);
+    if (rc != SONAR_OK) return rc;
+    ct = d;
+  }
   const Settings st = settings_for(ct);                           // GetGenerationConfig -> buildFeatureConfig
   sonar_feature_config fc;
   sonar_feature_config_default(&fc);

@@ -132,6 +132,13 @@ int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 int launch_formants(const double* pcm, int64_t frames, int64_t hop, int W, int p, int sr, int frame_ok_len,
                     const double* ham, sonar_formant_frame* out, double* coeffs, double* refl, hipStream_t s);
 
+// ---- ContentDetector (content_kernels.hip) ------------------------------------------
+// words[0] zero crossings, words[1] bits of max |x|, words[2] bits of min |x| > 1e-10 (+Inf)
+int launch_detect_scan(const double* x, int64_t n, unsigned long long* words, hipStream_t s);
+int launch_frame_sums(const double* x, int64_t n, int64_t frames, int64_t hop, int64_t fs, double* out,
+                      hipStream_t s);
+int launch_dft_mag(const double* x, int N, double* mag, hipStream_t s);
+
 // ---- FingerprintComparator (compare_kernels.hip) -------------------------------------
 // sequences summarised per fingerprint (mean, std), in compare order (comparison.go:646-770)
 enum { SEQ_CENTROID = 0, SEQ_ROLLOFF, SEQ_FLUX, SEQ_RMS, SEQ_VOICING, SEQ_HARMONIC, SEQ_PITCH, SEQ_COUNT };

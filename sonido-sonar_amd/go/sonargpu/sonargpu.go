@@ -7,6 +7,8 @@
 //	GenerateFingerprint   <- fingerprint/fingerprint.go:137 (FingerprintGenerator.GenerateFingerprint)
 //	ExtractSpeech         <- fingerprint/extractors/speech.go:135 (SpeechFeatureExtractor.ExtractFeatures)
 //	AlignFeatures         <- fingerprint/extractors/alignment.go:139 (AlignmentExtractor.ExtractAlignmentFeatures)
+//	DetectFromAudio       <- fingerprint/content_detector.go:72 (ContentDetector.DetectFromAudio)
+//	Gallery (compare.go)  <- fingerprint/comparison.go (FingerprintComparator)
 //	Fingerprint / DTW / NCC are the lower seams: analyzers/spectral.go:385 + spectral/mfcc.go:167,
 //	stats/dtw.go:55, stats/correlation.go:131.
 //
@@ -173,14 +175,37 @@ type FingerprintConfig struct {
 	FeatureWindowSize, FeatureHopSize int // FingerprintConfig.FeatureConfig.{WindowSize,HopSize}
 	EnableContentDetect               bool
 	Precision                         int
+	// ContentConfig (config.ContentAwareConfig) and the rest of AudioData.Metadata, read by
+	// ContentDetector.DetectContentType when the content type is unknown
+	EnableContentDetection bool
+	DefaultContentType     int // SONAR_CT_*
+	AutoDetectThreshold    float64
+	Genre, Station, URL    string
 }
 
 // DefaultFingerprintConfig mirrors DefaultFingerprintConfig (fingerprint.go:70-98).
 func DefaultFingerprintConfig() FingerprintConfig {
 	var c C.sonar_fingerprint_config
 	C.sonar_fingerprint_config_default(&c)
-	return FingerprintConfig{int(c.window_size), int(c.hop_size), int(c.feature_window_size),
-		int(c.feature_hop_size), c.enable_content_detect != 0, int(c.precision)}
+	return FingerprintConfig{WindowSize: int(c.window_size), HopSize: int(c.hop_size),
+		FeatureWindowSize: int(c.feature_window_size), FeatureHopSize: int(c.feature_hop_size),
+		EnableContentDetect: c.enable_content_detect != 0, Precision: int(c.precision),
+		EnableContentDetection: c.acoustic_detection != 0, DefaultContentType: int(c.default_content_type),
+		AutoDetectThreshold: float64(c.auto_detect_threshold)}
+}
+
+// AcousticFeatures mirrors fingerprint.AcousticFeatures (content_detector.go:104-115).
+type AcousticFeatures C.sonar_acoustic_features
+
+// DetectFromAudio runs ContentDetector.DetectFromAudio (content_detector.go:72) on the GPU.
+func (x *Context) DetectFromAudio(pcm []float64, sampleRate int, threshold float64) (int, AcousticFeatures, error) {
+	var ct C.int32_t
+	var f C.sonar_acoustic_features
+	if rc := C.sonar_detect_from_audio(x.c, f64p(pcm), C.int64_t(len(pcm)), C.int32_t(sampleRate),
+		C.double(threshold), &ct, &f); rc != C.SONAR_OK {
+		return 0, AcousticFeatures{}, x.err(rc)
+	}
+	return int(ct), AcousticFeatures(f), nil
 }
 
 // GenerateFingerprint runs FingerprintGenerator.GenerateFingerprint's feature path
@@ -200,6 +225,18 @@ func (x *Context) GenerateFingerprint(pcm []float64, sampleRate int, contentType
 		cc.enable_content_detect = 1
 	}
 	cc.precision = C.int32_t(cfg.Precision)
+	cc.acoustic_detection = b2i(cfg.EnableContentDetection)
+	cc.default_content_type = C.int32_t(cfg.DefaultContentType)
+	cc.auto_detect_threshold = C.double(cfg.AutoDetectThreshold)
+	for _, m := range []struct {
+		s   string
+		dst **C.char
+	}{{cfg.Genre, &cc.genre}, {cfg.Station, &cc.station}, {cfg.URL, &cc.url}} {
+		if m.s != "" {
+			*m.dst = C.CString(m.s)
+			defer C.free(unsafe.Pointer(*m.dst))
+		}
+	}
 	ct := C.CString(contentType)
 	defer C.free(unsafe.Pointer(ct))
 	var res *C.sonar_result

@@ -59,7 +59,20 @@ class FpOut(C.Structure):
 class FingerprintConfig(C.Structure):
     _fields_ = [("window_size", C.c_int32), ("hop_size", C.c_int32), ("feature_window_size", C.c_int32),
                 ("feature_hop_size", C.c_int32), ("enable_content_detect", C.c_int32),
-                ("window_type", C.c_int32), ("precision", C.c_int32)]
+                ("window_type", C.c_int32), ("precision", C.c_int32),
+                ("acoustic_detection", C.c_int32), ("default_content_type", C.c_int32),
+                ("auto_detect_threshold", C.c_double), ("genre", C.c_char_p), ("station", C.c_char_p),
+                ("url", C.c_char_p)]
+
+
+class AcousticFeatures(C.Structure):
+    """sonar_acoustic_features (content_detector.go:104-115)."""
+    _fields_ = [(n, C.c_double) for n in ("zero_crossing_rate", "spectral_centroid", "energy_variance",
+                                          "silence_ratio", "harmonic_ratio", "low_freq_energy", "high_freq_energy",
+                                          "dynamic_range", "temporal_stability", "classification_confidence")]
+
+
+CONTENT_NAMES = ["music", "news", "sports", "talk", "mixed", "unknown"]
 
 
 class FeatureConfig(C.Structure):
@@ -171,6 +184,10 @@ def lib():
     L.sonar_formant_frame_count.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32]
     L.sonar_formant_frame_count.restype = C.c_int64
     L.sonar_formants.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, C.c_int32]
+    L.sonar_detect_from_audio.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_double, _i32p,
+                                          C.POINTER(AcousticFeatures)]
+    L.sonar_detect_content_type.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_char_p, C.c_char_p,
+                                            C.c_char_p, C.c_char_p, C.c_int32, C.c_int32, C.c_double, _i32p]
     L.sonar_gallery_create.argtypes = [_vp, C.POINTER(_vp)]
     L.sonar_gallery_destroy.argtypes = [_vp]
     L.sonar_gallery_destroy.restype = None
@@ -426,6 +443,28 @@ class Context:
                                                        sample_rate, content_type.encode(), C.byref(cfg),
                                                        C.byref(h)))
         return self._result(h)
+
+    def detect_from_audio(self, pcm, sample_rate, auto_detect_threshold=2.0):
+        """ContentDetector.DetectFromAudio -> (content type name, AcousticFeatures dict)."""
+        pcm = _f64(pcm)
+        ct = C.c_int32()
+        f = AcousticFeatures()
+        self._check(self._L.sonar_detect_from_audio(self._h, _ptr(pcm) if len(pcm) else None, len(pcm), sample_rate,
+                                                    auto_detect_threshold, C.byref(ct), C.byref(f)))
+        return CONTENT_NAMES[ct.value], {k: getattr(f, k) for k, _ in AcousticFeatures._fields_}
+
+    def detect_content_type(self, pcm, sample_rate, metadata=None, acoustic_detection=True,
+                            default_content_type="unknown", auto_detect_threshold=2.0):
+        """ContentDetector.DetectContentType; metadata = dict(content_type, genre, station, url) or None."""
+        pcm = _f64(pcm)
+        ct = C.c_int32()
+        md = metadata or {}
+        enc = lambda k: md.get(k, "").encode() if md.get(k) else None  # noqa: E731
+        self._check(self._L.sonar_detect_content_type(
+            self._h, _ptr(pcm) if len(pcm) else None, len(pcm), sample_rate, int(metadata is not None),
+            enc("content_type"), enc("genre"), enc("station"), enc("url"), int(acoustic_detection),
+            CONTENT_NAMES.index(default_content_type), auto_detect_threshold, C.byref(ct)))
+        return CONTENT_NAMES[ct.value]
 
     @staticmethod
     def feature_config(**kw):

@@ -69,8 +69,11 @@ def test_generate_fingerprint_talk_and_errors(ctx):
                                                      mfcc_coefficients=13))
     assert got["is_speech"] == ref["is_speech"]
     _cmp(got, ref, 1e-6)
-    with pytest.raises(sonar.SonarError, match="content detection"):
-        ctx.generate_fingerprint(x, 16000, "speech", cfg)           # F12: "speech" is not a content type
+    # F12: "speech" is not a content type -> ContentDetector.DetectContentType runs (acoustic)
+    det = ctx.generate_fingerprint(x, 16000, "speech", cfg)
+    want, _ = O.detect_from_audio(x, 16000)
+    assert int(det["content_type"].reshape(-1)[0]) == ["music", "news", "sports", "talk", "mixed",
+                                                        "unknown"].index(want)
     with pytest.raises(sonar.SonarError, match="signal too short"):
         ctx.generate_fingerprint(x[:300], 16000, "news", cfg)
 
