@@ -26,6 +26,8 @@
  *   sonar_formants             <- FormantAnalyzer.AnalyzeMultipleFrames / AnalyzeFormants
  *                                 (algorithms/speech/format.go:85-449) over LPCAnalyzer.Analyze
  *                                 (algorithms/speech/lpc.go:44-265)
+ *   sonar_voice_quality        <- VoiceQualityAnalyzer.AnalyzeVoiceQuality
+ *                                 (algorithms/speech/voice_quality.go:56-111)
  *   sonar_generate_fingerprint <- FingerprintGenerator.GenerateFingerprint
  *                                 (fingerprint/fingerprint.go:137)
  *   sonar_extract_speech_features <- SpeechFeatureExtractor.ExtractFeatures
@@ -222,6 +224,24 @@ int64_t sonar_formant_frame_count(int64_t n, int32_t sample_rate, int32_t frame_
 int sonar_formants(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate, int32_t frame_size,
                    int32_t hop_size, sonar_formant_frame* out, double* lpc_coeffs, double* reflection,
                    int32_t device_ptrs);
+
+/* ---- VoiceQualityAnalyzer.AnalyzeVoiceQuality (algorithms/speech/voice_quality.go:56-111),
+ * the analysis AnalyzeSpeech runs on the speech extractor's pre-emphasised PCM
+ * (speech_analysis.go:77-80) and whose Jitter / Shimmer land in SpeechFeatures
+ * (extractors/speech.go:306-309).  Pitch periods come from a YIN scan of 1024-sample frames at
+ * hop 256 with a fresh PitchDetector (:114-157); voicing_strength is DetectPitch on the whole
+ * signal, which Go only accepts for exactly 1024 samples (else 0).  Errors, as Go:
+ * SONAR_ERR_TOO_SHORT "signal too short for voice quality analysis (need at least 1 second)"
+ * and "insufficient pitch periods for analysis (found k, need at least 3)". ------------------ */
+typedef struct {                     /* speech.VoiceQualityResult (voice_quality.go:21-43) */
+  double jitter, shimmer, hnr, noise_measure, f0_stability, amplitude_stability;
+  double voicing_strength, overall_quality;
+  int64_t num_periods;
+  double mean_f0, f0_range, analysis_quality;
+} sonar_voice_quality_result;
+
+int sonar_voice_quality(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate,
+                        sonar_voice_quality_result* out);
 
 /* ---- host mirror of the Go API (C++ above the kernels) ------------------ */
 typedef struct sonar_result sonar_result;   /* named float64 arrays + scalars */

@@ -56,6 +56,7 @@ def lib():
         L.or_yin_raw.argtypes = [_d, C.c_int, _d, _d, C.POINTER(C.c_int)]
         L.or_pitch_track.argtypes = [_d, C.c_int64, C.c_int, C.c_int, _d, _d, _d]
         L.or_pitch_track.restype = C.c_int64
+        L.or_voice_quality.argtypes = [_d, C.c_int64, C.c_int, _d]
         L.or_chroma_music.argtypes = [_d, C.c_int64, C.c_int64, C.c_int, C.c_int, _d]
         L.or_chroma_frames.argtypes = [_d, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, _d]
         L.or_ncc.argtypes = [_d, C.c_int64, _d, C.c_int64, C.c_int, _d, _d]
@@ -192,6 +193,21 @@ def pitch_track(pcm, sample_rate, passes=1):
     p, c, v = np.zeros(F), np.zeros(F), np.zeros(F)
     lib().or_pitch_track(_p(pcm), len(pcm), sample_rate, passes, _p(p), _p(c), _p(v))
     return p, c, v
+
+
+VOICE_QUALITY_KEYS = ("jitter", "shimmer", "hnr", "noise_measure", "f0_stability", "amplitude_stability",
+                      "voicing_strength", "overall_quality", "num_periods", "mean_f0", "f0_range",
+                      "analysis_quality")
+
+
+def voice_quality(signal, sample_rate):
+    """VoiceQualityAnalyzer.AnalyzeVoiceQuality (algorithms/speech/voice_quality.go:56-111).
+    Returns (dict, status): status 0 ok, -1 shorter than one second, -2 fewer than 3 periods
+    (the Go call returns an error and a nil result; the dict is then all zero)."""
+    signal = _f64(signal)
+    out = np.zeros(12)
+    st = lib().or_voice_quality(_p(signal), len(signal), sample_rate, _p(out))
+    return dict(zip(VOICE_QUALITY_KEYS, out.tolist())), int(st)
 
 
 def chroma_music(pcm, F, H, sample_rate):
@@ -363,6 +379,12 @@ def speech_features_reference(pcm, sample_rate, fc):
                 fq = fm["frequency"][0][:nv].reshape(1, nv) if nv else np.zeros((0, 0))
                 vtl = float(fm["vocal_tract_length"][0])
         out["formant_frequencies"], out["vocal_tract_length"] = fq, vtl
+        jit = shi = 0.0                                      # speech.go:287-288, 306-309
+        if sp:
+            vq, vst = voice_quality(pre, csr)                # AnalyzeSpeech -> AnalyzeVoiceQuality (:77-80)
+            if vst == 0:
+                jit, shi = vq["jitter"], vq["shimmer"]
+        out["jitter"], out["shimmer"] = jit, shi
         if sp:                                               # estimateSpeechRate (speech.go:779-797)
             with np.errstate(divide="ignore", invalid="ignore"):
                 dur = np.float64(len(pre)) / np.float64(csr)     # IEEE like Go: sr 0 -> +Inf

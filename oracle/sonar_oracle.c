@@ -572,6 +572,118 @@ int64_t or_pitch_track(const double* pcm, int64_t n, int sr, int passes, double*
 }
 
 /* ------------------------------------------------------------------ */
+/* VoiceQualityAnalyzer.AnalyzeVoiceQuality                              */
+/* (algorithms/speech/voice_quality.go:56-111) on the signal the speech  */
+/* extractor hands AnalyzeSpeech (the pre-emphasised PCM,                */
+/* speech_analysis.go:77).  out[12] = jitter, shimmer, hnr,              */
+/* noise_measure, f0_stability, amplitude_stability, voicing_strength,   */
+/* overall_quality, num_periods, mean_f0, f0_range, analysis_quality.    */
+/* Returns 0, -1 (shorter than one second, :57-59) or -2 (fewer than 3   */
+/* periods, :67-69); on error out[] is left zero (the Go result is nil). */
+/* ------------------------------------------------------------------ */
+int or_voice_quality(const double* sig, int64_t n, int sr, double* out) {
+    for (int k = 0; k < 12; k++) out[k] = 0.0;
+    if (n < (int64_t)sr) return -1;
+    /* extractPitchPeriodsAndF0 :114-157: fresh PitchDetector (NewVoiceQualityAnalyzer :51),
+     * frames of 1024 at hop 256 while i < len-1024 */
+    int64_t cap = n > 1024 ? (n - 1025) / 256 + 1 : 0;
+    int64_t* ps = (int64_t*)malloc(sizeof(int64_t) * (cap + 1));
+    int64_t* pl = (int64_t*)malloc(sizeof(int64_t) * (cap + 1));
+    double* f0v = (double*)malloc(sizeof(double) * (cap + 1));
+    int64_t np_ = 0, last_end = 0;
+    yin_track st; memset(&st, 0, sizeof(st));
+    for (int64_t i = 0; i < n - 1024; i += 256) {
+        double p, c, v;
+        or_yin_raw(sig + i, sr, &p, &c, NULL);
+        yin_track_step(&st, &p, &c, &v);
+        if (v > 0.5 && c > 0.5 && p >= 50.0 && p <= 500.0) {
+            int64_t len = go_f2i((double)sr / p);
+            int64_t s0 = i > last_end ? i : last_end;
+            int64_t e0 = s0 + len;
+            if (e0 < n) { ps[np_] = s0; pl[np_] = len; f0v[np_] = p; np_++; last_end = e0; }
+        }
+    }
+    /* calculateVoicingStrength :363-371: DetectPitch on the whole signal, which only accepts
+     * exactly 1024 samples (pitch_detection.go:226); the tracker state carries over */
+    double vstr = 0.0;
+    if (n == 1024) { double p, c; or_yin_raw(sig, sr, &p, &c, NULL); yin_track_step(&st, &p, &c, &vstr); }
+    int rc = 0;
+    if (np_ < 3) { rc = -2; goto done; }
+    {
+        double* amp = (double*)malloc(sizeof(double) * np_);
+        for (int64_t k = 0; k < np_; k++) {                       /* RMS per period :200-207 */
+            double r = 0.0;
+            for (int64_t j = 0; j < pl[k]; j++) r += sig[ps[k] + j] * sig[ps[k] + j];
+            amp[k] = sqrt(r / (double)pl[k]);
+        }
+        /* calculateJitter :160-191 */
+        double avg = 0.0, js = 0.0;
+        for (int64_t k = 0; k < np_; k++) avg += (double)pl[k];
+        avg /= (double)np_;
+        for (int64_t k = 1; k < np_; k++) js += fabs((double)pl[k] - (double)pl[k - 1]);
+        double jitter = avg == 0 ? 0.0 : (js / (double)(np_ - 1)) / avg * 100.0;
+        /* calculateShimmer :194-229 */
+        double aavg = 0.0, ss = 0.0;
+        for (int64_t k = 0; k < np_; k++) aavg += amp[k];
+        aavg /= (double)np_;
+        for (int64_t k = 1; k < np_; k++) ss += fabs(amp[k] - amp[k - 1]);
+        double shimmer = aavg == 0 ? 0.0 : (ss / (double)(np_ - 1)) / aavg * 100.0;
+        /* calculateHNR :232-294 (mean F0, 2048-sample frame at the middle) */
+        double hnr = 0.0, mf = 0.0;
+        for (int64_t k = 0; k < np_; k++) mf += f0v[k];
+        mf /= (double)np_;
+        if (n >= 2048) {
+            int64_t s0 = n / 2 - 1024; if (s0 < 0) s0 = 0;
+            const double* fr = sig + s0;
+            double* ac = (double*)malloc(sizeof(double) * 2048);
+            for (int lag = 0; lag < 2048; lag++) {
+                double s = 0.0; int cnt = 0;
+                for (int i = 0; i < 2048 - lag; i++) { s += fr[i] * fr[i + lag]; cnt++; }
+                ac[lag] = cnt > 0 ? s / (double)cnt : 0.0;
+            }
+            int64_t el = go_f2i((double)sr / mf);
+            if (el < 2048) {
+                double mc = 0.0;
+                int64_t sr_ = el / 4, a = el - sr_ > 1 ? el - sr_ : 1, b = el + sr_ < 2047 ? el + sr_ : 2047;
+                for (int64_t i = a; i <= b; i++) if (ac[i] > mc) mc = ac[i];
+                if (mc > 0 && mc < ac[0]) hnr = 10.0 * log10(mc / (ac[0] - mc));
+            }
+            free(ac);
+        }
+        /* calculateF0Stability :297-322 */
+        double var = 0.0;
+        for (int64_t k = 0; k < np_; k++) { double d = f0v[k] - mf; var += d * d; }
+        var /= (double)np_;
+        double f0s = mf == 0 ? 0.0 : go_max(0.0, 1.0 - sqrt(var) / mf);
+        /* calculateAmplitudeStability :325-360 */
+        double av = 0.0;
+        for (int64_t k = 0; k < np_; k++) { double d = amp[k] - aavg; av += d * d; }
+        av /= (double)np_;
+        double ams = aavg == 0 ? 0.0 : go_max(0.0, 1.0 - sqrt(av) / aavg);
+        /* calculateNoiseMeasure :374-398 */
+        double nm = 0.0;
+        if (n >= 1024) {
+            double hf = 0.0, te = 0.0;
+            for (int i = 1; i < 1024; i++) { double d = sig[i] - sig[i - 1]; hf += d * d; te += sig[i] * sig[i]; }
+            nm = te == 0 ? 0.0 : hf / te;
+        }
+        /* calculateF0Statistics :401-426 */
+        double lo = f0v[0], hi = f0v[0];
+        for (int64_t k = 0; k < np_; k++) { if (f0v[k] < lo) lo = f0v[k]; if (f0v[k] > hi) hi = f0v[k]; }
+        /* calculateOverallQuality :429-437, calculateAnalysisQuality :440-451 */
+        double oq = (go_max(0, 1.0 - jitter / 5.0) + go_max(0, 1.0 - shimmer / 10.0) +
+                     go_min(1.0, go_max(0, hnr / 20.0)) + f0s) / 4.0;
+        double aq = (go_min(1.0, (double)np_ / 10.0) + f0s + go_min(1.0, go_max(0, hnr / 15.0))) / 3.0;
+        out[0] = jitter; out[1] = shimmer; out[2] = hnr; out[3] = nm; out[4] = f0s; out[5] = ams;
+        out[6] = vstr; out[7] = oq; out[8] = (double)np_; out[9] = mf; out[10] = hi - lo; out[11] = aq;
+        free(amp);
+    }
+done:
+    free(ps); free(pl); free(f0v);
+    return rc;
+}
+
+/* ------------------------------------------------------------------ */
 /* Chroma: MusicFeatureExtractor.extractChromaFeatures                   */
 /* (fingerprint/extractors/music.go:327-376) -> ChromaSTFT.ComputeChroma */
 /* (algorithms/chroma/chroma_stft.go:45-138)                             */

@@ -48,6 +48,7 @@ int64_t or_short_time_energy(const double* x, int64_t n, int W, int H, double* o
 int64_t or_pitch_frames(int64_t n);
 void   or_yin_raw(const double* frame1024, int sample_rate, double* pitch, double* conf, int* tau);
 int64_t or_pitch_track(const double* pcm, int64_t n, int sample_rate, int passes, double* pitch, double* conf, double* voicing);
+int    or_voice_quality(const double* sig, int64_t n, int sample_rate, double* out12);
 int    or_chroma_music(const double* pcm, int64_t n, int64_t F, int H, int sample_rate, double* out);
 int    or_chroma_frames(const double* y, int64_t n, int64_t F, int H, int fs, int sample_rate, double* out);
 void   or_dc_removal(const double* x, int64_t n, double R, double* out);

@@ -80,6 +80,8 @@ int detect_content_type(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, 
                         const char* genre, const char* station, const char* url, int32_t acoustic,
                         int32_t dflt, double thr, int32_t* out);
 void timed_end(sonar_ctx* c, hipStream_t s, hipEvent_t end);
+// VoiceQualityAnalyzer.AnalyzeVoiceQuality on device-resident float64 samples (voice_api.cpp)
+int voice_quality(sonar_ctx* c, const double* dsig, int64_t n, int32_t sr, sonar_voice_quality_result* out);
 }  // namespace detail
 }  // namespace sonar
 

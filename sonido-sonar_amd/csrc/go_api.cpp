@@ -11,9 +11,9 @@
 // Every per-frame / per-cell array is produced by a HIP kernel (sonar_fingerprint,
 // YIN, NCC, DTW, energy, tilt, stats); this file only runs what the Go code runs
 // sequentially on O(frames) data: YIN temporal tracking, percentile thresholds,
-// onset peak picking, scorer formulas.  Not produced (outside the GPU hot path,
-// SURVEY.md section 2): formant / voice-quality heuristics (format.go, voice_quality.go),
-// content detection (content_detector.go), fingerprint ID/timestamp metadata.
+// onset peak picking, scorer formulas.  Formants (lpc_kernels.hip), voice quality
+// (voice_api.cpp) and content detection (content_api.cpp) run on their own kernels;
+// fingerprint ID/timestamp metadata is not produced.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -174,7 +174,7 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   double* dpit = (double*)dbuf(c, "sx.pitch", std::max<int64_t>(Fp, 1) * 8);
   double* dcon = (double*)dbuf(c, "sx.conf", std::max<int64_t>(Fp, 1) * 8);
   if (!dpit || !dcon) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (pitch)");
-  if (sonar::launch_yin(dy, n, Fp, csr, dpit, dcon, nullptr, s) != 0) return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
+  if (sonar::launch_yin(dy, n, Fp, 512, csr, dpit, dcon, nullptr, s) != 0) return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
   // whole-signal statistics of the pre-emphasised PCM
   const int SB = 256;
   double* dpart = (double*)dbuf(c, "sx.stats", SB * 4 * 8);
@@ -259,6 +259,17 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     }
     res->put("formant_frequencies", formants, formants.empty() ? 0 : 1, (int64_t)formants.size());   // convertFormantData
     res->scalar("vocal_tract_length", vtl);
+    // AnalyzeSpeech -> VoiceQualityAnalyzer.AnalyzeVoiceQuality(preprocessed PCM) (speech_analysis.go:76-80);
+    // a failed analysis leaves VoiceQualityResult nil and Jitter/Shimmer 0 (speech.go:287-288, 306-309)
+    double jitter = 0.0, shimmer = 0.0;
+    if (sp) {
+      sonar_voice_quality_result vq;
+      const int rc = sonar::detail::voice_quality(c, dy, n, csr, &vq);
+      if (rc == SONAR_ERR_DEVICE || rc == SONAR_ERR_NOMEM) { delete res; return rc; }
+      if (rc == SONAR_OK) { jitter = vq.jitter; shimmer = vq.shimmer; }
+    }
+    res->scalar("jitter", jitter);
+    res->scalar("shimmer", shimmer);
     if (sp) {
       // estimateSpeechRate (speech.go:779-797) on the energy frames of the pre-emphasised PCM
       const double dur = (double)n / (double)csr;

@@ -88,9 +88,13 @@ int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H,
                void* out, int out_f64, hipStream_t s);
 int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H, double alpha,
                   void* out, int out_f64, hipStream_t s);
-// YIN raw per-frame results (misc_kernels.hip)
-int launch_yin(const double* pcm, int64_t n, int64_t frames, int sample_rate, double* pitch, double* conf,
-               int32_t* tau, hipStream_t s);
+// YIN raw per-frame results (misc_kernels.hip); frames start at 0, hop, 2 hop, ...
+int launch_yin(const double* pcm, int64_t n, int64_t frames, int64_t hop, int sample_rate, double* pitch,
+               double* conf, int32_t* tau, hipStream_t s);
+// VoiceQualityAnalyzer helpers (misc_kernels.hip): per-period RMS, 2048-lag HNR autocorrelation
+int launch_period_rms(const double* y, const int64_t* start, const int64_t* len, int64_t np, double* amp,
+                      hipStream_t s);
+int launch_hnr_autocorr(const double* frame2048, double* ac, hipStream_t s);
 // Chroma STFT (misc_kernels.hip)
 int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, const double* window,
                   const double* trig, const int* chroma_map, double* out, hipStream_t s);

@@ -72,17 +72,18 @@ __global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f6
   store_out(out, out_f64, t, sqrt(__ddiv_rn(ss, (double)W)));
 }
 
-// YIN per 1024-sample frame at hop 512: one block of 256 threads per frame
+// YIN per 1024-sample frame (hop 512 for extractHarmonicFeatures, 256 for the voice-quality
+// period scan): one block of 256 threads per frame
 __constant__ double c_yin_win[1024];
 
-__global__ __launch_bounds__(256) void yin_kernel(const double* pcm, int64_t n, int64_t frames, int sr,
+__global__ __launch_bounds__(256) void yin_kernel(const double* pcm, int64_t n, int64_t frames, int64_t hop, int sr,
                                                   double* pitch, double* conf, int32_t* tau_out) {
   __shared__ double xw[1024];
   __shared__ double diff[512];
   __shared__ double cm[512];
   const int64_t fi = blockIdx.x;
   if (fi >= frames) return;
-  const int64_t s = fi * 512;
+  const int64_t s = fi * hop;
   const bool full = (s + 1024 <= n);
   if (!full) {   // DetectPitch rejects frames != WindowSize (pitch_detection.go:226)
     if (threadIdx.x == 0) { pitch[fi] = 0; conf[fi] = 0; if (tau_out) tau_out[fi] = -2; }
@@ -274,8 +275,8 @@ int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, in
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int launch_yin(const double* pcm, int64_t n, int64_t frames, int sr, double* pitch, double* conf, int32_t* tau,
-               hipStream_t s) {
+int launch_yin(const double* pcm, int64_t n, int64_t frames, int64_t hop, int sr, double* pitch, double* conf,
+               int32_t* tau, hipStream_t s) {
   static bool init = false;
   if (!init) {   // symmetric Hann without normalisation, pitch_detection.go:314-318
     double w[1024];
@@ -284,7 +285,44 @@ int launch_yin(const double* pcm, int64_t n, int64_t frames, int sr, double* pit
     init = true;
   }
   if (frames <= 0) return 0;
-  hipLaunchKernelGGL(yin_kernel, dim3((unsigned)frames), dim3(256), 0, s, pcm, n, frames, sr, pitch, conf, tau);
+  hipLaunchKernelGGL(yin_kernel, dim3((unsigned)frames), dim3(256), 0, s, pcm, n, frames, hop, sr, pitch, conf, tau);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// VoiceQualityAnalyzer period amplitudes (algorithms/speech/voice_quality.go:200-207, 330-338):
+// RMS of each extracted pitch period, one thread per period, summed in Go's sample order
+__global__ __launch_bounds__(256) void period_rms_kernel(const double* y, const int64_t* start, const int64_t* len,
+                                                         int64_t np, double* amp) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= np) return;
+  const double* p = y + start[k];
+  const int64_t L = len[k];
+  double r = 0.0;
+  for (int64_t j = 0; j < L; ++j) r = __dadd_rn(r, __dmul_rn(p[j], p[j]));
+  amp[k] = sqrt(__ddiv_rn(r, (double)L));
+}
+
+// calculateHNR autocorrelation (voice_quality.go:255-267) of one 2048-sample frame:
+// ac[lag] = sum_{i < 2048-lag} x[i] x[i+lag] / (2048-lag), one thread per lag, Go's order
+__global__ __launch_bounds__(256) void hnr_autocorr_kernel(const double* fr, double* ac) {
+  __shared__ double x[2048];
+  for (int i = threadIdx.x; i < 2048; i += 256) x[i] = fr[i];
+  __syncthreads();
+  const int lag = blockIdx.x * 256 + threadIdx.x;
+  double sm = 0.0;
+  for (int i = 0; i < 2048 - lag; ++i) sm = __dadd_rn(sm, __dmul_rn(x[i], x[i + lag]));
+  ac[lag] = __ddiv_rn(sm, (double)(2048 - lag));
+}
+
+int launch_period_rms(const double* y, const int64_t* start, const int64_t* len, int64_t np, double* amp,
+                      hipStream_t s) {
+  if (np <= 0) return 0;
+  hipLaunchKernelGGL(period_rms_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, y, start, len, np, amp);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_hnr_autocorr(const double* frame2048, double* ac, hipStream_t s) {
+  hipLaunchKernelGGL(hnr_autocorr_kernel, dim3(8), dim3(256), 0, s, frame2048, ac);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -525,7 +525,7 @@ int sonar_pitch_yin(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, doub
     HIP_TRY(c, hipMemcpyAsync(b, pcm, n * 8, hipMemcpyHostToDevice, s));
     dp = (const double*)b;
   }
-  if (sonar::launch_yin(dp, n, F, sr, dpi, dco, dta, s) != 0) return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
+  if (sonar::launch_yin(dp, n, F, 512, sr, dpi, dco, dta, s) != 0) return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
   if (!device_ptrs) {
     HIP_TRY(c, hipMemcpyAsync(pitch, dpi, F * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipMemcpyAsync(conf, dco, F * 8, hipMemcpyDeviceToHost, s));

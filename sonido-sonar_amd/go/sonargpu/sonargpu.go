@@ -208,6 +208,20 @@ func (x *Context) DetectFromAudio(pcm []float64, sampleRate int, threshold float
 	return int(ct), AcousticFeatures(f), nil
 }
 
+// VoiceQuality mirrors speech.VoiceQualityResult (algorithms/speech/voice_quality.go:21-43).
+type VoiceQuality C.sonar_voice_quality_result
+
+// AnalyzeVoiceQuality runs VoiceQualityAnalyzer.AnalyzeVoiceQuality (voice_quality.go:56) on
+// the GPU; errors carry the Go messages (shorter than one second, fewer than 3 periods).
+func (x *Context) AnalyzeVoiceQuality(signal []float64, sampleRate int) (VoiceQuality, error) {
+	var q C.sonar_voice_quality_result
+	if rc := C.sonar_voice_quality(x.c, f64p(signal), C.int64_t(len(signal)), C.int32_t(sampleRate),
+		&q); rc != C.SONAR_OK {
+		return VoiceQuality{}, x.err(rc)
+	}
+	return VoiceQuality(q), nil
+}
+
 // GenerateFingerprint runs FingerprintGenerator.GenerateFingerprint's feature path
 // (content-type resolution, F1 SampleRate=0 extractor, STFT, features) on the GPU.
 // contentType is audioData.Metadata.ContentType.

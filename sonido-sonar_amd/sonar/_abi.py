@@ -88,6 +88,14 @@ class FormantFrame(C.Structure):
                 ("residual_energy", C.c_double), ("stable", C.c_int32), ("lpc_order", C.c_int32)]
 
 
+class VoiceQuality(C.Structure):
+    """sonar_voice_quality (speech.VoiceQualityResult, voice_quality.go:21-43)."""
+    _fields_ = [(n, C.c_double) for n in ("jitter", "shimmer", "hnr", "noise_measure", "f0_stability",
+                                          "amplitude_stability", "voicing_strength", "overall_quality")] + \
+               [("num_periods", C.c_int64)] + \
+               [(n, C.c_double) for n in ("mean_f0", "f0_range", "analysis_quality")]
+
+
 class FpFeatures(C.Structure):
     """sonar_fp_features (one AudioFingerprint as FingerprintComparator reads it)."""
     _fields_ = [("id", C.c_int64), ("present", C.c_uint32), ("content_type", C.c_int32),
@@ -184,6 +192,7 @@ def lib():
     L.sonar_formant_frame_count.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32]
     L.sonar_formant_frame_count.restype = C.c_int64
     L.sonar_formants.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, C.c_int32]
+    L.sonar_voice_quality.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(VoiceQuality)]
     L.sonar_detect_from_audio.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_double, _i32p,
                                           C.POINTER(AcousticFeatures)]
     L.sonar_detect_content_type.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_char_p, C.c_char_p,
@@ -392,6 +401,14 @@ class Context:
         if want_lpc:
             out["lpc_coeffs"], out["reflection"] = co, rf
         return out
+
+    def voice_quality(self, signal, sample_rate):
+        """VoiceQualityAnalyzer.AnalyzeVoiceQuality -> dict of VoiceQualityResult fields."""
+        x = _f64(signal)
+        q = VoiceQuality()
+        self._check(self._L.sonar_voice_quality(self._h, _ptr(x) if len(x) else None, len(x), sample_rate,
+                                                C.byref(q)))
+        return {k: getattr(q, k) for k, _ in VoiceQuality._fields_}
 
     def dtw(self, q, r, band=-1, want_cost=False):
         q, r = _f64(q), _f64(r)

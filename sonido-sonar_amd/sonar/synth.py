@@ -77,3 +77,17 @@ def c4_speech(seconds=1800.0, sr=16000, seed=99):
 def c5_pair(k, seconds=60.0, sr=SR):
     lag = np.random.Generator(np.random.PCG64(2024 + k)).uniform(0, 20.0)
     return c3_pair(seconds, lag, sr, seed=1000 + k, env_seed=5000 + k) + (lag,)
+
+
+def voiced(seconds=4.0, sr=16000, f0=140.0, vibrato=12.0, seed=5, harmonics=12, noise=3e-4):
+    """Voiced speech-like test signal for the voice-quality path: `harmonics` partials (1/h) of a
+    glottal rate f0 + vibrato (3 Hz), 5 Hz amplitude tremor, Gaussian noise (seeded).  The YIN of
+    DetectPitch runs on twice pre-emphasised samples (extractor + detector), which buries a
+    low fundamental under much noise -- keep `noise` small."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = int(round(seconds * sr))
+    t = np.arange(n) / sr
+    f = f0 + vibrato * np.sin(2 * np.pi * 3.0 * t)
+    ph = 2 * np.pi * np.cumsum(f) / sr
+    x = sum(np.sin(h * ph) / h for h in range(1, harmonics + 1))
+    return 0.3 * x * (1.0 + 0.2 * np.sin(2 * np.pi * 5.0 * t)) + noise * rng.standard_normal(n)

@@ -64,6 +64,20 @@ def test_golden_speech_formants_yin():
         assert (pp, cc, tt) == (p, c, t)
 
 
+def test_golden_voice_quality():
+    g = load("voice_quality_16k")
+    x = g["pcm"].astype(np.float64)
+    vq, st = O.voice_quality(O.preemphasis(x, 0.97), 16000)
+    assert st == int(g["status"])
+    close(np.array([vq[k] for k in O.VOICE_QUALITY_KEYS]), g["vq"])
+    fc = dict(sample_rate=16000, window_size=512, hop_size=128, stft_window_size=512, stft_hop_size=128,
+              enable_mfcc=1, enable_speech_features=1, enable_temporal_features=1, mfcc_coefficients=13)
+    ref = O.speech_features_reference(x, 16000, fc)
+    assert ref["is_speech"] == float(g["sx_is_speech"])
+    close(np.float64(ref["jitter"]), g["sx_jitter"])
+    close(np.float64(ref["shimmer"]), g["sx_shimmer"])
+
+
 def test_golden_chroma_alignment():
     g = load("chroma_44k")
     close(O.chroma_music(g["pcm"].astype(np.float64), int(g["n_frames"]), 256, 44100), g["chroma"])

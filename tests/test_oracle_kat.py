@@ -115,3 +115,37 @@ def test_formant_frame_structure():
     assert short["status"][0] == 1
     silent = O.formant_frame(np.zeros(4096), 16000)
     assert silent["status"][0] == 3                               # "zero energy signal"
+
+
+def test_voice_quality_kat():
+    """AnalyzeVoiceQuality (voice_quality.go:56-111): a steady 200 Hz harmonic tone gives
+    periods of int(16000 / f0) = 79..80 samples, zero jitter and F0 near 200 Hz; errors for
+    < 1 s (:57) and for noise without pitch periods (:67)."""
+    sr = 16000
+    t = np.arange(2 * sr) / sr
+    x = np.sin(2 * np.pi * 200 * t) + 0.3 * np.sin(2 * np.pi * 400 * t)
+    vq, st = O.voice_quality(x, sr)
+    assert st == 0 and vq["num_periods"] > 100
+    assert abs(vq["mean_f0"] - 200) < 1 and vq["jitter"] == 0.0 and vq["f0_stability"] > 0.99
+    assert vq["hnr"] > 20 and 0.9 < vq["overall_quality"] <= 1.0
+    assert O.voice_quality(x[: sr - 1], sr)[1] == -1
+    assert O.voice_quality(np.random.default_rng(0).standard_normal(2 * sr), sr)[1] == -2
+    v, st = O.voice_quality(O.preemphasis(synth.voiced(), 0.97), sr)
+    assert st == 0 and v["jitter"] > 0 and v["shimmer"] > 0 and abs(v["mean_f0"] - 140) < 5
+
+
+def test_voice_quality_kat():
+    """AnalyzeVoiceQuality (voice_quality.go:56-111): a steady 200 Hz harmonic tone gives
+    periods of int(16000 / f0) samples, zero jitter and F0 near 200 Hz; errors for < 1 s
+    (:57) and for noise without pitch periods (:67)."""
+    sr = 16000
+    t = np.arange(2 * sr) / sr
+    x = np.sin(2 * np.pi * 200 * t) + 0.3 * np.sin(2 * np.pi * 400 * t)
+    vq, st = O.voice_quality(x, sr)
+    assert st == 0 and vq["num_periods"] > 100
+    assert abs(vq["mean_f0"] - 200) < 1 and vq["jitter"] == 0.0 and vq["f0_stability"] > 0.99
+    assert vq["hnr"] > 20 and 0.9 < vq["overall_quality"] <= 1.0
+    assert O.voice_quality(x[: sr - 1], sr)[1] == -1
+    assert O.voice_quality(np.random.default_rng(0).standard_normal(2 * sr), sr)[1] == -2
+    v, st = O.voice_quality(O.preemphasis(synth.voiced(), 0.97), sr)
+    assert st == 0 and v["jitter"] > 0 and v["shimmer"] > 0 and abs(v["mean_f0"] - 140) < 5

@@ -57,6 +57,14 @@ def main():
     save("speech_c4_16k", pcm=sp, **{"sx_" + k: np.asarray(v, dtype=np.float64) for k, v in ref.items()},
          **{"fm_" + k: np.asarray(v) for k, v in fm.items()},
          yin_pitch=np.array(p), yin_conf=np.array(c), yin_tau=np.array(t, dtype=np.int32))
+    # VoiceQualityAnalyzer.AnalyzeVoiceQuality on the pre-emphasised voiced signal (3 s, 16 kHz)
+    vo = synth.voiced(seconds=3.0).astype(np.float32)
+    vq, vst = O.voice_quality(O.preemphasis(vo.astype(np.float64), 0.97), 16000)
+    vfc = dict(fc, sample_rate=16000)
+    vref = O.speech_features_reference(vo.astype(np.float64), 16000, vfc)
+    save("voice_quality_16k", pcm=vo, status=np.int32(vst), vq=np.array([vq[k] for k in O.VOICE_QUALITY_KEYS]),
+         sx_jitter=np.float64(vref["jitter"]), sx_shimmer=np.float64(vref["shimmer"]),
+         sx_is_speech=np.float64(vref["is_speech"]))
     # chroma (music extractor): 1 s of the bench stream, F = 169 frames at hop 256
     F = O.stft_frames(len(x), 1024, 256)
     save("chroma_44k", pcm=pcm, chroma=O.chroma_music(x, F, 256, 44100), n_frames=np.int64(F))
