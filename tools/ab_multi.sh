@@ -1,0 +1,11 @@
+#!/bin/bash
+# Alternate the headline microbench across library variants: default lib plus lib_<tag>... (N rounds).
+# Usage: bash tools/ab_multi.sh N tag1 tag2 ...
+N=$1; shift
+R="$GRAFT_REPO_ROOT"; [ -z "$R" ] && R=/root/repo
+for i in $(seq $N); do
+  echo -n "default "; timeout -k 10 100 python "$R/tools/fp_microbench.py" mfcc || exit 1
+  for t in "$@"; do
+    echo -n "$t "; SONAR_LIB="$R/sonido-sonar_amd/lib_$t/libsonar_gpu.so" timeout -k 10 100 python "$R/tools/fp_microbench.py" mfcc || exit 1
+  done
+done
