@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--c6-reps", type=int, default=3)
     ap.add_argument("--c6-cpu-seconds", type=float, default=5.0)
     ap.add_argument("--c7-seconds", type=float, default=600.0, help="DetectFromAudio input length (0 = skip row f2)")
+    ap.add_argument("--c3-seconds", type=float, default=300.0, help="C3 stream length (0 = skip)")
+    ap.add_argument("--c4-seconds", type=float, default=1800.0, help="C4 speech length at 16 kHz (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=0.0, help="force CPU-baseline sample length")
     return ap.parse_args()
@@ -175,6 +177,90 @@ def bench_c5(args, world, rank, dev):
     return {"c5_pairs_per_s": P / dt, "c5_ms": dt * 1e3, "c5_pairs": P, "c5_seconds_per_stream": args.c5_seconds,
             "c5_max_lag_s": args.c5_max_lag, "c5_workers_per_rank": args.c5_workers,
             "c5_lag_recovered": float(ok.mean()), "c5_dtw_cells_per_pair": int((args.c5_seconds * SR - W) // H + 1) ** 2}
+
+
+def bench_c3(args, ctx, dev):
+    """BASELINE config C3 (path B, one GPU): two 5-min 44.1 kHz streams with an injected 12.34 s lag
+    (C3 recipe, generated on the device), the music extractor's energy + chroma for both and
+    ExtractAlignmentFeatures with maxOffsetSeconds = 60 (NCC over 20,671 lags, chroma DTW over
+    51,676 x 51,676 cells, the scorers).  Timed: the whole align_pair call (feature kernels,
+    D2H of the features, the alignment entry with its H2D)."""
+    q, r = pairs.c3_pair_device(args.c3_seconds, 12.34, 42, 7, device=dev)
+    torch.cuda.synchronize()
+    pairs.align_pair(ctx, q[: SR * 20], r[: SR * 20], max_lag_seconds=60.0)       # warm-up (small)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rec, res = pairs.align_pair(ctx, q, r, max_lag_seconds=60.0, lag_seconds_true=12.34)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    F = (q.numel() - W) // H + 1
+    lag = float(rec[pairs.RECORD_FIELDS.index("peak_lag")])
+    want = 12.34 * SR / H
+    return {"c3_align": {"seconds_per_stream": args.c3_seconds, "ms": dt * 1e3, "frames_per_stream": F,
+                         "dtw_cells": F * F, "dtw_cells_per_s_end_to_end": F * F / dt,
+                         "peak_lag_frames": lag, "injected_lag_frames": want,
+                         "lag_recovered": bool(min(abs(lag - want), abs(lag + want)) <= 1.5),
+                         "temporal_offset_s": float(rec[0]), "method": float(rec[4])}}
+
+
+def bench_c4(args, ctx):
+    """BASELINE config C4: SpeechFeatureExtractor.ExtractFeatures on 30 min of synthetic 16 kHz
+    speech-like noise (C4 recipe), FeatureConfig.SampleRate = 16000, W = 512, H = 128 (STFT + MFCC +
+    descriptors + ZCR + energy + YIN + LPC formants + voice quality + temporal features).  The C
+    entry takes host float64 PCM (as the cgo path hands it over): the H2D copy is inside the
+    timed call.  CPU baseline: the oracle composition of the same extractor on 60 s, float64."""
+    from sonar import synth
+    sr = 16000
+    x = synth.c4_speech(seconds=args.c4_seconds, sr=sr)
+    fc = dict(sample_rate=sr, window_size=512, hop_size=128, stft_window_size=512, stft_hop_size=128,
+              enable_mfcc=1, enable_speech_features=1, enable_temporal_features=1, mfcc_coefficients=13)
+    cfg = ctx.feature_config(is_news=0, **fc)
+    ctx.extract_speech_features(x[: sr * 10], sr, cfg)                        # warm-up
+    ts = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        got = ctx.extract_speech_features(x, sr, cfg)
+        ts.append(time.perf_counter() - t0)
+    dt = min(ts)
+    F = sonar.stft_frames(len(x), 512, 128)
+    out = {"c4_speech": {"seconds": args.c4_seconds, "samples": len(x), "stft_frames": F,
+                         "pitch_frames": int(len(got["pitch_estimate"])), "ms": dt * 1e3,
+                         "frames_per_s": F / dt, "is_speech": float(np.ravel(got.get("is_speech", [0]))[0]),
+                         "precision": "f64 (parity mode, the extractor's default)"}}
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        n = sr * 60
+        t0 = time.perf_counter()
+        O.speech_features_reference(x[:n], sr, fc)
+        dtc = time.perf_counter() - t0
+        Fc = sonar.stft_frames(n, 512, 128)
+        out["c4_cpu_baseline"] = {"value": Fc / dtc, "unit": "frames/s", "cores": 8, "kind": "port",
+                                  "sample": f"60 s of the C4 signal ({Fc} STFT frames): oracle speech-extractor "
+                                            "composition, float64 (STFT over 8 threads, the rest 1 thread)"}
+    return out
+
+
+def c5_cpu_baseline(args):
+    """The oracle's alignment of one C5 pair (60 s streams): music-extractor energy + chroma of both
+    streams, NCC over the lags, chroma DTW, scorers; float64, 1 thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    q, r, lag = pairs.c5_pair_device(0, args.c5_seconds, device="cpu")
+    q, r = q.numpy(), r.numpy()
+    t0 = time.perf_counter()
+    feats = []
+    for x in (q, r):
+        y = O.preemphasis(O.dc_removal(x, 0.995), 0.95)
+        e = O.short_time_energy(y, W, H)
+        F = O.stft_frames(len(x), W, H)
+        feats.append((e, O.chroma_music(x, F, H, SR)))
+    O.align_features_reference(feats[0][0], feats[1][0], feats[0][1], feats[1][1], len(q), len(r), SR, SR, H,
+                               args.c5_max_lag)
+    dt = time.perf_counter() - t0
+    return {"value": 1.0 / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"one C5 pair ({args.c5_seconds:.0f} s streams): oracle music features + NCC + chroma DTW "
+                      "+ scorers, float64, 1 thread"}
 
 
 def bench_c6(args, ctx, dev):
@@ -390,6 +476,12 @@ def main():
         extra = bench_dtw(ctx, args.dtw_len, args.dtw_steps)
     if args.c5_pairs > 0:
         extra.update(bench_c5(args, world, rank, dev))
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            extra["c5_cpu_baseline"] = c5_cpu_baseline(args)
+    if args.c3_seconds > 0:
+        extra.update(bench_c3(args, ctx, dev))
+    if args.c4_seconds > 0:
+        extra.update(bench_c4(args, ctx))
     if args.c6_gallery > 0:
         extra.update(bench_c6(args, ctx, dev))
         if rank == 0 and world == 1 and not args.no_cpu_baseline:

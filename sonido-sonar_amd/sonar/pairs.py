@@ -35,25 +35,32 @@ def _envelope(n, sr, gen, device, smooth_s=0.5):
     return pts[i0] * (1 - frac) + pts[i0 + 1] * frac
 
 
-def c5_pair_device(k: int, seconds: float = 60.0, sr: int = SR, device="cuda"):
-    """C3's recipe on the device for pair k: one-pole (a = 0.95) filtered N(0,1) noise times a
-    0.5 s piecewise-linear random envelope, query = base[lag:lag+n], reference = base[:n], lag
-    uniform in [0, 20) s.  Returns (query, reference, lag_seconds) as float64 device tensors.
-    The one-pole IIR is applied as a 1024-tap FIR (0.95^1024 < 1e-22) through an FFT."""
-    lag_s = float(np.random.Generator(np.random.PCG64(2024 + k)).uniform(0, 20.0))
+def c3_pair_device(seconds: float, lag_s: float, seed: int, env_seed: int, sr: int = SR, device="cuda"):
+    """C3's recipe on the device: one-pole (a = 0.95) filtered N(0,1) noise times a 0.5 s
+    piecewise-linear random envelope, query = base[lag:lag+n], reference = base[:n].  Returns
+    (query, reference) as float64 device tensors.  The one-pole IIR is applied as a 1024-tap
+    FIR (0.95^1024 < 1e-22) through an FFT."""
     n = int(round(seconds * sr))
     lag = int(round(lag_s * sr))
     total = n + lag
     gen = torch.Generator(device=device)
-    gen.manual_seed(1000 + k)
+    gen.manual_seed(seed)
     x = torch.randn(total + 1023, generator=gen, device=device, dtype=torch.float64)
     h = 0.95 ** torch.arange(1024, device=device, dtype=torch.float64)
     L = 1 << (x.numel() + 1024).bit_length()
     base = torch.fft.irfft(torch.fft.rfft(x, L) * torch.fft.rfft(h, L), L)[1023:1023 + total]   # causal FIR
-    gen.manual_seed(5000 + k)
+    gen.manual_seed(env_seed)
     base = base * _envelope(total, sr, gen, device)
     base = base / base.abs().max()
-    return base[lag:lag + n].contiguous(), base[:n].contiguous(), lag_s
+    return base[lag:lag + n].contiguous(), base[:n].contiguous()
+
+
+def c5_pair_device(k: int, seconds: float = 60.0, sr: int = SR, device="cuda"):
+    """C5 pair k: C3's recipe with seed 1000 + k, envelope seed 5000 + k and a lag uniform in
+    [0, 20) s (PCG64 seed 2024 + k).  Returns (query, reference, lag_seconds)."""
+    lag_s = float(np.random.Generator(np.random.PCG64(2024 + k)).uniform(0, 20.0))
+    q, r = c3_pair_device(seconds, lag_s, 1000 + k, 5000 + k, sr, device)
+    return q, r, lag_s
 
 
 def align_pair(ctx, q, r, sample_rate=SR, stft_window=1024, hop=256, feature_window=1024, max_lag_seconds=60.0,
