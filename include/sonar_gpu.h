@@ -313,6 +313,14 @@ int sonar_align_features(sonar_ctx* ctx,
                          int32_t feature_sample_rate, int32_t hop_size, int32_t window_size,
                          double max_lag_seconds, sonar_result** out);
 
+/* One stream pair end to end (the C5 unit): sonar_music_alignment_features of both device-resident
+ * float64 PCM streams into ctx buffers (stft_window / hop; energy frames feature_window / hop), then
+ * sonar_align_features on those device arrays with feature_sample_rate = sample_rate.  Same result
+ * arrays as sonar_align_features; only the feature round trip through the host is gone. */
+int sonar_align_pair_device(sonar_ctx* ctx, const double* q_pcm, int64_t nq, const double* r_pcm, int64_t nr,
+                            int32_t sample_rate, int32_t stft_window, int32_t hop, int32_t feature_window,
+                            double max_lag_seconds, sonar_result** out);
+
 /* The two MusicFeatureExtractor.ExtractFeatures outputs that the alignment extractor consumes
  * (fingerprint/extractors/music.go:178-245): preprocessAudio (DC removal R = 0.995, then
  * pre-emphasis 0.95, :245-259) -> extractEnergyFeatures' ShortTimeEnergy with the extractor's

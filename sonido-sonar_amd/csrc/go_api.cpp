@@ -469,10 +469,16 @@ int sonar_music_alignment_features(sonar_ctx* c, const double* pcm, int64_t n, i
   return SONAR_OK;
 }
 
-int sonar_align_features(sonar_ctx* c, const double* qe, int64_t nqe, const double* re, int64_t nre, const double* qc,
-                         int64_t nqc, const double* rc_, int64_t nrc, int64_t q_pcm_len, int64_t r_pcm_len,
-                         int32_t sample_rate, int32_t feature_sample_rate, int32_t hop, int32_t win,
-                         double max_lag_seconds, sonar_result** out) {
+}  // extern "C"
+
+namespace {
+
+// AlignmentExtractor.ExtractAlignmentFeatures body; dev = the four feature arrays are device
+// pointers on the ctx's device (no H2D), else host arrays
+int align_impl(sonar_ctx* c, const double* qe, int64_t nqe, const double* re, int64_t nre, const double* qc,
+               int64_t nqc, const double* rc_, int64_t nrc, int64_t q_pcm_len, int64_t r_pcm_len,
+               int32_t sample_rate, int32_t feature_sample_rate, int32_t hop, int32_t win,
+               double max_lag_seconds, int32_t dev, sonar_result** out) {
   if (!c || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
   *out = nullptr;
   if (hop <= 0) return fail(c, SONAR_ERR_INVALID, "hop size must be positive (NewAlignmentExtractor divides by it)");
@@ -493,7 +499,11 @@ int sonar_align_features(sonar_ctx* c, const double* qe, int64_t nqe, const doub
     mlf = std::min(mlf, minf - 1);
     const int64_t L = std::max<int64_t>(0, std::min({mlf, nqe - 1, nre - 1}));
     std::vector<double> cr(2 * L + 1), met(10);
-    const int rc = sonar_ncc(c, qe, nqe, re, nre, (int32_t)mlf, cr.data(), met.data(), 0);
+    double* dcorr = dev ? (double*)dbuf(c, "al.corr", (2 * L + 1) * 8) : nullptr;
+    if (dev && !dcorr) { delete res; return fail(c, SONAR_ERR_NOMEM, "device allocation failed"); }
+    int rc = sonar_ncc(c, qe, nqe, re, nre, (int32_t)mlf, dev ? dcorr : cr.data(), met.data(), dev);
+    if (rc == SONAR_OK && dev) rc = d2h(c, cr, dcorr, cr.size());   // sonar_ncc synchronised the stream
+    if (rc == SONAR_OK && dev && hipStreamSynchronize(c->stream) != hipSuccess) rc = SONAR_ERR_DEVICE;
     if (rc != SONAR_OK) { delete res; return rc; }
     sonar::host::NccMetrics m;
     m.peak_corr = met[0]; m.peak_lag = (int64_t)met[1]; m.peak_index = (int64_t)met[2]; m.p_value = met[3];
@@ -520,7 +530,18 @@ int sonar_align_features(sonar_ctx* c, const double* qe, int64_t nqe, const doub
     std::vector<int32_t> pq(cap), pr(cap);
     std::vector<double> pc(cap);
     int64_t P = 0; double dist = 0;
-    const int rc = sonar_dtw(c, qc, nqc, rc_, nrc, 12, -1, &dist, pq.data(), pr.data(), pc.data(), &P, nullptr, 0);
+    int32_t* dpq = dev ? (int32_t*)dbuf(c, "al.pq", cap * 4) : nullptr;
+    int32_t* dpr = dev ? (int32_t*)dbuf(c, "al.pr", cap * 4) : nullptr;
+    double* dpc = dev ? (double*)dbuf(c, "al.pc", cap * 8) : nullptr;
+    if (dev && (!dpq || !dpr || !dpc)) { delete res; return fail(c, SONAR_ERR_NOMEM, "device allocation failed"); }
+    int rc = sonar_dtw(c, qc, nqc, rc_, nrc, 12, -1, &dist, dev ? dpq : pq.data(), dev ? dpr : pr.data(),
+                       dev ? dpc : pc.data(), &P, nullptr, dev);
+    if (rc == SONAR_OK && dev && P > 0) {
+      rc = d2h(c, pq, dpq, (size_t)P);
+      if (rc == SONAR_OK) rc = d2h(c, pr, dpr, (size_t)P);
+      if (rc == SONAR_OK) rc = d2h(c, pc, dpc, (size_t)P);
+      if (rc == SONAR_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = SONAR_ERR_DEVICE;
+    }
     if (rc != SONAR_OK) { delete res; return rc; }
     chroma.ok = true; chroma.type = 2; chroma.dtw = true;
     chroma.s = sonar::host::dtw_scores(pq.data(), pr.data(), pc.data(), P, nqc, nrc, dist, sample_rate);
@@ -572,6 +593,43 @@ int sonar_align_features(sonar_ctx* c, const double* qe, int64_t nqe, const doub
   res->scalar("time_stretch", stretch);
   *out = res;
   return SONAR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sonar_align_features(sonar_ctx* c, const double* qe, int64_t nqe, const double* re, int64_t nre, const double* qc,
+                         int64_t nqc, const double* rc_, int64_t nrc, int64_t q_pcm_len, int64_t r_pcm_len,
+                         int32_t sample_rate, int32_t feature_sample_rate, int32_t hop, int32_t win,
+                         double max_lag_seconds, sonar_result** out) {
+  return align_impl(c, qe, nqe, re, nre, qc, nqc, rc_, nrc, q_pcm_len, r_pcm_len, sample_rate, feature_sample_rate,
+                    hop, win, max_lag_seconds, 0, out);
+}
+
+// One stream pair end to end from device-resident PCM: MusicFeatureExtractor energy + chroma of
+// both streams (music.go:245-259, :327-376, :460-466) into ctx buffers, then
+// ExtractAlignmentFeatures on those device arrays -- no feature round trip through the host.
+int sonar_align_pair_device(sonar_ctx* c, const double* q_pcm, int64_t nq, const double* r_pcm, int64_t nr,
+                            int32_t sample_rate, int32_t stft_window, int32_t hop, int32_t feature_window,
+                            double max_lag_seconds, sonar_result** out) {
+  if (!c || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (stft_window <= 0 || hop <= 0) return fail(c, SONAR_ERR_INVALID, "window and hop size must be positive");
+  const int64_t Fq = sonar_stft_frames(nq, stft_window, hop), Fr = sonar_stft_frames(nr, stft_window, hop);
+  if (Fq <= 0 || Fr <= 0) return fail(c, SONAR_ERR_TOO_SHORT, "signal too short for given window size and hop size");
+  const int64_t Eq = sonar_energy_frames(nq, feature_window, hop), Er = sonar_energy_frames(nr, feature_window, hop);
+  double* qe = (double*)dbuf(c, "ap.qe", std::max<int64_t>(Eq, 1) * 8);
+  double* re = (double*)dbuf(c, "ap.re", std::max<int64_t>(Er, 1) * 8);
+  double* qc = (double*)dbuf(c, "ap.qc", Fq * 12 * 8);
+  double* rc = (double*)dbuf(c, "ap.rc", Fr * 12 * 8);
+  if (!qe || !re || !qc || !rc) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+  int st = sonar_music_alignment_features(c, q_pcm, nq, sample_rate, stft_window, hop, feature_window, hop, qe, qc, 1);
+  if (st == SONAR_OK)
+    st = sonar_music_alignment_features(c, r_pcm, nr, sample_rate, stft_window, hop, feature_window, hop, re, rc, 1);
+  if (st != SONAR_OK) return st;
+  return align_impl(c, Eq > 0 ? qe : nullptr, Eq, Er > 0 ? re : nullptr, Er, qc, Fq, rc, Fr, nq, nr, sample_rate,
+                    sample_rate, hop, feature_window, max_lag_seconds, 1, out);
 }
 
 }  // extern "C"

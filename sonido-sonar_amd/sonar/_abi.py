@@ -192,6 +192,8 @@ def lib():
     L.sonar_formant_frame_count.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32]
     L.sonar_formant_frame_count.restype = C.c_int64
     L.sonar_formants.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, C.c_int32]
+    L.sonar_align_pair_device.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                          C.c_int32, C.c_double, C.POINTER(C.c_void_p)]
     L.sonar_voice_quality.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(VoiceQuality)]
     L.sonar_detect_from_audio.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_double, _i32p,
                                           C.POINTER(AcousticFeatures)]
@@ -375,6 +377,15 @@ class Context:
         self._check(self._L.sonar_music_alignment_features(
             self._h, C.c_void_p(pcm_ptr), n, sample_rate, stft_window, stft_hop, feature_window, feature_hop,
             C.c_void_p(energy_ptr), C.c_void_p(chroma_ptr), 1))
+
+    def align_pair_device(self, q_ptr, nq, r_ptr, nr, sample_rate=44100, stft_window=1024, hop=256,
+                          feature_window=1024, max_lag_seconds=60.0):
+        """sonar_align_pair_device: music features + ExtractAlignmentFeatures of one pair of
+        device-resident float64 streams; returns the align_features result dict."""
+        h = C.c_void_p()
+        self._check(self._L.sonar_align_pair_device(self._h, C.c_void_p(q_ptr), nq, C.c_void_p(r_ptr), nr, sample_rate,
+                                                    stft_window, hop, feature_window, max_lag_seconds, C.byref(h)))
+        return self._result(h)
 
     # -- path B ------------------------------------------------------------
     def ncc(self, a, b, max_lag):

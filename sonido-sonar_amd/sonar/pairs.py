@@ -65,7 +65,13 @@ def c5_pair_device(k: int, seconds: float = 60.0, sr: int = SR, device="cuda"):
 
 def align_pair(ctx, q, r, sample_rate=SR, stft_window=1024, hop=256, feature_window=1024, max_lag_seconds=60.0,
                lag_seconds_true=float("nan")):
-    """Alignment record of one pair; q, r are float64 device tensors (or numpy arrays)."""
+    """Alignment record of one pair; q, r are float64 device tensors (or numpy arrays).  Device
+    tensors go through sonar_align_pair_device (features stay in HBM, one C call per pair)."""
+    if isinstance(q, torch.Tensor) and isinstance(r, torch.Tensor) and q.is_cuda and r.is_cuda:
+        torch.cuda.current_stream(q.device).synchronize()     # q, r were written on torch's stream
+        res = ctx.align_pair_device(q.data_ptr(), q.numel(), r.data_ptr(), r.numel(), sample_rate, stft_window, hop,
+                                    feature_window, max_lag_seconds)
+        return record_of(res, lag_seconds_true), res
     feats = []
     for x in (q, r):
         if isinstance(x, torch.Tensor):

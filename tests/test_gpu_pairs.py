@@ -57,10 +57,13 @@ def test_pair_alignment_matches_oracle_composition(ctx):
 def test_pair_alignment_device_inputs(ctx):
     """Device-resident pair (the bench's path): same record as the host-array path."""
     q, r, lag_s = pairs.c5_pair_device(9, seconds=12.0, device="cuda")      # lag 1.72 s
-    rec_d, _ = pairs.align_pair(ctx, q, r, 44100, max_lag_seconds=4.0, lag_seconds_true=lag_s)
-    rec_h, _ = pairs.align_pair(ctx, q.cpu().numpy(), r.cpu().numpy(), 44100, max_lag_seconds=4.0,
-                                lag_seconds_true=lag_s)
+    rec_d, res_d = pairs.align_pair(ctx, q, r, 44100, max_lag_seconds=4.0, lag_seconds_true=lag_s)
+    rec_h, res_h = pairs.align_pair(ctx, q.cpu().numpy(), r.cpu().numpy(), 44100, max_lag_seconds=4.0,
+                                    lag_seconds_true=lag_s)
     assert np.array_equal(rec_d, rec_h, equal_nan=True)
+    assert sorted(res_d) == sorted(res_h)                       # sonar_align_pair_device: same result arrays
+    for k in res_h:
+        assert np.array_equal(res_d[k], res_h[k], equal_nan=True), k
     lag_frames = lag_s * 44100 / 256
     pl = rec_d[pairs.RECORD_FIELDS.index("peak_lag")]
     assert min(abs(pl - lag_frames), abs(pl + lag_frames)) <= 1.5
