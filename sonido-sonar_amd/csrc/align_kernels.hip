@@ -34,49 +34,52 @@ __device__ __forceinline__ double go_min(double x, double y) {
 
 // ---------------------------------------------------------------- NCC ----
 // stats[0..3] = mean_a, sd_a, mean_b, sd_b  (correlation.go:464-501, sequential sums)
-__global__ void ncc_stats_kernel(const double* a, int64_t na, const double* b, int64_t nb, double* stats) {
-  const int w = threadIdx.x;
-  if (w > 1) return;
+// Global z-score statistics (normalize :464-501): mean and population std of each input, every
+// sum sequential in Go's index order (bit-exact).  One wave per input: the wave loads 64
+// consecutive values per step (coalesced, the next step in flight), and every lane runs the
+// same sequential add chain over them through v_readlane broadcasts.
+__device__ __forceinline__ double lane_bcast(double v, int j) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), j);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__global__ __launch_bounds__(64) void ncc_stats_kernel(const double* a, int64_t na, const double* b, int64_t nb,
+                                                       double* stats) {
+  const int w = blockIdx.x;
+  const int lane = threadIdx.x;
   const double* s = w ? b : a;
   const int64_t n = w ? nb : na;
-  // sequential sums in Go's index order (bit-exact); loads run 16 ahead of the add chain
-  constexpr int B = 16;
   double mean = 0.0;
   {
-    double cur[B], nxt[B];
-    int64_t i = 0;
-#pragma unroll
-    for (int j = 0; j < B; j++) cur[j] = j < n ? s[j] : 0.0;
-    for (; i + B <= n; i += B) {
-#pragma unroll
-      for (int j = 0; j < B; j++) nxt[j] = i + B + j < n ? s[i + B + j] : 0.0;
-#pragma unroll
-      for (int j = 0; j < B; j++) mean = __dadd_rn(mean, cur[j]);
-#pragma unroll
-      for (int j = 0; j < B; j++) cur[j] = nxt[j];
+    double cur = lane < n ? s[lane] : 0.0;
+    for (int64_t i = 0; i < n; i += 64) {
+      const double nxt = i + 64 + lane < n ? s[i + 64 + lane] : 0.0;
+      const int m = n - i < 64 ? (int)(n - i) : 64;
+      for (int j = 0; j < m; j++) mean = __dadd_rn(mean, lane_bcast(cur, j));
+      cur = nxt;
     }
-    for (int j = 0; i + j < n; j++) mean = __dadd_rn(mean, cur[j]);
   }
   mean = __ddiv_rn(mean, (double)n);
   double var = 0.0;
   {
-    double cur[B], nxt[B];
-    int64_t i = 0;
-#pragma unroll
-    for (int j = 0; j < B; j++) cur[j] = j < n ? s[j] : 0.0;
-    for (; i + B <= n; i += B) {
-#pragma unroll
-      for (int j = 0; j < B; j++) nxt[j] = i + B + j < n ? s[i + B + j] : 0.0;
-#pragma unroll
-      for (int j = 0; j < B; j++) { const double d = __dsub_rn(cur[j], mean); var = __dadd_rn(var, __dmul_rn(d, d)); }
-#pragma unroll
-      for (int j = 0; j < B; j++) cur[j] = nxt[j];
+    double cur = lane < n ? __dsub_rn(s[lane], mean) : 0.0;
+    for (int64_t i = 0; i < n; i += 64) {
+      const double nxt = i + 64 + lane < n ? __dsub_rn(s[i + 64 + lane], mean) : 0.0;
+      const int m = n - i < 64 ? (int)(n - i) : 64;
+      for (int j = 0; j < m; j++) {
+        const double d = lane_bcast(cur, j);
+        var = __dadd_rn(var, __dmul_rn(d, d));
+      }
+      cur = nxt;
     }
-    for (int j = 0; i + j < n; j++) { const double d = __dsub_rn(cur[j], mean); var = __dadd_rn(var, __dmul_rn(d, d)); }
   }
   var = __ddiv_rn(var, (double)n);
-  stats[2 * w] = mean;
-  stats[2 * w + 1] = sqrt(var);
+  if (lane == 0) {
+    stats[2 * w] = mean;
+    stats[2 * w + 1] = sqrt(var);
+  }
 }
 
 __global__ void ncc_norm_kernel(const double* a, int64_t na, const double* b, int64_t nb, const double* stats,
@@ -92,47 +95,68 @@ __global__ void ncc_norm_kernel(const double* a, int64_t na, const double* b, in
   }
 }
 
-// one lag per thread (normalizedCrossCorrelation, correlation.go:373-409)
+// one lag per thread (normalizedCrossCorrelation, correlation.go:373-409), sums in Go's index
+// order (bit-exact).  A block owns 256 consecutive lags; their overlap windows start within 255
+// samples of each other (s1 = max(0, -lag), s2 = max(0, lag)), so each k-tile of both inputs is
+// staged once in LDS (coalesced) and every thread walks its own offsets there.
+constexpr int kNccTile = 1024;
 __global__ __launch_bounds__(256) void ncc_lag_kernel(const double* x, int64_t na, const double* y, int64_t nb,
                                                       int64_t L, double* corr) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= 2 * L + 1) return;
+  __shared__ double xs[kNccTile + 256], ys[kNccTile + 256];
+  __shared__ int64_t ovmax_s;
+  const int64_t nl = 2 * L + 1;
+  const int64_t idx0 = (int64_t)blockIdx.x * 256;
+  const int64_t idx = idx0 + threadIdx.x;
+  const bool active = idx < nl;
   const int64_t lag = idx - L;
-  int64_t s1, e1, s2, e2;                       // calculateOverlapRegion :421-449
+  int64_t s1 = 0, e1 = 0, s2 = 0, e2 = 0;         // calculateOverlapRegion :421-449
   if (lag >= 0) { s1 = 0; e1 = na; s2 = lag; e2 = nb; if (e1 > nb - lag) e1 = nb - lag; if (e2 > nb) e2 = nb; }
   else { s1 = -lag; e1 = na; s2 = 0; e2 = nb; if (e1 > na) e1 = na; if (e2 > na + lag) e2 = na + lag; }
-  const int64_t ov = (e1 - s1) < (e2 - s2) ? (e1 - s1) : (e2 - s2);
+  int64_t ov = (e1 - s1) < (e2 - s2) ? (e1 - s1) : (e2 - s2);
+  if (!active || ov < 0) ov = 0;
+  // window origins over the block's lags [idx0 - L, last - L]
+  const int64_t lastlag = (idx0 + 255 < nl ? idx0 + 255 : nl - 1) - L;
+  const int64_t x0 = lastlag < 0 ? -lastlag : 0;   // min s1
+  const int64_t y0 = idx0 - L > 0 ? idx0 - L : 0;   // min s2
+  if (threadIdx.x == 0) ovmax_s = 0;
+  __syncthreads();
+  atomicMax(reinterpret_cast<unsigned long long*>(&ovmax_s), (unsigned long long)ov);
+  __syncthreads();
+  const int64_t ovmax = ovmax_s;
+  const int ox = (int)(s1 - x0), oy = (int)(s2 - y0);   // 0..255 for active lags
+  double sm = 0.0, q1 = 0.0, q2 = 0.0;
+  for (int64_t k0 = 0; k0 < ovmax; k0 += kNccTile) {
+    for (int j = threadIdx.x; j < kNccTile + 256; j += 256) {
+      const int64_t gx = x0 + k0 + j, gy = y0 + k0 + j;
+      xs[j] = gx < na ? x[gx] : 0.0;
+      ys[j] = gy < nb ? y[gy] : 0.0;
+    }
+    __syncthreads();
+    int kend = ov - k0 < kNccTile ? (int)(ov - k0) : kNccTile;
+    if (kend < 0) kend = 0;
+    const double* px = xs + ox;
+    const double* py = ys + oy;
+    int k = 0;
+    for (; k + 4 <= kend; k += 4) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const double c1 = px[k + j], c2 = py[k + j];
+        sm = __dadd_rn(sm, __dmul_rn(c1, c2));
+        q1 = __dadd_rn(q1, __dmul_rn(c1, c1));
+        q2 = __dadd_rn(q2, __dmul_rn(c2, c2));
+      }
+    }
+    for (; k < kend; k++) {
+      const double c1 = px[k], c2 = py[k];
+      sm = __dadd_rn(sm, __dmul_rn(c1, c2));
+      q1 = __dadd_rn(q1, __dmul_rn(c1, c1));
+      q2 = __dadd_rn(q2, __dmul_rn(c2, c2));
+    }
+    __syncthreads();
+  }
+  if (!active) return;
   double c = 0.0;
   if (ov > 0) {
-    double sm = 0.0, q1 = 0.0, q2 = 0.0;
-    const double* px = x + s1;
-    const double* py = y + s2;
-    // Go's index order per lag (bit-exact); the next 8 pairs load while these 8 accumulate
-    constexpr int B = 8;
-    double c1[B], c2[B], n1[B], n2[B];
-#pragma unroll
-    for (int j = 0; j < B; j++) { c1[j] = j < ov ? px[j] : 0.0; c2[j] = j < ov ? py[j] : 0.0; }
-    int64_t k = 0;
-    for (; k + B <= ov; k += B) {
-#pragma unroll
-      for (int j = 0; j < B; j++) {
-        const bool in = k + B + j < ov;
-        n1[j] = in ? px[k + B + j] : 0.0; n2[j] = in ? py[k + B + j] : 0.0;
-      }
-#pragma unroll
-      for (int j = 0; j < B; j++) {
-        sm = __dadd_rn(sm, __dmul_rn(c1[j], c2[j]));
-        q1 = __dadd_rn(q1, __dmul_rn(c1[j], c1[j]));
-        q2 = __dadd_rn(q2, __dmul_rn(c2[j], c2[j]));
-      }
-#pragma unroll
-      for (int j = 0; j < B; j++) { c1[j] = n1[j]; c2[j] = n2[j]; }
-    }
-    for (int j = 0; k + j < ov; j++) {
-      sm = __dadd_rn(sm, __dmul_rn(c1[j], c2[j]));
-      q1 = __dadd_rn(q1, __dmul_rn(c1[j], c1[j]));
-      q2 = __dadd_rn(q2, __dmul_rn(c2[j], c2[j]));
-    }
     const double dn = sqrt(__dmul_rn(q1, q2));
     c = dn < 1e-10 ? 0.0 : __ddiv_rn(sm, dn);
   }
@@ -141,7 +165,7 @@ __global__ __launch_bounds__(256) void ncc_lag_kernel(const double* x, int64_t n
 
 int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t L, double* xa, double* xb,
                double* stats, double* corr, hipStream_t s) {
-  hipLaunchKernelGGL(ncc_stats_kernel, dim3(1), dim3(64), 0, s, a, na, b, nb, stats);
+  hipLaunchKernelGGL(ncc_stats_kernel, dim3(2), dim3(64), 0, s, a, na, b, nb, stats);
   const int64_t nmax = na > nb ? na : nb;
   hipLaunchKernelGGL(ncc_norm_kernel, dim3((unsigned)((nmax + 255) / 256)), dim3(256), 0, s, a, na, b, nb, stats, xa,
                      xb);

@@ -55,7 +55,9 @@ __global__ __launch_bounds__(256) void zcr_kernel(const void* pcm, int pcm_f64, 
   }
 }
 
-// one thread per energy frame, sequential sum in Go's order
+// one thread per energy frame, sequential sum in Go's order.  The frame's samples are read in
+// batches of 16 with the next batch in flight while this one accumulates (the dependent add
+// chain then no longer waits on every load: 0.39 -> see DESIGN Kernel 2).
 __global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H,
                                                      double alpha, void* out, int out_f64) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -63,10 +65,26 @@ __global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f6
   const int64_t s = t * H;
   double ss = 0.0;
   double prev = s > 0 ? pre_x(pcm, pcm_f64, s - 1) : 0.0;
-  for (int64_t j = s; j < s + W; ++j) {
-    const double x = pre_x(pcm, pcm_f64, j);
-    const double y = __dsub_rn(x, __dmul_rn(alpha, prev));
-    prev = x;
+  constexpr int B = 16;
+  double cur[B], nxt[B];
+#pragma unroll
+  for (int j = 0; j < B; j++) cur[j] = j < W ? pre_x(pcm, pcm_f64, s + j) : 0.0;
+  int k = 0;
+  for (; k + B <= W; k += B) {
+#pragma unroll
+    for (int j = 0; j < B; j++) nxt[j] = k + B + j < W ? pre_x(pcm, pcm_f64, s + k + B + j) : 0.0;
+#pragma unroll
+    for (int j = 0; j < B; j++) {
+      const double y = __dsub_rn(cur[j], __dmul_rn(alpha, prev));
+      prev = cur[j];
+      ss = __dadd_rn(ss, __dmul_rn(y, y));
+    }
+#pragma unroll
+    for (int j = 0; j < B; j++) cur[j] = nxt[j];
+  }
+  for (int j = 0; k + j < W; j++) {
+    const double y = __dsub_rn(cur[j], __dmul_rn(alpha, prev));
+    prev = cur[j];
     ss = __dadd_rn(ss, __dmul_rn(y, y));
   }
   store_out(out, out_f64, t, sqrt(__ddiv_rn(ss, (double)W)));
@@ -133,10 +151,11 @@ __global__ __launch_bounds__(256) void yin_kernel(const double* pcm, int64_t n, 
 }
 
 // chroma of one frame per block: direct DFT of length fs (any fs), |X|^2 folded to 12 bins.
-// trig table (cos, sin of -2 pi m/fs) lives in global memory (L1/L2 resident).
+// trig table (cos, sin of -2 pi m/fs): copied into LDS when it fits (trig_lds), else read from
+// global memory (L1/L2 resident).
 __global__ __launch_bounds__(256) void chroma_kernel(const double* y, int64_t n, int64_t frames, int hop, int fs,
-                                                     const double* win, const double* trig, const int* cmap,
-                                                     double* out) {
+                                                     const double* win, const double* trig_g, const int* cmap,
+                                                     double* out, int trig_lds) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* seg = (double*)smem;                 // fs
   double* pw = seg + fs;                        // K + 12
@@ -144,6 +163,13 @@ __global__ __launch_bounds__(256) void chroma_kernel(const double* y, int64_t n,
   const int64_t t = blockIdx.x;
   if (t >= frames) return;
   const int64_t s = t * hop;
+  const double* trig = trig_g;
+  if (trig_lds) {
+    double* tl = pw + K + 12 + ((K + 12) & 1);    // 16-B aligned, 2 fs
+    for (int i = threadIdx.x; i < fs; i += blockDim.x)
+      reinterpret_cast<double2*>(tl)[i] = reinterpret_cast<const double2*>(trig_g)[i];
+    trig = tl;
+  }
   for (int i = threadIdx.x; i < fs; i += blockDim.x) {
     const double v = (s + i < n) ? y[s + i] : 0.0;   // zero pad (music.go:351-357)
     seg[i] = v * win[i];
@@ -330,11 +356,16 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
                   const double* trig, const int* cmap, double* out, hipStream_t s) {
   if (frames <= 0) return 0;
   const int K = fs / 2 + 1;
-  const size_t lds = sizeof(double) * ((size_t)fs + K + 12);
+  size_t lds = sizeof(double) * ((size_t)fs + K + 12);
   if (lds > 160 * 1024) return -4;
+  // the trig table joins the frame in LDS while the block stays small (fs = 256 at every
+  // BASELINE config, F6): 6 KB per block instead of a global read per MAC
+  const size_t lds_t = sizeof(double) * ((size_t)fs + K + 12 + ((K + 12) & 1) + 2 * (size_t)fs);
+  const int trig_lds = lds_t <= 32 * 1024;
+  if (trig_lds) lds = lds_t;
   if (lds > 64 * 1024) hipFuncSetAttribute((const void*)chroma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(chroma_kernel, dim3((unsigned)frames), dim3(256), lds, s, y, n, frames, hop, fs, window, trig,
-                     cmap, out);
+                     cmap, out, trig_lds);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
