@@ -51,28 +51,37 @@ __global__ __launch_bounds__(64) void ncc_stats_kernel(const double* a, int64_t 
   const int lane = threadIdx.x;
   const double* s = w ? b : a;
   const int64_t n = w ? nb : na;
+  // full 64-value steps are unrolled (constant readlane indices, broadcasts issued ahead of the
+  // add chain); the tail runs the same chain with a runtime index
   double mean = 0.0;
   {
     double cur = lane < n ? s[lane] : 0.0;
-    for (int64_t i = 0; i < n; i += 64) {
+    int64_t i = 0;
+    for (; i + 64 <= n; i += 64) {
       const double nxt = i + 64 + lane < n ? s[i + 64 + lane] : 0.0;
-      const int m = n - i < 64 ? (int)(n - i) : 64;
-      for (int j = 0; j < m; j++) mean = __dadd_rn(mean, lane_bcast(cur, j));
+#pragma unroll
+      for (int j = 0; j < 64; j++) mean = __dadd_rn(mean, lane_bcast(cur, j));
       cur = nxt;
     }
+    for (int j = 0; j < (int)(n - i); j++) mean = __dadd_rn(mean, lane_bcast(cur, j));
   }
   mean = __ddiv_rn(mean, (double)n);
   double var = 0.0;
   {
     double cur = lane < n ? __dsub_rn(s[lane], mean) : 0.0;
-    for (int64_t i = 0; i < n; i += 64) {
+    int64_t i = 0;
+    for (; i + 64 <= n; i += 64) {
       const double nxt = i + 64 + lane < n ? __dsub_rn(s[i + 64 + lane], mean) : 0.0;
-      const int m = n - i < 64 ? (int)(n - i) : 64;
-      for (int j = 0; j < m; j++) {
+#pragma unroll
+      for (int j = 0; j < 64; j++) {
         const double d = lane_bcast(cur, j);
         var = __dadd_rn(var, __dmul_rn(d, d));
       }
       cur = nxt;
+    }
+    for (int j = 0; j < (int)(n - i); j++) {
+      const double d = lane_bcast(cur, j);
+      var = __dadd_rn(var, __dmul_rn(d, d));
     }
   }
   var = __ddiv_rn(var, (double)n);

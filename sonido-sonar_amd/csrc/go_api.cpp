@@ -450,7 +450,9 @@ int sonar_music_alignment_features(sonar_ctx* c, const double* pcm, int64_t n, i
   }
   double* y = (double*)dbuf(c, "mf.pre", n * 8);                 // processedPCM
   if (!y) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
-  if (sonar::launch_dc_preemph(dp, n, 0.995, 0.95, y, s) != 0) return fail(c, SONAR_ERR_DEVICE, "dc launch failed");
+  double* dcs = (double*)dbuf(c, "mf.dcscratch", sonar::dc_preemph_scratch_bytes(n));
+  if (!dcs) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+  if (sonar::launch_dc_preemph(dp, n, 0.995, 0.95, y, dcs, s) != 0) return fail(c, SONAR_ERR_DEVICE, "dc launch failed");
   const int64_t Fe = sonar_energy_frames(n, fw, fh);
   double* de = device_ptrs ? energy : (double*)dbuf(c, "mf.energy", std::max<int64_t>(Fe, 1) * 8);
   // ShortTimeEnergy of the already pre-emphasised signal: alpha 0 makes the kernel's

@@ -98,7 +98,8 @@ int launch_hnr_autocorr(const double* frame2048, double* ac, hipStream_t s);
 // Chroma STFT (misc_kernels.hip)
 int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, const double* window,
                   const double* trig, const int* chroma_map, double* out, hipStream_t s);
-int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, hipStream_t s);
+int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, double* scratch, hipStream_t s);
+size_t dc_preemph_scratch_bytes(int64_t n);
 // speech-extractor helpers (misc_kernels.hip)
 int launch_preemph(const void* pcm, int pcm_f64, int64_t n, double alpha, double* y, hipStream_t s);
 int launch_stats(const double* y, int64_t n, double* part, int blocks, hipStream_t s);

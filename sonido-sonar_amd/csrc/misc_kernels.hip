@@ -7,7 +7,7 @@
 //  yin_kernel      PitchDetector.detectPitchYin core (algorithms/tonal/pitch_detection.go:282-420)
 //  chroma_kernel   ChromaSTFT.ComputeChroma on one music-extractor frame
 //                  (algorithms/chroma/chroma_stft.go:45-138, fingerprint/extractors/music.go:327-376)
-//  dcpre_kernel    DCRemoval.Process + PreEmphasis.Process (music.go:245-259)
+//  dc_local/carry/apply_kernel  DCRemoval.Process + PreEmphasis.Process (music.go:245-259)
 //
 // Decision-bearing arithmetic (sign tests, sums feeding thresholds) is float64
 // with explicit _rn intrinsics: no FMA contraction, Go's evaluation order.
@@ -200,91 +200,6 @@ __global__ __launch_bounds__(256) void chroma_kernel(const double* y, int64_t n,
   }
 }
 
-// DC blocker y[n] = x[n] - x[n-1] + R y[n-1] followed by pre-emphasis z = y[n] - a y[n-1].
-// Each thread produces a chunk of outputs after a WARM-sample warm-up from zero
-// state; R^WARM < 1e-17, so the result equals the sequential filter to fp64 rounding.
-// One thread per chunk of `chunk` samples (a multiple of 16; chunk starts are 16-aligned).  The
-// DC-removal state at the chunk start is rebuilt by running the recurrence over the preceding
-// `warm` samples from a zero state (0.995^8192 ~ 1.6e-18: the start-up error is below float64
-// rounding of the state).  Samples move as double2 vectors, 16 per step: the warm-up loads and
-// the chunk's stores are whole 128-B lines per lane (scalar per-sample stores to lanes 16 KB
-// apart made this kernel 10x slower).
-// two consecutive samples starting at an even index; callers' buffers may be only 8-B aligned
-// (a torch slice), then the pair is read as two scalars
-__device__ __forceinline__ double2 ld2(const double* x, int64_t i, bool al) {
-  return al ? reinterpret_cast<const double2*>(x)[i >> 1] : make_double2(x[i], x[i + 1]);
-}
-
-__global__ __launch_bounds__(256) void dcpre_kernel(const double* x, int64_t n, double R, double alpha, double* z,
-                                                    int chunk, int warm) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t s = c * chunk;
-  if (s >= n) return;
-  const int64_t e = min(n, s + chunk);
-  const int64_t w0 = s > warm ? s - warm : 0;
-  double x1 = w0 > 0 ? x[w0 - 1] : 0.0, y1 = 0.0;
-  constexpr int B = 16;
-  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-  // warm-up: [w0, s) in whole 16-sample blocks (w0 and s are multiples of 16)
-  {
-    double2 cur[B / 2], nxt[B / 2];
-    if (w0 < s) {
-#pragma unroll
-      for (int j = 0; j < B / 2; j++) cur[j] = ld2(x, w0 + 2 * j, al);
-    }
-    for (int64_t i = w0; i < s; i += B) {
-      if (i + B < s) {
-#pragma unroll
-        for (int j = 0; j < B / 2; j++) nxt[j] = ld2(x, i + B + 2 * j, al);
-      }
-#pragma unroll
-      for (int j = 0; j < B / 2; j++) {
-        const double a = cur[j].x, b = cur[j].y;
-        double yv = __dadd_rn(__dsub_rn(a, x1), __dmul_rn(R, y1)); x1 = a; y1 = yv;
-        yv = __dadd_rn(__dsub_rn(b, x1), __dmul_rn(R, y1)); x1 = b; y1 = yv;
-      }
-#pragma unroll
-      for (int j = 0; j < B / 2; j++) cur[j] = nxt[j];
-    }
-  }
-  double yprev = y1;                                     // y[s-1] (0 at s = 0)
-  // the chunk: full 16-sample blocks as vectors, then a scalar tail (last chunk only)
-  const int64_t ef = s + ((e - s) / B) * B;
-  {
-    double2* zv = reinterpret_cast<double2*>(z);          // z: context buffer, 256-B aligned
-    double2 cur[B / 2], nxt[B / 2], out[B / 2];
-    if (s < ef) {
-#pragma unroll
-      for (int j = 0; j < B / 2; j++) cur[j] = ld2(x, s + 2 * j, al);
-    }
-    for (int64_t i = s; i < ef; i += B) {
-      if (i + B < ef) {
-#pragma unroll
-        for (int j = 0; j < B / 2; j++) nxt[j] = ld2(x, i + B + 2 * j, al);
-      }
-#pragma unroll
-      for (int j = 0; j < B / 2; j++) {
-        const double a = cur[j].x, b = cur[j].y;
-        double yv = __dadd_rn(__dsub_rn(a, x1), __dmul_rn(R, y1)); x1 = a; y1 = yv;
-        out[j].x = __dsub_rn(yv, __dmul_rn(alpha, yprev)); yprev = yv;
-        yv = __dadd_rn(__dsub_rn(b, x1), __dmul_rn(R, y1)); x1 = b; y1 = yv;
-        out[j].y = __dsub_rn(yv, __dmul_rn(alpha, yprev)); yprev = yv;
-      }
-#pragma unroll
-      for (int j = 0; j < B / 2; j++) zv[i / 2 + j] = out[j];
-#pragma unroll
-      for (int j = 0; j < B / 2; j++) cur[j] = nxt[j];
-    }
-  }
-  for (int64_t i = ef; i < e; ++i) {
-    const double xv = x[i];
-    const double yv = __dadd_rn(__dsub_rn(xv, x1), __dmul_rn(R, y1));
-    x1 = xv; y1 = yv;
-    z[i] = __dsub_rn(yv, __dmul_rn(alpha, yprev));
-    yprev = yv;
-  }
-}
-
 int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, double alpha, int sr, void* out,
                int out_f64, hipStream_t s) {
   if (F <= 0) return 0;
@@ -369,12 +284,97 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, hipStream_t s) {
+// DC removal y[n] = x[n] - x[n-1] + R y[n-1] (dc_removal.go:101-124) followed by pre-emphasis
+// z[n] = y[n] - alpha y[n-1] (pre_emphasis.go:135-155), both with zero state, as three passes
+// over chunks of kDcChunk samples: (1) each chunk's response from a zero state -> its end value;
+// (2) one wave chains the chunk carries Y_c = e_c + R^chunk Y_{c-1} in order; (3) each chunk
+// re-runs the recurrence from its true start state and writes z.  Every sample goes through
+// the same sequential recurrence as Go from a start state that equals Go's to rounding (the
+// warm-up version it replaces ran 8,192 extra samples per 1,024-sample chunk).
+constexpr int kDcChunk = 1024;
+
+template <bool WRITE>
+__device__ __forceinline__ double dc_run(const double* x, int64_t s, int64_t e, double R, double alpha, double y1,
+                                         double* z) {
+  double x1 = s > 0 ? x[s - 1] : 0.0;
+  constexpr int B = 16;
+  double cur[B], nxt[B];
+#pragma unroll
+  for (int j = 0; j < B; j++) cur[j] = s + j < e ? x[s + j] : 0.0;
+  int64_t i = s;
+  for (; i + B <= e; i += B) {
+#pragma unroll
+    for (int j = 0; j < B; j++) nxt[j] = i + B + j < e ? x[i + B + j] : 0.0;
+#pragma unroll
+    for (int j = 0; j < B; j++) {
+      const double yv = __dadd_rn(__dsub_rn(cur[j], x1), __dmul_rn(R, y1));
+      if (WRITE) z[i + j] = __dsub_rn(yv, __dmul_rn(alpha, y1));
+      x1 = cur[j]; y1 = yv;
+    }
+#pragma unroll
+    for (int j = 0; j < B; j++) cur[j] = nxt[j];
+  }
+  for (int j = 0; i + j < e; j++) {
+    const double yv = __dadd_rn(__dsub_rn(cur[j], x1), __dmul_rn(R, y1));
+    if (WRITE) z[i + j] = __dsub_rn(yv, __dmul_rn(alpha, y1));
+    x1 = cur[j]; y1 = yv;
+  }
+  return y1;
+}
+
+__global__ __launch_bounds__(256) void dc_local_kernel(const double* x, int64_t n, double R, double* ends) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t s = c * kDcChunk;
+  if (s >= n) return;
+  ends[c] = dc_run<false>(x, s, min(n, s + kDcChunk), R, 0.0, 0.0, nullptr);
+}
+
+__device__ __forceinline__ double lane_bcast_d(double v, int j) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), j);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// one wave: ystart[c] = Y_{c-1}, Y_c = ends[c] + RC Y_{c-1}, Y_{-1} = 0
+__global__ __launch_bounds__(64) void dc_carry_kernel(const double* ends, int64_t T, double RC, double* ystart) {
+  const int lane = threadIdx.x;
+  double Y = 0.0;
+  for (int64_t i = 0; i < T; i += 64) {
+    const double cur = i + lane < T ? ends[i + lane] : 0.0;
+    const int m = T - i < 64 ? (int)(T - i) : 64;
+    double mine = 0.0;
+    if (m == 64) {
+#pragma unroll
+      for (int j = 0; j < 64; j++) { if (lane == j) mine = Y; Y = __dadd_rn(lane_bcast_d(cur, j), __dmul_rn(RC, Y)); }
+    } else {
+      for (int j = 0; j < m; j++) { if (lane == j) mine = Y; Y = __dadd_rn(lane_bcast_d(cur, j), __dmul_rn(RC, Y)); }
+    }
+    if (lane < m) ystart[i + lane] = mine;
+  }
+}
+
+__global__ __launch_bounds__(256) void dc_apply_kernel(const double* x, int64_t n, double R, double alpha,
+                                                       const double* ystart, double* z) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t s = c * kDcChunk;
+  if (s >= n) return;
+  dc_run<true>(x, s, min(n, s + kDcChunk), R, alpha, ystart[c], z);
+}
+
+size_t dc_preemph_scratch_bytes(int64_t n) { return (size_t)(2 * ((n + kDcChunk - 1) / kDcChunk) + 2) * 8; }
+
+int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, double* scratch, hipStream_t s) {
   if (n <= 0) return 0;
-  const int chunk = 1024, warm = 8192;   // multiples of 16 (vector blocks)
-  const int64_t nthreads = (n + chunk - 1) / chunk;
-  hipLaunchKernelGGL(dcpre_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, s, x, n, R, alpha, y, chunk,
-                     warm);
+  const int64_t T = (n + kDcChunk - 1) / kDcChunk;
+  double* ends = scratch;
+  double* ystart = scratch + T;
+  double RC = 1.0;
+  for (int k = 0; k < kDcChunk; k++) RC *= R;                 // R^chunk (carry weight of a full chunk)
+  const unsigned g = (unsigned)((T + 255) / 256);
+  hipLaunchKernelGGL(dc_local_kernel, dim3(g), dim3(256), 0, s, x, n, R, ends);
+  hipLaunchKernelGGL(dc_carry_kernel, dim3(1), dim3(64), 0, s, ends, T, RC, ystart);
+  hipLaunchKernelGGL(dc_apply_kernel, dim3(g), dim3(256), 0, s, x, n, R, alpha, ystart, y);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

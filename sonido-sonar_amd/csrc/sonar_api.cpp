@@ -557,7 +557,9 @@ int sonar_chroma_stft(sonar_ctx* c, const double* pcm, int64_t n, int64_t F, int
   if (preprocess) {
     double* yb = (double*)dbuf(c, "chroma.y", n * 8);
     if (!yb) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
-    if (sonar::launch_dc_preemph(dp, n, 0.995, 0.95, yb, s) != 0) return fail(c, SONAR_ERR_DEVICE, "dc launch failed");
+    double* dcs = (double*)dbuf(c, "chroma.dcscratch", sonar::dc_preemph_scratch_bytes(n));
+    if (!dcs) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+    if (sonar::launch_dc_preemph(dp, n, 0.995, 0.95, yb, dcs, s) != 0) return fail(c, SONAR_ERR_DEVICE, "dc launch failed");
     y = yb;
   }
   const std::string key = std::to_string(fs) + "|" + std::to_string(sr);
