@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void yin_kernel(const double* pcm, int64_t n, 
 // global memory (L1/L2 resident).
 __global__ __launch_bounds__(256) void chroma_kernel(const double* y, int64_t n, int64_t frames, int hop, int fs,
                                                      const double* win, const double* trig_g, const int* cmap,
-                                                     double* out, int trig_lds) {
+                                                     double* out, int trig_lds, int fft) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* seg = (double*)smem;                 // fs
   double* pw = seg + fs;                        // K + 12
@@ -170,6 +170,39 @@ __global__ __launch_bounds__(256) void chroma_kernel(const double* y, int64_t n,
       reinterpret_cast<double2*>(tl)[i] = reinterpret_cast<const double2*>(trig_g)[i];
     trig = tl;
   }
+  if (fft) {
+    // power-of-two frame (fs = 256 at every BASELINE config, F6): radix-2 DIT FFT in LDS, like the
+    // go-dsp radix-2 path the reference runs (O(fs log fs) instead of the O(fs^2) direct DFT)
+    double* fre = pw + K + 12 + ((K + 12) & 1) + (trig_lds ? 2 * fs : 0);
+    double* fim = fre + fs;
+    int lg = 0;
+    while ((1 << lg) < fs) ++lg;
+    for (int i = threadIdx.x; i < fs; i += blockDim.x) {
+      const double v = (s + i < n) ? y[s + i] : 0.0;   // zero pad (music.go:351-357)
+      const int r = (int)(__brev((unsigned)i) >> (32 - lg));
+      fre[r] = v * win[i];
+      fim[r] = 0.0;
+    }
+    __syncthreads();
+    for (int h = 1; h < fs; h <<= 1) {
+      const int tstep = fs / (2 * h);
+      for (int bf = threadIdx.x; bf < fs / 2; bf += blockDim.x) {
+        const int k = bf & (h - 1), i0 = ((bf - k) << 1) + k, i1 = i0 + h;
+        const double wr = trig[2 * (k * tstep)], wi = trig[2 * (k * tstep) + 1];
+        const double xr = fre[i1], xi = fim[i1];
+        const double tr = xr * wr - xi * wi, ti = xr * wi + xi * wr;
+        const double ar = fre[i0], ai = fim[i0];
+        fre[i0] = ar + tr; fim[i0] = ai + ti;
+        fre[i1] = ar - tr; fim[i1] = ai - ti;
+      }
+      __syncthreads();
+    }
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+      const double mag = hypot(fre[k], fim[k]);
+      pw[k] = mag * mag;
+    }
+    __syncthreads();
+  } else {
   for (int i = threadIdx.x; i < fs; i += blockDim.x) {
     const double v = (s + i < n) ? y[s + i] : 0.0;   // zero pad (music.go:351-357)
     seg[i] = v * win[i];
@@ -187,6 +220,7 @@ __global__ __launch_bounds__(256) void chroma_kernel(const double* y, int64_t n,
     pw[k] = mag * mag;
   }
   __syncthreads();
+  }
   if (threadIdx.x < 12) {
     double acc = 0.0;
     for (int k = 0; k < K; ++k) if (cmap[k] == (int)threadIdx.x) acc += pw[k];  // ascending-k order
@@ -278,9 +312,12 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
   const size_t lds_t = sizeof(double) * ((size_t)fs + K + 12 + ((K + 12) & 1) + 2 * (size_t)fs);
   const int trig_lds = lds_t <= 32 * 1024;
   if (trig_lds) lds = lds_t;
+  // radix-2 FFT for power-of-two frames whose (re, im) work arrays still fit next to the rest
+  const int fft = (fs & (fs - 1)) == 0 && fs >= 2 && lds + 16 * (size_t)fs <= 48 * 1024;
+  if (fft) lds += 16 * (size_t)fs + 8;
   if (lds > 64 * 1024) hipFuncSetAttribute((const void*)chroma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(chroma_kernel, dim3((unsigned)frames), dim3(256), lds, s, y, n, frames, hop, fs, window, trig,
-                     cmap, out, trig_lds);
+                     cmap, out, trig_lds, fft);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
