@@ -321,6 +321,33 @@ int sonar_align_pair_device(sonar_ctx* ctx, const double* q_pcm, int64_t nq, con
                             int32_t sample_rate, int32_t stft_window, int32_t hop, int32_t feature_window,
                             double max_lag_seconds, sonar_result** out);
 
+/* ---- AlignmentAnalyzer.AnalyzeAlignmentConsistency (algorithms/stats/alignment.go:709-800) -----
+ * num_trials (< 2 -> 5) alignments of addNoise(query, 0.01) (:737-749: q[i][j] += sin(i*j+i+j)
+ * * 0.01 * q[i][j]) against reference with AlignFeatures (:84-106) for `method`, then the offset
+ * statistics (:751-800).  The perturbation is deterministic, so every trial aligns the same
+ * perturbed query: the alignment runs once and its offset is counted num_trials times (the
+ * statistics are those of num_trials equal offsets, as in Go).  query / reference: host
+ * row-major nq x dim / nr x dim float64.  method: SONAR_ALIGN_*; max_lag and hop as
+ * NewAlignmentAnalyzer (:60-81).  Errors: "no successful alignments" (empty input or an
+ * unsupported method, where every Go trial fails). */
+enum { SONAR_ALIGN_DTW = 0, SONAR_ALIGN_XCORR = 1, SONAR_ALIGN_PHASE = 2, SONAR_ALIGN_HYBRID = 3 };
+typedef struct {                     /* stats.AlignmentStats (alignment.go:700-707) */
+  double mean_offset, stddev_offset, median_offset, offset_range, consistency;
+  int64_t offset;                    /* the (single) AlignFeatures offset, samples or frames per method */
+  int32_t trials;
+} sonar_alignment_stats;
+
+int sonar_alignment_consistency(sonar_ctx* ctx, const double* query, int64_t nq, const double* reference, int64_t nr,
+                                int32_t dim, int32_t method, int32_t max_lag, int32_t hop, int32_t sample_rate,
+                                int32_t num_trials, sonar_alignment_stats* out);
+
+/* AlignmentExtractor.TruncateToAlignmentPCM (extractors/alignment.go:223-297) as sample indices:
+ * the aligned segments are pcm1[start1 : start1+length] and pcm2[start2 : start2+length] (the
+ * PCM stays where it is, e.g. in HBM).  Errors as Go: "offset too large ...", "no overlapping
+ * audio after alignment". */
+int sonar_truncate_to_alignment(sonar_ctx* ctx, int64_t n1, int64_t n2, int32_t sample_rate, double temporal_offset,
+                                int64_t* start1, int64_t* start2, int64_t* length);
+
 /* The two MusicFeatureExtractor.ExtractFeatures outputs that the alignment extractor consumes
  * (fingerprint/extractors/music.go:178-245): preprocessAudio (DC removal R = 0.995, then
  * pre-emphasis 0.95, :245-259) -> extractEnergyFeatures' ShortTimeEnergy with the extractor's

@@ -547,3 +547,87 @@ def detect_from_audio(pcm, sample_rate, thr=2.0):
     if rc:
         raise ValueError("sample rate < 10: the Go loop never ends")
     return CONTENT_NAMES[ct.value], dict(zip(ACOUSTIC_KEYS, out.tolist()))
+
+
+# ---------------------------------------------------------------------------
+# AlignmentAnalyzer.AnalyzeAlignmentConsistency / AlignmentExtractor.TruncateToAlignmentPCM
+# (SURVEY.md 8(f) rank 4), composed from the primitives above
+# ---------------------------------------------------------------------------
+
+ALIGN_DTW, ALIGN_XCORR, ALIGN_PHASE, ALIGN_HYBRID = 0, 1, 2, 3       # AlignmentMethod (stats/alignment.go:12-17)
+
+
+def add_noise(features, level=0.01):
+    """addNoise (stats/alignment.go:737-749): v + (sin(float64(i*j+i+j)) * level) * v."""
+    f = _f64(features)
+    i = np.arange(f.shape[0], dtype=np.int64)[:, None]
+    j = np.arange(f.shape[1], dtype=np.int64)[None, :]
+    return f + (np.sin((i * j + i + j).astype(np.float64)) * level) * f
+
+
+def align_offset_reference(query, reference, sample_rate, method, max_lag, hop):
+    """AlignFeatures (stats/alignment.go:84-106) -> result.Offset, for DTW / xcorr / hybrid."""
+    q, r = _f64(query), _f64(reference)
+    conf = None
+    if method in (ALIGN_XCORR, ALIGN_HYBRID):                         # alignWithCrossCorrelation :151-181
+        _, met = ncc(q[:, 0], r[:, 0], max_lag)                       # flatten2DFeatures :363-378
+        m = align_xcorr_metrics(met, hop, sample_rate, max_lag)
+        off, conf = int(m["offset"]), m["confidence"]
+        if method == ALIGN_XCORR or conf > 0.7:                       # alignWithHybrid :315-317
+            return off
+    res = dtw(q, r)                                                   # alignWithDTW :129-148
+    return int(align_dtw_metrics(res, len(q), len(r), sample_rate)["offset"])
+
+
+def alignment_consistency_reference(query, reference, sample_rate, method, max_lag, hop, num_trials=5):
+    """AnalyzeAlignmentConsistency (stats/alignment.go:709-735) + calculateOffsetStats (:751-800).
+    Every trial aligns the same deterministic perturbation, run here trial by trial as Go does."""
+    if num_trials < 2:
+        num_trials = 5
+    q, r = _f64(query), _f64(reference)
+    if len(q) == 0 or len(r) == 0 or method not in (ALIGN_DTW, ALIGN_XCORR, ALIGN_HYBRID):
+        raise ValueError("no successful alignments")
+    offs = [float(align_offset_reference(add_noise(q, 0.01), r, sample_rate, method, max_lag, hop))
+            for _ in range(num_trials)]
+    s = 0.0
+    for o in offs:
+        s += o
+    mean = s / len(offs)
+    ssd = 0.0
+    for o in offs:
+        ssd += (o - mean) * (o - mean)
+    sd = float(np.sqrt(ssd / len(offs)))
+    srt = sorted(offs)
+    n = len(srt)
+    median = (srt[n // 2 - 1] + srt[n // 2]) / 2 if n % 2 == 0 else srt[n // 2]
+    cons = 1.0 / (1.0 + sd / abs(mean)) if mean != 0 else 1.0
+    return {"mean_offset": mean, "stddev_offset": sd, "median_offset": median, "offset_range": srt[-1] - srt[0],
+            "consistency": cons, "offset": int(offs[0]), "trials": num_trials}
+
+
+def truncate_to_alignment_reference(n1, n2, sample_rate, offset_seconds):
+    """TruncateToAlignmentPCM (extractors/alignment.go:223-297) -> (start1, start2, length)."""
+    import math
+    sr = float(sample_rate)
+    def off_samples():
+        v = abs(offset_seconds) * sr
+        return int(math.floor(v + 0.5)) if v >= 0 else 0             # math.Round (half away from zero)
+    s1 = s2 = 0
+    if offset_seconds > 0:
+        s2 = off_samples()
+        if s2 >= n2:
+            raise ValueError(f"offset too large: need to skip {s2} samples but pcm2 only has {n2}")
+        common = min(n1, n2 - s2)
+    elif offset_seconds < 0:
+        s1 = off_samples()
+        if s1 >= n1:
+            raise ValueError(f"offset too large: need to skip {s1} samples but pcm1 only has {n1}")
+        common = min(n1 - s1, n2)
+    else:
+        common = min(n1, n2)
+    if common <= 0:
+        raise ValueError("no overlapping audio after alignment")
+    pad = int(0.5 * sr)
+    if common > 2 * pad:
+        s1, s2, common = s1 + pad, s2 + pad, common - 2 * pad
+    return s1, s2, common

@@ -183,6 +183,31 @@ int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// AlignmentAnalyzer.addNoise (alignment.go:737-749): out[i][j] = q + (sin(i*j+i+j) * level) * q
+__global__ void perturb_kernel(const double* q, int64_t nq, int dim, double level, double* out) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nq * dim) return;
+  const int64_t i = idx / dim, j = idx - i * dim;
+  const double v = q[idx];
+  out[idx] = __dadd_rn(v, __dmul_rn(__dmul_rn(sin((double)(i * j + i + j)), level), v));
+}
+// flatten2DFeatures (:363-378): the first component of every frame
+__global__ void first_column_kernel(const double* x, int64_t n, int dim, double* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = x[i * dim];
+}
+int launch_perturb(const double* q, int64_t nq, int dim, double level, double* out, hipStream_t s) {
+  const int64_t n = nq * dim;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(perturb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, nq, dim, level, out);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+int launch_first_column(const double* x, int64_t n, int dim, double* out, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(first_column_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n, dim, out);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 // ---------------------------------------------------------------- DTW ----
 // Forward sweep (fillCostMatrix + applyStepPattern "symmetric2", dtw.go:106-135,138-143)
 // as ONE persistent launch.  Rows are cut into bands of 64; one wave owns a band

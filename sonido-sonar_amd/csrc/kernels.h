@@ -107,6 +107,9 @@ int launch_tilt(const double* y, int64_t n, int64_t frames, double* tilt, hipStr
 // NCC (align_kernels.hip)
 int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t L, double* norm_a,
                double* norm_b, double* stats, double* corr, hipStream_t s);
+// AlignmentAnalyzer.addNoise and flatten2DFeatures (align_kernels.hip)
+int launch_perturb(const double* q, int64_t nq, int dim, double level, double* out, hipStream_t s);
+int launch_first_column(const double* x, int64_t n, int dim, double* out, hipStream_t s);
 // DTW (dtw.go:55-217).  Band-pipelined persistent kernel; see align_kernels.hip.
 struct DtwGeom {
   int64_t nq, nr;   // sequence lengths

@@ -208,6 +208,37 @@ func (x *Context) DetectFromAudio(pcm []float64, sampleRate int, threshold float
 	return int(ct), AcousticFeatures(f), nil
 }
 
+// AlignmentStats mirrors stats.AlignmentStats (algorithms/stats/alignment.go:700-707) plus the
+// AlignFeatures offset and the trial count.
+type AlignmentStats C.sonar_alignment_stats
+
+// AnalyzeAlignmentConsistency runs AlignmentAnalyzer.AnalyzeAlignmentConsistency
+// (stats/alignment.go:709) on the GPU; method is the stats.AlignmentMethod value.
+func (x *Context) AnalyzeAlignmentConsistency(query, reference [][]float64, sampleRate, method, maxLag, hopSize,
+	numTrials int) (AlignmentStats, error) {
+	q, dim := rows2(query)
+	r, _ := rows2(reference)
+	var st C.sonar_alignment_stats
+	if rc := C.sonar_alignment_consistency(x.c, f64p(q), C.int64_t(len(query)), f64p(r), C.int64_t(len(reference)),
+		C.int32_t(dim), C.int32_t(method), C.int32_t(maxLag), C.int32_t(hopSize), C.int32_t(sampleRate),
+		C.int32_t(numTrials), &st); rc != C.SONAR_OK {
+		return AlignmentStats{}, x.err(rc)
+	}
+	return AlignmentStats(st), nil
+}
+
+// TruncateToAlignmentPCM mirrors AlignmentExtractor.TruncateToAlignmentPCM
+// (extractors/alignment.go:223): the aligned sub-slices of the two streams.
+func (x *Context) TruncateToAlignmentPCM(pcm1, pcm2 []float64, sampleRate int, temporalOffset float64) ([]float64,
+	[]float64, error) {
+	var s1, s2, n C.int64_t
+	if rc := C.sonar_truncate_to_alignment(x.c, C.int64_t(len(pcm1)), C.int64_t(len(pcm2)), C.int32_t(sampleRate),
+		C.double(temporalOffset), &s1, &s2, &n); rc != C.SONAR_OK {
+		return nil, nil, x.err(rc)
+	}
+	return pcm1[int(s1) : int(s1)+int(n)], pcm2[int(s2) : int(s2)+int(n)], nil
+}
+
 // VoiceQuality mirrors speech.VoiceQualityResult (algorithms/speech/voice_quality.go:21-43).
 type VoiceQuality C.sonar_voice_quality_result
 

@@ -96,6 +96,15 @@ class VoiceQuality(C.Structure):
                [(n, C.c_double) for n in ("mean_f0", "f0_range", "analysis_quality")]
 
 
+class AlignmentStats(C.Structure):
+    """sonar_alignment_stats (stats.AlignmentStats, alignment.go:700-707) + the offset and trials."""
+    _fields_ = [(n, C.c_double) for n in ("mean_offset", "stddev_offset", "median_offset", "offset_range",
+                                          "consistency")] + [("offset", C.c_int64), ("trials", C.c_int32)]
+
+
+ALIGN_DTW, ALIGN_XCORR, ALIGN_PHASE, ALIGN_HYBRID = 0, 1, 2, 3
+
+
 class FpFeatures(C.Structure):
     """sonar_fp_features (one AudioFingerprint as FingerprintComparator reads it)."""
     _fields_ = [("id", C.c_int64), ("present", C.c_uint32), ("content_type", C.c_int32),
@@ -194,6 +203,10 @@ def lib():
     L.sonar_formants.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, C.c_int32]
     L.sonar_align_pair_device.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                           C.c_int32, C.c_double, C.POINTER(C.c_void_p)]
+    L.sonar_alignment_consistency.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                              C.c_int32, C.c_int32, C.c_int32, C.POINTER(AlignmentStats)]
+    L.sonar_truncate_to_alignment.argtypes = [_vp, C.c_int64, C.c_int64, C.c_int32, C.c_double,
+                                              C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.sonar_voice_quality.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(VoiceQuality)]
     L.sonar_detect_from_audio.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_double, _i32p,
                                           C.POINTER(AcousticFeatures)]
@@ -412,6 +425,27 @@ class Context:
         if want_lpc:
             out["lpc_coeffs"], out["reflection"] = co, rf
         return out
+
+    def alignment_consistency(self, query, reference, sample_rate, method=ALIGN_XCORR, max_lag=100, hop=256,
+                              num_trials=5):
+        """AlignmentAnalyzer.AnalyzeAlignmentConsistency -> dict of AlignmentStats (+ offset, trials)."""
+        q, r = _f64(query), _f64(reference)
+        if q.ndim == 1:
+            q = q[:, None]
+        if r.ndim == 1:
+            r = r[:, None]
+        st = AlignmentStats()
+        self._check(self._L.sonar_alignment_consistency(
+            self._h, _ptr(q) if q.size else None, len(q), _ptr(r) if r.size else None, len(r),
+            q.shape[1] if q.size else 1, method, max_lag, hop, sample_rate, num_trials, C.byref(st)))
+        return {k: getattr(st, k) for k, _ in AlignmentStats._fields_}
+
+    def truncate_to_alignment(self, n1, n2, sample_rate, temporal_offset):
+        """AlignmentExtractor.TruncateToAlignmentPCM -> (start1, start2, length)."""
+        a, b, n = C.c_int64(), C.c_int64(), C.c_int64()
+        self._check(self._L.sonar_truncate_to_alignment(self._h, n1, n2, sample_rate, temporal_offset, C.byref(a),
+                                                        C.byref(b), C.byref(n)))
+        return a.value, b.value, n.value
 
     def voice_quality(self, signal, sample_rate):
         """VoiceQualityAnalyzer.AnalyzeVoiceQuality -> dict of VoiceQualityResult fields."""

@@ -149,3 +149,27 @@ def test_voice_quality_kat():
     assert O.voice_quality(np.random.default_rng(0).standard_normal(2 * sr), sr)[1] == -2
     v, st = O.voice_quality(O.preemphasis(synth.voiced(), 0.97), sr)
     assert st == 0 and v["jitter"] > 0 and v["shimmer"] > 0 and abs(v["mean_f0"] - 140) < 5
+
+
+def test_alignment_consistency_and_truncate_kat():
+    """AnalyzeAlignmentConsistency (stats/alignment.go:709-800): the perturbation is deterministic,
+    so all trials agree (std 0, range 0, consistency 1) and a 9-frame shift is found by NCC (x hop)
+    and by the DTW mean offset; TruncateToAlignmentPCM (extractors/alignment.go:223-297) index rules."""
+    rng = np.random.default_rng(4)
+    base = np.abs(np.convolve(rng.standard_normal(700), np.ones(9) / 9, mode="same"))[:, None] * \
+        (1 + rng.random((700, 3)))
+    q, r = base[9:609], base[:600]
+    st = O.alignment_consistency_reference(q, r, 44100, O.ALIGN_XCORR, 50, 256, num_trials=4)
+    assert st["trials"] == 4 and abs(st["offset"]) == 9 * 256
+    assert st["stddev_offset"] == 0.0 and st["offset_range"] == 0.0 and st["consistency"] == 1.0
+    assert st["mean_offset"] == st["median_offset"] == st["offset"]
+    assert O.alignment_consistency_reference(q, r, 44100, O.ALIGN_XCORR, 50, 256, num_trials=1)["trials"] == 5
+    d = O.alignment_consistency_reference(q, r, 44100, O.ALIGN_DTW, 50, 256)
+    assert abs(d["offset"]) <= 9
+    with pytest.raises(ValueError, match="no successful alignments"):
+        O.alignment_consistency_reference(q, r, 44100, O.ALIGN_PHASE, 50, 256)
+    assert O.truncate_to_alignment_reference(44100 * 10, 44100 * 10, 44100, 2.0) == (22050, 88200 + 22050,
+                                                                                      441000 - 88200 - 44100)
+    assert O.truncate_to_alignment_reference(1000, 1000, 44100, 0.0) == (0, 0, 1000)      # no padding room
+    with pytest.raises(ValueError, match="offset too large"):
+        O.truncate_to_alignment_reference(1000, 1000, 44100, -1.0)
