@@ -71,6 +71,7 @@ def parse():
     ap.add_argument("--c7-seconds", type=float, default=600.0, help="DetectFromAudio input length (0 = skip row f2)")
     ap.add_argument("--c3-seconds", type=float, default=300.0, help="C3 stream length (0 = skip)")
     ap.add_argument("--c4-seconds", type=float, default=1800.0, help="C4 speech length at 16 kHz (0 = skip)")
+    ap.add_argument("--ingest-reps", type=int, default=3, help="row f3 PCM-ingest repetitions (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process (0 = leave as is)")
     ap.add_argument("--cpu-seconds", type=float, default=0.0, help="force CPU-baseline sample length")
@@ -432,6 +433,47 @@ def c6_cpu_baseline(args):
                       "statistics per call as comparison.go does, float64, 1 thread"}
 
 
+def bench_ingest(args, ctx, pcm, cfg, F):
+    """Row f3: the decoder's f64le byte stream of this rank's hour
+    (Decoder.bytesToFloat64, transcode/decoder.go:850-871) from pageable host memory into device
+    f32 PCM through sonar_ingest_f64le, then the headline MFCC launch: the PCIe-inclusive
+    frames/s.  Both conversion modes, plus a plain pageable torch copy of the f64 bytes + a
+    device cast as the naive comparison.  Best of --ingest-reps; not the headline `value`."""
+    dev = pcm.device
+    x = pcm.double().cpu().numpy()                 # the f64le stream as ffmpeg would hand it over
+    n = len(x)
+    buf = torch.empty(n, dtype=torch.float32, device=dev)
+    mf = torch.empty((F, N_MFCC), dtype=torch.float32, device=dev)
+
+    def timed(fn):
+        best = 1e30
+        for _ in range(args.ingest_reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        return best
+
+    res = {"samples": n, "f64le_bytes": 8 * n, "frames": F}
+    naive = timed(lambda: buf.copy_(torch.from_numpy(x).to(dev)))
+    res["pageable_torch_copy"] = {"ms": naive * 1e3, "gb_per_s": 8 * n / naive / 1e9}
+    for name, mode in (("device_convert", sonar.INGEST_DEVICE_CONVERT), ("host_convert", sonar.INGEST_HOST_CONVERT)):
+        ctx.ingest_f64le(x[: 1 << 20], buf.data_ptr(), sonar.F32, mode)       # pinned ring + pool warm-up
+        t_in = timed(lambda: ctx.ingest_f64le(x, buf.data_ptr(), sonar.F32, mode))
+        exact = bool(torch.equal(buf, pcm))
+
+        def e2e():
+            ctx.ingest_f64le(x, buf.data_ptr(), sonar.F32, mode)
+            ctx.fingerprint_device(buf.data_ptr(), n, cfg, mfcc=mf.data_ptr())
+        t_e2e = timed(e2e)
+        res[name] = {"ingest_ms": t_in * 1e3, "f64le_gb_per_s": 8 * n / t_in / 1e9,
+                     "pcie_bytes_per_sample": 8 if mode == sonar.INGEST_DEVICE_CONVERT else 4,
+                     "end_to_end_ms": t_e2e * 1e3, "end_to_end_frames_per_s": F / t_e2e,
+                     "bit_exact_vs_resident_pcm": exact}
+    return {"ingest_f64le": res}
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup()
@@ -485,6 +527,8 @@ def main():
     extra = {}
     if args.dtw_len > 0:
         extra = bench_dtw(ctx, args.dtw_len, args.dtw_steps)
+    if args.ingest_reps > 0:
+        extra.update(bench_ingest(args, ctx, pcm, cfg, F))
     if args.c5_pairs > 0:
         extra.update(bench_c5(args, world, rank, dev))
         if rank == 0 and world == 1 and not args.no_cpu_baseline:

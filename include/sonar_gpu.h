@@ -168,6 +168,28 @@ void sonar_fp_cfg_default(sonar_fp_cfg* cfg);
 int sonar_fingerprint(sonar_ctx* ctx, const void* pcm, int64_t n, const sonar_fp_cfg* cfg,
                       sonar_fp_out* out);
 
+/* ---- PCM ingest: the decoder's f64le byte stream -> device samples.
+ * Replaces Decoder.bytesToFloat64 + processFFmpegOutput's empty check (transcode/decoder.go:850-871,
+ * :782-787; ffmpeg "-f f64le" at :709): nbytes is trimmed to a multiple of 8, zero samples fail with
+ * SONAR_ERR_EMPTY "no audio samples decoded".  Samples keep the stream's (interleaved) order, as
+ * AudioData.PCM does.  The bytes go through a ring of pinned host slots filled by host_threads
+ * threads (0 = OMP_NUM_THREADS or min(16, cores)) while earlier slots DMA on the ctx stream:
+ *   SONAR_INGEST_DEVICE_CONVERT  f64 crosses PCIe, a kernel rounds to f32 (if out_dtype F32)
+ *   SONAR_INGEST_HOST_CONVERT    the filling threads round to f32 (half the PCIe bytes)
+ * Rounding is round-to-nearest-even in both (Go float32(x)).  d_out: device buffer of
+ * n_samples * (out_dtype F64 ? 8 : 4) bytes, 16-B aligned; NULL only reports *n_samples.
+ * Returns once the host bytes are consumed; the device writes complete in ctx-stream order. */
+#define SONAR_INGEST_DEVICE_CONVERT 0
+#define SONAR_INGEST_HOST_CONVERT 1
+int sonar_ingest_f64le(sonar_ctx* ctx, const void* bytes, int64_t nbytes, int32_t out_dtype, int32_t mode,
+                       int32_t host_threads, void* d_out, int64_t* n_samples);
+/* Decoder output straight into path A: sonar_ingest_f64le (f32, `mode`) into a ctx-owned device
+ * buffer, then sonar_fingerprint on it with cfg->pcm_dtype = F32; outputs are host buffers
+ * (cfg->device_ptrs must be 0).  Replaces bytesToFloat64 + ComputeSTFTWithWindow's upload of
+ * AudioData.PCM (decoder.go:850-871 -> analyzers/spectral.go:385) with one call. */
+int sonar_fingerprint_f64le(sonar_ctx* ctx, const void* bytes, int64_t nbytes, int32_t mode,
+                            const sonar_fp_cfg* cfg, sonar_fp_out* out);
+
 /* ---- YIN per-frame core (frames of 1024 at hop 512, PitchDetector defaults).
  * Writes the raw YIN result per frame (pitch Hz or 0, confidence 1-cmndf or 0)
  * before the sequential octave-correction / median tracking, which the host

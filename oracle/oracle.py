@@ -631,3 +631,18 @@ def truncate_to_alignment_reference(n1, n2, sample_rate, offset_seconds):
     if common > 2 * pad:
         s1, s2, common = s1 + pad, s2 + pad, common - 2 * pad
     return s1, s2, common
+
+
+def bytes_to_float64(data):
+    """Decoder.bytesToFloat64 (transcode/decoder.go:850-871): trim to a multiple of 8 bytes, then
+    binary.LittleEndian.Uint64 + math.Float64frombits per sample; None when no sample remains
+    (processFFmpegOutput then fails "no audio samples decoded", decoder.go:785-787)."""
+    b = np.frombuffer(bytes(data), dtype=np.uint8)
+    b = b[: len(b) - len(b) % 8]
+    if len(b) == 0:
+        return None
+    # little-endian assembly of each 8-byte group, written out rather than trusting the host order
+    u = np.zeros(len(b) // 8, dtype=np.uint64)
+    for k in range(8):
+        u |= b[k::8].astype(np.uint64) << np.uint64(8 * k)
+    return u.view(np.float64)

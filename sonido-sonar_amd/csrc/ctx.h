@@ -33,6 +33,8 @@ struct PairTables {
   int J = 0, JS = 0, NMP = 0, n_mels = 0, n_mfcc = 0, max_src = 0;
 };
 
+struct IngestState;  // pinned slots + host pool of sonar_ingest_f64le (ingest_api.cpp)
+
 struct sonar_ctx {
   int device = 0;
   hipStream_t own = nullptr;
@@ -50,6 +52,7 @@ struct sonar_ctx {
   size_t ev_used = 0;
   double last_ms = 0.0;
   const char* last_fp_kernel = "";
+  IngestState* ingest = nullptr;
 };
 
 struct sonar_result {
@@ -80,6 +83,11 @@ int detect_content_type(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, 
                         const char* genre, const char* station, const char* url, int32_t acoustic,
                         int32_t dflt, double thr, int32_t* out);
 void timed_end(sonar_ctx* c, hipStream_t s, hipEvent_t end);
+// frees the ingest ring and joins its host threads (ingest_api.cpp)
+void ingest_release(sonar_ctx* c);
+// sonar_fingerprint with the PCM already on the device and host outputs (sonar_api.cpp)
+int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cfg* cfg, sonar_fp_out* out,
+                     bool pcm_dev);
 // VoiceQualityAnalyzer.AnalyzeVoiceQuality on device-resident float64 samples (voice_api.cpp)
 int voice_quality(sonar_ctx* c, const double* dsig, int64_t n, int32_t sr, sonar_voice_quality_result* out);
 }  // namespace detail

@@ -104,6 +104,8 @@ size_t dc_preemph_scratch_bytes(int64_t n);
 int launch_preemph(const void* pcm, int pcm_f64, int64_t n, double alpha, double* y, hipStream_t s);
 int launch_stats(const double* y, int64_t n, double* part, int blocks, hipStream_t s);
 int launch_tilt(const double* y, int64_t n, int64_t frames, double* tilt, hipStream_t s);
+// PCM ingest: f64 -> f32 (RNE); both pointers 16-B aligned (misc_kernels.hip)
+int launch_f64_to_f32(const double* in, float* out, int64_t n, hipStream_t s);
 // NCC (align_kernels.hip)
 int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t L, double* norm_a,
                double* norm_b, double* stats, double* corr, hipStream_t s);

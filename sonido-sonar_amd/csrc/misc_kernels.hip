@@ -477,4 +477,27 @@ int launch_tilt(const double* y, int64_t n, int64_t frames, double* tilt, hipStr
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// ---- PCM ingest (sonar_ingest_f64le, ingest_api.cpp) ----------------------
+// f64 -> f32, round-to-nearest-even like Go's float32(x) and numpy astype; 4 samples per lane
+// (two 16-B loads, one 16-B store), HBM-bound at 12 B per sample.
+__global__ __launch_bounds__(256) void f64_to_f32_kernel(const double* __restrict__ in, float* __restrict__ out,
+                                                         int64_t n) {
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const double2 a = reinterpret_cast<const double2*>(in)[2 * i];
+    const double2 b = reinterpret_cast<const double2*>(in)[2 * i + 1];
+    reinterpret_cast<float4*>(out)[i] = make_float4((float)a.x, (float)a.y, (float)b.x, (float)b.y);
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = (float)in[i];
+}
+
+int launch_f64_to_f32(const double* in, float* out, int64_t n, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (((uintptr_t)in & 15) || ((uintptr_t)out & 15)) return -2;
+  int64_t blocks = ((n >> 2) + 255) / 256; if (blocks > 8192) blocks = 8192; if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(f64_to_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, out, n);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 }  // namespace sonar

@@ -218,6 +218,7 @@ void sonar_destroy(sonar_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
+  sonar::detail::ingest_release(c);
   for (auto& kv : c->bufs) if (kv.second.ptr) hipFree(kv.second.ptr);
   for (auto& kv : c->fp_tables) {
     FpTables& t = kv.second;
@@ -309,7 +310,14 @@ void sonar_fp_cfg_default(sonar_fp_cfg* c) {
 }
 
 // ======================================================= sonar_fingerprint ==
-int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cfg* cfg, sonar_fp_out* out) {
+}  // extern "C"
+
+namespace sonar {
+namespace detail {
+// pcm_dev: pcm is already device memory even though the outputs are host buffers
+// (cfg->device_ptrs == 0) -- the sonar_fingerprint_f64le path (ingest_api.cpp)
+int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cfg* cfg, sonar_fp_out* out,
+                     bool pcm_dev) {
   if (!c || !cfg || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
   // ComputeSTFTWithWindow validation order (spectral.go:386-412)
   if (n <= 0 || !pcm) return fail(c, SONAR_ERR_EMPTY, "empty signal");
@@ -332,7 +340,7 @@ int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_c
   const bool dev = cfg->device_ptrs != 0;
 
   const void* dpcm = pcm;
-  if (!dev) {
+  if (!dev && !pcm_dev) {
     void* p = dbuf(c, "fp.pcm", (size_t)n * esz_in);
     if (!p) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (pcm)");
     HIP_TRY(c, hipMemcpyAsync(p, pcm, (size_t)n * esz_in, hipMemcpyHostToDevice, s));
@@ -502,6 +510,14 @@ int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_c
     HIP_TRY(c, hipStreamSynchronize(s));
   }
   return SONAR_OK;
+}
+}  // namespace detail
+}  // namespace sonar
+
+extern "C" {
+
+int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cfg* cfg, sonar_fp_out* out) {
+  return sonar::detail::fingerprint_impl(c, pcm, n, cfg, out, cfg && cfg->device_ptrs != 0);
 }
 
 // ========================================================= YIN, chroma ====

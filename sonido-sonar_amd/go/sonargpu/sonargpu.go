@@ -379,6 +379,41 @@ func (x *Context) Fingerprint(pcm []float64, windowSize, hopSize, sampleRate int
 	return split(flat, frames, nc), nil
 }
 
+// FingerprintDecoded is Fingerprint fed by the decoder's raw output instead of AudioData.PCM:
+// `output` is the ffmpeg "-f f64le" byte stream (transcode/decoder.go:709) that
+// Decoder.bytesToFloat64 (decoder.go:850-871) would walk into a []float64.  The bytes cross
+// PCIe through pinned slots (HOST_CONVERT rounds them to float32 on the way, half the bytes),
+// so the []float64 copy of the stream is never built.  Float32 throughput mode only.
+func (x *Context) FingerprintDecoded(output []byte, windowSize, hopSize, sampleRate int, p MFCCParams) ([][]float64,
+	error) {
+	if len(output) < 8 {
+		return nil, fmt.Errorf("no audio samples decoded: %w", ErrEmpty)
+	}
+	var cfg C.sonar_fp_cfg
+	C.sonar_fp_cfg_default(&cfg)
+	cfg.window_size, cfg.hop_size, cfg.sample_rate = C.int32_t(windowSize), C.int32_t(hopSize), C.int32_t(sampleRate)
+	cfg.n_mfcc, cfg.n_filters = C.int32_t(p.NumCoefficients), C.int32_t(p.NumFilters)
+	cfg.low_freq, cfg.high_freq, cfg.lifter = C.double(p.LowFreq), C.double(p.HighFreq), C.double(p.LifterCoeff)
+	cfg.use_lifter = b2i(p.UseLiftering)
+	cfg.flags = C.SONAR_FP_MFCC
+	cfg.precision, cfg.pcm_dtype, cfg.out_dtype = C.SONAR_F32, C.SONAR_F32, C.SONAR_F64
+	frames := int(C.sonar_stft_frames(C.int64_t(len(output)/8), C.int32_t(windowSize), C.int32_t(hopSize)))
+	if frames <= 0 {
+		return nil, fmt.Errorf("signal too short for given window size and hop size: %w", ErrTooShort)
+	}
+	nc := p.NumCoefficients
+	if nc <= 0 {
+		nc = 13
+	}
+	flat := make([]float64, frames*nc)
+	out := C.sonar_fp_out{mfcc: unsafe.Pointer(&flat[0])}
+	if rc := C.sonar_fingerprint_f64le(x.c, unsafe.Pointer(&output[0]), C.int64_t(len(output)),
+		C.SONAR_INGEST_HOST_CONVERT, &cfg, &out); rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	return split(flat, frames, nc), nil
+}
+
 // DTWResult mirrors stats.DTWResult + AlignPoint (algorithms/stats/dtw.go:17-34).
 type DTWResult struct {
 	Distance   float64

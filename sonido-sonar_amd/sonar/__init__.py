@@ -31,5 +31,8 @@ from ._abi import (  # noqa: F401
     FP_GENERIC,
     F32,
     F64,
+    INGEST_DEVICE_CONVERT,
+    INGEST_HOST_CONVERT,
+    ERR_EMPTY,
     EXPORTED_SYMBOLS,
 )

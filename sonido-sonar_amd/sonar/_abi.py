@@ -17,6 +17,7 @@ OK, ERR_INVALID, ERR_TOO_SHORT, ERR_EMPTY, ERR_UNSUPPORTED, ERR_DEVICE, ERR_NOME
 FP_MFCC, FP_MAGNITUDE, FP_SPECTRAL, FP_ZCR, FP_ENERGY = 1, 2, 4, 8, 16
 FP_GENERIC = 1 << 30   # force the general fused kernel (A/B checks of the f32 MFCC path)
 F32, F64 = 0, 1
+INGEST_DEVICE_CONVERT, INGEST_HOST_CONVERT = 0, 1   # sonar_ingest_f64le modes
 WINDOWS = {"hann": 0, "hamming": 1, "blackman": 2, "blackman_harris": 3, "kaiser": 4,
            "tukey": 5, "rectangular": 6, "bartlett": 7, "welch": 8}
 SPECTRAL_NAMES = ["centroid", "rolloff", "bandwidth", "flatness", "crest", "slope", "flux",
@@ -208,6 +209,8 @@ def lib():
     L.sonar_truncate_to_alignment.argtypes = [_vp, C.c_int64, C.c_int64, C.c_int32, C.c_double,
                                               C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.sonar_voice_quality.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(VoiceQuality)]
+    L.sonar_fingerprint_f64le.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(FpConfig), C.POINTER(FpOut)]
+    L.sonar_ingest_f64le.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, _i64p]
     L.sonar_detect_from_audio.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_double, _i32p,
                                           C.POINTER(AcousticFeatures)]
     L.sonar_detect_content_type.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_char_p, C.c_char_p,
@@ -323,6 +326,21 @@ class Context:
         pcm = np.ascontiguousarray(pcm, dtype=np.float64 if cfg.pcm_dtype == F64 else np.float32)
         n = len(pcm)
         cfg.device_ptrs = 0
+        res, out = self._fp_outputs(n, cfg)
+        self._check(self._L.sonar_fingerprint(self._h, _ptr(pcm) if n else None, n, C.byref(cfg), C.byref(out)))
+        return res
+
+    def fingerprint_f64le(self, data, cfg: FpConfig, mode=INGEST_HOST_CONVERT):
+        """sonar_fingerprint_f64le: the decoder's f64le bytes (decoder.go:850-871) straight into path A."""
+        buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
+            else np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+        cfg.device_ptrs = 0
+        res, out = self._fp_outputs(buf.size // 8, cfg)
+        self._check(self._L.sonar_fingerprint_f64le(self._h, buf.ctypes.data if buf.size else None, buf.size, mode,
+                                                    C.byref(cfg), C.byref(out)))
+        return res
+
+    def _fp_outputs(self, n, cfg):
         F = stft_frames(n, cfg.window_size, cfg.hop_size) if n > 0 and cfg.window_size > 0 and cfg.hop_size > 0 else 0
         od = np.float64 if cfg.out_dtype == F64 else np.float32
         out, res = FpOut(), {}
@@ -346,8 +364,7 @@ class Context:
                 fe = energy_frames(n, cfg.energy_window, cfg.energy_hop)
                 res["energy"] = np.zeros(fe, od)
                 out.energy = res["energy"].ctypes.data if fe > 0 else None
-        self._check(self._L.sonar_fingerprint(self._h, _ptr(pcm) if n else None, n, C.byref(cfg), C.byref(out)))
-        return res
+        return res, out
 
     def fingerprint_device(self, pcm_ptr, n, cfg: FpConfig, **out_ptrs):
         """Device-pointer form (async on the ctx stream): out_ptrs name -> device address."""
@@ -446,6 +463,17 @@ class Context:
         self._check(self._L.sonar_truncate_to_alignment(self._h, n1, n2, sample_rate, temporal_offset, C.byref(a),
                                                         C.byref(b), C.byref(n)))
         return a.value, b.value, n.value
+
+    def ingest_f64le(self, data, d_out=None, out_dtype=F32, mode=INGEST_DEVICE_CONVERT, host_threads=0):
+        """Decoder.bytesToFloat64 (decoder.go:850-871) into device memory: `data` is the ffmpeg f64le
+        byte stream (bytes / bytearray / uint8 or float64 array), `d_out` a device pointer of
+        n * (4 if out_dtype == F32 else 8) bytes (None: only count).  Returns the sample count."""
+        buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
+            else np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+        n = C.c_int64()
+        self._check(self._L.sonar_ingest_f64le(self._h, buf.ctypes.data if buf.size else None, buf.size, out_dtype,
+                                               mode, host_threads, d_out, C.byref(n)))
+        return n.value
 
     def voice_quality(self, signal, sample_rate):
         """VoiceQualityAnalyzer.AnalyzeVoiceQuality -> dict of VoiceQualityResult fields."""

@@ -173,3 +173,15 @@ def test_alignment_consistency_and_truncate_kat():
     assert O.truncate_to_alignment_reference(1000, 1000, 44100, 0.0) == (0, 0, 1000)      # no padding room
     with pytest.raises(ValueError, match="offset too large"):
         O.truncate_to_alignment_reference(1000, 1000, 44100, -1.0)
+
+
+def test_bytes_to_float64_kat():
+    """Decoder.bytesToFloat64 (decoder.go:850-871): little-endian IEEE doubles, ragged tail trimmed."""
+    import oracle as O
+    data = bytes([0, 0, 0, 0, 0, 0, 0xF0, 0x3F,          # 1.0
+                  0, 0, 0, 0, 0, 0, 0, 0xC0,             # -2.0
+                  0x18, 0x2D, 0x44, 0x54, 0xFB, 0x21, 0x09, 0x40,   # pi
+                  1, 2, 3])                              # 3 trailing bytes: dropped
+    got = O.bytes_to_float64(data)
+    assert got.tolist() == [1.0, -2.0, 3.141592653589793]
+    assert O.bytes_to_float64(b"") is None and O.bytes_to_float64(b"\x00" * 7) is None

@@ -12,7 +12,7 @@ timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 echo "trace done"
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/$c" -o run -- \
-      python3 "$R/bench.py" --no-cpu-baseline --dtw-len 0 --c5-pairs 0 --c6-gallery 0 --c7-seconds 0 --steps 5 --warmup 1 > "$OUT/$c.log" 2>&1 \
+      python3 "$R/bench.py" --no-cpu-baseline --dtw-len 0 --c5-pairs 0 --c6-gallery 0 --c7-seconds 0 --ingest-reps 0 --steps 5 --warmup 1 > "$OUT/$c.log" 2>&1 \
       || { echo "pmc $c failed"; exit 1; }
   echo "$c done"
 done
