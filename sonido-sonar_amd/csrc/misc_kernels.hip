@@ -327,8 +327,12 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
 // (2) one wave chains the chunk carries Y_c = e_c + R^chunk Y_{c-1} in order; (3) each chunk
 // re-runs the recurrence from its true start state and writes z.  Every sample goes through
 // the same sequential recurrence as Go from a start state that equals Go's to rounding (the
-// warm-up version it replaces ran 8,192 extra samples per 1,024-sample chunk).
-constexpr int kDcChunk = 1024;
+// warm-up version it replaces ran 8,192 extra samples per 1,024-sample chunk).  256-sample chunks:
+// 4x the lanes of 1,024 for the latency-bound passes, C5 726 -> ~760 pairs/s (tools/dc_ab.sh).
+#ifndef SONAR_DC_CHUNK
+#define SONAR_DC_CHUNK 256
+#endif
+constexpr int kDcChunk = SONAR_DC_CHUNK;
 
 template <bool WRITE>
 __device__ __forceinline__ double dc_run(const double* x, int64_t s, int64_t e, double R, double alpha, double y1,
