@@ -55,9 +55,13 @@ __global__ __launch_bounds__(256) void zcr_kernel(const void* pcm, int pcm_f64, 
   }
 }
 
+#ifndef SONAR_ENERGY_B
+#define SONAR_ENERGY_B 16
+#endif
 // one thread per energy frame, sequential sum in Go's order.  The frame's samples are read in
 // batches of 16 with the next batch in flight while this one accumulates (the dependent add
-// chain then no longer waits on every load: 0.39 -> see DESIGN Kernel 2).
+// chain then no longer waits on every load: 0.39 -> see DESIGN Kernel 2).  Fallback for windows whose
+// block span does not fit the LDS budget of energy_lds_kernel below.
 __global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H,
                                                      double alpha, void* out, int out_f64) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -65,7 +69,7 @@ __global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f6
   const int64_t s = t * H;
   double ss = 0.0;
   double prev = s > 0 ? pre_x(pcm, pcm_f64, s - 1) : 0.0;
-  constexpr int B = 16;
+  constexpr int B = SONAR_ENERGY_B;
   double cur[B], nxt[B];
 #pragma unroll
   for (int j = 0; j < B; j++) cur[j] = j < W ? pre_x(pcm, pcm_f64, s + j) : 0.0;
@@ -88,6 +92,53 @@ __global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f6
     ss = __dadd_rn(ss, __dmul_rn(y, y));
   }
   store_out(out, out_f64, t, sqrt(__ddiv_rn(ss, (double)W)));
+}
+
+// The same per-frame chains with the block's samples staged in LDS first: a block owns kEnFpb
+// consecutive frames, its 256 threads copy the span [t0*H - 1, (t0+kEnFpb-1)*H + W) with coalesced
+// loads (one padding slot per 256 samples keeps the lanes' hop-strided LDS reads off one bank),
+// then lane f runs frame t0+f's Go-order chain out of LDS.  Same operations in the same order as
+// energy_kernel (bit-identical); the chains no longer wait on a global round trip per batch.
+constexpr int kEnFpb = 16;
+__device__ __forceinline__ int en_slot(int i) { return i + (i >> 8); }
+
+__global__ __launch_bounds__(256) void energy_lds_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W,
+                                                         int H, double alpha, void* out, int out_f64) {
+  extern __shared__ double xs[];
+  const int64_t t0 = (int64_t)blockIdx.x * kEnFpb;
+  const int nf = (int)min((int64_t)kEnFpb, Fe - t0);
+  const int64_t base = t0 * H - 1;
+  const int span = (nf - 1) * H + W + 1;
+  for (int i = threadIdx.x; i < span; i += 256) {
+    const int64_t g = base + i;
+    xs[en_slot(i)] = (g >= 0 && g < n) ? pre_x(pcm, pcm_f64, g) : 0.0;
+  }
+  __syncthreads();
+  const int f = threadIdx.x;
+  if (f >= nf) return;
+  const int o = f * H;                         // xs index of x[s-1]; x[s-1] = 0 when s = 0 (g = -1)
+  double prev = xs[en_slot(o)];
+  double ss = 0.0;
+  constexpr int B = 16;
+  double cur[B];
+  int k = 0;
+  for (; k + B <= W; k += B) {
+#pragma unroll
+    for (int j = 0; j < B; j++) cur[j] = xs[en_slot(o + 1 + k + j)];
+#pragma unroll
+    for (int j = 0; j < B; j++) {
+      const double y = __dsub_rn(cur[j], __dmul_rn(alpha, prev));
+      prev = cur[j];
+      ss = __dadd_rn(ss, __dmul_rn(y, y));
+    }
+  }
+  for (; k < W; k++) {
+    const double c = xs[en_slot(o + 1 + k)];
+    const double y = __dsub_rn(c, __dmul_rn(alpha, prev));
+    prev = c;
+    ss = __dadd_rn(ss, __dmul_rn(y, y));
+  }
+  store_out(out, out_f64, t0 + f, sqrt(__ddiv_rn(ss, (double)W)));
 }
 
 // YIN per 1024-sample frame (hop 512 for extractHarmonicFeatures, 256 for the voice-quality
@@ -245,6 +296,13 @@ int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H,
 int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H, double alpha, void* out,
                   int out_f64, hipStream_t s) {
   if (Fe <= 0) return 0;
+  const int64_t span = (int64_t)(kEnFpb - 1) * H + W + 1;
+  const size_t lds = (size_t)(span + (span >> 8) + 1) * sizeof(double);
+  if (lds <= 48 * 1024) {
+    hipLaunchKernelGGL(energy_lds_kernel, dim3((unsigned)((Fe + kEnFpb - 1) / kEnFpb)), dim3(256), lds, s, pcm,
+                       pcm_f64, n, Fe, W, H, alpha, out, out_f64);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+  }
   hipLaunchKernelGGL(energy_kernel, dim3((unsigned)((Fe + 255) / 256)), dim3(256), 0, s, pcm, pcm_f64, n, Fe, W, H,
                      alpha, out, out_f64);
   return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -370,28 +428,26 @@ __global__ __launch_bounds__(256) void dc_local_kernel(const double* x, int64_t 
   ends[c] = dc_run<false>(x, s, min(n, s + kDcChunk), R, 0.0, 0.0, nullptr);
 }
 
-__device__ __forceinline__ double lane_bcast_d(double v, int j) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), j);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-// one wave: ystart[c] = Y_{c-1}, Y_c = ends[c] + RC Y_{c-1}, Y_{-1} = 0
+// one wave: ystart[c] = Y_{c-1}, Y_c = ends[c] + RC Y_{c-1}, Y_{-1} = 0.  Each 64-chunk block is
+// a 6-step Kogge-Stone scan of the affine maps Y -> B + A Y (lane c ends with the map of chunks
+// [i, c]), then one carry from the previous block: 162 blocks x 6 shuffle steps for a 60 s stream
+// instead of 10,336 dependent steps.  Rounding differs from the serial chain by a few ulp of the
+// carry, which the DC filter then decays by R per sample.
 __global__ __launch_bounds__(64) void dc_carry_kernel(const double* ends, int64_t T, double RC, double* ystart) {
   const int lane = threadIdx.x;
-  double Y = 0.0;
+  double Yin = 0.0;
   for (int64_t i = 0; i < T; i += 64) {
-    const double cur = i + lane < T ? ends[i + lane] : 0.0;
-    const int m = T - i < 64 ? (int)(T - i) : 64;
-    double mine = 0.0;
-    if (m == 64) {
+    double B = i + lane < T ? ends[i + lane] : 0.0;
+    double A = RC;
 #pragma unroll
-      for (int j = 0; j < 64; j++) { if (lane == j) mine = Y; Y = __dadd_rn(lane_bcast_d(cur, j), __dmul_rn(RC, Y)); }
-    } else {
-      for (int j = 0; j < m; j++) { if (lane == j) mine = Y; Y = __dadd_rn(lane_bcast_d(cur, j), __dmul_rn(RC, Y)); }
+    for (int d = 1; d < 64; d <<= 1) {
+      const double Bp = __shfl_up(B, d, 64), Ap = __shfl_up(A, d, 64);
+      if (lane >= d) { B = __dadd_rn(B, __dmul_rn(A, Bp)); A = __dmul_rn(A, Ap); }
     }
-    if (lane < m) ystart[i + lane] = mine;
+    const double Y = __dadd_rn(B, __dmul_rn(A, Yin));    // Y_{i+lane}
+    const double prev = __shfl_up(Y, 1, 64);
+    if (i + lane < T) ystart[i + lane] = lane == 0 ? Yin : prev;
+    Yin = __shfl(Y, 63, 64);
   }
 }
 
