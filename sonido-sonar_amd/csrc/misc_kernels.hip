@@ -392,18 +392,18 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
 #endif
 constexpr int kDcChunk = SONAR_DC_CHUNK;
 
-template <bool WRITE>
-__device__ __forceinline__ double dc_run(const double* x, int64_t s, int64_t e, double R, double alpha, double y1,
+template <bool WRITE, typename LD>
+__device__ __forceinline__ double dc_run(LD x, int64_t s, int64_t e, double R, double alpha, double y1,
                                          double* z) {
-  double x1 = s > 0 ? x[s - 1] : 0.0;
+  double x1 = s > 0 ? x(s - 1) : 0.0;
   constexpr int B = 16;
   double cur[B], nxt[B];
 #pragma unroll
-  for (int j = 0; j < B; j++) cur[j] = s + j < e ? x[s + j] : 0.0;
+  for (int j = 0; j < B; j++) cur[j] = s + j < e ? x(s + j) : 0.0;
   int64_t i = s;
   for (; i + B <= e; i += B) {
 #pragma unroll
-    for (int j = 0; j < B; j++) nxt[j] = i + B + j < e ? x[i + B + j] : 0.0;
+    for (int j = 0; j < B; j++) nxt[j] = i + B + j < e ? x(i + B + j) : 0.0;
 #pragma unroll
     for (int j = 0; j < B; j++) {
       const double yv = __dadd_rn(__dsub_rn(cur[j], x1), __dmul_rn(R, y1));
@@ -421,11 +421,33 @@ __device__ __forceinline__ double dc_run(const double* x, int64_t s, int64_t e, 
   return y1;
 }
 
-__global__ __launch_bounds__(256) void dc_local_kernel(const double* x, int64_t n, double R, double* ends) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Passes (1) and (3) on LDS-staged input: a block owns kDcCpb consecutive chunks, its 256 threads
+// copy x[c0*chunk - 1, (c0+kDcCpb)*chunk) with coalesced loads (one padding slot per 256 samples:
+// the lanes' chunk-strided reads land on distinct banks), then lane c runs chunk c0+c's
+// recurrence out of LDS -- the same operations as from global memory, without a global round
+// trip per 16-sample batch.
+constexpr int kDcCpb = 16;
+constexpr int kDcSpan = kDcCpb * kDcChunk + 1;
+__device__ __forceinline__ int dc_slot(int i) { return i + (i >> 8); }
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void dc_pass_kernel(const double* x, int64_t n, double R, double alpha,
+                                                      const double* ystart, double* ends, double* z) {
+  __shared__ double xs[kDcSpan + (kDcSpan >> 8) + 1];
+  const int64_t c0 = (int64_t)blockIdx.x * kDcCpb;
+  const int64_t base = c0 * kDcChunk - 1;
+  const int span = (int)(min(n, (c0 + kDcCpb) * kDcChunk) - base);
+  for (int i = threadIdx.x; i < span; i += 256) {
+    const int64_t g = base + i;
+    xs[dc_slot(i)] = g >= 0 ? x[g] : 0.0;
+  }
+  __syncthreads();
+  const int64_t c = c0 + threadIdx.x;
   const int64_t s = c * kDcChunk;
-  if (s >= n) return;
-  ends[c] = dc_run<false>(x, s, min(n, s + kDcChunk), R, 0.0, 0.0, nullptr);
+  if ((int)threadIdx.x >= kDcCpb || s >= n) return;
+  auto ld = [&](int64_t g) { return xs[dc_slot((int)(g - base))]; };
+  if (WRITE) dc_run<true>(ld, s, min(n, s + kDcChunk), R, alpha, ystart[c], z);
+  else ends[c] = dc_run<false>(ld, s, min(n, s + kDcChunk), R, 0.0, 0.0, nullptr);
 }
 
 // one wave: ystart[c] = Y_{c-1}, Y_c = ends[c] + RC Y_{c-1}, Y_{-1} = 0.  Each 64-chunk block is
@@ -451,13 +473,6 @@ __global__ __launch_bounds__(64) void dc_carry_kernel(const double* ends, int64_
   }
 }
 
-__global__ __launch_bounds__(256) void dc_apply_kernel(const double* x, int64_t n, double R, double alpha,
-                                                       const double* ystart, double* z) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t s = c * kDcChunk;
-  if (s >= n) return;
-  dc_run<true>(x, s, min(n, s + kDcChunk), R, alpha, ystart[c], z);
-}
 
 size_t dc_preemph_scratch_bytes(int64_t n) { return (size_t)(2 * ((n + kDcChunk - 1) / kDcChunk) + 2) * 8; }
 
@@ -468,10 +483,10 @@ int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double
   double* ystart = scratch + T;
   double RC = 1.0;
   for (int k = 0; k < kDcChunk; k++) RC *= R;                 // R^chunk (carry weight of a full chunk)
-  const unsigned g = (unsigned)((T + 255) / 256);
-  hipLaunchKernelGGL(dc_local_kernel, dim3(g), dim3(256), 0, s, x, n, R, ends);
+  const unsigned g = (unsigned)((T + kDcCpb - 1) / kDcCpb);
+  hipLaunchKernelGGL(dc_pass_kernel<false>, dim3(g), dim3(256), 0, s, x, n, R, 0.0, nullptr, ends, nullptr);
   hipLaunchKernelGGL(dc_carry_kernel, dim3(1), dim3(64), 0, s, ends, T, RC, ystart);
-  hipLaunchKernelGGL(dc_apply_kernel, dim3(g), dim3(256), 0, s, x, n, R, alpha, ystart, y);
+  hipLaunchKernelGGL(dc_pass_kernel<true>, dim3(g), dim3(256), 0, s, x, n, R, alpha, ystart, nullptr, y);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
