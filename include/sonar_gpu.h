@@ -183,8 +183,9 @@ int sonar_fingerprint(sonar_ctx* ctx, const void* pcm, int64_t n, const sonar_fp
 #define SONAR_INGEST_HOST_CONVERT 1
 int sonar_ingest_f64le(sonar_ctx* ctx, const void* bytes, int64_t nbytes, int32_t out_dtype, int32_t mode,
                        int32_t host_threads, void* d_out, int64_t* n_samples);
-/* Decoder output straight into path A: sonar_ingest_f64le (f32, `mode`) into a ctx-owned device
- * buffer, then sonar_fingerprint on it with cfg->pcm_dtype = F32; outputs are host buffers
+/* Decoder output straight into path A: sonar_ingest_f64le (in cfg->pcm_dtype, `mode`) into a
+ * ctx-owned device buffer, then sonar_fingerprint on it; pcm_dtype F64 (the default) keeps Go's
+ * []float64 samples end to end, F32 rounds them to nearest even; outputs are host buffers
  * (cfg->device_ptrs must be 0).  Replaces bytesToFloat64 + ComputeSTFTWithWindow's upload of
  * AudioData.PCM (decoder.go:850-871 -> analyzers/spectral.go:385) with one call. */
 int sonar_fingerprint_f64le(sonar_ctx* ctx, const void* bytes, int64_t nbytes, int32_t mode,

@@ -61,6 +61,8 @@ def lib():
         L.or_chroma_frames.argtypes = [_d, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, _d]
         L.or_ncc.argtypes = [_d, C.c_int64, _d, C.c_int64, C.c_int, _d, _d]
         L.or_dtw.argtypes = [_d, C.c_int64, _d, C.c_int64, C.c_int, C.c_int, _d, _i32, _i32, _d, _i64, _d]
+        L.or_dtw_stripes.argtypes = [_d, C.c_int64, _d, C.c_int64, C.c_int, C.c_int, C.c_int, _i32, _i32, _d, _i64,
+                                     _d]
         L.or_align_dtw_metrics.argtypes = [_i32, _i32, _d, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_int, _d]
         L.or_align_xcorr_metrics.argtypes = [_d, C.c_int, C.c_int, C.c_int, _d]
         L.or_autocorr_fft.argtypes = [_d, C.c_int, C.c_int, _d]
@@ -263,6 +265,33 @@ def dtw(q, r, band=-1, want_cost=False):
         raise MemoryError("oracle dtw failed")
     P = plen.value
     return {"distance": dist.value, "path_q": pq[:P], "path_r": pr[:P], "path_cost": pc[:P], "cost": cost}
+
+
+def dtw_full(q, r, band=-1, nthreads=8):
+    """dtw() at any size (dtw_oracle.c): the same values, without the (N+1)(M+1) matrix; the
+    fill runs as a stripe wavefront over `nthreads` threads."""
+    q = _f64(q)
+    r = _f64(r)
+    if q.ndim == 1:
+        q = q[:, None]
+    if r.ndim == 1:
+        r = r[:, None]
+    nq, d = q.shape
+    nr = r.shape[0]
+    if nq == 0 or nr == 0:
+        raise ValueError("empty sequences provided")
+    cap = nq + nr + 1
+    pq = np.zeros(cap, np.int32)
+    pr = np.zeros(cap, np.int32)
+    pc = np.zeros(cap)
+    plen = C.c_int64()
+    dist = C.c_double()
+    rc = lib().or_dtw_stripes(_p(q), nq, _p(r), nr, d, band, nthreads, pq.ctypes.data_as(_i32),
+                              pr.ctypes.data_as(_i32), _p(pc), C.byref(plen), C.byref(dist))
+    if rc != 0:
+        raise MemoryError("oracle dtw_full failed")
+    P = plen.value
+    return {"distance": dist.value, "path_q": pq[:P], "path_r": pr[:P], "path_cost": pc[:P]}
 
 
 def align_dtw_metrics(res, nq, nr, sample_rate):

@@ -463,7 +463,7 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
       const int k0 = g * CH, k1 = min(K, k0 + CH);
       const T fscale = (T)((double)p.sample_rate / (double)((K - 1) * 2));   // freqBins[i] = i sr / (2(K-1))
       const T inv_ln10 = (T)0.43429448190325182765;
-      T s_m = 0, s_fm = 0, s_m2 = 0, mx = 0, s_ln = 0, s_lo = 0, s_fx = 0;
+      T s_m = 0, s_fm = 0, s_m2 = 0, mx = 0, s_ln = 0, s_lo = 0, s_hi = 0, s_fx = 0;
       double sx = 0, sy = 0, sxy = 0, sxx = 0;    // regression sums: f32 would cancel catastrophically
       int n_ln = 0, n_sl = 0;
       if (act) {
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
           const T fk = (T)k * fscale;
           s_m += m; s_fm += fk * m; s_m2 += m * m;
           if (m > mx) mx = m;
-          if (k < K / 4) s_lo += m * m;
+          if (k < K / 4) s_lo += m * m; else s_hi += m * m;       // speech.go:438-458: two sums
           if (m > (T)1e-10) {
             const T lm = dev_log(m);
             s_ln += lm; n_ln++;
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
       auto redi = [&](int v) { for (int o = NG / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64); return v; };
       auto redmax = [&](T v) { for (int o = NG / 2; o > 0; o >>= 1) { const T u = __shfl_xor(v, o, 64); v = u > v ? u : v; } return v; };
       const T S_m = red(s_m), S_fm = red(s_fm), S_m2 = red(s_m2), MX = redmax(mx), S_ln = red(s_ln);
-      const T S_lo = red(s_lo), S_fx = red(s_fx);
+      const T S_lo = red(s_lo), S_hi = red(s_hi), S_fx = red(s_fx);
       const double SX = redd(sx), SY = redd(sy), SXY = redd(sxy), SXX = redd(sxx);
       const int N_ln = redi(n_ln), N_sl = redi(n_sl);
       const T cen = (S_m == (T)0) ? (T)0 : S_fm / S_m;                       // spectral_centroid.go:18-41
@@ -502,15 +502,48 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
         for (int j = 0; j < CH; ++j) { const int k = k0 + j; if (k >= k1) break; const T d = (T)k * fscale - cen; s_bw += d * d * row[k]; }
       }
       const T S_bw = red(s_bw);
-      // rolloff (spectral_rolloff.go:18-52): first k with cumulative m^2 >= 0.85 total
-      const T target = (T)0.85 * S_m2;
-      T incl = s_m2;                                                         // inclusive scan over the frame's lanes
-      for (int o = 1; o < NG; o <<= 1) { const T u = __shfl_up(incl, o, NG); if (g >= o) incl += u; }
-      T cum = incl - s_m2;
+      // rolloff (spectral_rolloff.go:29-49): the first k whose cumulative m^2 reaches 0.85 of the
+      // total, both sums sequential in Go.  Fast path: per-lane double partials + a lane scan
+      // locate the bin and its two margins; the parallel sums differ from Go's sequential ones by
+      // at most K u total each, so a bin whose margins both exceed 8 K u total is Go's bin.  Any
+      // other frame re-runs Go's two chains (unfused, ascending k) on its g == 0 lane.  m^2 is
+      // formed in double: exact for f32 magnitudes, Go's rounding for f64 ones.
       int ridx = 1 << 30;
-      if (act && S_m2 != (T)0)
-        for (int k = k0; k < k1; ++k) { cum += row[k] * row[k]; if (cum >= target) { ridx = k; break; } }
-      for (int o = NG / 2; o > 0; o >>= 1) { const int u = __shfl_xor(ridx, o, 64); ridx = u < ridx ? u : ridx; }
+      bool roll_zero = true;
+      {
+#pragma clang fp contract(off)
+        double d_m2 = 0;
+        if (act)
+          for (int k = k0; k < k1; ++k) { const double m = (double)row[k]; d_m2 += m * m; }
+        double incl = d_m2;                                                  // inclusive scan over the frame's lanes
+        for (int o = 1; o < NG; o <<= 1) { const double u = __shfl_up(incl, o, NG); if (g >= o) incl += u; }
+        const double tot = __shfl(incl, (lane / NG) * NG + NG - 1, 64);
+        const double target = 0.85 * tot;
+        const double delta = 8.0 * (double)K * 1.1102230246251565e-16 * tot;
+        double cum = incl - d_m2, margin = 0;
+        if (act && tot != 0.0)
+          for (int k = k0; k < k1; ++k) {
+            const double m = (double)row[k], prev_cum = cum;
+            cum += m * m;
+            if (cum >= target) { ridx = k; margin = fmin(cum - target, target - prev_cum); break; }
+          }
+        bool owner = ridx < (1 << 30);
+        for (int o = NG / 2; o > 0; o >>= 1) { const int u = __shfl_xor(ridx, o, 64); ridx = u < ridx ? u : ridx; }
+        owner = owner && ridx >= k0 && ridx < k1;
+        int unsure = (owner && !(margin > delta)) ? 1 : 0;
+        for (int o = NG / 2; o > 0; o >>= 1) unsure |= __shfl_xor(unsure, o, 64);
+        if (act && tot != 0.0 && ridx >= K) unsure = 1;                     // rounding kept cum below target
+        roll_zero = (tot == 0.0);
+        if (act && g == 0 && unsure) {                                       // Go's chains, verbatim order
+          double gt = 0;
+          for (int k = 0; k < K; ++k) { const double m = (double)row[k]; gt += m * m; }
+          roll_zero = (gt == 0.0);
+          const double gtarget = 0.85 * gt;
+          double gc = 0;
+          ridx = K;
+          for (int k = 0; k < K; ++k) { const double m = (double)row[k]; gc += m * m; if (gc >= gtarget) { ridx = k; break; } }
+        }
+      }
       if (act && g == 0) {
         const T fl_geo = N_ln > 0 ? exp(S_ln / (T)N_ln) : (T)0;              // spectral_flatness.go:31-73
         const T am = S_m / (T)K;
@@ -520,9 +553,9 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
         T slope = 0;                                                         // spectral_slope.go:23-63
         if (N_sl >= 2) { const double dn = (double)N_sl * SXX - SX * SX; if (dn != 0.0) slope = (T)(((double)N_sl * SXY - SX * SY) / dn); }
         T roll = 0;
-        if (S_m2 != (T)0) roll = (T)(ridx < K ? ridx : K - 1) * fscale;
+        if (!roll_zero) roll = (T)((double)(ridx < K ? ridx : K - 1) * (double)p.sample_rate / (double)((K - 1) * 2));
         const T vals[9] = {cen, roll, (S_m == (T)0) ? (T)0 : sqrt(S_bw / S_m), flat, rms == (T)0 ? (T)0 : MX / rms,
-                           slope, sqrt(S_fx), S_m2 > (T)0 ? S_lo / S_m2 : (T)0, S_m2 > (T)0 ? (S_m2 - S_lo) / S_m2 : (T)0};
+                           slope, sqrt(S_fx), S_m2 > (T)0 ? S_lo / S_m2 : (T)0, S_m2 > (T)0 ? S_hi / S_m2 : (T)0};
 #pragma unroll
         for (int d = 0; d < 9; d++) {
           if (!p.out_spec[d]) continue;

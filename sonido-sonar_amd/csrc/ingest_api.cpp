@@ -144,11 +144,22 @@ int sonar_ingest_f64le(sonar_ctx* c, const void* bytes, int64_t nbytes, int32_t 
 
   IngestState* st = c->ingest;
   if (!st) {
-    st = c->ingest = new IngestState();
-    for (int i = 0; i < kSlots; i++) {
-      HIP_TRY(c, hipHostMalloc(&st->slot[i], kSlotBytes, hipHostMallocDefault));
-      HIP_TRY(c, hipEventCreateWithFlags(&st->ev[i], hipEventDisableTiming));
+    // build the whole state before publishing it: a failure part-way leaves c->ingest null
+    IngestState* fresh = new IngestState();
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < kSlots && e == hipSuccess; i++) {
+      e = hipHostMalloc(&fresh->slot[i], kSlotBytes, hipHostMallocDefault);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&fresh->ev[i], hipEventDisableTiming);
     }
+    if (e != hipSuccess) {
+      for (int i = 0; i < kSlots; i++) {
+        if (fresh->slot[i]) (void)hipHostFree(fresh->slot[i]);
+        if (fresh->ev[i]) (void)hipEventDestroy(fresh->ev[i]);
+      }
+      delete fresh;
+      return fail(c, SONAR_ERR_DEVICE, hipGetErrorString(e));
+    }
+    st = c->ingest = fresh;
   }
   const int T = host_threads > 0 ? std::min(host_threads, 64) : default_threads();
   if (!st->pool || st->pool->size() != T) {
@@ -210,18 +221,23 @@ int sonar_fingerprint_f64le(sonar_ctx* c, const void* bytes, int64_t nbytes, int
                            const sonar_fp_cfg* cfg, sonar_fp_out* out) {
   if (!c || !cfg || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
   if (cfg->device_ptrs) return fail(c, SONAR_ERR_INVALID, "sonar_fingerprint_f64le takes host output buffers");
+  // the samples reach the device in the caller's pcm_dtype: F64 keeps Go's []float64 end to end,
+  // F32 rounds each sample to nearest even (float32(x)) on the host threads or on the device
+  const int32_t pdt = cfg->pcm_dtype == SONAR_F64 ? SONAR_F64 : SONAR_F32;
+  if (cfg->pcm_dtype != SONAR_F32 && cfg->pcm_dtype != SONAR_F64) return fail(c, SONAR_ERR_INVALID, "pcm_dtype");
+  const size_t esz = pdt == SONAR_F64 ? 8 : 4;
   int64_t n = 0;
-  int rc = sonar_ingest_f64le(c, bytes, nbytes, SONAR_F32, mode, 0, nullptr, &n);
+  int rc = sonar_ingest_f64le(c, bytes, nbytes, pdt, mode, 0, nullptr, &n);
   if (rc != SONAR_OK) return rc;
   // same validation order as ComputeSTFTWithWindow before any device work (spectral.go:386-412)
   if (cfg->window_size <= 0 || cfg->hop_size <= 0 || (n - cfg->window_size) / cfg->hop_size + 1 <= 0)
     return sonar::detail::fingerprint_impl(c, bytes, n, cfg, out, false);
-  void* d = dbuf(c, "ingest.pcm", (size_t)n * 4);
+  void* d = dbuf(c, "ingest.pcm", (size_t)n * esz);
   if (!d) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (ingest pcm)");
-  rc = sonar_ingest_f64le(c, bytes, nbytes, SONAR_F32, mode, 0, d, &n);
+  rc = sonar_ingest_f64le(c, bytes, nbytes, pdt, mode, 0, d, &n);
   if (rc != SONAR_OK) return rc;
   sonar_fp_cfg f = *cfg;
-  f.pcm_dtype = SONAR_F32;
+  f.pcm_dtype = pdt;
   return sonar::detail::fingerprint_impl(c, d, n, &f, out, true);
 }
 

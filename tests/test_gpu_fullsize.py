@@ -1,0 +1,98 @@
+"""The BASELINE configs at their own sizes against the oracle (BASELINE.json configs[1..3]).
+
+* C2: the headline 1 h STFT(1024/256) -> mel(40) -> MFCC(13), float32 kernel, every one of the
+  620,153 frames against the float64 oracle.
+* C3: two 5-min 44.1 kHz streams with the injected 12.34 s lag: the music extractor's energy and
+  chroma of both (DC removal over 13.2 M samples: 51,679 chunk carries through the scanned
+  carry kernel), the NCC over 2 x 10,335 + 1 lags (maxOffsetSeconds = 60) bit-exact against
+  or_ncc, and a 20,000 x 20,000 slice of the chroma DTW bit-exact against the striped oracle
+  (dtw_oracle.c: the same cells as or_dtw without the 21.4 GB matrix).  The 51,676^2 DTW itself
+  is checked in bench.py's parity block.
+* C4: the speech extractor (SampleRate 16000, W 512 / H 128) on the full 30 min, float64.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import sonar
+from parity import assert_mfcc, assert_rel, assert_rolloff
+from sonar import synth
+
+pytestmark = pytest.mark.gpu
+
+SR = 44100
+
+
+def test_c2_full_hour_mfcc(ctx):
+    x = synth.c2_hour()                                                     # 158.76 M f32 samples
+    cfg = ctx.config(window_size=1024, hop_size=256, sample_rate=SR, n_filters=40, n_mfcc=13,
+                     precision=sonar.F32, pcm_dtype=sonar.F32, out_dtype=sonar.F32, flags=sonar.FP_MFCC)
+    got = ctx.fingerprint(x, cfg)["mfcc"]
+    assert ctx.last_fp_kernel() == "mfcc_pair_kernel"
+    assert got.shape == (620153, 13)
+    ref = O.mfcc_frames(O.stft_mag(x.astype(np.float64), 1024, 256, nthreads=16), SR, n_coef=13, n_mels=40)
+    assert_mfcc(got, ref, 1e-4)
+
+
+@pytest.fixture(scope="module")
+def c3(ctx):
+    q, r = synth.c3_pair(300.0, 12.34)
+    eq, cq = ctx.music_alignment_features(q, SR)
+    er, cr = ctx.music_alignment_features(r, SR)
+    return q, r, eq, cq, er, cr
+
+
+def test_c3_music_features_full_size(c3):
+    q, r, eq, cq, er, cr = c3
+    for x, e, c in ((q, eq, cq), (r, er, cr)):
+        y = O.preemphasis(O.dc_removal(x, 0.995), 0.95)
+        # the DC carries come from a scan of affine maps: a few ulp from Go's serial chain
+        assert_rel(e, O.short_time_energy(y, 1024, 256), 1e-12, 1e-300, "energy")
+        F = O.stft_frames(len(x), 1024, 256)
+        assert F == 51676
+        ref_c = O.chroma_music(x, F, 256, SR)
+        assert_rel(c, ref_c, 1e-9, 1e-9, "chroma")
+
+
+def test_c3_ncc_max_offset_60s(ctx, c3):
+    _, _, eq, _, er, _ = c3
+    L = min(int(60.0 * SR) // 256, min(len(eq), len(er)) - 1)
+    assert L == 10335
+    corr, met = ctx.ncc(eq, er, L)
+    ref, rmet = O.ncc(eq, er, L)
+    assert np.array_equal(corr, ref)
+    assert met["peak_lag"] == rmet["peak_lag"] and met["peak_correlation"] == rmet["peak_correlation"]
+    # query = base delayed: the injected 12.34 s = 2,125.76 frames
+    assert abs(abs(met["peak_lag"]) - 12.34 * SR / 256) <= 1.0
+
+
+def test_c3_dtw_20000_slice_bit_exact(ctx, c3):
+    _, _, _, cq, _, cr = c3
+    n = 20000
+    got = ctx.dtw(cq[:n], cr[:n])
+    ref = O.dtw_full(cq[:n], cr[:n], nthreads=16)
+    assert np.array_equal(got["path_q"], ref["path_q"]) and np.array_equal(got["path_r"], ref["path_r"])
+    assert np.array_equal(got["path_cost"], ref["path_cost"])
+    assert got["distance"] == ref["distance"]
+
+
+def test_c4_full_30min_speech(ctx):
+    x = synth.c4_speech(seconds=1800.0, sr=16000)
+    fc = dict(sample_rate=16000, window_size=512, hop_size=128, stft_window_size=512, stft_hop_size=128,
+              enable_mfcc=1, enable_speech_features=1, enable_temporal_features=1, mfcc_coefficients=13)
+    got = ctx.extract_speech_features(x, 16000, ctx.feature_config(is_news=0, precision=sonar.F64, **fc))
+    ref = O.speech_features_reference(x, 16000, fc)
+    for k in ("pitch_estimate", "pitch_confidence", "voicing_strength", "zero_crossing_rate", "short_time_energy"):
+        assert np.array_equal(got[k], ref[k]), k
+    assert len(got["pitch_estimate"]) == 56249
+    mag = O.stft_mag(x, 512, 128, nthreads=16)
+    assert mag.shape[0] == 224997
+    for k, v in ref.items():
+        if k == "spectral_rolloff":
+            assert_rolloff(got[k], v, mag, 1e-12)
+        elif k == "mfcc":
+            assert_mfcc(got[k], v, 1e-9)
+        else:
+            b = np.asarray(v, float)
+            peak = np.max(np.abs(np.nan_to_num(b))) if b.size else 0.0
+            assert_rel(got[k], v, 1e-6, max(peak * 1e-6, 1e-30), k)

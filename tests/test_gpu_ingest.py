@@ -107,6 +107,24 @@ def test_fingerprint_f64le_matches_host_entry(ctx, mode):
         assert np.array_equal(got[k], want[k], equal_nan=True), k
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_fingerprint_f64le_default_cfg_keeps_f64(ctx, mode):
+    """The default cfg (pcm_dtype F64, precision F64) stays float64 end to end: the result equals
+    sonar_fingerprint on the float64 samples, not on float32-rounded ones (Go's []float64)."""
+    n = 44100 * 3 + 5
+    x = np.sin(np.arange(n) * 0.0031) * 0.4 + 0.05 * np.random.default_rng(12).standard_normal(n)
+    cfg = ctx.config(window_size=1024, hop_size=256, sample_rate=44100,
+                     flags=sonar.FP_MFCC | sonar.FP_SPECTRAL | sonar.FP_ZCR | sonar.FP_ENERGY,
+                     energy_window=1024, energy_hop=256)
+    want = ctx.fingerprint(x, cfg)
+    got = ctx.fingerprint_f64le(x.astype("<f8").tobytes(), cfg, mode)
+    assert set(got) == set(want)
+    for k in want:
+        assert np.array_equal(got[k], want[k], equal_nan=True), k
+    rounded = ctx.fingerprint(x.astype(np.float32).astype(np.float64), cfg)
+    assert not np.array_equal(got["energy"], rounded["energy"])
+
+
 def test_fingerprint_f64le_errors(ctx):
     cfg = ctx.config(window_size=1024, hop_size=256, sample_rate=44100, precision=sonar.F32,
                      pcm_dtype=sonar.F32, out_dtype=sonar.F32)
