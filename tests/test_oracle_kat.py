@@ -134,23 +134,6 @@ def test_voice_quality_kat():
     assert st == 0 and v["jitter"] > 0 and v["shimmer"] > 0 and abs(v["mean_f0"] - 140) < 5
 
 
-def test_voice_quality_kat():
-    """AnalyzeVoiceQuality (voice_quality.go:56-111): a steady 200 Hz harmonic tone gives
-    periods of int(16000 / f0) samples, zero jitter and F0 near 200 Hz; errors for < 1 s
-    (:57) and for noise without pitch periods (:67)."""
-    sr = 16000
-    t = np.arange(2 * sr) / sr
-    x = np.sin(2 * np.pi * 200 * t) + 0.3 * np.sin(2 * np.pi * 400 * t)
-    vq, st = O.voice_quality(x, sr)
-    assert st == 0 and vq["num_periods"] > 100
-    assert abs(vq["mean_f0"] - 200) < 1 and vq["jitter"] == 0.0 and vq["f0_stability"] > 0.99
-    assert vq["hnr"] > 20 and 0.9 < vq["overall_quality"] <= 1.0
-    assert O.voice_quality(x[: sr - 1], sr)[1] == -1
-    assert O.voice_quality(np.random.default_rng(0).standard_normal(2 * sr), sr)[1] == -2
-    v, st = O.voice_quality(O.preemphasis(synth.voiced(), 0.97), sr)
-    assert st == 0 and v["jitter"] > 0 and v["shimmer"] > 0 and abs(v["mean_f0"] - 140) < 5
-
-
 def test_alignment_consistency_and_truncate_kat():
     """AnalyzeAlignmentConsistency (stats/alignment.go:709-800): the perturbation is deterministic,
     so all trials agree (std 0, range 0, consistency 1) and a 9-frame shift is found by NCC (x hop)
