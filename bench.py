@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process (0 = leave as is)")
     ap.add_argument("--cpu-seconds", type=float, default=0.0, help="force CPU-baseline sample length")
+    ap.add_argument("--reps", type=int, default=3, help="repetitions of the C3 / C4 / C5 legs (median reported)")
+    ap.add_argument("--no-f64", action="store_true", help="skip the float64 headline variant")
     return ap.parse_args()
 
 
@@ -116,50 +118,206 @@ def make_shard(seconds, world, rank, device):
 
 def load_traffic(kernel_name):
     """Per-launch HBM bytes of `kernel_name` from the newest committed rocprofv3 PMC summary
-    (profiles/<round>_traffic.json, FETCH_SIZE x2 + WRITE_SIZE; tools/traffic_summary.py)."""
+    (profiles/<round>_traffic.json, FETCH_SIZE x2 + WRITE_SIZE; tools/traffic_summary.py).  PMC
+    counters need their own rocprofv3 passes, so they cannot be collected inside this run."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
         with open(path) as f:
             d = json.load(f)
         if kernel_name and kernel_name in d.get("kernel", ""):
-            return d.get("hbm_bytes_per_launch")
-    return None
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return None, None
 
 
-def cpu_baseline(seconds_hint):
+def bench_headline_f64(args, ctx, pcm, F, dev):
+    """The headline configuration at the reference's precision: float64 PCM in, every stage in
+    float64 (fp_wave_kernel<double>), float64 MFCC out -- what the Go path computes.  HIP events
+    around 5 launches after 2 warm-ups; the PCM is converted to float64 on the device before."""
+    pcm64 = pcm.double()
+    n = pcm64.numel()
+    out64 = torch.empty((F, N_MFCC), dtype=torch.float64, device=dev)
+    cfg = ctx.config(window_size=W, hop_size=H, sample_rate=SR, n_filters=N_MELS, n_mfcc=N_MFCC,
+                     precision=sonar.F64, pcm_dtype=sonar.F64, out_dtype=sonar.F64, flags=sonar.FP_MFCC)
+    for _ in range(2):
+        ctx.fingerprint_device(pcm64.data_ptr(), n, cfg, mfcc=out64.data_ptr())
+    torch.cuda.synchronize()
+    ctx.last_kernel_ms()
+    ctx.enable_kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ctx.fingerprint_device(pcm64.data_ptr(), n, cfg, mfcc=out64.data_ptr())
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / 5
+    ctx.enable_kernel_timing(False)
+    kms = ctx.last_kernel_ms()
+    res = {"frames_per_s": F / dt, "ms_per_step": dt * 1e3, "kernel": ctx.last_fp_kernel(), "kernel_ms": kms,
+           "dtype": "f64", "pcm_dtype": "f64",
+           "fp64_tflops": F * FLOPS_PER_FRAME / (kms * 1e-3) / 1e12,
+           "fp64_frac": F * FLOPS_PER_FRAME / (kms * 1e-3) / 1e12 / FP64_PEAK_TFS,
+           "hbm_gbs": F * (8 * H + 8 * N_MFCC) / (kms * 1e-3) / 1e9}
+    host = out64.cpu().numpy()
+    del pcm64, out64
+    return res, host
+
+
+def host_info():
+    """The CPU the baselines ran on (BASELINE.md protocol: nproc, model, SMT state, pinning)."""
+    info = {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0))}
+    try:
+        with open("/proc/cpuinfo") as f:
+            info["cpu_model"] = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        info["cpu_model"] = None
+    try:
+        with open("/sys/devices/system/cpu/smt/active") as f:
+            info["smt_active"] = f.read().strip() == "1"
+    except OSError:
+        info["smt_active"] = None
+    return info
+
+
+def cpu_threads():
+    """Host threads for the CPU baselines: the job's share of the box (OMP_NUM_THREADS, 16 on the
+    GPU box; the box's nproc shows the whole machine), capped by the CPUs this process may use."""
+    share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(share, len(os.sched_getaffinity(0))))
+
+
+class pinned:
+    """Pin this process (and the oracle's pthreads, which inherit it) to the first n allowed CPUs."""
+    def __init__(self, n):
+        self.old = os.sched_getaffinity(0)
+        self.cpus = sorted(self.old)[:n]
+
+    def __enter__(self):
+        os.sched_setaffinity(0, self.cpus)
+        return self.cpus
+
+    def __exit__(self, *a):
+        os.sched_setaffinity(0, self.old)
+
+
+def timed_runs(fn, reps=5, warmup=1):
+    """BASELINE.md protocol: warm-up, then the median (and spread) of `reps` timed runs."""
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), float(min(ts)), float(max(ts))
+
+
+def oracle_module():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    threads = os.cpu_count() or 1
-    threads = min(threads, 16)      # the GPU box shares its CPUs: 16 is this job's share
-    probe = 60.0
-    x = shard.stream_pcm(0, int(probe * SR)).double().numpy()
-    t0 = time.perf_counter()
-    m = O.stft_mag(x, W, H, nthreads=threads)
-    O.mfcc_frames(m, SR, n_coef=N_MFCC, n_mels=N_MELS)
-    dt = time.perf_counter() - t0
-    secs = seconds_hint or min(3600.0, max(probe, probe * 15.0 / max(dt, 1e-6)))   # ~15 s of CPU work
-    x = shard.stream_pcm(0, int(secs * SR)).double().numpy()
-    t0 = time.perf_counter()
-    m = O.stft_mag(x, W, H, nthreads=threads)
-    O.mfcc_frames(m, SR, n_coef=N_MFCC, n_mels=N_MELS)
-    dt = time.perf_counter() - t0
-    return {"value": len(m) / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{secs:.0f} s of the bench stream ({len(m)} frames), float64: STFT over {threads} threads "
-                      "(Go worker-pool shape), MFCC.ComputeFrames single-threaded, as in the Go path"}
+    return O
 
 
-def bench_dtw(ctx, n, steps):
+def mfcc_parity(got, ref, tol=1e-4):
+    """Full-size parity of an MFCC output against the oracle (tests/parity.py's measures): the max
+    error relative to the row L2 norm (the pass criterion), and per coefficient the max relative
+    error over coefficients with |ref| above 1e-3 / 1e-2 / 1e-1 of the row norm, with the number
+    of frames where such a coefficient is off by more than `tol` of itself (small coefficients
+    carry the row's absolute rounding, so their own relative error grows as 1 / |c|)."""
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    norms = np.linalg.norm(ref, axis=1)[:, None]
+    norms = np.where(norms == 0, 1.0, norms)
+    e_row = np.abs(got - ref) / norms
+    out = {"frames": int(len(ref)), "max_rel_err_row_norm": float(e_row.max()), "tolerance": tol,
+           "frames_over_tol_row_norm": int(np.count_nonzero(e_row.max(axis=1) > tol)), "per_coef": {}}
+    for fl in (1e-3, 1e-2, 1e-1):
+        big = np.abs(ref) > fl * norms
+        e = np.where(big, np.abs(got - ref) / np.where(big, np.abs(ref), 1.0), 0.0)
+        out["per_coef"][f"|c|>{fl:g}*|row|"] = {"max_rel_err": float(e.max()),
+                                                 "frames_over_tol": int(np.count_nonzero(e.max(axis=1) > tol))}
+    out["pass"] = bool(e_row.max() < tol)
+    return out
+
+
+def cpu_baseline(seconds_hint, gpu_mfcc, seconds_total, gpu_mfcc64=None):
+    """The oracle (a float64 C restatement of the Go path) on the box's host, pinned: STFT over
+    `threads` threads (Go's worker-pool shape), MFCC.ComputeFrames single-threaded, as in Go.  One
+    pass over the WHOLE hour doubles as the warm-up and as the parity check of the GPU output;
+    the timed value is the median of 5 runs on a bounded sample (~3 s each)."""
+    O = oracle_module()
+    threads = cpu_threads()
+    with pinned(threads) as cpus:
+        x = shard.stream_pcm(0, int(seconds_total * SR)).double().numpy()
+        ref = O.mfcc_frames(O.stft_mag(x, W, H, nthreads=threads), SR, n_coef=N_MFCC, n_mels=N_MELS)
+        parity = mfcc_parity(gpu_mfcc[: len(ref)], ref)
+        parity64 = None
+        if gpu_mfcc64 is not None:                     # the float64 headline variant
+            parity64 = mfcc_parity(gpu_mfcc64[: len(ref)], ref, tol=1e-6)   # device log/exp are not correctly rounded
+        del ref
+        probe = x[: int(60 * SR)]
+        t0 = time.perf_counter()
+        O.mfcc_frames(O.stft_mag(probe, W, H, nthreads=threads), SR, n_coef=N_MFCC, n_mels=N_MELS)
+        dt = time.perf_counter() - t0
+        secs = seconds_hint or min(seconds_total, max(60.0, 60.0 * 3.0 / max(dt, 1e-6)))
+        xs = x[: int(secs * SR)]
+        F = O.stft_frames(len(xs), W, H)
+        med, lo, hi = timed_runs(lambda: O.mfcc_frames(O.stft_mag(xs, W, H, nthreads=threads), SR,
+                                                       n_coef=N_MFCC, n_mels=N_MELS), reps=5, warmup=0)
+    base = {"value": F / med, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{secs:.0f} s of the bench stream ({F} frames), float64: STFT over {threads} threads "
+                      "(Go worker-pool shape), MFCC.ComputeFrames single-threaded, as in the Go path; "
+                      "median of 5 runs after a warm-up pass over the whole hour",
+            "runs": 5, "spread_frames_per_s": [F / hi, F / lo], "pinned_cpus": cpus, **host_info()}
+    return base, parity, parity64
+
+
+DTW_BYTES_PER_CELL = 8.25     # C store (8 B, the reference's CostMatrix) + 2-bit direction code
+FP64_PEAK_TFS = 78.6          # MI355X FP64 vector (AMD spec; SURVEY.md 8(d))
+
+
+def bench_dtw(ctx, n, steps, parity=False):
+    """C3-size DTW (51,676 x 51,676, 12-dim) through the sonar_dtw host entry (H2D of the inputs,
+    D2H of the path): cells/s end to end, per-kernel HIP-event times (band sweep, walk, path
+    decode) and the band sweep's roofline: 8.25 B/cell of HBM writes (C + direction codes)."""
     rng = np.random.default_rng(7)
     q = rng.random((n, 12))
     r = np.roll(q, 37, axis=0) + 0.01 * rng.random((n, 12))
     ctx.dtw(q[:256], r[:256])       # warm-up / allocation of small buffers
     ctx.dtw(q, r)                   # allocation of the (n+1)^2 cost matrix
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    walls, parts = [], []
     for _ in range(steps):
+        t0 = time.perf_counter()
         res = ctx.dtw(q, r)
-    dt = (time.perf_counter() - t0) / steps
-    return {"dtw_cells_per_s": n * n / dt, "dtw_ms": dt * 1e3, "dtw_n": n, "dtw_dim": 12,
-            "dtw_path_len": int(len(res["path_q"]))}
+        walls.append(time.perf_counter() - t0)
+        parts.append(ctx.dtw_last_timing())
+    dt = float(np.median(walls))
+    band_ms, walk_ms, dec_ms = (float(v) for v in np.median(np.array(parts), axis=0))
+    cells = n * n
+    out = {"dtw_cells_per_s": cells / dt, "dtw_ms": dt * 1e3, "dtw_ms_spread": [min(walls) * 1e3, max(walls) * 1e3],
+           "dtw_n": n, "dtw_dim": 12, "dtw_path_len": int(len(res["path_q"])), "dtw_reps": steps,
+           "dtw_kernel_ms": {"band_sweep": band_ms, "walk": walk_ms, "path_decode": dec_ms},
+           "dtw_roofline": {"bound": "hbm", "kernel": "dtw_band_kernel",
+                            "achieved": cells * DTW_BYTES_PER_CELL / (band_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": cells * DTW_BYTES_PER_CELL / (band_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                            "algorithmic_bytes_per_cell": DTW_BYTES_PER_CELL,
+                            "sweep_cells_per_s": cells / (band_ms * 1e-3),
+                            "fp64_tflops": cells * 40 / (band_ms * 1e-3) / 1e12,
+                            "fp64_frac": cells * 40 / (band_ms * 1e-3) / 1e12 / FP64_PEAK_TFS,
+                            "note": "40 flop/cell (12-dim Euclidean + min + add, SURVEY.md 8(d)); the sweep is a "
+                                    "wavefront of nq + nr dependent steps, latency-bound below both roofs"}}
+    if parity:
+        O = oracle_module()
+        threads = cpu_threads()
+        with pinned(threads):
+            t0 = time.perf_counter()
+            ref = O.dtw_full(q, r, nthreads=threads)
+            dtc = time.perf_counter() - t0
+        out["dtw_parity"] = {"cells": cells, "path_equal": bool(np.array_equal(res["path_q"], ref["path_q"]) and
+                                                               np.array_equal(res["path_r"], ref["path_r"])),
+                             "path_cost_equal": bool(np.array_equal(res["path_cost"], ref["path_cost"])),
+                             "distance_equal": bool(res["distance"] == ref["distance"]),
+                             "oracle": "dtw_oracle.c stripe wavefront (same cells and order as or_dtw)"}
+        out["dtw_cpu_baseline"] = {"value": cells / dtc, "unit": "cells/s", "cores": threads, "kind": "port",
+                                   "sample": f"the same {n} x {n} 12-dim DTW, oracle stripe wavefront over "
+                                             f"{threads} threads (the Go reference fills serially), one run"}
+    return out
 
 
 def bench_c5(args, world, rank, dev):
@@ -175,18 +333,25 @@ def bench_c5(args, world, rank, dev):
     # warm-up on one pair: tables, buffers, kernel code objects
     pairs.align_pairs([a], lambda k: data[k], max_lag_seconds=args.c5_max_lag, workers=1, device=dev.index)
     torch.cuda.synchronize()
-    barrier(world)
-    t0 = time.perf_counter()
-    recs = pairs.align_pairs(range(a, b), lambda k: data[k], max_lag_seconds=args.c5_max_lag,
-                             workers=args.c5_workers, device=dev.index)
-    torch.cuda.synchronize()
-    barrier(world)
-    dt = max_over_ranks(time.perf_counter() - t0, world)
+    dts = []
+    for _ in range(args.reps):
+        barrier(world)
+        t0 = time.perf_counter()
+        recs = pairs.align_pairs(range(a, b), lambda k: data[k], max_lag_seconds=args.c5_max_lag,
+                                 workers=args.c5_workers, device=dev.index)
+        torch.cuda.synchronize()
+        barrier(world)
+        dts.append(max_over_ranks(time.perf_counter() - t0, world))
+    dt = float(np.median(dts))
     allrec = pairs.gather_records(torch.tensor(recs, dtype=torch.float64, device=dev), world, counts).cpu().numpy()
     ipl, itrue = pairs.RECORD_FIELDS.index("peak_lag"), pairs.RECORD_FIELDS.index("lag_seconds_true")
     lag_frames = allrec[:, itrue] * SR / H
     ok = np.minimum(np.abs(allrec[:, ipl] - lag_frames), np.abs(allrec[:, ipl] + lag_frames)) <= 1.5
-    return {"c5_pairs_per_s": P / dt, "c5_ms": dt * 1e3, "c5_pairs": P, "c5_seconds_per_stream": args.c5_seconds,
+    F = int((args.c5_seconds * SR - W) // H + 1)
+    return {"c5_pairs_per_s": P / dt, "c5_ms": dt * 1e3, "c5_reps": len(dts),
+            "c5_pairs_per_s_spread": [P / max(dts), P / min(dts)],
+            "c5_frames_per_s": 2 * P * F / dt, "c5_frames_note": "both streams' STFT frames of every pair (BASELINE configs[4])",
+            "c5_pairs": P, "c5_seconds_per_stream": args.c5_seconds,
             "c5_max_lag_s": args.c5_max_lag, "c5_workers_per_rank": args.c5_workers,
             "c5_lag_recovered": float(ok.mean()), "c5_dtw_cells_per_pair": int((args.c5_seconds * SR - W) // H + 1) ** 2}
 
@@ -201,14 +366,18 @@ def bench_c3(args, ctx, dev):
     torch.cuda.synchronize()
     pairs.align_pair(ctx, q[: SR * 20], r[: SR * 20], max_lag_seconds=60.0)       # warm-up (small)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    rec, res = pairs.align_pair(ctx, q, r, max_lag_seconds=60.0, lag_seconds_true=12.34)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dts = []
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        rec, res = pairs.align_pair(ctx, q, r, max_lag_seconds=60.0, lag_seconds_true=12.34)
+        torch.cuda.synchronize()
+        dts.append(time.perf_counter() - t0)
+    dt = float(np.median(dts))
     F = (q.numel() - W) // H + 1
     lag = float(rec[pairs.RECORD_FIELDS.index("peak_lag")])
     want = 12.34 * SR / H
-    return {"c3_align": {"seconds_per_stream": args.c3_seconds, "ms": dt * 1e3, "frames_per_stream": F,
+    return {"c3_align": {"seconds_per_stream": args.c3_seconds, "ms": dt * 1e3, "reps": len(dts),
+                         "ms_spread": [min(dts) * 1e3, max(dts) * 1e3], "frames_per_stream": F,
                          "dtw_cells": F * F, "dtw_cells_per_s_end_to_end": F * F / dt,
                          "peak_lag_frames": lag, "injected_lag_frames": want,
                          "lag_recovered": bool(min(abs(lag - want), abs(lag + want)) <= 1.5),
@@ -218,9 +387,15 @@ def bench_c3(args, ctx, dev):
 def bench_c4(args, ctx):
     """BASELINE config C4: SpeechFeatureExtractor.ExtractFeatures on 30 min of synthetic 16 kHz
     speech-like noise (C4 recipe), FeatureConfig.SampleRate = 16000, W = 512, H = 128 (STFT + MFCC +
-    descriptors + ZCR + energy + YIN + LPC formants + voice quality + temporal features).  The C
-    entry takes host float64 PCM (as the cgo path hands it over): the H2D copy is inside the
-    timed call.  CPU baseline: the oracle composition of the same extractor on 60 s, float64."""
+    descriptors + ZCR + energy + YIN + temporal features), float64 parity mode.  The C entry takes
+    host float64 PCM (as the cgo path hands it over): the H2D copy is inside the timed call.
+    The C4 noise has no periodicity, so detectSpeech fails and the extractor skips formants and
+    voice quality exactly as the oracle does; the LPC named by configs[3] is therefore timed in two
+    more legs: FormantAnalyzer.AnalyzeMultipleFrames (sonar_formants, LPC order 28 on 2048-sample
+    frames, hop 1024) over the same 30 min, and the extractor on a voiced 30-min signal
+    (synth.voiced: 12 harmonics of 140 Hz + vibrato) that passes detectSpeech, so formants and
+    voice quality run inside the call.  Median of --reps runs each.  CPU baselines: the oracle on
+    60 s (extractor) and on the same frames' first 60 s (formants), median of 5."""
     from sonar import synth
     sr = 16000
     x = synth.c4_speech(seconds=args.c4_seconds, sr=sr)
@@ -228,51 +403,81 @@ def bench_c4(args, ctx):
               enable_mfcc=1, enable_speech_features=1, enable_temporal_features=1, mfcc_coefficients=13)
     cfg = ctx.feature_config(is_news=0, **fc)
     ctx.extract_speech_features(x[: sr * 10], sr, cfg)                        # warm-up
-    ts = []
-    for _ in range(2):
-        t0 = time.perf_counter()
-        got = ctx.extract_speech_features(x, sr, cfg)
-        ts.append(time.perf_counter() - t0)
-    dt = min(ts)
+
+    def reps_of(fn):
+        ts = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            r_ = fn()
+            ts.append(time.perf_counter() - t0)
+        return r_, float(np.median(ts)), [min(ts) * 1e3, max(ts) * 1e3]
+
+    got, dt, spread = reps_of(lambda: ctx.extract_speech_features(x, sr, cfg))
     F = sonar.stft_frames(len(x), 512, 128)
     out = {"c4_speech": {"seconds": args.c4_seconds, "samples": len(x), "stft_frames": F,
-                         "pitch_frames": int(len(got["pitch_estimate"])), "ms": dt * 1e3,
-                         "frames_per_s": F / dt, "is_speech": float(np.ravel(got.get("is_speech", [0]))[0]),
+                         "pitch_frames": int(len(got["pitch_estimate"])), "ms": dt * 1e3, "ms_spread": spread,
+                         "reps": args.reps, "frames_per_s": F / dt,
+                         "is_speech": float(np.ravel(got.get("is_speech", [0]))[0]),
                          "precision": "f64 (parity mode, the extractor's default)"}}
+    ctx.formants(x[: sr * 10], sr)                                             # warm-up
+    fm, dtf, spf = reps_of(lambda: ctx.formants(x, sr))
+    nf = len(fm["status"])
+    out["c4_formants"] = {"frames": nf, "lpc_order": 28, "frame": 2048, "hop": 1024, "ms": dtf * 1e3,
+                          "ms_spread": spf, "frames_per_s": nf / dtf,
+                          "ok_frames": int(np.count_nonzero(np.asarray(fm["status"]) == 0))}
+    v = synth.voiced(seconds=args.c4_seconds, sr=sr)
+    ctx.extract_speech_features(v[: sr * 10], sr, cfg)
+    gv, dtv, spv = reps_of(lambda: ctx.extract_speech_features(v, sr, cfg))
+    out["c4_speech_voiced"] = {"seconds": args.c4_seconds, "stft_frames": sonar.stft_frames(len(v), 512, 128),
+                               "ms": dtv * 1e3, "ms_spread": spv, "frames_per_s": sonar.stft_frames(len(v), 512, 128) / dtv,
+                               "is_speech": float(np.ravel(gv.get("is_speech", [0]))[0]),
+                               "jitter": float(np.ravel(gv.get("jitter", [0]))[0]),
+                               "vocal_tract_length": float(np.ravel(gv.get("vocal_tract_length", [0]))[0]),
+                               "note": "synth.voiced passes detectSpeech: formants (LPC) and voice quality run "
+                                       "inside the extractor call"}
     if not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as O
+        O = oracle_module()
+        threads = cpu_threads()
         n = sr * 60
-        t0 = time.perf_counter()
-        O.speech_features_reference(x[:n], sr, fc)
-        dtc = time.perf_counter() - t0
         Fc = sonar.stft_frames(n, 512, 128)
-        out["c4_cpu_baseline"] = {"value": Fc / dtc, "unit": "frames/s", "cores": 8, "kind": "port",
+        with pinned(threads) as cpus:
+            med, lo, hi = timed_runs(lambda: O.speech_features_reference(x[:n], sr, fc), reps=5)
+            medf, _, _ = timed_runs(lambda: O.formant_frames(x[:n], sr), reps=5)
+        nfc = len(O.formant_frames(x[:n], sr)["status"])
+        out["c4_cpu_baseline"] = {"value": Fc / med, "unit": "frames/s", "cores": threads, "kind": "port",
                                   "sample": f"60 s of the C4 signal ({Fc} STFT frames): oracle speech-extractor "
-                                            "composition, float64 (STFT over 8 threads, the rest 1 thread)"}
+                                            f"composition, float64 (STFT over {threads} threads, the rest 1 thread), "
+                                            "median of 5", "spread_frames_per_s": [Fc / hi, Fc / lo],
+                                  "pinned_cpus": cpus}
+        out["c4_formants_cpu_baseline"] = {"value": nfc / medf, "unit": "frames/s", "cores": 1, "kind": "port",
+                                           "sample": f"AnalyzeMultipleFrames on 60 s of the C4 signal ({nfc} frames), "
+                                                     "oracle, 1 thread, median of 5"}
     return out
 
 
 def c5_cpu_baseline(args):
     """The oracle's alignment of one C5 pair (60 s streams): music-extractor energy + chroma of both
     streams, NCC over the lags, chroma DTW, scorers; float64, 1 thread."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
+    O = oracle_module()
     q, r, lag = pairs.c5_pair_device(0, args.c5_seconds, device="cpu")
     q, r = q.numpy(), r.numpy()
-    t0 = time.perf_counter()
-    feats = []
-    for x in (q, r):
-        y = O.preemphasis(O.dc_removal(x, 0.995), 0.95)
-        e = O.short_time_energy(y, W, H)
-        F = O.stft_frames(len(x), W, H)
-        feats.append((e, O.chroma_music(x, F, H, SR)))
-    O.align_features_reference(feats[0][0], feats[1][0], feats[0][1], feats[1][1], len(q), len(r), SR, SR, H,
-                               args.c5_max_lag)
-    dt = time.perf_counter() - t0
-    return {"value": 1.0 / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+
+    def one_pair():
+        feats = []
+        for x in (q, r):
+            y = O.preemphasis(O.dc_removal(x, 0.995), 0.95)
+            e = O.short_time_energy(y, W, H)
+            F = O.stft_frames(len(x), W, H)
+            feats.append((e, O.chroma_music(x, F, H, SR)))
+        O.align_features_reference(feats[0][0], feats[1][0], feats[0][1], feats[1][1], len(q), len(r), SR, SR, H,
+                                   args.c5_max_lag)
+    with pinned(1) as cpus:
+        med, lo, hi = timed_runs(one_pair, reps=5)
+    F = O.stft_frames(len(q), W, H)
+    return {"value": 1.0 / med, "unit": "pairs/s", "cores": 1, "kind": "port", "frames_per_s": 2 * F / med,
             "sample": f"one C5 pair ({args.c5_seconds:.0f} s streams): oracle music features + NCC + chroma DTW "
-                      "+ scorers, float64, 1 thread"}
+                      "+ scorers, float64, 1 thread, median of 5", "spread_pairs_per_s": [1.0 / hi, 1.0 / lo],
+            "pinned_cpus": cpus}
 
 
 def bench_c6(args, ctx, dev):
@@ -525,8 +730,12 @@ def main():
         assert torch.equal(timeline[f0:f0 + F], out)
 
     extra = {}
+    out64 = None
+    if not args.no_f64:
+        extra["headline_f64"], out64 = bench_headline_f64(args, ctx, pcm, F, dev)
     if args.dtw_len > 0:
-        extra = bench_dtw(ctx, args.dtw_len, args.dtw_steps)
+        extra.update(bench_dtw(ctx, args.dtw_len, args.dtw_steps,
+                               parity=rank == 0 and world == 1 and not args.no_cpu_baseline))
     if args.ingest_reps > 0:
         extra.update(bench_ingest(args, ctx, pcm, cfg, F))
     if args.c5_pairs > 0:
@@ -544,12 +753,15 @@ def main():
     if args.c7_seconds > 0:
         extra.update(bench_c7(args, ctx))
 
-    cpu = None
+    cpu, parity = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu, parity, parity64 = cpu_baseline(args.cpu_seconds, out.cpu().numpy(), args.seconds, out64)
+        if parity64 is not None:
+            extra["headline_f64"]["parity"] = parity64
 
     achieved_gbs = F * BYTES_PER_FRAME / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(kernel_name)
+    achieved_tfs = F * FLOPS_PER_FRAME / (kernel_ms * 1e-3) / 1e12
+    traffic, traffic_src = load_traffic(kernel_name)
     line = {
         "metric": "audio frames/sec (STFT->MFCC, 1024/256)",
         "value": value,
@@ -567,13 +779,16 @@ def main():
         "config": {"workload": "STFT(W=1024,H=256,Hann)->mel(40)->ln->DCT-II(13)->lifter(22) on 1 h of "
                                "44.1 kHz float32 PCM per GPU", "frames_total": F_total, "frames_rank0": F,
                    "samples_rank0": n, "parallelism": f"frame-shard x{world}"},
-        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved_gbs / HBM_PEAK_GBS,
-                     "traffic": traffic, "kernel": kernel_name, "kernel_ms": kernel_ms,
-                     "algorithmic_bytes_per_frame": BYTES_PER_FRAME,
-                     "valu_tflops": F * FLOPS_PER_FRAME / (kernel_ms * 1e-3) / 1e12,
-                     "valu_frac": F * FLOPS_PER_FRAME / (kernel_ms * 1e-3) / 1e12 / FP32_PEAK_TFS},
+        # 31,136 flop/frame against 1,076 B/frame is above the FP32 ridge, so the
+        # binding roof is the FP32 VALU (157.3 TF); the north star's HBM figure is kept beside it
+        "roofline": {"bound": "valu", "achieved": achieved_tfs, "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": achieved_tfs / FP32_PEAK_TFS,
+                     "traffic": traffic, "traffic_source": traffic_src, "kernel": kernel_name, "kernel_ms": kernel_ms,
+                     "algorithmic_flops_per_frame": FLOPS_PER_FRAME, "algorithmic_bytes_per_frame": BYTES_PER_FRAME,
+                     "hbm_achieved_gbs": achieved_gbs, "hbm_peak_gbs": HBM_PEAK_GBS,
+                     "hbm_frac": achieved_gbs / HBM_PEAK_GBS},
         "cpu_baseline": cpu,
+        "parity": parity,
     }
     if gather_ms is not None:
         line["allgather_ms"] = gather_ms

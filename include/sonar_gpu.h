@@ -113,6 +113,10 @@ int sonar_enable_kernel_timing(sonar_ctx* ctx, int on);
 /* Name of the fused path-A kernel the last sonar_fingerprint call launched
  * ("mfcc_pair_kernel" or "fp_wave_kernel"; "" if none) -- diagnostics. */
 const char* sonar_last_fp_kernel(sonar_ctx* ctx);
+/* HIP-event durations (ms) of the kernels of the last sonar_dtw call on this
+ * context: ms3[0] the band sweep (dtw_band_kernel), ms3[1] the backtrack walk,
+ * ms3[2] the path decode -- diagnostics and the bench's DTW roofline. */
+int sonar_dtw_last_timing(sonar_ctx* ctx, double* ms3);
 
 /* ---- sizes (same integer rules as the Go code) ------------------------ */
 /* (n - W)/H + 1, Go truncating division; <= 0 -> SONAR_ERR_TOO_SHORT

@@ -52,6 +52,8 @@ struct sonar_ctx {
   size_t ev_used = 0;
   double last_ms = 0.0;
   const char* last_fp_kernel = "";
+  hipEvent_t dtw_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // band | walk | decode boundaries
+  double dtw_ms[3] = {0.0, 0.0, 0.0};
   IngestState* ingest = nullptr;
 };
 

@@ -130,9 +130,11 @@ int64_t dtw_cn_index(const DtwGeom& g, int64_t i, int64_t j);
 int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, const DtwGeom& g, double* Cn,
                uint32_t* Dn, uint64_t* E, int32_t* sync_words /* [0] ticket, [1] error */,
                uint32_t* codes /* walk moves, 2 bits each */, int64_t* plen,
-               uint64_t* trace /* nullable, [nb][4] diagnostics */, hipStream_t s);
-int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const uint32_t* codes, int64_t P, int32_t* pq,
-                         int32_t* pr, double* pc, hipStream_t s);
+               uint64_t* trace /* nullable, [nb][8] diagnostics */, hipStream_t s,
+               hipEvent_t mid = nullptr /* recorded between the sweep and the walk */);
+// wstart: scratch of (P + 15) / 16 int2 (each code word's starting cell)
+int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const uint32_t* codes, int64_t P, int2* wstart,
+                         int32_t* pq, int32_t* pr, double* pc, hipStream_t s);
 // costMatrix[1:] (nq x (nr+1), column 0 = +Inf) from the band-skewed store
 int launch_dtw_cost_rowmajor(const double* Cn, const DtwGeom& g, double* out, hipStream_t s);
 // sets *flag = 1 if any of the n values is not finite

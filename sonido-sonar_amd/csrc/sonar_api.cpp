@@ -230,6 +230,8 @@ void sonar_destroy(sonar_ctx* c) {
   for (auto& e : c->ev_pool) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
+  for (auto& e : c->dtw_ev)
+    if (e) hipEventDestroy(e);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -256,6 +258,12 @@ int sonar_enable_kernel_timing(sonar_ctx* c, int on) {
 }
 
 const char* sonar_last_fp_kernel(sonar_ctx* c) { return c ? c->last_fp_kernel : ""; }
+
+int sonar_dtw_last_timing(sonar_ctx* c, double* ms3) {
+  if (!c || !ms3) return SONAR_ERR_INVALID;
+  for (int k = 0; k < 3; ++k) ms3[k] = c->dtw_ms[k];
+  return SONAR_OK;
+}
 
 int sonar_last_kernel_ms(sonar_ctx* c, double* ms) {
   if (!c || !ms) return SONAR_ERR_INVALID;
@@ -688,13 +696,17 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
   }
   // SONAR_DTW_TRACE=<file>: per-band timestamps of the sweep (diagnostics only)
   const char* trace_path = std::getenv("SONAR_DTW_TRACE");
-  uint64_t* trace = trace_path ? (uint64_t*)dbuf(c, "dtw.trace", (size_t)g.nb * 32) : nullptr;
+  uint64_t* trace = trace_path ? (uint64_t*)dbuf(c, "dtw.trace", (size_t)g.nb * 64) : nullptr;
+  for (auto& e : c->dtw_ev)
+    if (!e) HIP_TRY(c, hipEventCreate(&e));
   hipEvent_t tend = timed_begin(c, s);
-  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, codes, pl, trace, s) != 0)
+  HIP_TRY(c, hipEventRecord(c->dtw_ev[0], s));
+  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, codes, pl, trace, s, c->dtw_ev[1]) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
+  HIP_TRY(c, hipEventRecord(c->dtw_ev[2], s));
   timed_end(c, s, tend);
   if (trace) {
-    std::vector<uint64_t> t((size_t)g.nb * 4);
+    std::vector<uint64_t> t((size_t)g.nb * 8);
     HIP_TRY(c, hipMemcpyAsync(t.data(), trace, t.size() * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     if (FILE* f = std::fopen(trace_path, "wb")) { std::fwrite(t.data(), 8, t.size(), f); std::fclose(f); }
@@ -712,8 +724,11 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
     oc = (double*)dbuf(c, "dtw.pc", cap * 8);
     if (!oq || !orr || !oc) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (path)");
   }
-  if (sonar::launch_dtw_path_cost(Cn, g, codes, P, oq, orr, oc, s) != 0)
+  int2* wstart = (int2*)dbuf(c, "dtw.wstart", (size_t)((P + 15) / 16 + 1) * sizeof(int2));
+  if (!wstart) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (path)");
+  if (sonar::launch_dtw_path_cost(Cn, g, codes, P, wstart, oq, orr, oc, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw path launch failed");
+  HIP_TRY(c, hipEventRecord(c->dtw_ev[3], s));
   double cNM = 0;
   HIP_TRY(c, hipMemcpyAsync(&cNM, Cn + sonar::dtw_cn_index(g, nq, nr), 8, hipMemcpyDeviceToHost, s));
   double* cost_dev = cost;
@@ -730,6 +745,11 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
     if (cost) HIP_TRY(c, hipMemcpyAsync(cost, cost_dev, (size_t)nq * (nr + 1) * 8, hipMemcpyDeviceToHost, s));
   }
   HIP_TRY(c, hipStreamSynchronize(s));
+  for (int k = 0; k < 3; ++k) {
+    float f = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&f, c->dtw_ev[k], c->dtw_ev[k + 1]));
+    c->dtw_ms[k] = f;
+  }
   if (path_len) *path_len = P;
   if (distance) *distance = cNM / (double)P;                      // dtw.go:88-91
   return SONAR_OK;

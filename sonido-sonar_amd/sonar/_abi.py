@@ -171,6 +171,7 @@ def lib():
     L.sonar_synchronize.argtypes = [_vp]
     L.sonar_last_kernel_ms.argtypes = [_vp, _d]
     L.sonar_enable_kernel_timing.argtypes = [_vp, C.c_int]
+    L.sonar_dtw_last_timing.argtypes = [_vp, C.POINTER(C.c_double)]
     L.sonar_last_fp_kernel.argtypes = [_vp]
     L.sonar_last_fp_kernel.restype = C.c_char_p
     for f in ("sonar_stft_frames", "sonar_energy_frames"):
@@ -305,6 +306,12 @@ class Context:
         v = C.c_double()
         self._check(self._L.sonar_last_kernel_ms(self._h, C.byref(v)))
         return v.value
+
+    def dtw_last_timing(self):
+        """(band sweep, walk, path decode) kernel ms of the last dtw call (HIP events)."""
+        v = (C.c_double * 3)()
+        self._check(self._L.sonar_dtw_last_timing(self._h, v))
+        return tuple(v)
 
     def last_fp_kernel(self):
         """Name of the fused kernel the last fingerprint call launched (diagnostics)."""
