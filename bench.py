@@ -320,40 +320,49 @@ def bench_dtw(ctx, n, steps, parity=False):
     return out
 
 
-def bench_c5(args, world, rank, dev):
+def bench_c5(args, world, rank, dev, ctx):
     """BASELINE config C5 (path B): P stream pairs sharded over the ranks by contiguous pair ranges
     (sonar/pairs.py), each pair through the music-extractor energy + chroma and
     ExtractAlignmentFeatures (NCC + chroma DTW); no data-path collective, the per-pair records
     are all-gathered over RCCL after the timed region.  Pairs are generated on the device
-    before timing ("inputs resident in HBM")."""
+    before timing ("inputs resident in HBM").  The timed call is the product entry
+    sonar_align_pairs (worker streams inside the library, no Python threads)."""
     P = args.c5_pairs
     a, b = pairs.pair_range(P, world, rank)
     counts = [pairs.pair_range(P, world, g)[1] - pairs.pair_range(P, world, g)[0] for g in range(world)]
-    data = {k: pairs.c5_pair_device(k, args.c5_seconds, device=dev) for k in range(a, b)}
-    # warm-up on one pair: tables, buffers, kernel code objects
-    pairs.align_pairs([a], lambda k: data[k], max_lag_seconds=args.c5_max_lag, workers=1, device=dev.index)
+    data = [pairs.c5_pair_device(k, args.c5_seconds, device=dev) for k in range(a, b)]
+    torch.cuda.synchronize()
+    qp, rp = [q.data_ptr() for q, _, _ in data], [r.data_ptr() for _, r, _ in data]
+    nq, nr = [q.numel() for q, _, _ in data], [r.numel() for _, r, _ in data]
+
+    def run(idx):
+        return ctx.align_pairs([qp[i] for i in idx], [rp[i] for i in idx], nq=[nq[i] for i in idx],
+                               nr=[nr[i] for i in idx], max_lag_seconds=args.c5_max_lag,
+                               workers=args.c5_workers, device_ptrs=True)
+    run([0])                                   # warm-up: worker contexts, tables, buffers
+    run(list(range(min(len(data), args.c5_workers))))
     torch.cuda.synchronize()
     dts = []
     for _ in range(args.reps):
         barrier(world)
         t0 = time.perf_counter()
-        recs = pairs.align_pairs(range(a, b), lambda k: data[k], max_lag_seconds=args.c5_max_lag,
-                                 workers=args.c5_workers, device=dev.index)
+        recd = run(list(range(len(data))))
         torch.cuda.synchronize()
         barrier(world)
         dts.append(max_over_ranks(time.perf_counter() - t0, world))
     dt = float(np.median(dts))
+    recs = np.stack([recd[f] for f in sonar.PAIR_FIELDS] + [np.array([lag for _, _, lag in data])], axis=1)
     allrec = pairs.gather_records(torch.tensor(recs, dtype=torch.float64, device=dev), world, counts).cpu().numpy()
-    ipl, itrue = pairs.RECORD_FIELDS.index("peak_lag"), pairs.RECORD_FIELDS.index("lag_seconds_true")
-    lag_frames = allrec[:, itrue] * SR / H
+    ipl = sonar.PAIR_FIELDS.index("peak_lag")
+    lag_frames = allrec[:, -1] * SR / H
     ok = np.minimum(np.abs(allrec[:, ipl] - lag_frames), np.abs(allrec[:, ipl] + lag_frames)) <= 1.5
     F = int((args.c5_seconds * SR - W) // H + 1)
     return {"c5_pairs_per_s": P / dt, "c5_ms": dt * 1e3, "c5_reps": len(dts),
             "c5_pairs_per_s_spread": [P / max(dts), P / min(dts)],
             "c5_frames_per_s": 2 * P * F / dt, "c5_frames_note": "both streams' STFT frames of every pair (BASELINE configs[4])",
             "c5_pairs": P, "c5_seconds_per_stream": args.c5_seconds,
-            "c5_max_lag_s": args.c5_max_lag, "c5_workers_per_rank": args.c5_workers,
-            "c5_lag_recovered": float(ok.mean()), "c5_dtw_cells_per_pair": int((args.c5_seconds * SR - W) // H + 1) ** 2}
+            "c5_max_lag_s": args.c5_max_lag, "c5_workers_per_rank": args.c5_workers, "c5_entry": "sonar_align_pairs",
+            "c5_lag_recovered": float(ok.mean()), "c5_dtw_cells_per_pair": F * F}
 
 
 def bench_c3(args, ctx, dev):
@@ -739,7 +748,7 @@ def main():
     if args.ingest_reps > 0:
         extra.update(bench_ingest(args, ctx, pcm, cfg, F))
     if args.c5_pairs > 0:
-        extra.update(bench_c5(args, world, rank, dev))
+        extra.update(bench_c5(args, world, rank, dev, ctx))
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             extra["c5_cpu_baseline"] = c5_cpu_baseline(args)
     if args.c3_seconds > 0:

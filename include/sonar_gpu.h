@@ -348,6 +348,74 @@ int sonar_align_pair_device(sonar_ctx* ctx, const double* q_pcm, int64_t nq, con
                             int32_t sample_rate, int32_t stft_window, int32_t hop, int32_t feature_window,
                             double max_lag_seconds, sonar_result** out);
 
+/* ---- many stream pairs (the C5 workload) -----------------------------------------
+ * The fixed-size record a caller of ExtractAlignmentFeatures keeps per pair
+ * (extractors/alignment.go:139-219: TemporalOffset, OffsetConfidence, AlignmentSimilarity,
+ * AlignmentQuality, Method; the NCC candidate's offset and peak lag; the chroma DTW distance). */
+typedef struct {
+  double temporal_offset;        /* seconds                                       */
+  double offset_confidence;
+  double alignment_similarity;
+  double alignment_quality;
+  double method;                 /* SONAR_ALIGN_* of the chosen candidate          */
+  double corr_offset_seconds;    /* the energy-NCC candidate (NaN if none)         */
+  double dtw_distance;           /* the chroma-DTW candidate (NaN if none)         */
+  double peak_lag;               /* NCC peak lag in feature frames (NaN if none)   */
+  int32_t status;                /* SONAR_OK or this pair's error code             */
+  int32_t reserved;
+} sonar_pair_record;
+
+/* sonar_align_pair_device over npairs pairs: q_pcm[k] / r_pcm[k] float64 streams of nq[k] / nr[k]
+ * samples (device pointers on ctx's device if device_ptrs, else host arrays).  `workers` (<= 0:
+ * 16) worker contexts on ctx's device, one HIP stream and one host thread each, take pairs in
+ * order, so the pairs' latency-bound kernels (the DC-removal scan, the Go-order NCC sums, the DTW
+ * band pipeline and walk) overlap on the GPU.  HIP maps a process's streams onto
+ * GPU_MAX_HW_QUEUES hardware queues (4 by default): set it to >= workers in the environment before
+ * the first HIP call.  out[k] is filled for every pair; the return is SONAR_OK or the first error. */
+int sonar_align_pairs(sonar_ctx* ctx, int64_t npairs, const double* const* q_pcm, const int64_t* nq,
+                      const double* const* r_pcm, const int64_t* nr, int32_t sample_rate, int32_t stft_window,
+                      int32_t hop, int32_t feature_window, double max_lag_seconds, int32_t workers,
+                      int32_t device_ptrs, sonar_pair_record* out);
+
+/* ---- one process, several GPUs: a context per device plus an RCCL communicator
+ * over them (ncclCommInitAll; collectives run over xGMI). ------------------------------------- */
+typedef struct sonar_multi sonar_multi;
+int sonar_multi_create(const int32_t* devices, int32_t n_devices, sonar_multi** out);
+void sonar_multi_destroy(sonar_multi* m);
+const char* sonar_multi_last_error(const sonar_multi* m);
+int32_t sonar_multi_size(const sonar_multi* m);
+sonar_ctx* sonar_multi_ctx(sonar_multi* m, int32_t rank);   /* the rank's context (do not destroy) */
+
+/* Frame shard g of G over n samples at W/H: frames [f0, f1) = [g F / G, (g+1) F / G) with
+ * F = sonar_stft_frames(n, W, H), and the samples they read [s0, s1) = [f0 H, (f1-1) H + W)
+ * (empty shard: f0 == f1, s0 == s1).  Pure arithmetic, the same on every host. */
+int sonar_multi_shard(int64_t n, int32_t window_size, int32_t hop_size, int32_t n_shards, int32_t shard,
+                      int64_t* f0, int64_t* f1, int64_t* s0, int64_t* s1);
+
+/* sonar_fingerprint with the STFT frames sharded over the devices: device g runs frames [f0, f1)
+ * of sonar_multi_shard on its sample slice (host pcm, cfg->device_ptrs must be 0) and writes its
+ * rows of every requested output straight into the host arrays.  Frames are independent, so the
+ * result equals the single-device call.  Supported flags: SONAR_FP_MFCC, SONAR_FP_MAGNITUDE and
+ * SONAR_FP_SPECTRAL without flux (out->flux must be NULL: frame f0's flux needs frame f0-1); the
+ * pre-emphasised outputs (ZCR, energy) read the sample before the slice -> SONAR_ERR_UNSUPPORTED. */
+int sonar_fingerprint_multi(sonar_multi* m, const void* pcm, int64_t n, const sonar_fp_cfg* cfg,
+                            sonar_fp_out* out);
+
+/* The MFCC timeline assembled on EVERY device over RCCL: device g holds its shard's sample slice
+ * pcm_dev[g] (samples [s0, s1) of sonar_multi_shard, cfg->pcm_dtype), computes its frames, and one
+ * ncclAllGather (shards padded to the largest) fills mfcc_dev[g] (F x n_mfcc, cfg->out_dtype) on
+ * every device -- the device-resident timeline a comparator on any GPU can read.  Synchronous. */
+int sonar_fingerprint_multi_gather(sonar_multi* m, const void* const* pcm_dev, int64_t n, const sonar_fp_cfg* cfg,
+                                   void* const* mfcc_dev);
+
+/* sonar_align_pairs with the pairs split into contiguous ranges over the devices (host PCM; each
+ * device aligns its range with `workers` worker streams); the per-device records are then
+ * all-gathered over RCCL and device 0's gathered copy is returned in out[npairs]. */
+int sonar_align_pairs_multi(sonar_multi* m, int64_t npairs, const double* const* q_pcm, const int64_t* nq,
+                            const double* const* r_pcm, const int64_t* nr, int32_t sample_rate,
+                            int32_t stft_window, int32_t hop, int32_t feature_window, double max_lag_seconds,
+                            int32_t workers, sonar_pair_record* out);
+
 /* ---- AlignmentAnalyzer.AnalyzeAlignmentConsistency (algorithms/stats/alignment.go:709-800) -----
  * num_trials (< 2 -> 5) alignments of addNoise(query, 0.01) (:737-749: q[i][j] += sin(i*j+i+j)
  * * 0.01 * q[i][j]) against reference with AlignFeatures (:84-106) for `method`, then the offset

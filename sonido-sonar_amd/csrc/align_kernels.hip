@@ -310,6 +310,12 @@ constexpr int DTW_EAHEAD = 64;    // the feeder fetches edge columns up to min(p
 #ifndef DTW_NDW
 #define DTW_NDW 3                 // distance waves per block
 #endif
+#ifndef DTW_DG
+#define DTW_DG 8                  // distance cells interleaved per pass (a divisor of DTW_ECH)
+#endif
+#ifndef DTW_MINWAVES
+#define DTW_MINWAVES 4            // waves per SIMD the register budget must allow
+#endif
 constexpr int DTW_WAVES = 4 + DTW_NDW;
 // wave roles: 0 sweep, 1..NDW distance, then the ring feeder, the code wave and the edge poller
 constexpr int DTW_FEEDER_WAVE = DTW_NDW + 1;
@@ -332,7 +338,7 @@ __device__ __forceinline__ int64_t dtw_cn_off(int64_t b, int64_t S2, int64_t s, 
 
 template <int D, bool FAST, bool BANDED>
 // (2 blocks of 7 waves per CU: at least 4 waves per SIMD, <= 128 VGPRs)
-__global__ __launch_bounds__(64 * DTW_WAVES, 4) void dtw_band_kernel(DtwArgs a) {
+__global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(DtwArgs a) {
   constexpr int DR = D > 0 ? D : 1;
   constexpr int DS = dtw_ring_stride<D>();
   __shared__ __attribute__((aligned(16))) double ring[(DTW_RROWS + DTW_RMIR) * DS];
@@ -369,7 +375,11 @@ __global__ __launch_bounds__(64 * DTW_WAVES, 4) void dtw_band_kernel(DtwArgs a) 
   const int64_t nq = a.nq, nr = a.nr, S = a.S, S2 = (a.S + 1) >> 1;
   const int dim = D > 0 ? D : a.dim;
   constexpr uint64_t INF_BITS = 0x7FF0000000000000ull;
+#ifdef DTW_DBG_NOEDGE   // A/B diagnostics: every band independent (wrong results; throughput ceiling)
+  const uint64_t* Ein = nullptr;
+#else
   const uint64_t* Ein = b > 0 ? a.E + (b - 1) * (nr + 1) : nullptr;       // C[64b][j] at index j
+#endif
   const int64_t nblk = (nr + DTW_RBLK - 1) / DTW_RBLK;
   const int64_t i = 64 * b + 1 + lane;
   const bool row_ok = i <= nq;
@@ -580,33 +590,36 @@ __global__ __launch_bounds__(64 * DTW_WAVES, 4) void dtw_band_kernel(DtwArgs a) 
         // cells advance together, one dimension at a time: each sum is Go's sequential chain,
         // the chains interleave.
         const double* rw0 = ring + (int)((t0 - lane) & (DTW_RROWS - 1)) * DS;
-        double sum[DTW_ECH];
-        if constexpr (D % 2 == 0) {
 #pragma unroll
-          for (int k = 0; k < D; k += 2) {
-            double2 rv[DTW_ECH];
+        for (int g0 = 0; g0 < DTW_ECH; g0 += DTW_DG) {   // DTW_DG interleaved chains at a time
+          double sum[DTW_DG];
+          if constexpr (D % 2 == 0) {
 #pragma unroll
-            for (int u = 0; u < DTW_ECH; ++u) rv[u] = *reinterpret_cast<const double2*>(rw0 + u * DS + k);
+            for (int k = 0; k < D; k += 2) {
+              double2 rv[DTW_DG];
 #pragma unroll
-            for (int u = 0; u < DTW_ECH; ++u) {
-              const double d0 = qv[k] - rv[u].x;
-              sum[u] = k == 0 ? d0 * d0 : sum[u] + d0 * d0;   // 0.0 + x == x for x >= +0 or NaN
-              const double d1 = qv[k + 1] - rv[u].y;
-              sum[u] = sum[u] + d1 * d1;
+              for (int u = 0; u < DTW_DG; ++u) rv[u] = *reinterpret_cast<const double2*>(rw0 + (g0 + u) * DS + k);
+#pragma unroll
+              for (int u = 0; u < DTW_DG; ++u) {
+                const double d0 = qv[k] - rv[u].x;
+                sum[u] = k == 0 ? d0 * d0 : sum[u] + d0 * d0;   // 0.0 + x == x for x >= +0 or NaN
+                const double d1 = qv[k + 1] - rv[u].y;
+                sum[u] = sum[u] + d1 * d1;
+              }
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+#pragma unroll
+              for (int u = 0; u < DTW_DG; ++u) {
+                const double d0 = qv[k] - rw0[(g0 + u) * DS + k];
+                sum[u] = k == 0 ? d0 * d0 : sum[u] + d0 * d0;
+              }
             }
           }
-        } else {
 #pragma unroll
-          for (int k = 0; k < D; ++k) {
-#pragma unroll
-            for (int u = 0; u < DTW_ECH; ++u) {
-              const double d0 = qv[k] - rw0[u * DS + k];
-              sum[u] = k == 0 ? d0 * d0 : sum[u] + d0 * d0;
-            }
-          }
+          for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt(sum[u]);
         }
-#pragma unroll
-        for (int u = 0; u < DTW_ECH; ++u) dv[u] = sqrt(sum[u]);
 #endif
       } else {
 #pragma unroll
@@ -669,9 +682,15 @@ __global__ __launch_bounds__(64 * DTW_WAVES, 4) void dtw_band_kernel(DtwArgs a) 
       ech[u] = e2.x; ech[u + 1] = e2.y;
     }
   };
-  auto fix_edges = [&](int64_t s0, double (&ech)[DTW_ECH]) {   // columns s0+1.. >= 1
+  // columns s0+1.. >= 1; the values are uniform (broadcast reads), so they move to SGPRs
+  auto fix_edges = [&](int64_t s0, double (&ech)[DTW_ECH]) {
 #pragma unroll
-    for (int u = 0; u < DTW_ECH; ++u) ech[u] = (!Ein || s0 + 1 + u > nr) ? inf : ech[u];
+    for (int u = 0; u < DTW_ECH; ++u) {
+      const double e = (!Ein || s0 + 1 + u > nr) ? inf : ech[u];
+      const int2 e2 = __builtin_bit_cast(int2, e);
+      ech[u] = __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readfirstlane(e2.x),
+                                                    __builtin_amdgcn_readfirstlane(e2.y)));
+    }
   };
   // one sweep step: lane l relaxes C[i][s-l+1] with local distance d; l0up = C[64b][s+1] for lane
   // 0.  FULL: every lane's column is in [1, nr] (s in [63, nr-1]), so no per-lane predicate is

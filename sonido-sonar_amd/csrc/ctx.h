@@ -55,6 +55,7 @@ struct sonar_ctx {
   hipEvent_t dtw_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // band | walk | decode boundaries
   double dtw_ms[3] = {0.0, 0.0, 0.0};
   IngestState* ingest = nullptr;
+  std::vector<sonar_ctx*> workers;   // sonar_align_pairs' worker contexts (multi_api.cpp)
 };
 
 struct sonar_result {

@@ -216,6 +216,8 @@ int sonar_create(int device, sonar_ctx** out) {
 
 void sonar_destroy(sonar_ctx* c) {
   if (!c) return;
+  for (sonar_ctx* w : c->workers) sonar_destroy(w);
+  c->workers.clear();
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   sonar::detail::ingest_release(c);

@@ -15,7 +15,11 @@ from ._abi import (  # noqa: F401
     LIB_PATH,
     SonarError,
     Context,
+    Multi,
     FpConfig,
+    PairRecord,
+    PAIR_FIELDS,
+    multi_shard,
     WINDOWS,
     abi_version,
     build,

@@ -145,6 +145,15 @@ class Match(C.Structure):
                 ("similarity", Similarity)]
 
 
+class PairRecord(C.Structure):
+    """sonar_pair_record: what ExtractAlignmentFeatures leaves per pair (extractors/alignment.go:139-219)."""
+    _fields_ = [(n, C.c_double) for n in ("temporal_offset", "offset_confidence", "alignment_similarity",
+                                          "alignment_quality", "method", "corr_offset_seconds", "dtw_distance",
+                                          "peak_lag")] + [("status", C.c_int32), ("reserved", C.c_int32)]
+
+
+PAIR_FIELDS = [f for f, _ in PairRecord._fields_[:8]]
+
 _lib = None
 _vp, _d, _i32p, _i64p = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
 
@@ -205,6 +214,23 @@ def lib():
     L.sonar_formants.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, C.c_int32]
     L.sonar_align_pair_device.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                           C.c_int32, C.c_double, C.POINTER(C.c_void_p)]
+    _pairs = [C.c_int64, C.POINTER(C.c_void_p), _i64p, C.POINTER(C.c_void_p), _i64p, C.c_int32, C.c_int32,
+              C.c_int32, C.c_int32, C.c_double, C.c_int32]
+    L.sonar_align_pairs.argtypes = [_vp] + _pairs + [C.c_int32, C.POINTER(PairRecord)]
+    L.sonar_align_pairs_multi.argtypes = [_vp] + _pairs + [C.POINTER(PairRecord)]
+    L.sonar_multi_create.argtypes = [_i32p, C.c_int32, C.POINTER(C.c_void_p)]
+    L.sonar_multi_destroy.argtypes = [_vp]
+    L.sonar_multi_destroy.restype = None
+    L.sonar_multi_last_error.argtypes = [_vp]
+    L.sonar_multi_last_error.restype = C.c_char_p
+    L.sonar_multi_size.argtypes = [_vp]
+    L.sonar_multi_ctx.argtypes = [_vp, C.c_int32]
+    L.sonar_multi_ctx.restype = _vp
+    L.sonar_multi_shard.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _i64p, _i64p, _i64p,
+                                    _i64p]
+    L.sonar_fingerprint_multi.argtypes = [_vp, _vp, C.c_int64, C.POINTER(FpConfig), C.POINTER(FpOut)]
+    L.sonar_fingerprint_multi_gather.argtypes = [_vp, C.POINTER(C.c_void_p), C.c_int64, C.POINTER(FpConfig),
+                                                 C.POINTER(C.c_void_p)]
     L.sonar_alignment_consistency.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                               C.c_int32, C.c_int32, C.c_int32, C.POINTER(AlignmentStats)]
     L.sonar_truncate_to_alignment.argtypes = [_vp, C.c_int64, C.c_int64, C.c_int32, C.c_double,
@@ -255,6 +281,38 @@ def energy_frames(n, W, H):
 
 def pitch_frames(n):
     return int(lib().sonar_pitch_frames(n))
+
+
+def multi_shard(n, W, H, n_shards, shard):
+    """sonar_multi_shard: (f0, f1, s0, s1) of frame shard `shard` of `n_shards` (pure arithmetic)."""
+    v = [C.c_int64() for _ in range(4)]
+    rc = lib().sonar_multi_shard(n, W, H, n_shards, shard, *[C.byref(x) for x in v])
+    if rc != OK:
+        raise SonarError(rc, "sonar_multi_shard")
+    return tuple(x.value for x in v)
+
+
+def _pair_arrays(qs, rs):
+    """ctypes pointer/length arrays of two lists of streams (device int pointers or numpy arrays)."""
+    keep = []
+
+    def ptr(x):
+        if isinstance(x, (int, np.integer)):
+            return int(x)
+        a = _f64(x)
+        keep.append(a)
+        return a.ctypes.data
+    n = len(qs)
+    qp = (C.c_void_p * n)(*[ptr(x) for x in qs])
+    rp = (C.c_void_p * n)(*[ptr(x) for x in rs])
+    return qp, rp, keep
+
+
+def records_dict(recs):
+    """sonar_pair_record array -> dict of numpy arrays (PAIR_FIELDS + status)."""
+    out = {f: np.array([getattr(r, f) for r in recs]) for f in PAIR_FIELDS}
+    out["status"] = np.array([r.status for r in recs], dtype=np.int32)
+    return out
 
 
 def _ptr(a):
@@ -424,6 +482,21 @@ class Context:
                                                     stft_window, hop, feature_window, max_lag_seconds, C.byref(h)))
         return self._result(h)
 
+    def align_pairs(self, qs, rs, nq=None, nr=None, sample_rate=44100, stft_window=1024, hop=256,
+                    feature_window=1024, max_lag_seconds=20.0, workers=16, device_ptrs=False):
+        """sonar_align_pairs: records of many pairs.  qs / rs: lists of host arrays, or of device
+        pointers (ints) with device_ptrs=True and the lengths in nq / nr."""
+        n = len(qs)
+        qp, rp, keep = _pair_arrays(qs, rs)
+        nqa = (C.c_int64 * n)(*(nq if nq is not None else [len(x) for x in qs]))
+        nra = (C.c_int64 * n)(*(nr if nr is not None else [len(x) for x in rs]))
+        recs = (PairRecord * max(n, 1))()
+        self._check(self._L.sonar_align_pairs(self._h, n, qp, nqa, rp, nra, sample_rate, stft_window, hop,
+                                              feature_window, max_lag_seconds, workers, int(bool(device_ptrs)),
+                                              recs))
+        del keep
+        return records_dict(recs[:n])
+
     # -- path B ------------------------------------------------------------
     def ncc(self, a, b, max_lag):
         a, b = _f64(a), _f64(b)
@@ -592,3 +665,76 @@ class Context:
             q_pcm_len, r_pcm_len, sample_rate, feature_sample_rate, hop_size, window_size, max_lag_seconds,
             C.byref(h)))
         return self._result(h)
+
+
+class Multi:
+    """sonar_multi: one context per device + an RCCL communicator over them (one process)."""
+
+    def __init__(self, devices):
+        L = lib()
+        devs = (C.c_int32 * len(devices))(*devices)
+        h = C.c_void_p()
+        rc = L.sonar_multi_create(devs, len(devices), C.byref(h))
+        if rc != OK:
+            raise SonarError(rc, "sonar_multi_create failed (GPUs / RCCL)")
+        self._h, self._L, self.devices = h, L, list(devices)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.sonar_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != OK:
+            raise SonarError(rc, self._L.sonar_multi_last_error(self._h).decode())
+
+    def size(self):
+        return int(self._L.sonar_multi_size(self._h))
+
+    def fingerprint(self, pcm, cfg: FpConfig):
+        """sonar_fingerprint_multi (host PCM, host outputs): MFCC / magnitude / descriptors."""
+        F = stft_frames(len(pcm), cfg.window_size, cfg.hop_size)
+        if F <= 0:
+            raise SonarError(-2, "signal too short for given window size and hop size")
+        pdt = np.float32 if cfg.pcm_dtype == F32 else np.float64
+        odt = np.float32 if cfg.out_dtype == F32 else np.float64
+        x = np.ascontiguousarray(pcm, dtype=pdt)
+        res, o = {}, FpOut()
+        if cfg.flags & FP_MFCC:
+            res["mfcc"] = np.zeros((F, max(cfg.n_mfcc, 1)), odt)
+            o.mfcc = res["mfcc"].ctypes.data
+        if cfg.flags & FP_MAGNITUDE:
+            res["magnitude"] = np.zeros((F, cfg.window_size // 2 + 1), odt)
+            o.magnitude = res["magnitude"].ctypes.data
+        if cfg.flags & FP_SPECTRAL:
+            for k in ("centroid", "rolloff", "bandwidth", "flatness", "crest", "slope", "low_ratio", "high_ratio"):
+                res[k] = np.zeros(F, odt)
+                setattr(o, k, res[k].ctypes.data)
+        self._check(self._L.sonar_fingerprint_multi(self._h, x.ctypes.data, len(x), C.byref(cfg), C.byref(o)))
+        return res
+
+    def fingerprint_gather(self, pcm_ptrs, n, cfg: FpConfig, mfcc_ptrs):
+        """sonar_fingerprint_multi_gather: device slices in, the MFCC timeline on every device."""
+        G = len(pcm_ptrs)
+        pp = (C.c_void_p * G)(*pcm_ptrs)
+        mp = (C.c_void_p * G)(*mfcc_ptrs)
+        self._check(self._L.sonar_fingerprint_multi_gather(self._h, pp, n, C.byref(cfg), mp))
+
+    def align_pairs(self, qs, rs, sample_rate=44100, stft_window=1024, hop=256, feature_window=1024,
+                    max_lag_seconds=20.0, workers=16):
+        """sonar_align_pairs_multi: host streams, pair ranges per device, records all-gathered over RCCL."""
+        n = len(qs)
+        qp, rp, keep = _pair_arrays(qs, rs)
+        nqa = (C.c_int64 * n)(*[len(x) for x in qs])
+        nra = (C.c_int64 * n)(*[len(x) for x in rs])
+        recs = (PairRecord * max(n, 1))()
+        self._check(self._L.sonar_align_pairs_multi(self._h, n, qp, nqa, rp, nra, sample_rate, stft_window, hop,
+                                                    feature_window, max_lag_seconds, workers, recs))
+        del keep
+        return records_dict(recs[:n])

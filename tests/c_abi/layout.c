@@ -26,6 +26,7 @@ PIN(sonar_fp_features, 272);
 PIN(sonar_compare_cfg, 24);
 PIN(sonar_similarity, 136);
 PIN(sonar_match, 152);
+PIN(sonar_pair_record, 72);
 
 int main(void) {
   S(sonar_fp_cfg);
@@ -115,5 +116,10 @@ int main(void) {
 
   S(sonar_match);
   F(sonar_match, candidate); F(sonar_match, rank); F(sonar_match, match_type); F(sonar_match, similarity);
+  S(sonar_pair_record);
+  F(sonar_pair_record, temporal_offset); F(sonar_pair_record, offset_confidence);
+  F(sonar_pair_record, alignment_similarity); F(sonar_pair_record, alignment_quality);
+  F(sonar_pair_record, method); F(sonar_pair_record, corr_offset_seconds); F(sonar_pair_record, dtw_distance);
+  F(sonar_pair_record, peak_lag); F(sonar_pair_record, status); F(sonar_pair_record, reserved);
   return 0;
 }

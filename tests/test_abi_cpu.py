@@ -44,7 +44,8 @@ MIRRORS = {"sonar_fp_cfg": _abi.FpConfig, "sonar_fp_out": _abi.FpOut, "sonar_for
            "sonar_voice_quality_result": _abi.VoiceQuality, "sonar_fingerprint_config": _abi.FingerprintConfig,
            "sonar_feature_config": _abi.FeatureConfig, "sonar_alignment_stats": _abi.AlignmentStats,
            "sonar_acoustic_features": _abi.AcousticFeatures, "sonar_fp_features": _abi.FpFeatures,
-           "sonar_compare_cfg": _abi.CompareCfg, "sonar_similarity": _abi.Similarity, "sonar_match": _abi.Match}
+           "sonar_compare_cfg": _abi.CompareCfg, "sonar_similarity": _abi.Similarity, "sonar_match": _abi.Match,
+           "sonar_pair_record": _abi.PairRecord}
 
 
 def _c_layout():
