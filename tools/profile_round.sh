@@ -7,18 +7,18 @@ TAG=${1:-r01}
 R="$GRAFT_REPO_ROOT"; [ -z "$R" ] && R=/root/repo
 OUT="$R/gpurun_out/prof_$TAG"; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 "$R/bench.py" > "$OUT/bench_traced.log" 2>&1 || { echo "trace pass failed"; exit 1; }
 echo "trace done"
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/$c" -o run -- \
-      python3 "$R/bench.py" --no-cpu-baseline --dtw-len 0 --c5-pairs 0 --c6-gallery 0 --c7-seconds 0 --ingest-reps 0 --steps 5 --warmup 1 > "$OUT/$c.log" 2>&1 \
+      python3 "$R/bench.py" --no-cpu-baseline --dtw-len 0 --c5-pairs 0 --c6-gallery 0 --c7-seconds 0 --ingest-reps 0 --no-f64 --c3-seconds 0 --c4-seconds 0 --steps 5 --warmup 1 > "$OUT/$c.log" 2>&1 \
       || { echo "pmc $c failed"; exit 1; }
   echo "$c done"
 done
 # per-launch HBM bytes -> profiles/<tag>_traffic.json (read by bench.py's roofline.traffic)
 (cd "$R" && python3 tools/traffic_summary.py "$OUT" "$TAG" mfcc_pair_kernel > "$OUT/traffic_summary.log") \
     || { echo "traffic summary failed"; exit 1; }
-timeout -k 10 420 python3 "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; exit 1; }
+timeout -k 10 600 python3 "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; exit 1; }
 cat "$OUT/bench.json"
 cp "$OUT/bench.json" "$R/profiles/${TAG}_bench.json"
