@@ -233,18 +233,29 @@ constexpr int DTW_ECH = 8;                          // edge values polled per ch
 constexpr uint64_t DTW_SENT = 0x7FF000017FF00001ull;  // signalling NaN: never an arithmetic result
 constexpr int DTW_SPIN_LIMIT = 1 << 22;
 
-struct DtwArgs {
-  const double* q;
-  const double* r;
-  int dim, band;
-  int64_t nq, nr, nb, S, SW;
-  double* Cn;
-  uint32_t* Dn;
-  uint64_t* E;
-  int32_t* sync;   // [0] band ticket, [1] error flag
-  uint64_t* trace; // optional [nb][8]: t_start, t_first_edge, t_end, sweep wait ticks (s_memrealtime, 100 MHz),
-                   // shader clock at start and end (s_memtime), distance-wave-0 and code-wave wait ticks
+static_assert(sizeof(DtwArgs) % 4 == 0, "read as dwords");
+
+// Many independent DTWs in one band-kernel launch: a block's ticket t runs over every DTW's bands
+// in order (DTW k owns tickets [start[k], start[k+1])), so each DTW's bands still start in band
+// order, and a DTW's first band starts as soon as the previous DTW's last band holds a slot.
+struct DtwBatch {
+  const DtwArgs* args;
+  const int64_t* start;
+  int n;
+  int32_t* ticket;
 };
+
+namespace {
+// a DtwArgs at a wave-uniform address into SGPRs (every field read through readfirstlane)
+__device__ __forceinline__ DtwArgs load_args_uniform(const DtwArgs* p) {
+  DtwArgs r;
+  const int* src = reinterpret_cast<const int*>(p);
+  int* dst = reinterpret_cast<int*>(&r);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(DtwArgs) / 4); ++k) dst[k] = __builtin_amdgcn_readfirstlane(src[k]);
+  return r;
+}
+}  // namespace
 
 namespace {
 __device__ __forceinline__ double shr1(double v, double lane0) {
@@ -336,12 +347,23 @@ __device__ __forceinline__ int64_t dtw_cn_off(int64_t b, int64_t S2, int64_t s, 
   return ((b * S2 + (s >> 1)) << 7) + 2 * l + (s & 1);
 }
 
-template <int D, bool FAST, bool BANDED>
+// PRE: the local distances come precomputed from dtw_dist_kernel (a.Dd), so the block is only
+// the sweep, a distance LOADER wave (global -> the LDS distance ring, several chunks of loads in
+// flight), the code wave and the edge poller: 4 waves and no reference-row ring, which lets 4
+// blocks share a CU (every band of a 51,676-row problem resident at once)
+constexpr int dtw_block_waves(bool pre) { return pre ? 4 : DTW_WAVES; }
+#ifndef DTW_PF
+#define DTW_PF 4                  // loader: distance chunks of global loads in flight
+#endif
+template <int D, bool FAST, bool BANDED, bool BATCH = false, bool PRE = false>
 // (2 blocks of 7 waves per CU: at least 4 waves per SIMD, <= 128 VGPRs)
-__global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(DtwArgs a) {
+__global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
   constexpr int DR = D > 0 ? D : 1;
   constexpr int DS = dtw_ring_stride<D>();
-  __shared__ __attribute__((aligned(16))) double ring[(DTW_RROWS + DTW_RMIR) * DS];
+  constexpr int FEEDER_WAVE = PRE ? -1 : DTW_FEEDER_WAVE;
+  constexpr int CODE_WAVE = PRE ? 2 : DTW_CODE_WAVE;
+  constexpr int EDGE_WAVE = PRE ? 3 : DTW_EDGE_WAVE;
+  __shared__ __attribute__((aligned(16))) double ring[PRE ? 2 : (DTW_RROWS + DTW_RMIR) * DS];
   __shared__ __attribute__((aligned(16))) double dring[64][DTW_DROW];   // distance of step t at [l][t % DQ]
   __shared__ __attribute__((aligned(16))) double oring[64][DTW_OROW];   // C of step t at [l][t % OQ]
   __shared__ __attribute__((aligned(16))) double eqa[DTW_EQ];           // C[64b][c] at slot c - 1
@@ -351,6 +373,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
   // (highest ring block ready)
   __shared__ __attribute__((aligned(16))) int ctr[8];
   __shared__ int64_t shb;
+  __shared__ int shk;
 #define SONAR_LDS_LD(x) __hip_atomic_load(&(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
 #define SONAR_LDS_ST(x, v) __hip_atomic_store(&(x), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
   int& efill = ctr[3];
@@ -361,7 +384,18 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const double inf = __builtin_inf();
   if (threadIdx.x == 0) {
-    shb = atomicAdd(&a.sync[0], 1);
+    if constexpr (BATCH) {
+      const int64_t t = atomicAdd(bt.ticket, 1);
+      int lo = 0, hi = bt.n;                          // start[lo] <= t < start[lo + 1]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (bt.start[mid] <= t) lo = mid; else hi = mid;
+      }
+      shk = lo;
+      shb = t - bt.start[lo];                         // >= nb past the last DTW: the block exits
+    } else {
+      shb = atomicAdd(&a_in.sync[0], 1);
+    }
     for (int k = 0; k < 8; ++k) ctr[k] = 0;
     rdy = -1;
   }
@@ -371,6 +405,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
   }
   __syncthreads();
   const int64_t b = shb;
+  const DtwArgs a = BATCH ? load_args_uniform(bt.args + __builtin_amdgcn_readfirstlane(shk)) : a_in;
   if (b >= a.nb) return;
   const int64_t nq = a.nq, nr = a.nr, S = a.S, S2 = (a.S + 1) >> 1;
   const int dim = D > 0 ? D : a.dim;
@@ -400,10 +435,10 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
   } while (0)
 
-  if (wave == DTW_FEEDER_WAVE || wave == DTW_EDGE_WAVE) {
+  if (wave == FEEDER_WAVE || wave == EDGE_WAVE) {
     // ------------------------------------------------ ring feeder / edge poller
     // two waves, so the edge poll's global-load latency never delays a ring refill
-    const bool do_ring = wave == DTW_FEEDER_WAVE;
+    const bool do_ring = !PRE && wave == FEEDER_WAVE;
     int64_t nextblk = 0, have = 0;
     uint64_t idle = 0;
     const int64_t ecols = Ein ? nr : 0;
@@ -415,11 +450,11 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
 #pragma unroll
       for (int k = 0; k < DR; ++k) pv[k] = (lane < DTW_RBLK && row < nr) ? a.r[row * D + k] : 0.0;
     };
-    if constexpr (D > 0) prefetch(0);
+    if constexpr (D > 0 && !PRE) prefetch(0);
     while (true) {
       const int64_t p = SONAR_LDS_LD(prog), cp = SONAR_LDS_LD(cprog);
       bool work = false;
-      if (D > 0 && do_ring) {
+      if (D > 0 && !PRE && do_ring) {
         // block m overwrites rows up to r = RBLK*m - RROWS + RBLK - 1, which distance chunks up to
         // index (r + 63) / ECH read (chunk t0 reads rows t0-63 .. t0+7): all of them are done once
         // every distance wave's counter is above that index (wave w has finished every chunk
@@ -488,7 +523,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
     return;
   }
 
-  if (wave == DTW_CODE_WAVE) {
+  if (wave == CODE_WAVE) {
     // --------------------------------------------------------------- code wave
     // step s, lane l: up = C of lane l-1 at step s-1, left = own at s-1, diag = lane l-1 at s-2;
     // lane 0's left neighbour is the band's top edge: C[64b][s+1] / C[64b][s]
@@ -549,7 +584,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
   }
 
   double qv[DR];
-  if constexpr (D > 0) {
+  if constexpr (D > 0 && !PRE) {
 #pragma unroll
     for (int k = 0; k < D; ++k) qv[k] = a.q[qrow * D + k];
   }
@@ -569,7 +604,51 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
     return sqrt(sum);
   };
 
-  if (wave >= 1) {
+  if (PRE && wave == 1) {
+    // ---------------------------------------------------------- distance loader (PRE)
+    // chunk c = steps 8c .. 8c+7: four 16-B loads per lane (its pairs of steps in Dd), DTW_PF
+    // chunks ahead in registers; written to the distance ring once the sweep has freed the slots
+    // (the same rule as the distance waves), then every dchunk counter is set to c + 1
+    const double* Db = a.Dd + dtw_cn_off(b, S2, 0, lane);
+    const int64_t nch = (S + DTW_ECH - 1) / DTW_ECH;
+    double buf[DTW_PF][DTW_ECH];
+    auto fetch = [&](int64_t c, double (&v)[DTW_ECH]) {
+      const int64_t p0 = (DTW_ECH * c) >> 1;
+#pragma unroll
+      for (int u = 0; u < DTW_ECH / 2; ++u) {
+        double2 x = make_double2(0.0, 0.0);
+        if (p0 + u < S2) x = *reinterpret_cast<const double2*>(Db + ((p0 + u) << 7));
+        v[2 * u] = x.x;
+        v[2 * u + 1] = x.y;
+      }
+    };
+#pragma unroll
+    for (int k = 0; k < DTW_PF; ++k)
+      if (k < nch) fetch(k, buf[k]);
+    for (int64_t c0 = 0; c0 < nch; c0 += DTW_PF) {
+#pragma unroll
+      for (int k = 0; k < DTW_PF; ++k) {
+        const int64_t c = c0 + k;
+        if (c < nch) {
+          const int64_t t0 = DTW_ECH * c;
+          SONAR_SPIN_UNTIL(SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW_DQ);
+          double* drow = &dring[lane][t0 & (DTW_DQ - 1)];
+#pragma unroll
+          for (int u = 0; u < DTW_ECH; u += 2)
+            *reinterpret_cast<double2*>(drow + u) = make_double2(buf[k][u], buf[k][u + 1]);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) {
+            SONAR_LDS_ST(ctr[0], (int)(c + 1));
+            SONAR_LDS_ST(ctr[1], (int)(c + 1));
+            SONAR_LDS_ST(ctr[2], (int)(c + 1));
+          }
+          if (c + DTW_PF < nch) fetch(c + DTW_PF, buf[k]);
+        }
+      }
+    }
+    return;
+  }
+  if (!PRE && wave >= 1) {
     // ---------------------------------------------------------- distance waves
     const int w = wave - 1;
     for (int64_t c = w; DTW_ECH * c < S; c += DTW_NDW) {
@@ -798,8 +877,8 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
 // dynamic register indexing -- followed by scalar bit-field work.  The next band's window is
 // prefetched on band entry around the current column.
 #define DTW_WIN 16
-__global__ __launch_bounds__(64) void dtw_walk_kernel(const uint32_t* Dn, int64_t nq, int64_t nr, int64_t SW,
-                                                      uint32_t* codes, int64_t* plen) {
+__device__ __forceinline__ void dtw_walk_body(const uint32_t* Dn, int64_t nq, int64_t nr, int64_t SW,
+                                              uint32_t* codes, int64_t* plen) {
   const int lane = threadIdx.x;
   uint32_t win[DTW_WIN], nxt[DTW_WIN];
 #pragma unroll
@@ -883,6 +962,17 @@ __global__ __launch_bounds__(64) void dtw_walk_kernel(const uint32_t* Dn, int64_
   if (lane == 0) *plen = P;
 }
 
+__global__ __launch_bounds__(64) void dtw_walk_kernel(const uint32_t* Dn, int64_t nq, int64_t nr, int64_t SW,
+                                                      uint32_t* codes, int64_t* plen) {
+  dtw_walk_body(Dn, nq, nr, SW, codes, plen);
+}
+
+// one block per DTW of a batch (the walks are independent)
+__global__ __launch_bounds__(64) void dtw_walk_batch_kernel(const DtwArgs* args) {
+  const DtwArgs a = load_args_uniform(args + blockIdx.x);
+  dtw_walk_body(a.Dn, a.nq, a.nr, a.SW, a.codes, a.plen);
+}
+
 namespace {
 __device__ __forceinline__ double cn_at(const double* Cn, int64_t S, int64_t i, int64_t j) {
   if (i == 0) return j == 0 ? 0.0 : __builtin_inf();
@@ -900,10 +990,17 @@ __device__ __forceinline__ double cn_at(const double* Cn, int64_t S, int64_t i, 
 //  dtw_path_points_kernel (one thread per word): replays its 16 moves from that cell.  Point k
 //    of the walk is (i_k - 1, j_k - 1) with cost C[i][j] - C[i-1][j-1] (0 on the borders);
 //    output is in forward order (index P-1-k).  The 32 cost loads of a thread are independent.
+// (BATCH: one block per DTW of a batch, its P read from the walk's output, and C[nq][nr] saved)
+template <bool BATCH>
 __global__ __launch_bounds__(1024) void dtw_path_scan_kernel(const uint32_t* codes, int64_t P, int64_t nq,
-                                                             int64_t nr, int2* wstart) {
+                                                             int64_t nr, int2* wstart, const DtwArgs* args) {
   __shared__ int64_t wsum[2][16];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if constexpr (BATCH) {
+    const DtwArgs a = load_args_uniform(args + blockIdx.x);
+    codes = a.codes; P = *a.plen; nq = a.nq; nr = a.nr; wstart = a.wstart;
+    if (t == 0) *a.cnm = cn_at(a.Cn, a.S, nq, nr);
+  }
   const int64_t nw = (P + 15) >> 4;
   const int64_t per = (nw + 1023) / 1024;
   const int64_t w0 = t * per < nw ? t * per : nw, w1 = (t + 1) * per < nw ? (t + 1) * per : nw;
@@ -940,9 +1037,15 @@ __global__ __launch_bounds__(1024) void dtw_path_scan_kernel(const uint32_t* cod
   }
 }
 
+// (BATCH: blockIdx.y = the DTW of a batch)
+template <bool BATCH>
 __global__ __launch_bounds__(256) void dtw_path_points_kernel(const uint32_t* codes, const int2* wstart, int64_t P,
                                                               const double* Cn, int64_t S, int32_t* pq, int32_t* pr,
-                                                              double* pc) {
+                                                              double* pc, const DtwArgs* args) {
+  if constexpr (BATCH) {
+    const DtwArgs a = load_args_uniform(args + blockIdx.y);
+    codes = a.codes; wstart = a.wstart; P = *a.plen; Cn = a.Cn; S = a.S; pq = a.pq; pr = a.pr; pc = a.pc;
+  }
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= ((P + 15) >> 4)) return;
   const uint32_t x = codes[w];
@@ -990,6 +1093,66 @@ __global__ __launch_bounds__(256) void dtw_cost_rowmajor_kernel(const double* Cn
   }
 }
 
+// Local distances (EuclideanDistanceFunc, distance.go:29-36: Go's sequential sum, unfused, then
+// sqrt) of every band-step cell into Dd, in Cn's paired band-skewed layout, for the PRE band
+// kernel.  Block = band b x 64 steps; the 127 reference rows those steps touch are staged in LDS
+// (rows padded to 14 doubles: conflict-free 16-B reads), lane l keeps query row 64b+l in
+// registers, and wave w computes steps 16w .. 16w+15 as 8 interleaved chains at a time.  Cells
+// outside the matrix get 0 (the sweep never stores them).
+constexpr int DTW_DIST_TS = 64;
+template <int D>
+__global__ __launch_bounds__(256) void dtw_dist_kernel(const double* q, const double* r, int64_t nq, int64_t nr,
+                                                       int64_t S, double* Dd) {
+  static_assert(D == 12, "the precomputed path is built for chroma (12 dimensions)");
+  constexpr int DS = dtw_ring_stride<D>();
+  constexpr int NR = DTW_DIST_TS + 63;
+  __shared__ __attribute__((aligned(16))) double rr[NR * DS];
+  const int64_t b = blockIdx.y, s0 = (int64_t)blockIdx.x * DTW_DIST_TS, S2 = (S + 1) >> 1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t rbase = s0 - 63;                    // reference row (j - 1) of local row 0
+  for (int e = threadIdx.x; e < NR * D; e += 256) {
+    const int row = e / D, k = e - row * D;
+    const int64_t jr = rbase + row;
+    rr[row * DS + k] = (jr >= 0 && jr < nr) ? r[jr * D + k] : 0.0;
+  }
+  const int64_t i0 = 64 * b + lane;                 // query row (i - 1)
+  double qv[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) qv[k] = i0 < nq ? q[i0 * D + k] : 0.0;
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < 16; g += 8) {
+    const int sl = 16 * w + g;                        // local step of chain 0
+    const double* rw0 = rr + (sl - lane + 63) * DS;   // local row of (step sl, lane)
+    double sum[8];
+#pragma unroll
+    for (int k = 0; k < D; k += 2) {
+      double2 rv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) rv[u] = *reinterpret_cast<const double2*>(rw0 + u * DS + k);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double d0 = qv[k] - rv[u].x;
+        sum[u] = k == 0 ? d0 * d0 : sum[u] + d0 * d0;   // 0.0 + x == x for x >= +0 or NaN
+        const double d1 = qv[k + 1] - rv[u].y;
+        sum[u] = sum[u] + d1 * d1;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      const int64_t s = s0 + sl + u;
+      if ((s >> 1) >= S2) break;
+      double v[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t jr = s + h - lane;
+        v[h] = (i0 < nq && jr >= 0 && jr < nr) ? sqrt(sum[u + h]) : 0.0;
+      }
+      *reinterpret_cast<double2*>(Dd + dtw_cn_off(b, S2, s, lane)) = make_double2(v[0], v[1]);
+    }
+  }
+}
+
 __global__ void nonfinite_kernel(const double* x, int64_t n, int32_t* flag) {
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
     if (!__builtin_isfinite(x[k])) *flag = 1;
@@ -1011,25 +1174,45 @@ int64_t dtw_cn_index(const DtwGeom& g, int64_t i, int64_t j) {
   return ((b * ((g.S + 1) / 2) + (s >> 1)) << 7) + 2 * l + (s & 1);
 }
 
+void launch_dtw_dist(const double* q, const double* r, const DtwGeom& g, double* Dd, hipStream_t s) {
+  const dim3 grid((unsigned)((g.S + DTW_DIST_TS - 1) / DTW_DIST_TS), (unsigned)g.nb);
+  hipLaunchKernelGGL(dtw_dist_kernel<12>, grid, dim3(256), 0, s, q, r, g.nq, g.nr, g.S, Dd);
+}
+
 int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, const DtwGeom& g, double* Cn,
                uint32_t* Dn, uint64_t* E, int32_t* sync_words, uint32_t* codes, int64_t* plen, uint64_t* trace,
-               hipStream_t s, hipEvent_t mid) {
+               hipStream_t s, hipEvent_t mid, double* Dd) {
   if (hipMemsetAsync(sync_words, 0, 2 * sizeof(int32_t), s) != hipSuccess) return -5;
   if (g.nb > 1 && hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, dtw_edge_bytes(g) / 4, s) != hipSuccess) return -5;
   DtwArgs a{q, r, dim, band, g.nq, g.nr, g.nb, g.S, g.SW, Cn, Dn, reinterpret_cast<uint64_t*>(E), sync_words,
             trace};
-  const dim3 grid((unsigned)g.nb), block(64 * DTW_WAVES);
+  const DtwBatch nob{};
+  const bool pre = Dd && dim == 12;
+  if (pre) {
+    a.Dd = Dd;
+    launch_dtw_dist(q, r, g, Dd, s);
+  }
+  const dim3 grid((unsigned)g.nb), block(64 * DTW_WAVES), pblock(64 * dtw_block_waves(true));
 #define SONAR_DTW_LAUNCH(DD)                                                                          \
   do {                                                                                                \
     if (band > 0) {                                                                                   \
-      if (fast) hipLaunchKernelGGL((dtw_band_kernel<DD, true, true>), grid, block, 0, s, a);          \
-      else hipLaunchKernelGGL((dtw_band_kernel<DD, false, true>), grid, block, 0, s, a);              \
+      if (fast) hipLaunchKernelGGL((dtw_band_kernel<DD, true, true>), grid, block, 0, s, a, nob);     \
+      else hipLaunchKernelGGL((dtw_band_kernel<DD, false, true>), grid, block, 0, s, a, nob);         \
     } else {                                                                                          \
-      if (fast) hipLaunchKernelGGL((dtw_band_kernel<DD, true, false>), grid, block, 0, s, a);         \
-      else hipLaunchKernelGGL((dtw_band_kernel<DD, false, false>), grid, block, 0, s, a);             \
+      if (fast) hipLaunchKernelGGL((dtw_band_kernel<DD, true, false>), grid, block, 0, s, a, nob);    \
+      else hipLaunchKernelGGL((dtw_band_kernel<DD, false, false>), grid, block, 0, s, a, nob);        \
     }                                                                                                 \
   } while (0)
-  if (dim == 12) SONAR_DTW_LAUNCH(12);
+  if (pre) {
+    if (band > 0) {
+      if (fast) hipLaunchKernelGGL((dtw_band_kernel<12, true, true, false, true>), grid, pblock, 0, s, a, nob);
+      else hipLaunchKernelGGL((dtw_band_kernel<12, false, true, false, true>), grid, pblock, 0, s, a, nob);
+    } else {
+      if (fast) hipLaunchKernelGGL((dtw_band_kernel<12, true, false, false, true>), grid, pblock, 0, s, a, nob);
+      else hipLaunchKernelGGL((dtw_band_kernel<12, false, false, false, true>), grid, pblock, 0, s, a, nob);
+    }
+  }
+  else if (dim == 12) SONAR_DTW_LAUNCH(12);
   else if (dim == 1) SONAR_DTW_LAUNCH(1);
   else SONAR_DTW_LAUNCH(0);
 #undef SONAR_DTW_LAUNCH
@@ -1042,9 +1225,38 @@ int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const uint32_t* cod
                          int32_t* pq, int32_t* pr, double* pc, hipStream_t s) {
   if (P <= 0) return 0;
   const int64_t nw = (P + 15) >> 4;
-  hipLaunchKernelGGL(dtw_path_scan_kernel, dim3(1), dim3(1024), 0, s, codes, P, g.nq, g.nr, wstart);
-  hipLaunchKernelGGL(dtw_path_points_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, codes,
-                     (const int2*)wstart, P, Cn, g.S, pq, pr, pc);
+  hipLaunchKernelGGL(dtw_path_scan_kernel<false>, dim3(1), dim3(1024), 0, s, codes, P, g.nq, g.nr, wstart,
+                     (const DtwArgs*)nullptr);
+  hipLaunchKernelGGL(dtw_path_points_kernel<false>, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, codes,
+                     (const int2*)wstart, P, Cn, g.S, pq, pr, pc, (const DtwArgs*)nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
+                     int64_t max_cap, int32_t* ticket, hipStream_t s) {
+  if (n <= 0 || total_bands <= 0) return 0;
+  if (total_bands > INT32_MAX) return -1;
+  const DtwArgs none{};
+  const DtwBatch bt{dargs, dstart, n, ticket};
+  const bool pre = hargs[0].Dd != nullptr;
+  if (pre) {
+    for (int k = 0; k < n; ++k) {
+      const DtwGeom g = dtw_geom(hargs[k].nq, hargs[k].nr);
+      launch_dtw_dist(hargs[k].q, hargs[k].r, g, hargs[k].Dd, s);
+    }
+    hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true, true>), dim3((unsigned)total_bands),
+                       dim3(64 * dtw_block_waves(true)), 0, s, none, bt);
+  } else {
+    hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
+                       0, s, none, bt);
+  }
+  hipLaunchKernelGGL(dtw_walk_batch_kernel, dim3((unsigned)n), dim3(64), 0, s, dargs);
+  hipLaunchKernelGGL(dtw_path_scan_kernel<true>, dim3((unsigned)n), dim3(1024), 0, s, (const uint32_t*)nullptr,
+                     (int64_t)0, (int64_t)0, (int64_t)0, (int2*)nullptr, dargs);
+  const int64_t nw = (max_cap + 15) >> 4;
+  hipLaunchKernelGGL(dtw_path_points_kernel<true>, dim3((unsigned)((nw + 255) / 256), (unsigned)n), dim3(256), 0, s,
+                     (const uint32_t*)nullptr, (const int2*)nullptr, (int64_t)0, (const double*)nullptr, (int64_t)0,
+                     (int32_t*)nullptr, (int32_t*)nullptr, (double*)nullptr, dargs);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

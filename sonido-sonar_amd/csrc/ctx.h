@@ -41,9 +41,10 @@ struct sonar_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   std::map<std::string, DevBuf> bufs;
+  std::map<std::string, DevBuf> hbufs;   // pinned host staging (hipHostMalloc)
   std::map<std::string, FpTables> fp_tables;
   std::map<std::string, PairTables> pair_tables;
-  struct ChromaT { void* win; void* trig; void* map; };
+  struct ChromaT { void* win; void* trig; void* map; void* cls; };
   std::map<std::string, ChromaT> chroma_tables;
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;   // spare pair (kept for ABI simplicity)
@@ -78,6 +79,42 @@ namespace sonar {
 namespace detail {
 int fail(sonar_ctx* c, int code, const std::string& msg);
 void* dbuf(sonar_ctx* c, const std::string& name, size_t bytes);
+void* hbuf(sonar_ctx* c, const std::string& name, size_t bytes);
+// DTW with the local distances precomputed (dtw_dist_kernel + the 4-wave band kernel) for this
+// feature dimension; opt-in with SONAR_DTW_PRE=1 (the distance waves inside the band kernel are
+// the default: faster at C3 and C5 sizes)
+bool dtw_pre_enabled(int dim);
+// NCC + chroma DTW of one stream pair with two stream synchronisations (align_impl's device
+// path, sonar_api.cpp): ncc_enqueue and dtw_enqueue only launch and queue their small results
+// into pinned host memory; after one hipStreamSynchronize, ncc_metrics_host reads the
+// correlation and dtw_finish decodes the warping path into pinned host arrays (second sync).
+struct DtwPending {
+  const double *dq = nullptr, *dr = nullptr;
+  int64_t nq = 0, nr = 0;
+  int32_t dim = 0, band = -1;
+  int64_t* st = nullptr;   // pinned: [0] path length, [1] sync words 0..1, [2] non-finite flag
+};
+int ncc_enqueue(sonar_ctx* c, const double* da, int64_t na, const double* db, int64_t nb, int32_t max_lag,
+                double** hcorr, int64_t* L);
+void ncc_metrics_host(const double* corr, int64_t L, int64_t na, int64_t nb, double* metrics);
+int dtw_enqueue(sonar_ctx* c, const double* dq, int64_t nq, const double* dr, int64_t nr, int32_t dim, int32_t band,
+                DtwPending* p);
+int dtw_finish(sonar_ctx* c, DtwPending* p, const int32_t** hq, const int32_t** hr, const double** hc, int64_t* P,
+               double* distance);
+// ExtractAlignmentFeatures' host tail over the GPU results of one pair (go_api.cpp): the scorers,
+// selectBestAlignment and the time-stretch estimate, into a result handle and/or a pair record
+struct AlignIn {
+  const double* corr = nullptr;   // energy correlation, 2L+1 lags (null: no correlation candidate)
+  int64_t L = 0, nqe = 0, nre = 0, mlf = 0;
+  bool has_dtw = false;           // chroma DTW candidate
+  const int32_t *pq = nullptr, *pr = nullptr;
+  const double* pc = nullptr;
+  int64_t P = 0, nqc = 0, nrc = 0;
+  double dist = 0.0;
+  int64_t q_pcm_len = 0, r_pcm_len = 0;
+  int32_t sample_rate = 0, hop = 0;
+};
+void align_finish(const AlignIn& in, sonar_result* res, sonar_pair_record* rec);
 hipEvent_t timed_begin(sonar_ctx* c, hipStream_t s);
 // ContentDetector (content_api.cpp)
 int detect_from_audio(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, double thr, int32_t* out,

@@ -473,94 +473,66 @@ int sonar_music_alignment_features(sonar_ctx* c, const double* pcm, int64_t n, i
 
 }  // extern "C"
 
-namespace {
+namespace sonar {
+namespace detail {
 
-// AlignmentExtractor.ExtractAlignmentFeatures body; dev = the four feature arrays are device
-// pointers on the ctx's device (no H2D), else host arrays
-int align_impl(sonar_ctx* c, const double* qe, int64_t nqe, const double* re, int64_t nre, const double* qc,
-               int64_t nqc, const double* rc_, int64_t nrc, int64_t q_pcm_len, int64_t r_pcm_len,
-               int32_t sample_rate, int32_t feature_sample_rate, int32_t hop, int32_t win,
-               double max_lag_seconds, int32_t dev, sonar_result** out) {
-  if (!c || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
-  *out = nullptr;
-  if (hop <= 0) return fail(c, SONAR_ERR_INVALID, "hop size must be positive (NewAlignmentExtractor divides by it)");
-  (void)win;
-  const int64_t max_lag_samples = (int64_t)(max_lag_seconds * (double)feature_sample_rate);   // alignment.go:104
-  auto* res = new sonar_result();
-  const double qlen = (double)q_pcm_len / (double)sample_rate, rlen = (double)r_pcm_len / (double)sample_rate;
-  res->scalar("query_length", qlen);
-  res->scalar("reference_length", rlen);
-
+// ExtractAlignmentFeatures after the GPU work (alignment.go:139-476): the candidates' scorers,
+// selectBestAlignment (:412-446) and estimateTimeStretch (:448-476)
+void align_finish(const AlignIn& in, sonar_result* res, sonar_pair_record* rec) {
+  const double qlen = (double)in.q_pcm_len / (double)in.sample_rate, rlen = (double)in.r_pcm_len / (double)in.sample_rate;
+  if (res) {
+    res->scalar("query_length", qlen);
+    res->scalar("reference_length", rlen);
+  }
+  if (rec) {
+    std::memset(rec, 0, sizeof(*rec));
+    rec->temporal_offset = rec->offset_confidence = rec->alignment_similarity = rec->alignment_quality = NAN;
+    rec->corr_offset_seconds = rec->dtw_distance = rec->peak_lag = NAN;
+  }
   struct Cand { bool ok = false; int type = 0; sonar::host::AlignScores s; bool dtw = false;
                 int64_t p0q = 0, p0r = 0, p1q = 0, p1r = 0, plen = 0; };
   Cand corr, chroma;
-  // 2. energy cross-correlation (performMultiFeatureAlignment :320-333 -> alignWithFeatures :357-410)
-  if (qe && re && nqe > 0 && nre > 0) {
-    const int64_t minf = std::min(nqe, nre);
-    int64_t mlf = max_lag_samples / hop;
-    mlf = std::min(mlf, minf - 1);
-    const int64_t L = std::max<int64_t>(0, std::min({mlf, nqe - 1, nre - 1}));
-    std::vector<double> cr(2 * L + 1), met(10);
-    double* dcorr = dev ? (double*)dbuf(c, "al.corr", (2 * L + 1) * 8) : nullptr;
-    if (dev && !dcorr) { delete res; return fail(c, SONAR_ERR_NOMEM, "device allocation failed"); }
-    int rc = sonar_ncc(c, qe, nqe, re, nre, (int32_t)mlf, dev ? dcorr : cr.data(), met.data(), dev);
-    if (rc == SONAR_OK && dev) rc = d2h(c, cr, dcorr, cr.size());   // sonar_ncc synchronised the stream
-    if (rc == SONAR_OK && dev && hipStreamSynchronize(c->stream) != hipSuccess) rc = SONAR_ERR_DEVICE;
-    if (rc != SONAR_OK) { delete res; return rc; }
-    sonar::host::NccMetrics m;
-    m.peak_corr = met[0]; m.peak_lag = (int64_t)met[1]; m.peak_index = (int64_t)met[2]; m.p_value = met[3];
-    m.snr = met[4]; m.sharpness = met[5]; m.second_peak = met[6]; m.psl = met[7]; m.overlap = (int64_t)met[8];
-    m.num_lags = (int64_t)met[9];
+  if (in.corr) {     // alignWithFeatures (:357-410) on the energy correlation
+    const auto m = sonar::host::ncc_metrics(in.corr, 2 * in.L + 1, in.L, in.nqe, in.nre);
     corr.ok = true; corr.type = 1;
-    corr.s = sonar::host::xcorr_scores(m, hop, sample_rate, (int)mlf);
-    res->vec("correlations", cr);
-    res->scalar("peak_lag", (double)m.peak_lag);
-    res->scalar("peak_correlation", m.peak_corr);
-    res->scalar("corr_snr", m.snr);
-    res->scalar("corr_sharpness", m.sharpness);
-    res->scalar("corr_peak_to_sidelobe", m.psl);
-    res->scalar("corr_offset", (double)corr.s.offset);
-    res->scalar("corr_offset_seconds", corr.s.offset_seconds);
-    res->scalar("corr_similarity", corr.s.similarity);
-    res->scalar("corr_confidence", corr.s.confidence);
-    res->scalar("corr_quality", corr.s.quality);
-    res->scalar("corr_noise_level", corr.s.noise_level);
-  }
-  // 4. chroma DTW (:346-351)
-  if (qc && rc_ && nqc > 0 && nrc > 0) {
-    const int64_t cap = nqc + nrc + 1;
-    std::vector<int32_t> pq(cap), pr(cap);
-    std::vector<double> pc(cap);
-    int64_t P = 0; double dist = 0;
-    int32_t* dpq = dev ? (int32_t*)dbuf(c, "al.pq", cap * 4) : nullptr;
-    int32_t* dpr = dev ? (int32_t*)dbuf(c, "al.pr", cap * 4) : nullptr;
-    double* dpc = dev ? (double*)dbuf(c, "al.pc", cap * 8) : nullptr;
-    if (dev && (!dpq || !dpr || !dpc)) { delete res; return fail(c, SONAR_ERR_NOMEM, "device allocation failed"); }
-    int rc = sonar_dtw(c, qc, nqc, rc_, nrc, 12, -1, &dist, dev ? dpq : pq.data(), dev ? dpr : pr.data(),
-                       dev ? dpc : pc.data(), &P, nullptr, dev);
-    if (rc == SONAR_OK && dev && P > 0) {
-      rc = d2h(c, pq, dpq, (size_t)P);
-      if (rc == SONAR_OK) rc = d2h(c, pr, dpr, (size_t)P);
-      if (rc == SONAR_OK) rc = d2h(c, pc, dpc, (size_t)P);
-      if (rc == SONAR_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = SONAR_ERR_DEVICE;
+    corr.s = sonar::host::xcorr_scores(m, in.hop, in.sample_rate, (int)in.mlf);
+    if (rec) { rec->peak_lag = (double)m.peak_lag; rec->corr_offset_seconds = corr.s.offset_seconds; }
+    if (res) {
+      res->vec("correlations", std::vector<double>(in.corr, in.corr + 2 * in.L + 1));
+      res->scalar("peak_lag", (double)m.peak_lag);
+      res->scalar("peak_correlation", m.peak_corr);
+      res->scalar("corr_snr", m.snr);
+      res->scalar("corr_sharpness", m.sharpness);
+      res->scalar("corr_peak_to_sidelobe", m.psl);
+      res->scalar("corr_offset", (double)corr.s.offset);
+      res->scalar("corr_offset_seconds", corr.s.offset_seconds);
+      res->scalar("corr_similarity", corr.s.similarity);
+      res->scalar("corr_confidence", corr.s.confidence);
+      res->scalar("corr_quality", corr.s.quality);
+      res->scalar("corr_noise_level", corr.s.noise_level);
     }
-    if (rc != SONAR_OK) { delete res; return rc; }
+  }
+  if (in.has_dtw) {  // alignWithDTW (:129-148)
+    const int64_t P = in.P;
     chroma.ok = true; chroma.type = 2; chroma.dtw = true;
-    chroma.s = sonar::host::dtw_scores(pq.data(), pr.data(), pc.data(), P, nqc, nrc, dist, sample_rate);
+    chroma.s = sonar::host::dtw_scores(in.pq, in.pr, in.pc, P, in.nqc, in.nrc, in.dist, in.sample_rate);
     chroma.plen = P;
-    if (P > 0) { chroma.p0q = pq[0]; chroma.p0r = pr[0]; chroma.p1q = pq[P - 1]; chroma.p1r = pr[P - 1]; }
-    std::vector<double> vq(P), vr(P), vc(P);
-    for (int64_t i = 0; i < P; i++) { vq[i] = pq[i]; vr[i] = pr[i]; vc[i] = pc[i]; }
-    res->scalar("dtw_distance", dist);
-    res->vec("dtw_path_query", vq);
-    res->vec("dtw_path_reference", vr);
-    res->vec("dtw_path_cost", vc);
-    res->scalar("dtw_offset", (double)chroma.s.offset);
-    res->scalar("dtw_offset_seconds", chroma.s.offset_seconds);
-    res->scalar("dtw_similarity", chroma.s.similarity);
-    res->scalar("dtw_confidence", chroma.s.confidence);
-    res->scalar("dtw_quality", chroma.s.quality);
-    res->scalar("dtw_stability", chroma.s.stability);
+    if (P > 0) { chroma.p0q = in.pq[0]; chroma.p0r = in.pr[0]; chroma.p1q = in.pq[P - 1]; chroma.p1r = in.pr[P - 1]; }
+    if (rec) rec->dtw_distance = in.dist;
+    if (res) {
+      std::vector<double> vq(P), vr(P), vc(P);
+      for (int64_t i = 0; i < P; i++) { vq[i] = in.pq[i]; vr[i] = in.pr[i]; vc[i] = in.pc[i]; }
+      res->scalar("dtw_distance", in.dist);
+      res->vec("dtw_path_query", vq);
+      res->vec("dtw_path_reference", vr);
+      res->vec("dtw_path_cost", vc);
+      res->scalar("dtw_offset", (double)chroma.s.offset);
+      res->scalar("dtw_offset_seconds", chroma.s.offset_seconds);
+      res->scalar("dtw_similarity", chroma.s.similarity);
+      res->scalar("dtw_confidence", chroma.s.confidence);
+      res->scalar("dtw_quality", chroma.s.quality);
+      res->scalar("dtw_stability", chroma.s.stability);
+    }
   }
   // selectBestAlignment (:412-446); Go iterates a map (random order) with strict >:
   // here corr_energy is visited first, so exact ties go to it deterministically
@@ -574,11 +546,20 @@ int align_impl(sonar_ctx* c, const double* qe, int64_t nqe, const double* re, in
   }
   double stretch = 1.0;                                           // estimateTimeStretch (:448-476)
   if (best) {
-    res->scalar("temporal_offset", best->s.offset_seconds);
-    res->scalar("offset_confidence", best->s.confidence);
-    res->scalar("alignment_similarity", best->s.similarity);
-    res->scalar("alignment_quality", best->s.quality);
-    res->scalar("method", (double)best->type);
+    if (res) {
+      res->scalar("temporal_offset", best->s.offset_seconds);
+      res->scalar("offset_confidence", best->s.confidence);
+      res->scalar("alignment_similarity", best->s.similarity);
+      res->scalar("alignment_quality", best->s.quality);
+      res->scalar("method", (double)best->type);
+    }
+    if (rec) {
+      rec->temporal_offset = best->s.offset_seconds;
+      rec->offset_confidence = best->s.confidence;
+      rec->alignment_similarity = best->s.similarity;
+      rec->alignment_quality = best->s.quality;
+      rec->method = (double)best->type;
+    }
     if (qlen > 0 && rlen > 0) {
       const double lr = qlen / rlen;
       stretch = lr;
@@ -587,12 +568,78 @@ int align_impl(sonar_ctx* c, const double* qe, int64_t nqe, const double* re, in
         if (rs > 0) stretch = 0.7 * (qs / rs) + 0.3 * lr;
       }
     }
-  } else {
+  } else if (res) {
     res->scalar("method", 0.0);
   }
-  if (corr.ok) res->scalar("feature_similarity_corr_energy", corr.s.similarity);
-  if (chroma.ok) res->scalar("feature_similarity_dtw_chroma", chroma.s.similarity);
-  res->scalar("time_stretch", stretch);
+  if (res) {
+    if (corr.ok) res->scalar("feature_similarity_corr_energy", corr.s.similarity);
+    if (chroma.ok) res->scalar("feature_similarity_dtw_chroma", chroma.s.similarity);
+    res->scalar("time_stretch", stretch);
+  }
+}
+
+}  // namespace detail
+}  // namespace sonar
+
+namespace {
+
+// AlignmentExtractor.ExtractAlignmentFeatures body; dev = the four feature arrays are device
+// pointers on the ctx's device (no H2D), else host arrays
+int align_impl(sonar_ctx* c, const double* qe, int64_t nqe, const double* re, int64_t nre, const double* qc,
+               int64_t nqc, const double* rc_, int64_t nrc, int64_t q_pcm_len, int64_t r_pcm_len,
+               int32_t sample_rate, int32_t feature_sample_rate, int32_t hop, int32_t win,
+               double max_lag_seconds, int32_t dev, sonar_result** out) {
+  if (!c || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (hop <= 0) return fail(c, SONAR_ERR_INVALID, "hop size must be positive (NewAlignmentExtractor divides by it)");
+  (void)win;
+  const int64_t max_lag_samples = (int64_t)(max_lag_seconds * (double)feature_sample_rate);   // alignment.go:104
+  const bool want_corr = qe && re && nqe > 0 && nre > 0, want_dtw = qc && rc_ && nqc > 0 && nrc > 0;
+  const int64_t mlf = want_corr ? std::min(max_lag_samples / hop, std::min(nqe, nre) - 1) : 0;
+  // device arrays: the NCC and the DTW are both queued before one stream synchronisation; their
+  // small results (correlation, path length, status words) arrive in pinned host memory
+  double* hcorr = nullptr;
+  int64_t hL = 0;
+  sonar::detail::DtwPending pend;
+  if (dev) {
+    HIP_TRY(c, hipSetDevice(c->device));
+    int st = SONAR_OK;
+    if (want_corr) st = sonar::detail::ncc_enqueue(c, qe, nqe, re, nre, (int32_t)mlf, &hcorr, &hL);
+    if (st == SONAR_OK && want_dtw) st = sonar::detail::dtw_enqueue(c, qc, nqc, rc_, nrc, 12, -1, &pend);
+    if (st != SONAR_OK) return st;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
+  sonar::detail::AlignIn in;
+  in.q_pcm_len = q_pcm_len; in.r_pcm_len = r_pcm_len; in.sample_rate = sample_rate; in.hop = hop;
+  std::vector<double> cr;
+  if (want_corr) {   // 2. energy cross-correlation (performMultiFeatureAlignment :320-333)
+    const int64_t L = std::max<int64_t>(0, std::min({mlf, nqe - 1, nre - 1}));
+    if (dev) {
+      cr.assign(hcorr, hcorr + 2 * hL + 1);
+    } else {
+      cr.resize(2 * L + 1);
+      const int rc = sonar_ncc(c, qe, nqe, re, nre, (int32_t)mlf, cr.data(), nullptr, 0);
+      if (rc != SONAR_OK) return rc;
+    }
+    in.corr = cr.data(); in.L = L; in.nqe = nqe; in.nre = nre; in.mlf = mlf;
+  }
+  std::vector<int32_t> vpq, vpr;
+  std::vector<double> vpc;
+  if (want_dtw) {    // 4. chroma DTW (:346-351)
+    int rc;
+    if (dev) {
+      rc = sonar::detail::dtw_finish(c, &pend, &in.pq, &in.pr, &in.pc, &in.P, &in.dist);
+    } else {
+      const int64_t cap = nqc + nrc + 1;
+      vpq.resize(cap); vpr.resize(cap); vpc.resize(cap);
+      rc = sonar_dtw(c, qc, nqc, rc_, nrc, 12, -1, &in.dist, vpq.data(), vpr.data(), vpc.data(), &in.P, nullptr, 0);
+      in.pq = vpq.data(); in.pr = vpr.data(); in.pc = vpc.data();
+    }
+    if (rc != SONAR_OK) return rc;
+    in.has_dtw = true; in.nqc = nqc; in.nrc = nrc;
+  }
+  auto* res = new sonar_result();
+  sonar::detail::align_finish(in, res, nullptr);
   *out = res;
   return SONAR_OK;
 }

@@ -96,8 +96,9 @@ int launch_period_rms(const double* y, const int64_t* start, const int64_t* len,
                       hipStream_t s);
 int launch_hnr_autocorr(const double* frame2048, double* ac, hipStream_t s);
 // Chroma STFT (misc_kernels.hip)
+// cls (nullable): [13 class offsets][bins ascending per class] -> wave-per-frame FFT kernel (fs 256 / 512)
 int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, const double* window,
-                  const double* trig, const int* chroma_map, double* out, hipStream_t s);
+                  const double* trig, const int* chroma_map, const int* cls, double* out, hipStream_t s);
 int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, double* scratch, hipStream_t s);
 size_t dc_preemph_scratch_bytes(int64_t n);
 // speech-extractor helpers (misc_kernels.hip)
@@ -131,12 +132,44 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
                uint32_t* Dn, uint64_t* E, int32_t* sync_words /* [0] ticket, [1] error */,
                uint32_t* codes /* walk moves, 2 bits each */, int64_t* plen,
                uint64_t* trace /* nullable, [nb][8] diagnostics */, hipStream_t s,
-               hipEvent_t mid = nullptr /* recorded between the sweep and the walk */);
+               hipEvent_t mid = nullptr /* recorded between the sweep and the walk */,
+               double* Dd = nullptr /* dim 12: dtw_cn_bytes of scratch -> precomputed distances */);
 // wstart: scratch of (P + 15) / 16 int2 (each code word's starting cell)
 int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const uint32_t* codes, int64_t P, int2* wstart,
                          int32_t* pq, int32_t* pr, double* pc, hipStream_t s);
 // costMatrix[1:] (nq x (nr+1), column 0 = +Inf) from the band-skewed store
 int launch_dtw_cost_rowmajor(const double* Cn, const DtwGeom& g, double* out, hipStream_t s);
+// One DTW's arguments (the band kernel's parameter; an array of them for launch_dtw_batch)
+struct DtwArgs {
+  const double* q;
+  const double* r;
+  int dim, band;
+  int64_t nq, nr, nb, S, SW;
+  double* Cn;
+  uint32_t* Dn;
+  uint64_t* E;
+  int32_t* sync;   // [0] band ticket, [1] error flag, [2] non-finite input flag
+  uint64_t* trace; // optional [nb][8]: t_start, t_first_edge, t_end, sweep wait ticks (s_memrealtime, 100 MHz),
+                   // shader clock at start and end (s_memtime), distance-wave-0 and code-wave wait ticks
+  // batched launches only (launch_dtw_batch): the walk / path-decode outputs of this DTW
+  uint32_t* codes;
+  int64_t* plen;
+  int2* wstart;
+  int32_t *pq, *pr;
+  double* pc;
+  double* cnm;     // C[nq][nr]
+  // precomputed local distances in Cn's layout (dtw_dist_kernel); null: computed inside the band kernel
+  double* Dd;
+};
+// n DTWs of 12-dim finite sequences, unbanded (the chroma DTWs of sonar_align_pairs), from a
+// device array of DtwArgs: the band kernel over all of them (block tickets run through DTW k's
+// bands at dstart[k] .. dstart[k+1]-1; dstart[n] = total_bands), the walks (one block each), the
+// path scans (which also save C[nq][nr]) and the path points, in four launches and no host
+// round trip.  The caller zeroes each DTW's sync words and *ticket and fills each E with the
+// sentinel words 0x7FF00001 first; max_cap >= every nq + nr + 1.
+// (hargs: the same array on the host; every Dd set -> distances precomputed per DTW first)
+int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
+                     int64_t max_cap, int32_t* ticket, hipStream_t s);
 // sets *flag = 1 if any of the n values is not finite
 int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 

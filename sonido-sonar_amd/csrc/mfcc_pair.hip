@@ -380,6 +380,11 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     }
     wave_lds_sync();
     // ---- DCT-II (+ lifter): lane = q + 16 f + 32 h, half h of the filters ----------------
+#ifdef MFCC_DBG_NODCT   // A/B diagnostics: the DCT's share of the kernel (the most MFMA could save)
+    if ((lane & 15) < p.n_mfcc && (lane >> 5) == 0 && 2 * pi + ((lane >> 4) & 1) < p.F)
+      p.out[(2 * pi + ((lane >> 4) & 1)) * p.n_mfcc + (lane & 15)] = reinterpret_cast<const float*>(wb + kLogOff)[lane & 15];
+    if (false)
+#endif
     {
       const int q = lane & 15, f = (lane >> 4) & 1, hh = lane >> 5;
       const int half = NH ? NH : (nmp >> 1);

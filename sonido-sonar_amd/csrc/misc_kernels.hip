@@ -285,6 +285,91 @@ __global__ __launch_bounds__(256) void chroma_kernel(const double* y, int64_t n,
   }
 }
 
+// chroma_kernel's FFT path for power-of-two frames of 256..2048 samples, one wave per frame and
+// 4 frames per block: the same radix-2 DIT butterflies (same pairs, twiddles and operation order,
+// so the same bits), but a lane holds the 4 points of a two-stage group in registers, so a frame
+// makes one LDS round trip per two stages with no block barrier after the twiddle table; |X|^2
+// folds into the 12 classes through per-class bin lists (ascending bins: chroma_kernel's order).
+// cls = [13 offsets][bins]: class b owns cls[13 + cls[b] .. 13 + cls[b+1]).
+template <int PPL>
+__global__ __launch_bounds__(256) void chroma_wave_kernel(const double* y, int64_t n, int64_t frames, int hop,
+                                                          const double* win, const double* trig_g, const int* cls,
+                                                          double* out) {
+  constexpr int FS = 64 * PPL, K = FS / 2 + 1;
+  constexpr int LG = PPL == 4 ? 8 : (PPL == 8 ? 9 : (PPL == 16 ? 10 : 11));
+  static_assert((1 << LG) == FS, "power-of-two frame");
+  __shared__ __attribute__((aligned(16))) double2 tw[FS / 2];
+  __shared__ __attribute__((aligned(16))) double2 xs[4][FS];
+  __shared__ double pw[4][K + 12];
+  for (int m = threadIdx.x; m < FS / 2; m += 256) tw[m] = reinterpret_cast<const double2*>(trig_g)[m];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t t = (int64_t)blockIdx.x * 4 + w;
+  if (t >= frames) return;
+  const int64_t s = t * hop;
+  double2* x = xs[w];
+  double* p = pw[w];
+#pragma unroll
+  for (int u = 0; u < PPL; ++u) {
+    const int i = lane + 64 * u;
+    const double v = (s + i < n) ? y[s + i] : 0.0;      // zero pad (music.go:351-357)
+    x[__brev((unsigned)i) >> (32 - LG)] = make_double2(v * win[i], 0.0);
+  }
+  // a ← a + t, b ← a - t with t = b * w (chroma_kernel's operation order)
+  auto bfly = [](double2& a, double2& b, double2 wv) {
+    const double tr = b.x * wv.x - b.y * wv.y, ti = b.x * wv.y + b.y * wv.x;
+    const double ar = a.x, ai = a.y;
+    a = make_double2(ar + tr, ai + ti);
+    b = make_double2(ar - tr, ai - ti);
+  };
+  int h = 1;
+  for (; 4 * h <= FS; h *= 4) {                          // stages h and 2h
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int ts1 = FS / (2 * h), ts2 = FS / (4 * h);
+#pragma unroll
+    for (int u = 0; u < PPL / 4; ++u) {
+      const int g = lane + 64 * u, k = g & (h - 1), p0 = ((g - k) << 2) + k;
+      double2 a0 = x[p0], a1 = x[p0 + h], a2 = x[p0 + 2 * h], a3 = x[p0 + 3 * h];
+      const double2 w1 = tw[k * ts1];
+      bfly(a0, a1, w1);
+      bfly(a2, a3, w1);
+      bfly(a0, a2, tw[k * ts2]);
+      bfly(a1, a3, tw[(k + h) * ts2]);
+      x[p0] = a0; x[p0 + h] = a1; x[p0 + 2 * h] = a2; x[p0 + 3 * h] = a3;
+    }
+  }
+  if (h < FS) {                                          // odd stage count: the last stage alone
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int u = 0; u < PPL / 2; ++u) {
+      const int k = lane + 64 * u;                       // h = FS / 2: twiddle step 1
+      double2 a0 = x[k], a1 = x[k + h];
+      bfly(a0, a1, tw[k]);
+      x[k] = a0; x[k + h] = a1;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  for (int k = lane; k < K; k += 64) {
+    const double2 c = x[k];
+    const double mag = hypot(c.x, c.y);
+    p[k] = mag * mag;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (lane < 12) {
+    double acc = 0.0;
+    for (int e = cls[lane]; e < cls[lane + 1]; ++e) acc += p[cls[13 + e]];
+    p[K + lane] = acc;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (lane < 12) {
+    double tot = 0.0;
+#pragma unroll
+    for (int b = 0; b < 12; ++b) tot += p[K + b];
+    const double v = p[K + lane];
+    out[t * 12 + lane] = (tot > 1e-10) ? v / tot : v;
+  }
+}
+
 int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, double alpha, int sr, void* out,
                int out_f64, hipStream_t s) {
   if (F <= 0) return 0;
@@ -360,8 +445,14 @@ int launch_hnr_autocorr(const double* frame2048, double* ac, hipStream_t s) {
 }
 
 int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, const double* window,
-                  const double* trig, const int* cmap, double* out, hipStream_t s) {
+                  const double* trig, const int* cmap, const int* cls, double* out, hipStream_t s) {
   if (frames <= 0) return 0;
+  if (cls && (fs == 256 || fs == 512)) {
+    const dim3 grid((unsigned)((frames + 3) / 4));
+    if (fs == 256) hipLaunchKernelGGL(chroma_wave_kernel<4>, grid, dim3(256), 0, s, y, n, frames, hop, window, trig, cls, out);
+    else hipLaunchKernelGGL(chroma_wave_kernel<8>, grid, dim3(256), 0, s, y, n, frames, hop, window, trig, cls, out);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+  }
   const int K = fs / 2 + 1;
   size_t lds = sizeof(double) * ((size_t)fs + K + 12);
   if (lds > 160 * 1024) return -4;

@@ -25,12 +25,14 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "ctx.h"
+#include "kernels.h"
 
 using sonar::detail::dbuf;
 using sonar::detail::fail;
@@ -103,6 +105,153 @@ int align_one(sonar_ctx* w, const double* q, int64_t nq, const double* r, int64_
 
 int elt_size(int32_t dtype) { return dtype == SONAR_F32 ? 4 : 8; }
 
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct PairGeo {
+  int64_t k = 0, nq = 0, nr = 0, Fq = 0, Fr = 0, Eq = 0, Er = 0, L = 0, mlf = 0, cap = 0;
+  bool corr = false;
+  sonar::DtwGeom g{};
+  size_t chroma = 0, cn = 0, dn = 0, e = 0, codes = 0, wst = 0, path = 0, corr_off = 0;   // region offsets
+};
+
+// device bytes one pair of a batch holds (chroma, the DTW stores, the path)
+size_t pair_bytes(const PairGeo& p) {
+  return al256((size_t)(p.Fq + p.Fr) * 96) + 2 * al256(sonar::dtw_cn_bytes(p.g)) + al256(sonar::dtw_dn_bytes(p.g)) +
+         al256(sonar::dtw_edge_bytes(p.g)) + al256((size_t)((p.cap + 1023) / 1024) * 256) +
+         al256((size_t)((p.cap + 15) / 16 + 1) * 8) + al256((size_t)p.cap * 16) + al256((size_t)(2 * p.L + 1) * 8);
+}
+
+// A batch of pairs on worker w's stream with one host synchronisation: every pair's music
+// features and energy NCC (stream-ordered launches), then ONE launch_dtw_batch over all their
+// chroma DTWs, then the correlations, path arrays and status words in three copies.  Pairs whose
+// chroma is not finite (the DTW ran the finite-input kernel) are redone one by one through
+// align_one (exact math.Min rules); their indices are appended to `redo`.
+int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* const* q_pcm, const double* const* r_pcm,
+                int32_t sr, int32_t sw, int32_t hop, int32_t fw, int32_t device_ptrs, sonar_pair_record* out,
+                std::vector<int64_t>* redo) {
+  const int n = (int)in.size();
+  if (n == 0) return SONAR_OK;
+  HIP_TRY(w, hipSetDevice(w->device));
+  hipStream_t s = w->stream;
+  std::vector<PairGeo> pg = in;
+  size_t chroma_b = 0, cn_b = 0, dn_b = 0, e_b = 0, codes_b = 0, wst_b = 0, path_b = 0, corr_b = 0;
+  int64_t maxE = 1, maxn = 1, max_cap = 1, total_bands = 0;
+  for (auto& p : pg) {
+    p.chroma = chroma_b; chroma_b += al256((size_t)(p.Fq + p.Fr) * 96);
+    p.cn = cn_b; cn_b += al256(sonar::dtw_cn_bytes(p.g));
+    p.dn = dn_b; dn_b += al256(sonar::dtw_dn_bytes(p.g));
+    p.e = e_b; e_b += al256(sonar::dtw_edge_bytes(p.g));
+    p.codes = codes_b; codes_b += al256((size_t)((p.cap + 1023) / 1024) * 256);
+    p.wst = wst_b; wst_b += al256((size_t)((p.cap + 15) / 16 + 1) * 8);
+    p.path = path_b; path_b += al256((size_t)p.cap * 16);
+    p.corr_off = corr_b; corr_b += al256((size_t)(2 * p.L + 1) * 8);
+    maxE = std::max({maxE, p.Eq, p.Er});
+    maxn = std::max({maxn, p.nq, p.nr});
+    max_cap = std::max(max_cap, p.cap);
+    total_bands += p.g.nb;
+  }
+  const size_t stat_b = al256((size_t)n * 32 + 16), args_b = al256((size_t)n * sizeof(sonar::DtwArgs)),
+               start_b = al256((size_t)(n + 1) * 8);
+  char* chroma = (char*)dbuf(w, "pb.chroma", chroma_b);
+  char* Cn = (char*)dbuf(w, "pb.Cn", cn_b);
+  const bool pre = sonar::detail::dtw_pre_enabled(12);
+  char* Dd = pre ? (char*)dbuf(w, "pb.Dd", cn_b) : nullptr;
+  char* Dn = (char*)dbuf(w, "pb.Dn", dn_b);
+  char* E = (char*)dbuf(w, "pb.E", e_b);
+  char* codes = (char*)dbuf(w, "pb.codes", codes_b);
+  char* wst = (char*)dbuf(w, "pb.wstart", wst_b);
+  char* path = (char*)dbuf(w, "pb.path", path_b);
+  char* corr = (char*)dbuf(w, "pb.corr", corr_b);
+  char* small = (char*)dbuf(w, "pb.small", stat_b + args_b + start_b);
+  double* eq = (double*)dbuf(w, "pb.eq", (size_t)maxE * 8);
+  double* er = (double*)dbuf(w, "pb.er", (size_t)maxE * 8);
+  double* xa = (double*)dbuf(w, "ncc.xa", (size_t)maxE * 8);
+  double* xb = (double*)dbuf(w, "ncc.xb", (size_t)maxE * 8);
+  double* st = (double*)dbuf(w, "ncc.stats", 64);
+  double* up_q = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.q", (size_t)maxn * 8);
+  double* up_r = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.r", (size_t)maxn * 8);
+  char* h = (char*)sonar::detail::hbuf(w, "pb.host", stat_b + args_b + start_b + corr_b + path_b);
+  if (!chroma || !Cn || (pre && !Dd) || !Dn || !E || !codes || !wst || !path || !corr || !small || !eq || !er || !xa || !xb || !st ||
+      (!device_ptrs && (!up_q || !up_r)) || !h)
+    return fail(w, SONAR_ERR_NOMEM, "allocation failed (pair batch)");
+  int32_t* dstat = (int32_t*)small;                 // per pair: [0..1] plen, [2..3] C[nq][nr], [4..7] sync
+  int32_t* ticket = (int32_t*)(small + (size_t)n * 32);
+  sonar::DtwArgs* dargs = (sonar::DtwArgs*)(small + stat_b);
+  int64_t* dstart = (int64_t*)(small + stat_b + args_b);
+  char* hstat = h;
+  sonar::DtwArgs* hargs = (sonar::DtwArgs*)(h + stat_b);
+  int64_t* hstart = (int64_t*)(h + stat_b + args_b);
+  char* hcorr = h + stat_b + args_b + start_b;
+  char* hpath = hcorr + corr_b;
+  HIP_TRY(w, hipMemsetAsync(small, 0, stat_b, s));
+  if (e_b) HIP_TRY(w, hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, e_b / 4, s));
+  int64_t acc = 0;
+  for (int i = 0; i < n; ++i) {
+    const PairGeo& p = pg[i];
+    const double *dq = q_pcm[p.k], *dr = r_pcm[p.k];
+    double* cq = (double*)(chroma + p.chroma);
+    double* cr = cq + p.Fq * 12;
+    if (!device_ptrs) {
+      HIP_TRY(w, hipMemcpyAsync(up_q, dq, (size_t)p.nq * 8, hipMemcpyHostToDevice, s));
+      HIP_TRY(w, hipMemcpyAsync(up_r, dr, (size_t)p.nr * 8, hipMemcpyHostToDevice, s));
+      dq = up_q; dr = up_r;
+    }
+    int rc = sonar_music_alignment_features(w, dq, p.nq, sr, sw, hop, fw, hop, eq, cq, 1);
+    if (rc == SONAR_OK) rc = sonar_music_alignment_features(w, dr, p.nr, sr, sw, hop, fw, hop, er, cr, 1);
+    if (rc != SONAR_OK) return rc;
+    if (p.corr && sonar::launch_ncc(eq, p.Eq, er, p.Er, p.L, xa, xb, st, (double*)(corr + p.corr_off), s) != 0)
+      return fail(w, SONAR_ERR_DEVICE, "ncc launch failed");
+    int32_t* sync = dstat + 8 * i + 4;
+    if (sonar::launch_nonfinite(cq, p.Fq * 12, sync + 2, s) || sonar::launch_nonfinite(cr, p.Fr * 12, sync + 2, s))
+      return fail(w, SONAR_ERR_DEVICE, "dtw launch failed");
+    sonar::DtwArgs& a = hargs[i];
+    a = sonar::DtwArgs{};
+    a.q = cq; a.r = cr; a.dim = 12; a.band = -1;
+    a.nq = p.g.nq; a.nr = p.g.nr; a.nb = p.g.nb; a.S = p.g.S; a.SW = p.g.SW;
+    a.Cn = (double*)(Cn + p.cn); a.Dn = (uint32_t*)(Dn + p.dn); a.E = (uint64_t*)(E + p.e); a.sync = sync;
+    a.codes = (uint32_t*)(codes + p.codes); a.plen = (int64_t*)(dstat + 8 * i); a.wstart = (int2*)(wst + p.wst);
+    a.pc = (double*)(path + p.path); a.pq = (int32_t*)(a.pc + p.cap); a.pr = a.pq + p.cap;
+    a.cnm = (double*)(dstat + 8 * i + 2);
+    a.Dd = pre ? (double*)(Dd + p.cn) : nullptr;
+    hstart[i] = acc;
+    acc += p.g.nb;
+  }
+  hstart[n] = acc;
+  HIP_TRY(w, hipMemcpyAsync(dargs, hargs, args_b + start_b, hipMemcpyHostToDevice, s));
+  if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s) != 0)
+    return fail(w, SONAR_ERR_DEVICE, "dtw batch launch failed");
+  HIP_TRY(w, hipMemcpyAsync(hstat, small, (size_t)n * 32, hipMemcpyDeviceToHost, s));
+  if (corr_b) HIP_TRY(w, hipMemcpyAsync(hcorr, corr, corr_b, hipMemcpyDeviceToHost, s));
+  HIP_TRY(w, hipMemcpyAsync(hpath, path, path_b, hipMemcpyDeviceToHost, s));
+  HIP_TRY(w, hipStreamSynchronize(s));
+  for (int i = 0; i < n; ++i) {
+    const PairGeo& p = pg[i];
+    const char* ps = hstat + (size_t)i * 32;
+    int64_t P;
+    double cnm;
+    int32_t sync[4];
+    std::memcpy(&P, ps, 8);
+    std::memcpy(&cnm, ps + 8, 8);
+    std::memcpy(sync, ps + 16, 16);
+    sonar_pair_record* rec = &out[p.k];
+    if (sync[2]) { redo->push_back(p.k); continue; }
+    if (sync[1]) {
+      std::memset(rec, 0, sizeof(*rec));
+      rec->status = fail(w, SONAR_ERR_DEVICE, "dtw band pipeline timed out");
+      continue;
+    }
+    sonar::detail::AlignIn ai;
+    ai.q_pcm_len = p.nq; ai.r_pcm_len = p.nr; ai.sample_rate = sr; ai.hop = hop;
+    if (p.corr) { ai.corr = (const double*)(hcorr + p.corr_off); ai.L = p.L; ai.nqe = p.Eq; ai.nre = p.Er; ai.mlf = p.mlf; }
+    const double* pc = (const double*)(hpath + p.path);
+    ai.has_dtw = true; ai.pc = pc; ai.pq = (const int32_t*)(pc + p.cap); ai.pr = ai.pq + p.cap;
+    ai.P = P; ai.nqc = p.Fq; ai.nrc = p.Fr; ai.dist = cnm / (double)P;   // dtw.go:88-91
+    sonar::detail::align_finish(ai, nullptr, rec);
+    rec->status = SONAR_OK;
+  }
+  return SONAR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -115,27 +264,101 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
   if (npairs < 0 || (npairs > 0 && (!q_pcm || !nq || !r_pcm || !nr || !out)))
     return fail(c, SONAR_ERR_INVALID, "null pair arrays");
   if (npairs == 0) return SONAR_OK;
-  const int nw = (int)std::min<int64_t>(workers > 0 ? workers : 16, npairs);
-  int rc = SONAR_OK;
-  std::vector<sonar_ctx*>& ws = workers_of(c, nw, &rc);
-  if (rc != SONAR_OK) return fail(c, rc, "worker context creation failed");
-  std::atomic<int64_t> next{0};
+  const int64_t inflight = workers > 0 ? workers : 16;
   std::atomic<int> first_err{SONAR_OK};
+  auto note = [&](int r, int64_t k, sonar_ctx* w) {
+    if (r == SONAR_OK) return;
+    int expect = SONAR_OK;
+    if (first_err.compare_exchange_strong(expect, r)) c->err = std::string("pair ") + std::to_string(k) + ": " + w->err;
+  };
+  // SONAR_PAIR_BATCH=0: one pair at a time per worker stream (the unbatched path, for A/B)
+  const char* bev = std::getenv("SONAR_PAIR_BATCH");
+  const bool batched = !(bev && std::atoi(bev) == 0);
+  const char* sev = std::getenv("SONAR_PAIR_STREAMS");
+  const int nstreams = batched ? (int)std::max<int64_t>(1, std::min<int64_t>(sev ? std::atoi(sev) : 8, npairs))
+                               : (int)std::min<int64_t>(inflight, npairs);
+  int rc = SONAR_OK;
+  std::vector<sonar_ctx*>& ws = workers_of(c, nstreams, &rc);
+  if (rc != SONAR_OK) return fail(c, rc, "worker context creation failed");
   std::vector<std::thread> th;
-  for (int t = 0; t < nw; ++t) {
+  if (!batched) {
+    std::atomic<int64_t> next{0};
+    for (int t = 0; t < nstreams; ++t) {
+      th.emplace_back([&, t] {
+        sonar_ctx* w = ws[t];
+        for (int64_t k = next.fetch_add(1); k < npairs; k = next.fetch_add(1))
+          note(align_one(w, q_pcm[k], nq[k], r_pcm[k], nr[k], sample_rate, stft_window, hop, feature_window,
+                         max_lag_seconds, device_ptrs, &out[k]), k, w);
+      });
+    }
+    for (auto& x : th) x.join();
+    return first_err.load();
+  }
+  // batched: pairs validated and sized here; each stream takes batches of up to `per` pairs (the
+  // in-flight count split over the streams), cut further by a device-memory budget
+  const int64_t per = std::max<int64_t>(1, (inflight + nstreams - 1) / nstreams);
+  const char* mev = std::getenv("SONAR_PAIR_BATCH_GB");
+  const size_t budget = (size_t)((mev ? std::atof(mev) : 24.0) * (1ull << 30));
+  const int64_t max_lag_samples = (int64_t)(max_lag_seconds * (double)sample_rate);   // alignment.go:104
+  std::vector<PairGeo> geo;
+  for (int64_t k = 0; k < npairs; ++k) {
+    sonar_pair_record* rec = &out[k];
+    std::memset(rec, 0, sizeof(*rec));
+    int st = SONAR_OK;
+    PairGeo p;
+    p.k = k; p.nq = nq[k]; p.nr = nr[k];
+    if (!q_pcm[k] || !r_pcm[k] || p.nq <= 0 || p.nr <= 0) st = fail(c, SONAR_ERR_EMPTY, "empty signal");
+    else if (stft_window <= 0 || hop <= 0) st = fail(c, SONAR_ERR_INVALID, "window and hop size must be positive");
+    if (st == SONAR_OK) {
+      p.Fq = sonar_stft_frames(p.nq, stft_window, hop);
+      p.Fr = sonar_stft_frames(p.nr, stft_window, hop);
+      if (p.Fq <= 0 || p.Fr <= 0) st = fail(c, SONAR_ERR_TOO_SHORT, "signal too short for given window size and hop size");
+      else if (p.Fq + p.Fr > (int64_t)INT32_MAX) st = fail(c, SONAR_ERR_UNSUPPORTED, "sequence too long");
+    }
+    if (st != SONAR_OK) { rec->status = st; note(st, k, c); continue; }
+    p.Eq = sonar_energy_frames(p.nq, feature_window, hop);
+    p.Er = sonar_energy_frames(p.nr, feature_window, hop);
+    p.corr = p.Eq > 0 && p.Er > 0;
+    if (p.corr) {
+      p.mlf = std::min(max_lag_samples / hop, std::min(p.Eq, p.Er) - 1);
+      p.L = std::max<int64_t>(0, std::min({p.mlf, p.Eq - 1, p.Er - 1}));
+    }
+    p.g = sonar::dtw_geom(p.Fq, p.Fr);
+    p.cap = p.Fq + p.Fr + 1;
+    geo.push_back(p);
+  }
+  std::vector<std::vector<PairGeo>> batches;
+  for (size_t i = 0; i < geo.size();) {
+    std::vector<PairGeo> b;
+    size_t bytes = 0;
+    while (i < geo.size() && (int64_t)b.size() < per && (b.empty() || bytes + pair_bytes(geo[i]) <= budget)) {
+      bytes += pair_bytes(geo[i]);
+      b.push_back(geo[i++]);
+    }
+    batches.push_back(std::move(b));
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::vector<int64_t>> redo(nstreams);
+  for (int t = 0; t < nstreams; ++t) {
     th.emplace_back([&, t] {
       sonar_ctx* w = ws[t];
-      for (int64_t k = next.fetch_add(1); k < npairs; k = next.fetch_add(1)) {
-        const int r = align_one(w, q_pcm[k], nq[k], r_pcm[k], nr[k], sample_rate, stft_window, hop, feature_window,
-                                max_lag_seconds, device_ptrs, &out[k]);
-        if (r != SONAR_OK) {
-          int expect = SONAR_OK;
-          if (first_err.compare_exchange_strong(expect, r)) c->err = std::string("pair ") + std::to_string(k) + ": " + w->err;
-        }
+      for (size_t bi = next.fetch_add(1); bi < batches.size(); bi = next.fetch_add(1)) {
+        const int r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window,
+                                  device_ptrs, out, &redo[t]);
+        if (r != SONAR_OK)
+          for (const auto& p : batches[bi]) { out[p.k].status = r; note(r, p.k, w); }
       }
+      for (int64_t k : redo[t])                    // non-finite chroma: exact single-pair path
+        note(align_one(w, q_pcm[k], nq[k], r_pcm[k], nr[k], sample_rate, stft_window, hop, feature_window,
+                       max_lag_seconds, device_ptrs, &out[k]), k, w);
     });
   }
   for (auto& x : th) x.join();
+  for (int64_t k = 0; k < npairs && first_err.load() == SONAR_OK; ++k)   // per-pair device flags
+    if (out[k].status != SONAR_OK) {
+      first_err = out[k].status;
+      c->err = std::string("pair ") + std::to_string(k) + ": dtw band pipeline timed out";
+    }
   return first_err.load();
 }
 

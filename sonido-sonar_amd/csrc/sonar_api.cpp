@@ -46,6 +46,23 @@ void* dbuf(sonar_ctx* c, const std::string& name, size_t bytes) {
   return b.ptr;
 }
 
+void* hbuf(sonar_ctx* c, const std::string& name, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  DevBuf& b = c->hbufs[name];
+  if (b.cap < bytes) {
+    if (b.ptr) { hipStreamSynchronize(c->stream); hipHostFree(b.ptr); b.ptr = nullptr; b.cap = 0; }
+    if (hipHostMalloc(&b.ptr, bytes, hipHostMallocDefault) != hipSuccess) { b.ptr = nullptr; return nullptr; }
+    b.cap = bytes;
+  }
+  return b.ptr;
+}
+
+bool dtw_pre_enabled(int dim) {
+  if (dim != 12) return false;
+  const char* e = std::getenv("SONAR_DTW_PRE");                   // opt-in: measured slower
+  return e && std::atoi(e) != 0;
+}
+
 // brackets the dominant kernel of a call with a HIP event pair on its stream
 hipEvent_t timed_begin(sonar_ctx* c, hipStream_t s) {
   if (!c->timing) return nullptr;
@@ -222,13 +239,16 @@ void sonar_destroy(sonar_ctx* c) {
   hipStreamSynchronize(c->stream);
   sonar::detail::ingest_release(c);
   for (auto& kv : c->bufs) if (kv.second.ptr) hipFree(kv.second.ptr);
+  for (auto& kv : c->hbufs) if (kv.second.ptr) hipHostFree(kv.second.ptr);
   for (auto& kv : c->fp_tables) {
     FpTables& t = kv.second;
     for (void* p : {(void*)t.window, (void*)t.mel_lo, (void*)t.mel_hi, (void*)t.mel_woff, (void*)t.grp_off,
                     (void*)t.grp_mels, t.mel_w, t.dct, t.lift})
       if (p) hipFree(p);
   }
-  for (auto& kv : c->chroma_tables) { hipFree(kv.second.win); hipFree(kv.second.trig); hipFree(kv.second.map); }
+  for (auto& kv : c->chroma_tables) {
+    hipFree(kv.second.win); hipFree(kv.second.trig); hipFree(kv.second.map); hipFree(kv.second.cls);
+  }
   for (auto& e : c->ev_pool) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
@@ -599,10 +619,21 @@ int sonar_chroma_stft(sonar_ctx* c, const double* pcm, int64_t n, int64_t F, int
       trig[2 * m] = std::cos(2.0 * M_PI * (double)m / (double)fs);
       trig[2 * m + 1] = -std::sin(2.0 * M_PI * (double)m / (double)fs);
     }
-    it = c->chroma_tables.emplace(key, sonar_ctx::ChromaT{upload(win), upload(trig), upload(map)}).first;
+    // per chroma class, its bins in ascending order (the fold order of music.go:366-372)
+    std::vector<int> cls(13 + map.size());
+    int e = 0;
+    for (int b = 0; b < 12; ++b) {
+      cls[b] = e;
+      for (size_t k = 0; k < map.size(); ++k)
+        if (map[k] == b) cls[13 + e++] = (int)k;
+    }
+    cls[12] = e;
+    it = c->chroma_tables.emplace(key, sonar_ctx::ChromaT{upload(win), upload(trig), upload(map), upload(cls)}).first;
   }
+  const char* cw = std::getenv("SONAR_CHROMA_WAVE");              // 0: the block-per-frame kernel (A/B)
+  const int* cls = (cw && std::atoi(cw) == 0) ? nullptr : (const int*)it->second.cls;
   if (sonar::launch_chroma(y, n, F, hop, fs, (const double*)it->second.win, (const double*)it->second.trig,
-                           (const int*)it->second.map, dout, s) != 0)
+                           (const int*)it->second.map, cls, dout, s) != 0)
     return fail(c, SONAR_ERR_UNSUPPORTED, "chroma launch failed (frame size too large for LDS?)");
   if (!device_ptrs) {
     HIP_TRY(c, hipMemcpyAsync(chroma, dout, F * 12 * 8, hipMemcpyDeviceToHost, s));
@@ -703,7 +734,9 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
     if (!e) HIP_TRY(c, hipEventCreate(&e));
   hipEvent_t tend = timed_begin(c, s);
   HIP_TRY(c, hipEventRecord(c->dtw_ev[0], s));
-  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, codes, pl, trace, s, c->dtw_ev[1]) != 0)
+  double* Dd = sonar::detail::dtw_pre_enabled(dim) ? (double*)dbuf(c, "dtw.Dd", sonar::dtw_cn_bytes(g)) : nullptr;
+  if (sonar::detail::dtw_pre_enabled(dim) && !Dd) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (distances)");
+  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, codes, pl, trace, s, c->dtw_ev[1], Dd) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
   HIP_TRY(c, hipEventRecord(c->dtw_ev[2], s));
   timed_end(c, s, tend);
@@ -756,6 +789,128 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
   if (distance) *distance = cNM / (double)P;                      // dtw.go:88-91
   return SONAR_OK;
 }
+
+}  // extern "C"
+
+// ============================================= deferred-sync pair pieces ====
+namespace sonar {
+namespace detail {
+
+void ncc_metrics_host(const double* corr, int64_t L, int64_t na, int64_t nb, double* metrics) {
+  const auto m = sonar::host::ncc_metrics(corr, 2 * L + 1, L, na, nb);
+  const double v[10] = {m.peak_corr, (double)m.peak_lag, (double)m.peak_index, m.p_value, m.snr, m.sharpness,
+                        m.second_peak, m.psl, (double)m.overlap, (double)m.num_lags};
+  std::memcpy(metrics, v, sizeof(v));
+}
+
+// sonar_ncc's launch half: the correlation lands in pinned host memory once the stream drains
+int ncc_enqueue(sonar_ctx* c, const double* da, int64_t na, const double* db, int64_t nb, int32_t max_lag,
+                double** hcorr, int64_t* Lout) {
+  if (na <= 0 || nb <= 0 || !da || !db) return fail(c, SONAR_ERR_EMPTY, "empty signals provided");
+  int64_t L = max_lag;                                            // calculateActualMaxLag :452-461
+  L = std::max<int64_t>(std::min({L, na - 1, nb - 1}), 0);
+  const int64_t nl = 2 * L + 1;
+  hipStream_t s = c->stream;
+  double* xa = (double*)dbuf(c, "ncc.xa", na * 8);
+  double* xb = (double*)dbuf(c, "ncc.xb", nb * 8);
+  double* st = (double*)dbuf(c, "ncc.stats", 64);
+  double* dc = (double*)dbuf(c, "ncc.corr", nl * 8);
+  double* hc = (double*)hbuf(c, "ncc.corr", nl * 8);
+  if (!xa || !xb || !st || !dc || !hc) return fail(c, SONAR_ERR_NOMEM, "allocation failed (ncc)");
+  if (sonar::launch_ncc(da, na, db, nb, L, xa, xb, st, dc, s) != 0) return fail(c, SONAR_ERR_DEVICE, "ncc launch failed");
+  HIP_TRY(c, hipMemcpyAsync(hc, dc, nl * 8, hipMemcpyDeviceToHost, s));
+  *hcorr = hc;
+  *Lout = L;
+  return SONAR_OK;
+}
+
+// sonar_dtw's launch half for device sequences: the non-finite probe runs on the device and the
+// FAST (finite-input) pipeline is launched without waiting for it; dtw_finish re-runs the exact
+// math.Min pipeline in the rare case the probe fired
+int dtw_enqueue(sonar_ctx* c, const double* dq, int64_t nq, const double* dr, int64_t nr, int32_t dim, int32_t band,
+                DtwPending* p) {
+  if (nq <= 0 || nr <= 0 || !dq || !dr) return fail(c, SONAR_ERR_EMPTY, "empty sequences provided");
+  if (dim <= 0) return fail(c, SONAR_ERR_INVALID, "feature dimension must be positive");
+  if (nq + nr > (int64_t)INT32_MAX) return fail(c, SONAR_ERR_UNSUPPORTED, "sequence too long");
+  hipStream_t s = c->stream;
+  const sonar::DtwGeom g = sonar::dtw_geom(nq, nr);
+  double* Cn = (double*)dbuf(c, "dtw.Cn", sonar::dtw_cn_bytes(g));
+  uint32_t* Dn = (uint32_t*)dbuf(c, "dtw.Dn", sonar::dtw_dn_bytes(g));
+  uint64_t* E = (uint64_t*)dbuf(c, "dtw.E", sonar::dtw_edge_bytes(g));
+  int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", 16);
+  const int64_t cap = nq + nr + 1;
+  uint32_t* codes = (uint32_t*)dbuf(c, "dtw.codes", ((cap + 1023) / 1024) * 64 * 4);
+  int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
+  int64_t* st = (int64_t*)hbuf(c, "dtw.status", 32);
+  if (!Cn || !Dn || !E || !sync || !codes || !pl || !st) return fail(c, SONAR_ERR_NOMEM, "allocation failed (dtw)");
+  HIP_TRY(c, hipMemsetAsync(sync + 2, 0, 4, s));
+  if (sonar::launch_nonfinite(dq, nq * dim, sync + 2, s) || sonar::launch_nonfinite(dr, nr * dim, sync + 2, s))
+    return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
+  double* Dd = sonar::detail::dtw_pre_enabled(dim) ? (double*)dbuf(c, "dtw.Dd", sonar::dtw_cn_bytes(g)) : nullptr;
+  if (sonar::detail::dtw_pre_enabled(dim) && !Dd) return fail(c, SONAR_ERR_NOMEM, "allocation failed (dtw)");
+  if (sonar::launch_dtw(dq, dr, dim, band, true, g, Cn, Dn, E, sync, codes, pl, nullptr, s, nullptr, Dd) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
+  HIP_TRY(c, hipMemcpyAsync(st, pl, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(st + 1, sync, 12, hipMemcpyDeviceToHost, s));
+  *p = DtwPending{dq, dr, nq, nr, dim, band, st};
+  return SONAR_OK;
+}
+
+// after the caller's stream sync: decode the path into pinned host arrays (one more sync)
+int dtw_finish(sonar_ctx* c, DtwPending* p, const int32_t** hq, const int32_t** hr, const double** hc, int64_t* Pout,
+               double* distance) {
+  hipStream_t s = c->stream;
+  const sonar::DtwGeom g = sonar::dtw_geom(p->nq, p->nr);
+  const int64_t cap = p->nq + p->nr + 1;
+  double* Cn = (double*)dbuf(c, "dtw.Cn", sonar::dtw_cn_bytes(g));
+  uint32_t* Dn = (uint32_t*)dbuf(c, "dtw.Dn", sonar::dtw_dn_bytes(g));
+  uint64_t* E = (uint64_t*)dbuf(c, "dtw.E", sonar::dtw_edge_bytes(g));
+  int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", 16);
+  uint32_t* codes = (uint32_t*)dbuf(c, "dtw.codes", ((cap + 1023) / 1024) * 64 * 4);
+  int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
+  int32_t nfw[3];
+  std::memcpy(nfw, p->st + 1, 12);
+  if (nfw[2] != 0) {                                              // non-finite input: exact math.Min rules
+    double* Dd = sonar::detail::dtw_pre_enabled(p->dim) ? (double*)dbuf(c, "dtw.Dd", sonar::dtw_cn_bytes(g)) : nullptr;
+    if (sonar::launch_dtw(p->dq, p->dr, p->dim, p->band, false, g, Cn, Dn, E, sync, codes, pl, nullptr, s, nullptr, Dd))
+      return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
+    HIP_TRY(c, hipMemcpyAsync(p->st, pl, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(p->st + 1, sync, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    std::memcpy(nfw, p->st + 1, 8);
+  }
+  if (nfw[1]) return fail(c, SONAR_ERR_DEVICE, "dtw band pipeline timed out");
+  const int64_t P = p->st[0];
+  int32_t* oq = (int32_t*)dbuf(c, "dtw.pq", cap * 4);
+  int32_t* orr = (int32_t*)dbuf(c, "dtw.pr", cap * 4);
+  double* oc = (double*)dbuf(c, "dtw.pc", cap * 8);
+  int2* wstart = (int2*)dbuf(c, "dtw.wstart", (size_t)((P + 15) / 16 + 1) * sizeof(int2));
+  // one pinned block: cost(N,M), path costs, then the two index arrays
+  char* h = (char*)hbuf(c, "dtw.path", 8 + (size_t)cap * 16);
+  if (!oq || !orr || !oc || !wstart || !h) return fail(c, SONAR_ERR_NOMEM, "allocation failed (dtw path)");
+  if (sonar::launch_dtw_path_cost(Cn, g, codes, P, wstart, oq, orr, oc, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "dtw path launch failed");
+  double* hcnm = (double*)h;
+  double* hcost = hcnm + 1;
+  int32_t* hpq = (int32_t*)(hcost + cap);
+  int32_t* hpr = hpq + cap;
+  HIP_TRY(c, hipMemcpyAsync(hcnm, Cn + sonar::dtw_cn_index(g, p->nq, p->nr), 8, hipMemcpyDeviceToHost, s));
+  if (P > 0) {
+    HIP_TRY(c, hipMemcpyAsync(hcost, oc, P * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(hpq, oq, P * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(hpr, orr, P * 4, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(c, hipStreamSynchronize(s));
+  *hq = hpq; *hr = hpr; *hc = hcost;
+  *Pout = P;
+  *distance = *hcnm / (double)P;                                  // dtw.go:88-91
+  return SONAR_OK;
+}
+
+}  // namespace detail
+}  // namespace sonar
+
+extern "C" {
 
 // ========================================================= formants ====
 namespace {
