@@ -1,0 +1,94 @@
+"""The batched pair path of sonar_align_pairs (one band-kernel launch over a batch's chroma DTWs,
+batched walk / path decode, one host sync per batch) against the unbatched path
+(SONAR_PAIR_BATCH=0: one sonar_align_pair_device per pair), and the opt-in precomputed-distance
+DTW (SONAR_DTW_PRE=1: dtw_dist_kernel + the 4-wave band kernel) against the default band kernel.
+Pairs are independent and both paths run the same arithmetic, so records must be identical
+(NaN-aware), for pairs of different lengths, any batch cut, and a pair whose chroma is not finite
+(the batch redoes it through the exact math.Min path)."""
+import numpy as np
+import pytest
+
+import sonar
+from sonar import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return a.shape == b.shape and np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(
+        np.nan_to_num(a), np.nan_to_num(b))
+
+
+@pytest.fixture(scope="module")
+def mixed_pairs():
+    rng = np.random.default_rng(11)
+    qs, rs = [], []
+    for k, (sq, sr_) in enumerate([(6.0, 7.5), (9.0, 5.0), (3.3, 3.3), (12.0, 10.7), (4.1, 8.9)]):
+        q, r = synth.c3_pair(max(sq, sr_), 0.4 + 0.3 * k)[:2]
+        qs.append(np.ascontiguousarray(q[: int(sq * 44100)]))
+        rs.append(np.ascontiguousarray(r[: int(sr_ * 44100)] + 1e-3 * rng.standard_normal(int(sr_ * 44100))))
+    return qs, rs
+
+
+def _run(ctx, monkeypatch, qs, rs, **env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    try:
+        return ctx.align_pairs(qs, rs, max_lag_seconds=4.0, workers=4)
+    finally:
+        for k in env:
+            monkeypatch.delenv(k)
+
+
+@pytest.mark.parametrize("streams", [1, 2, 3])
+def test_batched_equals_unbatched_mixed_lengths(ctx, monkeypatch, mixed_pairs, streams):
+    qs, rs = mixed_pairs
+    ref = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_BATCH=0)
+    got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=streams)
+    assert np.all(ref["status"] == 0) and np.all(got["status"] == 0)
+    for f in sonar.PAIR_FIELDS:
+        assert _same(got[f], ref[f]), f
+
+
+def test_batched_memory_budget_cut(ctx, monkeypatch, mixed_pairs):
+    """A tiny device budget forces one pair per batch: same records."""
+    qs, rs = mixed_pairs
+    ref = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_BATCH=0)
+    got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=1, SONAR_PAIR_BATCH_GB=0.001)
+    for f in sonar.PAIR_FIELDS:
+        assert _same(got[f], ref[f]), f
+
+
+def test_batched_nonfinite_pair_redone_exactly(ctx, monkeypatch, mixed_pairs):
+    qs, rs = [x.copy() for x in mixed_pairs[0]], [x.copy() for x in mixed_pairs[1]]
+    qs[1][5000] = np.nan                      # chroma frames around it become NaN
+    rs[3][7000] = np.inf
+    ref = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_BATCH=0)
+    got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2)
+    assert np.array_equal(got["status"], ref["status"])
+    for f in sonar.PAIR_FIELDS:
+        assert _same(got[f], ref[f]), f
+
+
+@pytest.mark.parametrize("nq,nr,band", [(1000, 1000, -1), (700, 1333, -1), (1500, 960, 200), (63, 65, -1),
+                                        (4100, 3900, -1)])
+def test_precomputed_distance_dtw_bit_exact(ctx, monkeypatch, nq, nr, band):
+    rng = np.random.default_rng(nq + nr)
+    q = rng.random((nq, 12))
+    r = np.roll(rng.random((nr, 12)), 3, axis=0)
+    ref = ctx.dtw(q, r, band=band)
+    monkeypatch.setenv("SONAR_DTW_PRE", "1")
+    got = ctx.dtw(q, r, band=band)
+    monkeypatch.delenv("SONAR_DTW_PRE")
+    assert _same(got["distance"], ref["distance"])
+    for k in ("path_q", "path_r", "path_cost"):   # (banded: Inf - Inf costs are NaN in both)
+        assert _same(got[k], ref[k]), k
+
+
+def test_precomputed_distance_pairs(ctx, monkeypatch, mixed_pairs):
+    qs, rs = mixed_pairs
+    ref = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2)
+    got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2, SONAR_DTW_PRE=1)
+    for f in sonar.PAIR_FIELDS:
+        assert _same(got[f], ref[f]), f
