@@ -12,7 +12,8 @@ package sonargpu
 // The pair entries take arrays of stream pointers.  cgo forbids storing Go pointers in C memory
 // unless they are pinned, so the slices are pinned with runtime.Pinner (Go 1.21) for the call.
 // HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default): set it to
-// at least `workers` in the environment before the first call into the library.
+// at least the library's pair streams (SONAR_PAIR_STREAMS, default 8) in the environment before
+// the first call into the library.
 
 /*
 #include <stdlib.h>
