@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define SONAR_ABI_VERSION 2
+#define SONAR_ABI_VERSION 3
 
 enum {
   SONAR_OK = 0,
@@ -92,6 +92,8 @@ enum {
   SONAR_FP_SPECTRAL = 1u << 2,  /* centroid..slope, flux (F-1), low/high energy ratio */
   SONAR_FP_ZCR = 1u << 3,       /* out->zcr        F, on the pre-emphasised PCM       */
   SONAR_FP_ENERGY = 1u << 4,    /* out->energy     sonar_energy_frames(), pre-emphasised */
+  SONAR_FP_COMPLEX = 1u << 5,   /* out->complex    F x (W/2+1) x 2 (re, im)  SpectrogramResult.Complex */
+  SONAR_FP_PHASE = 1u << 6,     /* out->phase      F x (W/2+1), atan2(im, re) SpectrogramResult.Phase */
   SONAR_FP_GENERIC = 1u << 30   /* force the general fused kernel (A/B checks of the f32 MFCC path) */
 };
 
@@ -166,6 +168,8 @@ typedef struct {
   void* high_ratio; /* F                              */
   void* zcr;        /* F                              */
   void* energy;     /* sonar_energy_frames(n, ew, eh) */
+  void* complex;    /* F x (W/2+1) x 2, interleaved (re, im)   (spectral.go:491) */
+  void* phase;      /* F x (W/2+1)                             (spectral.go:493) */
 } sonar_fp_out;
 
 void sonar_fp_cfg_default(sonar_fp_cfg* cfg);
@@ -395,8 +399,8 @@ int sonar_multi_shard(int64_t n, int32_t window_size, int32_t hop_size, int32_t 
 /* sonar_fingerprint with the STFT frames sharded over the devices: device g runs frames [f0, f1)
  * of sonar_multi_shard on its sample slice (host pcm, cfg->device_ptrs must be 0) and writes its
  * rows of every requested output straight into the host arrays.  Frames are independent, so the
- * result equals the single-device call.  Supported flags: SONAR_FP_MFCC, SONAR_FP_MAGNITUDE and
- * SONAR_FP_SPECTRAL without flux (out->flux must be NULL: frame f0's flux needs frame f0-1); the
+ * result equals the single-device call.  Supported flags: SONAR_FP_MFCC, SONAR_FP_MAGNITUDE,
+ * SONAR_FP_COMPLEX, SONAR_FP_PHASE and SONAR_FP_SPECTRAL without flux (out->flux must be NULL: frame f0's flux needs frame f0-1); the
  * pre-emphasised outputs (ZCR, energy) read the sample before the slice -> SONAR_ERR_UNSUPPORTED. */
 int sonar_fingerprint_multi(sonar_multi* m, const void* pcm, int64_t n, const sonar_fp_cfg* cfg,
                             sonar_fp_out* out);

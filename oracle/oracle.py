@@ -42,6 +42,7 @@ def lib():
         L.or_stft_frames.restype = C.c_int64
         L.or_stft_mag.argtypes = [_d, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, _d]
         L.or_stft_mag_window.argtypes = [_d, C.c_int64, C.c_int, C.c_int, _d, C.c_int, _d]
+        L.or_stft_complex.argtypes = [_d, C.c_int64, C.c_int, C.c_int, C.c_int, _d, _d, _d]
         L.or_filterbank.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, _d]
         L.or_mfcc_frames.argtypes = [_d, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
                                      C.c_double, C.c_int, C.c_double, C.c_int, C.c_int, _d]
@@ -115,6 +116,19 @@ def stft_mag(pcm, W, H, window_type="hann", nthreads=1):
     if rc != 0:
         raise ValueError("stft failed")
     return out
+
+
+def stft_complex(pcm, W, H, window_type="hann"):
+    """(complex F x (W/2+1), phase F x (W/2+1)): SpectrogramResult.Complex / .Phase (spectral.go:490-494)"""
+    pcm = _f64(pcm)
+    F = stft_frames(len(pcm), W, H)
+    if F < 0:
+        raise ValueError("signal too short for given window size and hop size")
+    re, im, ph = np.zeros((F, W // 2 + 1)), np.zeros((F, W // 2 + 1)), np.zeros((F, W // 2 + 1))
+    rc = lib().or_stft_complex(_p(pcm), len(pcm), W, H, WINDOWS[window_type], _p(re), _p(im), _p(ph))
+    if rc != 0:
+        raise ValueError("stft failed")
+    return re + 1j * im, ph
 
 
 def filterbank(n_filters, fft_size, sample_rate, low, high, kind="mel"):

@@ -259,6 +259,30 @@ int or_stft_mag(const double* pcm, int64_t n, int W, int H, int window_type, int
     return rc;
 }
 
+/* SpectrogramResult.Complex / .Phase rows (spectral.go:490-494): fftResult[i] for the positive
+ * bins and cmplx.Phase = atan2(imag, real); skipped frames (:524-534) stay zero. */
+int or_stft_complex(const double* pcm, int64_t n, int W, int H, int window_type, double* re_out, double* im_out,
+                    double* phase) {
+    int64_t F = or_stft_frames(n, W, H);
+    if (F < 0) return -1;
+    int K = W / 2 + 1;
+    double* win = malloc(sizeof(double) * W);
+    if (or_window(window_type, W, 1, 1, 8.6, 0.5, win) != 0) { free(win); return -2; }
+    double* buf = malloc(sizeof(double) * W);
+    double* re = malloc(sizeof(double) * W); double* im = malloc(sizeof(double) * W);
+    for (int64_t t = 0; t < F; t++) {
+        int64_t s = t * H;
+        double *ro = re_out + t * K, *io = im_out + t * K, *po = phase + t * K;
+        if (s + W > n) { memset(ro, 0, sizeof(double) * K); memset(io, 0, sizeof(double) * K);
+                         memset(po, 0, sizeof(double) * K); continue; }
+        for (int i = 0; i < W; i++) buf[i] = pcm[s + i] * win[i];
+        or_fft(buf, NULL, W, re, im);
+        for (int k = 0; k < K; k++) { ro[k] = re[k]; io[k] = im[k]; po[k] = atan2(im[k], re[k]); }
+    }
+    free(buf); free(re); free(im); free(win);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ */
 /* Filterbanks: algorithms/spectral/mel_scale.go:19-86 and              */
 /* algorithms/spectral/bark_scale.go:20-93 (kind 0 = mel, 1 = bark)     */

@@ -116,7 +116,7 @@ template <typename P> struct Vec2;
 template <> struct Vec2<float> { using type = float2; };
 template <> struct Vec2<double> { using type = double2; };
 
-template <typename T, typename P, int R, bool SPEC>
+template <typename T, typename P, int R, bool SPEC, bool CPLX = false>
 __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
   constexpr int FR = (R >= 8) ? 1 : 8 / R;   // frames per FFT unit
   constexpr int V = R * FR;                   // values per lane
@@ -363,6 +363,7 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
       }
       // X_k = E + w O,  E = (A + B)/2, O = -i (A - B)/2, A = Z[k], B = conj(Z[M-k])
       const bool mag = SPEC || p.out_mag;
+      const int64_t uf = CPLX ? unit_frame(ui) : 0;
 #pragma unroll
       for (int gm = 0; gm < G; gm++) {
         const int col = 8 * gm + cl3, fr = col / R, c = col % R;
@@ -380,9 +381,25 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
           const T xi_ = ei + (wr * oi + wi * or_);
           const T pw = xr_ * xr_ + xi_ * xi_;
           row[k] = mag ? sqrt(pw) : pw;
+          const int64_t tg = uf + fr;   // this frame's global index
+          const bool own = CPLX && !(pre && ui == 0) && tg < f_end;
+          if (own) {                    // SpectrogramResult.Complex / .Phase (spectral.go:491-493)
+            if (p.out_cplx) {
+              store_out<T>(p.out_cplx, p.out_f64, 2 * (tg * K + k), xr_);
+              store_out<T>(p.out_cplx, p.out_f64, 2 * (tg * K + k) + 1, xi_);
+            }
+            if (p.out_phase) store_out<T>(p.out_phase, p.out_f64, tg * K + k, atan2(xi_, xr_));
+          }
           if (k == 0) {                 // Nyquist bin M = E_0 - O_0 (both real)
             const T xn = er - or_;
             row[M] = mag ? fabs(xn) : xn * xn;
+            if (own) {
+              if (p.out_cplx) {
+                store_out<T>(p.out_cplx, p.out_f64, 2 * (tg * K + M), xn);
+                store_out<T>(p.out_cplx, p.out_f64, 2 * (tg * K + M) + 1, (T)0);
+              }
+              if (p.out_phase) store_out<T>(p.out_phase, p.out_f64, tg * K + M, atan2((T)0, xn));
+            }
           }
         }
       }
@@ -575,9 +592,9 @@ bool fingerprint_supported(int W) {
   return W == 128 || W == 256 || W == 512 || W == 1024 || W == 2048;
 }
 
-template <typename T, typename P, int R, bool SPEC>
+template <typename T, typename P, int R, bool SPEC, bool CPLX>
 static int launch_t(const FpParams& p, hipStream_t s) {
-  auto kern = fp_wave_kernel<T, P, R, SPEC>;
+  auto kern = fp_wave_kernel<T, P, R, SPEC, CPLX>;
   if (p.lds_bytes > 64 * 1024)
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
   const int64_t waves = (p.F + p.frames_per_wave - 1) / p.frames_per_wave;
@@ -586,21 +603,25 @@ static int launch_t(const FpParams& p, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-template <typename T, typename P, bool SPEC>
+template <typename T, typename P, bool SPEC, bool CPLX>
 static int launch_r(const FpParams& p, hipStream_t s) {
   switch (p.W / 128) {
-    case 1: return launch_t<T, P, 1, SPEC>(p, s);
-    case 2: return launch_t<T, P, 2, SPEC>(p, s);
-    case 4: return launch_t<T, P, 4, SPEC>(p, s);
-    case 8: return launch_t<T, P, 8, SPEC>(p, s);
-    case 16: return launch_t<T, P, 16, SPEC>(p, s);
+    case 1: return launch_t<T, P, 1, SPEC, CPLX>(p, s);
+    case 2: return launch_t<T, P, 2, SPEC, CPLX>(p, s);
+    case 4: return launch_t<T, P, 4, SPEC, CPLX>(p, s);
+    case 8: return launch_t<T, P, 8, SPEC, CPLX>(p, s);
+    case 16: return launch_t<T, P, 16, SPEC, CPLX>(p, s);
   }
   return -4;
 }
 
+// SONAR_FP_SPECTRAL selects SPEC; Complex / Phase outputs select CPLX (its own instantiation: the
+// extra stores and atan2 cost registers the other variants keep)
 template <typename T, typename P>
 static int launch_s(const FpParams& p, hipStream_t s) {
-  return (p.flags & 4u) ? launch_r<T, P, true>(p, s) : launch_r<T, P, false>(p, s);   // SONAR_FP_SPECTRAL
+  const bool cplx = p.out_cplx || p.out_phase;
+  if (p.flags & 4u) return cplx ? launch_r<T, P, true, true>(p, s) : launch_r<T, P, true, false>(p, s);
+  return cplx ? launch_r<T, P, false, true>(p, s) : launch_r<T, P, false, false>(p, s);
 }
 
 int launch_fingerprint(const FpParams& p, int f64, hipStream_t s) {

@@ -42,6 +42,8 @@ struct FpParams {
   void* out_mfcc;
   void* out_mag;
   void* out_spec[9];    // centroid, rolloff, bandwidth, flatness, crest, slope, flux(F-1), low, high
+  void* out_cplx;       // F x K x 2 (re, im) straight from the FFT's real split (nullable)
+  void* out_phase;      // F x K atan2(im, re) (nullable)
   // LDS carve (bytes): shared twiddle tables, then one region per wave
   int lds_tab_t1, lds_tab_t2, lds_tab_t3, lds_tab_mel, lds_tab_w, lds_tab_dct, lds_wave0, lds_wave_stride;
   int nnz;              // packed filterbank weights

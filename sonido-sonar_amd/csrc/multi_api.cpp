@@ -440,6 +440,8 @@ int sonar_fingerprint_multi(sonar_multi* m, const void* pcm, int64_t n, const so
       sonar_fp_out o{};
       o.mfcc = at(out->mfcc, nm);
       o.magnitude = at(out->magnitude, K);
+      o.complex = at(out->complex, 2 * K);
+      o.phase = at(out->phase, K);
       o.centroid = at(out->centroid, 1);
       o.rolloff = at(out->rolloff, 1);
       o.bandwidth = at(out->bandwidth, 1);

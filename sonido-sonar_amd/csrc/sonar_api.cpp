@@ -360,7 +360,8 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
   const bool pcm64 = cfg->pcm_dtype == SONAR_F64;
   const bool o64 = cfg->out_dtype == SONAR_F64;
   const uint32_t flags = cfg->flags;
-  const bool need_fft = flags & (SONAR_FP_MFCC | SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL);
+  const bool need_fft = flags & (SONAR_FP_MFCC | SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_COMPLEX |
+                                 SONAR_FP_PHASE);
   if (need_fft && !sonar::fingerprint_supported(W))
     return fail(c, SONAR_ERR_UNSUPPORTED, "window size " + std::to_string(W) +
                                               " not supported by the GPU STFT (128, 256, 512, 1024, 2048)");
@@ -391,6 +392,10 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
   void* d_mag = (flags & SONAR_FP_MAGNITUDE) ? out_ptr(out->magnitude, "mag", (size_t)F * K) : nullptr;
   if ((flags & SONAR_FP_MFCC) && !d_mfcc) return fail(c, SONAR_ERR_INVALID, "out->mfcc is null or allocation failed");
   if ((flags & SONAR_FP_MAGNITUDE) && !d_mag) return fail(c, SONAR_ERR_INVALID, "out->magnitude is null");
+  void* d_cplx = (flags & SONAR_FP_COMPLEX) ? out_ptr(out->complex, "cplx", (size_t)F * K * 2) : nullptr;
+  void* d_phase = (flags & SONAR_FP_PHASE) ? out_ptr(out->phase, "phase", (size_t)F * K) : nullptr;
+  if ((flags & SONAR_FP_COMPLEX) && !d_cplx) return fail(c, SONAR_ERR_INVALID, "out->complex is null");
+  if ((flags & SONAR_FP_PHASE) && !d_phase) return fail(c, SONAR_ERR_INVALID, "out->phase is null");
   void* d_spec[9] = {nullptr};
   if (flags & SONAR_FP_SPECTRAL) {
     void* user[9] = {out->centroid, out->rolloff, out->bandwidth, out->flatness, out->crest, out->slope,
@@ -404,7 +409,8 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
 
   // headline path: float32 MFCC only at W = 1024 (mfcc_pair.hip); SONAR_FP_GENERIC forces fp_kernel.hip
   const bool pair_ok = need_fft && !f64 && !pcm64 && !o64 && W == 1024 && (flags & SONAR_FP_MFCC) &&
-                       !(flags & (SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_GENERIC | 0x80000000u));
+                       !(flags & (SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_COMPLEX | SONAR_FP_PHASE |
+                                  SONAR_FP_GENERIC | 0x80000000u));
   bool pair_done = false;
   c->last_fp_kernel = "";
   if (pair_ok) {
@@ -457,6 +463,8 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     p.out_f64 = o64;
     p.out_mfcc = d_mfcc;
     p.out_mag = d_mag;
+    p.out_cplx = d_cplx;
+    p.out_phase = d_phase;
     for (int d = 0; d < 9; d++) p.out_spec[d] = d_spec[d];
     // tables, cached per configuration
     char key[512];

@@ -379,6 +379,47 @@ func (x *Context) Fingerprint(pcm []float64, windowSize, hopSize, sampleRate int
 	return split(flat, frames, nc), nil
 }
 
+// Spectrogram mirrors the per-frame arrays of analyzers.SpectrogramResult
+// (fingerprint/analyzers/spectral.go:19-25): Magnitude, Phase and Complex, F x (W/2+1).
+type Spectrogram struct {
+	Magnitude [][]float64
+	Phase     [][]float64
+	Complex   [][]complex128
+}
+
+// ComputeSTFT is SpectralAnalyzer.ComputeSTFTWithWindow (spectral.go:385) on the GPU, float64:
+// the window is {Normalize, Symmetric} like spectral.go:415; frames that Go skips stay zero.
+// The complex128 rows are filled in place (Go lays complex128 out as (re, im) float64 pairs,
+// which is the C ABI's interleaved SONAR_FP_COMPLEX layout).
+func (x *Context) ComputeSTFT(pcm []float64, windowSize, hopSize, windowType int) (*Spectrogram, error) {
+	if len(pcm) == 0 {
+		return nil, fmt.Errorf("empty signal: %w", ErrEmpty)
+	}
+	frames := int(C.sonar_stft_frames(C.int64_t(len(pcm)), C.int32_t(windowSize), C.int32_t(hopSize)))
+	if frames <= 0 {
+		return nil, fmt.Errorf("signal too short for given window size and hop size: %w", ErrTooShort)
+	}
+	var cfg C.sonar_fp_cfg
+	C.sonar_fp_cfg_default(&cfg)
+	cfg.window_size, cfg.hop_size, cfg.window_type = C.int32_t(windowSize), C.int32_t(hopSize), C.int32_t(windowType)
+	cfg.flags = C.SONAR_FP_MAGNITUDE | C.SONAR_FP_PHASE | C.SONAR_FP_COMPLEX
+	cfg.precision, cfg.pcm_dtype, cfg.out_dtype = C.SONAR_F64, C.SONAR_F64, C.SONAR_F64
+	k := windowSize/2 + 1
+	mag, ph := make([]float64, frames*k), make([]float64, frames*k)
+	cx := make([]complex128, frames*k)
+	out := C.sonar_fp_out{magnitude: unsafe.Pointer(&mag[0]), phase: unsafe.Pointer(&ph[0]),
+		complex: unsafe.Pointer(&cx[0])}
+	if rc := C.sonar_fingerprint(x.c, unsafe.Pointer(&pcm[0]), C.int64_t(len(pcm)), &cfg, &out); rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	s := &Spectrogram{Magnitude: split(mag, frames, k), Phase: split(ph, frames, k),
+		Complex: make([][]complex128, frames)}
+	for t := range s.Complex {
+		s.Complex[t] = cx[t*k : (t+1)*k]
+	}
+	return s, nil
+}
+
 // FingerprintDecoded is Fingerprint fed by the decoder's raw output instead of AudioData.PCM:
 // `output` is the ffmpeg "-f f64le" byte stream (transcode/decoder.go:709) that
 // Decoder.bytesToFloat64 (decoder.go:850-871) would walk into a []float64.  The bytes cross

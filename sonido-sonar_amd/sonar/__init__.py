@@ -32,6 +32,8 @@ from ._abi import (  # noqa: F401
     FP_SPECTRAL,
     FP_ZCR,
     FP_ENERGY,
+    FP_COMPLEX,
+    FP_PHASE,
     FP_GENERIC,
     F32,
     F64,

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("SONAR_LIB") or os.path.join(_PKG, "lib", "libsonar_gp
 HEADER = os.path.join(_REPO, "include", "sonar_gpu.h")
 
 OK, ERR_INVALID, ERR_TOO_SHORT, ERR_EMPTY, ERR_UNSUPPORTED, ERR_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4, -5, -6
-FP_MFCC, FP_MAGNITUDE, FP_SPECTRAL, FP_ZCR, FP_ENERGY = 1, 2, 4, 8, 16
+FP_MFCC, FP_MAGNITUDE, FP_SPECTRAL, FP_ZCR, FP_ENERGY, FP_COMPLEX, FP_PHASE = 1, 2, 4, 8, 16, 32, 64
 FP_GENERIC = 1 << 30   # force the general fused kernel (A/B checks of the f32 MFCC path)
 F32, F64 = 0, 1
 INGEST_DEVICE_CONVERT, INGEST_HOST_CONVERT = 0, 1   # sonar_ingest_f64le modes
@@ -54,7 +54,8 @@ class FpConfig(C.Structure):
 
 class FpOut(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ["mfcc", "magnitude", "centroid", "rolloff", "bandwidth", "flatness",
-                                          "crest", "slope", "flux", "low_ratio", "high_ratio", "zcr", "energy"]]
+                                          "crest", "slope", "flux", "low_ratio", "high_ratio", "zcr", "energy",
+                                          "complex", "phase"]]
 
 
 class FingerprintConfig(C.Structure):
@@ -418,6 +419,12 @@ class Context:
             if cfg.flags & FP_MAGNITUDE:
                 res["magnitude"] = np.zeros((F, K), od)
                 out.magnitude = res["magnitude"].ctypes.data
+            if cfg.flags & FP_COMPLEX:      # (re, im) interleaved: a complex view of an F x K x 2 array
+                res["complex"] = np.zeros((F, K, 2), od)
+                out.complex = res["complex"].ctypes.data
+            if cfg.flags & FP_PHASE:
+                res["phase"] = np.zeros((F, K), od)
+                out.phase = res["phase"].ctypes.data
             if cfg.flags & FP_SPECTRAL:
                 for nme in SPECTRAL_NAMES:
                     res[nme] = np.zeros(max(F - 1, 0) if nme == "flux" else F, od)
@@ -712,6 +719,12 @@ class Multi:
         if cfg.flags & FP_MAGNITUDE:
             res["magnitude"] = np.zeros((F, cfg.window_size // 2 + 1), odt)
             o.magnitude = res["magnitude"].ctypes.data
+        if cfg.flags & FP_COMPLEX:
+            res["complex"] = np.zeros((F, cfg.window_size // 2 + 1, 2), odt)
+            o.complex = res["complex"].ctypes.data
+        if cfg.flags & FP_PHASE:
+            res["phase"] = np.zeros((F, cfg.window_size // 2 + 1), odt)
+            o.phase = res["phase"].ctypes.data
         if cfg.flags & FP_SPECTRAL:
             for k in ("centroid", "rolloff", "bandwidth", "flatness", "crest", "slope", "low_ratio", "high_ratio"):
                 res[k] = np.zeros(F, odt)

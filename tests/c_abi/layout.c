@@ -15,7 +15,7 @@
 #define F(T, m) printf("field %s.%s %zu\n", #T, #m, offsetof(T, m))
 
 PIN(sonar_fp_cfg, 104);
-PIN(sonar_fp_out, 104);
+PIN(sonar_fp_out, 120);
 PIN(sonar_formant_frame, 176);
 PIN(sonar_voice_quality_result, 96);
 PIN(sonar_fingerprint_config, 72);
@@ -42,7 +42,7 @@ int main(void) {
   F(sonar_fp_out, mfcc); F(sonar_fp_out, magnitude); F(sonar_fp_out, centroid); F(sonar_fp_out, rolloff);
   F(sonar_fp_out, bandwidth); F(sonar_fp_out, flatness); F(sonar_fp_out, crest); F(sonar_fp_out, slope);
   F(sonar_fp_out, flux); F(sonar_fp_out, low_ratio); F(sonar_fp_out, high_ratio); F(sonar_fp_out, zcr);
-  F(sonar_fp_out, energy);
+  F(sonar_fp_out, energy); F(sonar_fp_out, complex); F(sonar_fp_out, phase);
 
   S(sonar_formant_frame);
   F(sonar_formant_frame, status); F(sonar_formant_frame, n_formants); F(sonar_formant_frame, frequency);
