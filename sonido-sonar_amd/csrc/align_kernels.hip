@@ -887,6 +887,8 @@ __device__ __forceinline__ void dtw_walk_body(const uint32_t* Dn, int64_t nq, in
   int i = (int)nq, j = (int)nr, P = 0;
   int wb = -1, wlo = 0, pb = -1, plo = 0;
   uint32_t cacc = 0, vacc = 0;
+  // the open word is built in an SGPR; a completed word moves into lane (word % 64) of vacc, and
+  // the 64 words of vacc are stored once every 1,024 moves
   auto emit = [&](uint32_t code) {
     cacc |= code << (2 * (P & 15));
     ++P;
@@ -894,7 +896,7 @@ __device__ __forceinline__ void dtw_walk_body(const uint32_t* Dn, int64_t nq, in
       const int wi = (P >> 4) - 1;
       vacc = lane == (wi & 63) ? cacc : vacc;
       cacc = 0;
-      if ((wi & 63) == 63) codes[wi - 63 + lane] = vacc;
+      if ((P & 1023) == 0) codes[wi - 63 + lane] = vacc;
     }
   };
   auto load_win = [&](uint32_t (&dst)[DTW_WIN], int bnd, int lo) {
@@ -928,15 +930,24 @@ __device__ __forceinline__ void dtw_walk_body(const uint32_t* Dn, int64_t nq, in
     int ll = __builtin_amdgcn_readfirstlane(l);
     int bp = __builtin_amdgcn_readfirstlane(2 * (s & 15));          // bit position of step s
     int jj = __builtin_amdgcn_readfirstlane(j);
+    // a move: 0 up (l-1, s-1), 1 left (j-1, s-1), 2 diagonal (both, s-2), as arithmetic on the
+    // code: dl = 1 - (c & 1), dj = (c + 1) >> 1, dbp = 2 + (c & 2).  The words of the current
+    // lane (wc) and of the lane above (wu) are held in SGPRs; an up/diagonal move takes wu and
+    // fetches the next lane's word with a v_readlane whose result is needed only a move later,
+    // so the readlane latency is off the move-to-move chain.
 #define STEP_SLOT(K)                                                                  \
     case K: {                                                                         \
+      uint32_t wc = __builtin_amdgcn_readlane(win[K], ll);                            \
+      uint32_t wu = __builtin_amdgcn_readlane(win[K], ll > 0 ? ll - 1 : 0);           \
       do {                                                                            \
-        const uint32_t word = __builtin_amdgcn_readlane(win[K], ll);                  \
-        const uint32_t code = (word >> bp) & 3u;                                      \
+        const uint32_t code = (wc >> bp) & 3u;                                        \
         emit(code);                                                                   \
-        ll -= code != 1u;                                                             \
-        jj -= code != 0u;                                                             \
-        bp -= code == 2u ? 4 : 2;                                                     \
+        const int dl = 1 - (int)(code & 1u);                                          \
+        ll -= dl;                                                                     \
+        jj -= (int)((code + 1u) >> 1);                                                \
+        bp -= 2 + (int)(code & 2u);                                                   \
+        wc = dl ? wu : wc;                                                            \
+        wu = __builtin_amdgcn_readlane(win[K], ll > 0 ? ll - 1 : 0);                  \
       } while ((ll | bp | (jj - 1)) >= 0);                                            \
       break;                                                                          \
     }
@@ -953,10 +964,9 @@ __device__ __forceinline__ void dtw_walk_body(const uint32_t* Dn, int64_t nq, in
     emit(i == 0 ? 1u : 0u);
     if (i == 0) --j; else --i;
   }
-  const int nw = (P + 15) >> 4;
-  if (P & 15) vacc = lane == ((nw - 1) & 63) ? cacc : vacc;
-  if (nw > 0 && (nw & 63) != 0) {
-    const int base = (nw - 1) & ~63;
+  if (P & 15) vacc = lane == ((P >> 4) & 63) ? cacc : vacc;   // the partial last word
+  if (P & 1023) {             // the last, partly filled block of 64 words
+    const int base = (P >> 10) << 6, nw = (P + 15) >> 4;
     if (lane < nw - base) codes[base + lane] = vacc;
   }
   if (lane == 0) *plen = P;

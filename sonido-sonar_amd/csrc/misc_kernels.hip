@@ -464,7 +464,8 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
   // radix-2 FFT for power-of-two frames whose (re, im) work arrays still fit next to the rest
   const int fft = (fs & (fs - 1)) == 0 && fs >= 2 && lds + 16 * (size_t)fs <= 48 * 1024;
   if (fft) lds += 16 * (size_t)fs + 8;
-  if (lds > 64 * 1024) hipFuncSetAttribute((const void*)chroma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)chroma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(chroma_kernel, dim3((unsigned)frames), dim3(256), lds, s, y, n, frames, hop, fs, window, trig,
                      cmap, out, trig_lds, fft);
   return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -475,8 +476,13 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
 // over chunks of kDcChunk samples: (1) each chunk's response from a zero state -> its end value;
 // (2) one wave chains the chunk carries Y_c = e_c + R^chunk Y_{c-1} in order; (3) each chunk
 // re-runs the recurrence from its true start state and writes z.  Every sample goes through
-// the same sequential recurrence as Go from a start state that equals Go's to rounding (the
-// warm-up version it replaces ran 8,192 extra samples per 1,024-sample chunk).  256-sample chunks:
+// the same sequential recurrence as Go; only the chunk start states differ: pass (2) combines
+// the carries with a Kogge-Stone scan of affine maps (log2 64 = 6 levels, reassociated), so a
+// start state carries a few ulp of |Y| of rounding that Go's serial chain does not (measured max
+// |dY| 9e-16 on unit-variance input), decaying as 0.995^k inside the chunk: outputs agree with
+// Go to ~1e-15 relative, energies to 1e-12 (tests), the NCC peak exactly (test_gpu_fullsize:
+// 5-min streams against the oracle's serial chain).  (The warm-up version it replaces ran 8,192
+// extra samples per 1,024-sample chunk.)  256-sample chunks:
 // 4x the lanes of 1,024 for the latency-bound passes, C5 726 -> ~760 pairs/s (tools/dc_ab.sh).
 #ifndef SONAR_DC_CHUNK
 #define SONAR_DC_CHUNK 256
@@ -517,8 +523,11 @@ __device__ __forceinline__ double dc_run(LD x, int64_t s, int64_t e, double R, d
 // the lanes' chunk-strided reads land on distinct banks), then lane c runs chunk c0+c's
 // recurrence out of LDS -- the same operations as from global memory, without a global round
 // trip per 16-sample batch.
-constexpr int kDcCpb = 16;
+// chunks per block: 16, fewer for long chunks so the staged span fits 64 KB of static LDS
+constexpr int kDcCpb = 7936 / kDcChunk < 16 ? 7936 / kDcChunk : 16;
 constexpr int kDcSpan = kDcCpb * kDcChunk + 1;
+static_assert((kDcSpan + (kDcSpan >> 8) + 1) * sizeof(double) <= 64 * 1024,
+              "dc_pass_kernel stages kDcCpb chunks in static LDS: lower kDcCpb for longer chunks");
 __device__ __forceinline__ int dc_slot(int i) { return i + (i >> 8); }
 
 template <bool WRITE>

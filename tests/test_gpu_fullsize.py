@@ -66,6 +66,19 @@ def test_c3_ncc_max_offset_60s(ctx, c3):
     assert abs(abs(met["peak_lag"]) - 12.34 * SR / 256) <= 1.0
 
 
+def test_c3_ncc_from_oracle_energies(ctx, c3):
+    """The scanned DC carries (a few ulp from Go's serial chain) must not move the alignment: the
+    NCC of the GPU energies against the NCC of the ORACLE energies (serial DC chain), 5-min
+    streams (51,679 chunk carries), maxOffsetSeconds 60."""
+    q, r, eq, _, er, _ = c3
+    oe = [O.short_time_energy(O.preemphasis(O.dc_removal(x, 0.995), 0.95), 1024, 256) for x in (q, r)]
+    L = 10335
+    _, met = ctx.ncc(eq, er, L)
+    _, rmet = O.ncc(oe[0], oe[1], L)
+    assert met["peak_lag"] == rmet["peak_lag"]
+    assert abs(met["peak_correlation"] - rmet["peak_correlation"]) <= 1e-12 * abs(rmet["peak_correlation"])
+
+
 def test_c3_dtw_20000_slice_bit_exact(ctx, c3):
     _, _, _, cq, _, cr = c3
     n = 20000
