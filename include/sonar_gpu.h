@@ -173,6 +173,9 @@ typedef struct {
 } sonar_fp_out;
 
 void sonar_fp_cfg_default(sonar_fp_cfg* cfg);
+/* Window sizes: 128, 256, 512, 1024 and 2048 run the fused kernels (every flag); any other W up
+ * to 8192 runs the generic float64 DFT path (MFCC, magnitude, complex, phase, ZCR, energy; the
+ * spectral descriptors -> SONAR_ERR_UNSUPPORTED), as go-dsp's FFTReal takes any length. */
 int sonar_fingerprint(sonar_ctx* ctx, const void* pcm, int64_t n, const sonar_fp_cfg* cfg,
                       sonar_fp_out* out);
 

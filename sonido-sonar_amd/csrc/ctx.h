@@ -19,6 +19,7 @@ struct FpTables {
   void* window = nullptr;
   int *mel_lo = nullptr, *mel_hi = nullptr, *mel_woff = nullptr, *grp_off = nullptr, *grp_mels = nullptr;
   void *mel_w = nullptr, *dct = nullptr, *lift = nullptr;
+  void* trig = nullptr;   // generic-W path: (cos, -sin) of 2 pi m / W
   int n_mels = 0, n_mfcc = 0, nnz = 0;
 };
 

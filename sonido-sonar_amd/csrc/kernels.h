@@ -85,6 +85,16 @@ bool fingerprint_supported(int W);
 int fp_batch_frames(int W);
 int fp_pre_rows(int W, int spec);
 
+// STFT for window lengths outside the fused kernels (any W <= 8192, misc_kernels.hip): direct
+// float64 DFT per frame -> |X| scratch (F x (W/2+1)) + optional Magnitude / Complex / Phase
+// outputs; trig = (cos, -sin) of 2 pi m / W, m < W
+int launch_stft_dft(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, const double* win,
+                    const double* trig, double* mag, void* out_mag, void* out_cplx, void* out_phase, int out_f64,
+                    hipStream_t s);
+// MFCC.ComputeFrames from |X| rows (float64 tables of host::make_mfcc_tables)
+int launch_mfcc_rows(const double* mag, int64_t F, int K, const int* lo, const int* hi, const int* woff,
+                     const double* w, int n_mels, const double* dct, const double* lift, int n_mfcc, int input_power,
+                     void* out, int out_f64, hipStream_t s);
 // ZCR + short-time energy on the pre-emphasised PCM (misc_kernels.hip)
 int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, double alpha, int sample_rate,
                void* out, int out_f64, hipStream_t s);

@@ -370,6 +370,110 @@ __global__ __launch_bounds__(256) void chroma_wave_kernel(const double* y, int64
   }
 }
 
+// SpectralAnalyzer.ComputeSTFTWithWindow for a window length the fused kernels do not take
+// (any W up to 8192: go-dsp's FFTReal runs Bluestein for non-powers of two, analyzers/spectral.go:131):
+// one block per frame, the windowed frame (and the (cos, -sin) table when it fits) in LDS, one
+// thread per bin running the DFT sum in float64 in index order.  Writes |X| (float64 scratch for
+// the MFCC pass) and the requested Magnitude / Complex / Phase rows; frames Go skips
+// (spectral.go:524-534) stay zero.
+template <typename P>
+__global__ __launch_bounds__(256) void stft_dft_kernel(const P* pcm, int64_t n, int64_t F, int W, int H,
+                                                       const double* win, const double2* trig_g, int trig_lds,
+                                                       double* mag, void* out_mag, void* out_cplx, void* out_phase,
+                                                       int out_f64) {
+  extern __shared__ __attribute__((aligned(16))) double dsm[];
+  const int64_t t = blockIdx.x;
+  if (t >= F) return;
+  const int K = W / 2 + 1;
+  double2* tl = reinterpret_cast<double2*>(dsm);
+  double* xs = dsm + (trig_lds ? 2 * W : 0);
+  const int64_t s0 = t * H;
+  const bool valid = s0 + W <= n;
+  if (trig_lds)
+    for (int i = threadIdx.x; i < W; i += 256) tl[i] = trig_g[i];
+  for (int i = threadIdx.x; i < W; i += 256) xs[i] = valid ? (double)pcm[s0 + i] * win[i] : 0.0;
+  __syncthreads();
+  const double2* tr = trig_lds ? tl : trig_g;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    double re = 0.0, im = 0.0;
+    int idx = 0;
+    for (int m = 0; m < W; ++m) {
+      const double2 c = tr[idx];
+      re += xs[m] * c.x;
+      im += xs[m] * c.y;
+      idx += k;
+      if (idx >= W) idx -= W;
+    }
+    const double a = hypot(re, im);                  // cmplx.Abs (spectral.go:492)
+    const int64_t o = t * K + k;
+    mag[o] = a;
+    auto put = [&](void* dst, int64_t i, double v) {
+      if (out_f64) reinterpret_cast<double*>(dst)[i] = v; else reinterpret_cast<float*>(dst)[i] = (float)v;
+    };
+    if (out_mag) put(out_mag, o, a);
+    if (out_cplx) { put(out_cplx, 2 * o, re); put(out_cplx, 2 * o + 1, im); }
+    if (out_phase) put(out_phase, o, atan2(im, re));
+  }
+}
+
+// MFCC.ComputeFrames on |X| rows (mfcc.go:126-143, 215-227): one wave per frame, the mel sums in
+// ascending-bin order, ln with the 1e-10 floor, DCT-II in ascending order, lifter -- the
+// operations and order of the fused kernels' epilogue, in float64
+__global__ __launch_bounds__(64) void mfcc_rows_kernel(const double* mag, int64_t F, int K, const int* lo,
+                                                       const int* hi, const int* woff, const double* w, int n_mels,
+                                                       const double* dct, const double* lift, int n_mfcc,
+                                                       int input_power, void* out, int out_f64) {
+  __shared__ double lm[512];
+  const int64_t t = blockIdx.x;
+  if (t >= F) return;
+  const int lane = threadIdx.x;
+  const double* row = mag + t * K;
+  for (int m = lane; m < n_mels; m += 64) {
+    double sm = 0.0;
+    const double* wm = w + woff[m] - lo[m];
+    for (int k = lo[m]; k < hi[m]; ++k) {
+      double v = row[k] * row[k];                     // |X|^2
+      if (input_power) v = v * v;                     // F5
+      sm += v * wm[k];
+    }
+    lm[m] = sm > 0.0 ? log(sm) : log(1e-10);
+  }
+  __syncthreads();
+  for (int kk = lane; kk < n_mfcc; kk += 64) {
+    double sm = 0.0;
+    for (int q = 0; q < n_mels; ++q) sm += lm[q] * dct[kk * n_mels + q];
+    const double v = sm * lift[kk];
+    if (out_f64) reinterpret_cast<double*>(out)[t * n_mfcc + kk] = v;
+    else reinterpret_cast<float*>(out)[t * n_mfcc + kk] = (float)v;
+  }
+}
+
+int launch_stft_dft(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, const double* win,
+                    const double* trig, double* mag, void* out_mag, void* out_cplx, void* out_phase, int out_f64,
+                    hipStream_t s) {
+  if (F <= 0) return 0;
+  if (W > 8192) return -4;
+  const int trig_lds = (size_t)W * 24 <= 64 * 1024;
+  const size_t lds = (size_t)W * 8 * (trig_lds ? 3 : 1);
+  if (pcm_f64)
+    hipLaunchKernelGGL(stft_dft_kernel<double>, dim3((unsigned)F), dim3(256), lds, s, (const double*)pcm, n, F, W, H,
+                       win, (const double2*)trig, trig_lds, mag, out_mag, out_cplx, out_phase, out_f64);
+  else
+    hipLaunchKernelGGL(stft_dft_kernel<float>, dim3((unsigned)F), dim3(256), lds, s, (const float*)pcm, n, F, W, H,
+                       win, (const double2*)trig, trig_lds, mag, out_mag, out_cplx, out_phase, out_f64);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_mfcc_rows(const double* mag, int64_t F, int K, const int* lo, const int* hi, const int* woff,
+                     const double* w, int n_mels, const double* dct, const double* lift, int n_mfcc, int input_power,
+                     void* out, int out_f64, hipStream_t s) {
+  if (F <= 0) return 0;
+  if (n_mels > 512) return -4;
+  hipLaunchKernelGGL(mfcc_rows_kernel, dim3((unsigned)F), dim3(64), 0, s, mag, F, K, lo, hi, woff, w, n_mels, dct, lift,
+                     n_mfcc, input_power, out, out_f64);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, double alpha, int sr, void* out,
                int out_f64, hipStream_t s) {
   if (F <= 0) return 0;

@@ -426,7 +426,7 @@ int sonar_fingerprint_multi(sonar_multi* m, const void* pcm, int64_t n, const so
     return mfail(m, SONAR_ERR_TOO_SHORT, "signal too short for given window size and hop size");
   const int G = (int)m->ctx.size();
   const size_t oe = elt_size(cfg->out_dtype), pe = elt_size(cfg->pcm_dtype);
-  const size_t nm = std::max(cfg->n_mfcc, 1), K = (size_t)W / 2 + 1;
+  const size_t nm = cfg->n_mfcc > 0 ? cfg->n_mfcc : 13, K = (size_t)W / 2 + 1;
   std::vector<int> rcs(G, SONAR_OK);
   std::vector<std::thread> th;
   for (int g = 0; g < G; ++g) {
@@ -473,7 +473,7 @@ int sonar_fingerprint_multi_gather(sonar_multi* m, const void* const* pcm_dev, i
     sonar_multi_shard(n, W, H, G, g, &f0[g], &f1[g], &s0[g], &s1[g]);
     maxF = std::max(maxF, f1[g] - f0[g]);
   }
-  const size_t oe = elt_size(cfg->out_dtype), nm = std::max(cfg->n_mfcc, 1);
+  const size_t oe = elt_size(cfg->out_dtype), nm = cfg->n_mfcc > 0 ? cfg->n_mfcc : 13;
   const size_t shard_bytes = (size_t)maxF * nm * oe;
   sonar_fp_cfg c1 = *cfg;
   c1.flags = SONAR_FP_MFCC;

@@ -243,7 +243,7 @@ void sonar_destroy(sonar_ctx* c) {
   for (auto& kv : c->fp_tables) {
     FpTables& t = kv.second;
     for (void* p : {(void*)t.window, (void*)t.mel_lo, (void*)t.mel_hi, (void*)t.mel_woff, (void*)t.grp_off,
-                    (void*)t.grp_mels, t.mel_w, t.dct, t.lift})
+                    (void*)t.grp_mels, t.mel_w, t.dct, t.lift, t.trig})
       if (p) hipFree(p);
   }
   for (auto& kv : c->chroma_tables) {
@@ -362,9 +362,14 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
   const uint32_t flags = cfg->flags;
   const bool need_fft = flags & (SONAR_FP_MFCC | SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_COMPLEX |
                                  SONAR_FP_PHASE);
-  if (need_fft && !sonar::fingerprint_supported(W))
-    return fail(c, SONAR_ERR_UNSUPPORTED, "window size " + std::to_string(W) +
-                                              " not supported by the GPU STFT (128, 256, 512, 1024, 2048)");
+  // other window lengths (go-dsp takes any W, spectral.go:131) run the generic DFT path; the
+  // spectral descriptors exist only in the fused kernels
+  const bool generic = need_fft && !sonar::fingerprint_supported(W);
+  if (generic && (flags & SONAR_FP_SPECTRAL))
+    return fail(c, SONAR_ERR_UNSUPPORTED, "spectral descriptors need a window of 128, 256, 512, 1024 or 2048 (got " +
+                                              std::to_string(W) + ")");
+  if (generic && W > 8192)
+    return fail(c, SONAR_ERR_UNSUPPORTED, "window size " + std::to_string(W) + " above 8192 (generic STFT path)");
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const size_t esz_in = pcm64 ? 8 : 4, esz_out = o64 ? 8 : 4;
@@ -388,7 +393,7 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     if (d) copies.push_back({user, d, count * esz_out});
     return d;
   };
-  void* d_mfcc = (flags & SONAR_FP_MFCC) ? out_ptr(out->mfcc, "mfcc", (size_t)F * std::max(cfg->n_mfcc, 1)) : nullptr;
+  void* d_mfcc = (flags & SONAR_FP_MFCC) ? out_ptr(out->mfcc, "mfcc", (size_t)F * (cfg->n_mfcc > 0 ? cfg->n_mfcc : 13)) : nullptr;
   void* d_mag = (flags & SONAR_FP_MAGNITUDE) ? out_ptr(out->magnitude, "mag", (size_t)F * K) : nullptr;
   if ((flags & SONAR_FP_MFCC) && !d_mfcc) return fail(c, SONAR_ERR_INVALID, "out->mfcc is null or allocation failed");
   if ((flags & SONAR_FP_MAGNITUDE) && !d_mag) return fail(c, SONAR_ERR_INVALID, "out->magnitude is null");
@@ -407,12 +412,67 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     }
   }
 
+  c->last_fp_kernel = "";
+  if (generic) {
+    char key[512];
+    std::snprintf(key, sizeof(key), "gen|%d|%d|%d|%d|%d|%d|%.17g|%.17g|%d|%.17g", W, cfg->window_type,
+                  cfg->sample_rate, cfg->n_mfcc, cfg->n_filters, cfg->filterbank, cfg->low_freq, cfg->high_freq,
+                  cfg->use_lifter, cfg->lifter);
+    auto it = c->fp_tables.find(key);
+    if (it == c->fp_tables.end()) {
+      FpTables t;
+      std::vector<double> win;
+      if (!sonar::host::make_window(cfg->window_type, W, true, true, 8.6, 0.5, win))
+        return fail(c, SONAR_ERR_INVALID, "failed to generate window: unsupported window type");
+      std::vector<double> trig(2 * (size_t)W);
+      for (int m = 0; m < W; ++m) {
+        trig[2 * m] = std::cos(2.0 * M_PI * (double)m / (double)W);
+        trig[2 * m + 1] = -std::sin(2.0 * M_PI * (double)m / (double)W);
+      }
+      t.window = upload(win);
+      t.trig = upload(trig);
+      if (flags & SONAR_FP_MFCC) {
+        sonar::host::MfccTables mt;
+        if (!sonar::host::make_mfcc_tables(cfg->sample_rate, cfg->n_mfcc, cfg->n_filters, cfg->filterbank,
+                                           cfg->low_freq, cfg->high_freq, cfg->use_lifter != 0, cfg->lifter, W, mt))
+          return fail(c, SONAR_ERR_INVALID, "failed to initialize MFCC: failed to create mel filter bank");
+        t.mel_lo = (int*)upload(mt.lo); t.mel_hi = (int*)upload(mt.hi); t.mel_woff = (int*)upload(mt.woff);
+        t.mel_w = upload(mt.w); t.dct = upload(mt.dct); t.lift = upload(mt.lift);
+        t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc; t.nnz = (int)mt.w.size();
+        if (!t.mel_lo || !t.mel_w || !t.dct || !t.lift) return fail(c, SONAR_ERR_NOMEM, "table upload failed");
+      }
+      if (!t.window || !t.trig) return fail(c, SONAR_ERR_NOMEM, "table upload failed");
+      it = c->fp_tables.emplace(key, t).first;
+    }
+    FpTables& t = it->second;
+    if ((flags & SONAR_FP_MFCC) && !t.mel_lo) {                   // tables built by a non-MFCC call first
+      sonar::host::MfccTables mt;
+      if (!sonar::host::make_mfcc_tables(cfg->sample_rate, cfg->n_mfcc, cfg->n_filters, cfg->filterbank,
+                                         cfg->low_freq, cfg->high_freq, cfg->use_lifter != 0, cfg->lifter, W, mt))
+        return fail(c, SONAR_ERR_INVALID, "failed to initialize MFCC: failed to create mel filter bank");
+      t.mel_lo = (int*)upload(mt.lo); t.mel_hi = (int*)upload(mt.hi); t.mel_woff = (int*)upload(mt.woff);
+      t.mel_w = upload(mt.w); t.dct = upload(mt.dct); t.lift = upload(mt.lift);
+      t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc; t.nnz = (int)mt.w.size();
+    }
+    double* mag = (double*)dbuf(c, "fp.gen.mag", (size_t)F * K * 8);
+    if (!mag) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (spectrogram)");
+    hipEvent_t tend = timed_begin(c, s);
+    if (sonar::launch_stft_dft(dpcm, pcm64, n, F, W, H, (const double*)t.window, (const double*)t.trig, mag, d_mag,
+                               d_cplx, d_phase, o64, s) != 0)
+      return fail(c, SONAR_ERR_DEVICE, "stft launch failed");
+    if ((flags & SONAR_FP_MFCC) &&
+        sonar::launch_mfcc_rows(mag, F, K, t.mel_lo, t.mel_hi, t.mel_woff, (const double*)t.mel_w, t.n_mels,
+                                (const double*)t.dct, (const double*)t.lift, t.n_mfcc, cfg->mfcc_input_power, d_mfcc,
+                                o64, s) != 0)
+      return fail(c, SONAR_ERR_DEVICE, "mfcc launch failed");
+    timed_end(c, s, tend);
+    c->last_fp_kernel = "stft_dft_kernel";
+  }
   // headline path: float32 MFCC only at W = 1024 (mfcc_pair.hip); SONAR_FP_GENERIC forces fp_kernel.hip
-  const bool pair_ok = need_fft && !f64 && !pcm64 && !o64 && W == 1024 && (flags & SONAR_FP_MFCC) &&
+  const bool pair_ok = !generic && need_fft && !f64 && !pcm64 && !o64 && W == 1024 && (flags & SONAR_FP_MFCC) &&
                        !(flags & (SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_COMPLEX | SONAR_FP_PHASE |
                                   SONAR_FP_GENERIC | 0x80000000u));
   bool pair_done = false;
-  c->last_fp_kernel = "";
   if (pair_ok) {
     char key[512];
     std::snprintf(key, sizeof(key), "%d|%d|%d|%d|%.17g|%.17g|%d|%.17g|%d|%d", cfg->window_type, cfg->sample_rate,
@@ -450,7 +510,7 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
       c->last_fp_kernel = "mfcc_pair_kernel";
     }
   }
-  if (need_fft && !pair_done) {
+  if (need_fft && !generic && !pair_done) {
     const bool spec = (flags & SONAR_FP_SPECTRAL) != 0;
     const int NB = sonar::fp_batch_frames(W);
     const int PRE = sonar::fp_pre_rows(W, spec);

@@ -714,7 +714,7 @@ class Multi:
         x = np.ascontiguousarray(pcm, dtype=pdt)
         res, o = {}, FpOut()
         if cfg.flags & FP_MFCC:
-            res["mfcc"] = np.zeros((F, max(cfg.n_mfcc, 1)), odt)
+            res["mfcc"] = np.zeros((F, cfg.n_mfcc if cfg.n_mfcc > 0 else 13), odt)
             o.mfcc = res["mfcc"].ctypes.data
         if cfg.flags & FP_MAGNITUDE:
             res["magnitude"] = np.zeros((F, cfg.window_size // 2 + 1), odt)
