@@ -13,6 +13,7 @@
 //                           edge hand-off, lane = row, DPP neighbours, distance inline
 //                           (see the DTW section below for the layout)
 //       dtw_walk_kernel   : one wave walks the 2-bit direction codes from (N, M)
+#include <cstdlib>
 #include <type_traits>
 
 #include "kernels.h"
@@ -23,6 +24,23 @@ namespace sonar {
 
 namespace {
 // math.Min (Go): NaN propagates, -Inf wins, -0 < +0
+// sqrt(x) for x in [2^-767, +Inf): LLVM's correctly rounded f64 sqrt sequence (v_rsq_f64 + two
+// Goldschmidt/Newton refinements) without its range scaling (an ldexp by 0 there) and its
+// 0 / Inf class fix-up (not taken there), so the same bits as sqrt() in 10 instructions instead
+// of 18.  The caller checks the range for the whole wave.
+__device__ __forceinline__ double sqrt_normal(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+constexpr double DTW_SQRT_MIN = 0x1p-767;   // below: the full sqrt() (its scaled range)
+
 __device__ __forceinline__ double go_min(double x, double y) {
   if (__builtin_isinf(x) && x < 0) return x;
   if (__builtin_isinf(y) && y < 0) return y;
@@ -696,8 +714,23 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
               }
             }
           }
+          if constexpr (FAST) {
+            // finite inputs: sums are finite and >= 0; the short sqrt when every lane's DG sums
+            // are in its range (all but exact or near-exact zero distances), else sqrt()
+            double mn = sum[0];
 #pragma unroll
-          for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt(sum[u]);
+            for (int u = 1; u < DTW_DG; ++u) mn = vmin_f64(mn, sum[u]);
+            if (__builtin_amdgcn_ballot_w64(!(mn >= DTW_SQRT_MIN)) == 0) {
+#pragma unroll
+              for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt_normal(sum[u]);
+            } else {
+#pragma unroll
+              for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt(sum[u]);
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt(sum[u]);
+          }
         }
 #endif
       } else {
@@ -1198,9 +1231,27 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
             trace};
   const DtwBatch nob{};
   const bool pre = Dd && dim == 12;
+  // SONAR_DTW_DBG_CONC=1 (timing experiment only, WRONG results): the distance kernel on a side
+  // stream concurrently with the band kernel, which does not wait for it
+  static hipStream_t side = nullptr;
+  static hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  const char* conc_env = std::getenv("SONAR_DTW_DBG_CONC");
+  const bool conc = pre && conc_env && conc_env[0] == '1';
   if (pre) {
     a.Dd = Dd;
-    launch_dtw_dist(q, r, g, Dd, s);
+    if (conc) {
+      if (!side) {
+        hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
+        hipEventCreateWithFlags(&ev_a, hipEventDisableTiming);
+        hipEventCreateWithFlags(&ev_b, hipEventDisableTiming);
+      }
+      hipEventRecord(ev_a, s);
+      hipStreamWaitEvent(side, ev_a, 0);
+      launch_dtw_dist(q, r, g, Dd, side);
+      hipEventRecord(ev_b, side);
+    } else {
+      launch_dtw_dist(q, r, g, Dd, s);
+    }
   }
   const dim3 grid((unsigned)g.nb), block(64 * DTW_WAVES), pblock(64 * dtw_block_waves(true));
 #define SONAR_DTW_LAUNCH(DD)                                                                          \
@@ -1227,6 +1278,7 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
   else SONAR_DTW_LAUNCH(0);
 #undef SONAR_DTW_LAUNCH
   if (mid) hipEventRecord(mid, s);
+  if (conc) hipStreamWaitEvent(s, ev_b, 0);
   hipLaunchKernelGGL(dtw_walk_kernel, dim3(1), dim3(64), 0, s, Dn, g.nq, g.nr, g.SW, codes, plen);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
