@@ -305,8 +305,9 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 // has read the count that covers it; LDS requests of one wave complete in order, so data loads
 // issued AFTER a counter load see everything the counter covers).  Wave order: sweep, NDW
 // distance waves, feeder, code, edge -- a block's waves go to SIMDs in the cyclic order 0, 2, 1,
-// 3 (MI355X_MICROARCH.md, LDS), so with NDW = 3 the sweep shares its SIMD with the feeder
-// (mostly asleep) rather than with a distance wave.
+// 3 (MI355X_MICROARCH.md, LDS).  NDW = 4 (A/B against 3, 5, 6 and DG 4 in
+// tools/scratch/ab_ndw.sh: C3 band 21.1 -> 20.3 ms, C5 +1 %; 5 or 6 waves need DG 4 to keep two
+// blocks per CU and lose more to the shorter interleave).
 //  sweep     the min-chain of every cell and the band's bottom edge.  Per step only DPP -> min
 //            -> add is on the chain.  A single wave issues LDS and memory instructions slowly
 //            (each moves its 64 lanes' data), so the sweep does few: per 8-step chunk 4 paired
@@ -337,7 +338,7 @@ constexpr int DTW_OROW = DTW_OQ + 2;       // multiple of 4 dwords plus 4 (mod 6
 constexpr int DTW_EQ = 128;       // edge values in the LDS rings
 constexpr int DTW_EAHEAD = 64;    // the feeder fetches edge columns up to min(prog, cprog) + EAHEAD
 #ifndef DTW_NDW
-#define DTW_NDW 3                 // distance waves per block
+#define DTW_NDW 4                 // distance waves per block (A/B: tools/scratch/ab_ndw.sh)
 #endif
 #ifndef DTW_DG
 #define DTW_DG 8                  // distance cells interleaved per pass (a divisor of DTW_ECH)
@@ -350,7 +351,13 @@ constexpr int DTW_WAVES = 4 + DTW_NDW;
 constexpr int DTW_FEEDER_WAVE = DTW_NDW + 1;
 constexpr int DTW_CODE_WAVE = DTW_NDW + 2;
 constexpr int DTW_EDGE_WAVE = DTW_NDW + 3;
-static_assert(DTW_NDW == 3, "the sweep reads {dchunk[0..2], efill} as one 16-B quad");
+static_assert(DTW_NDW >= 1 && DTW_NDW <= 7, "distance counters live in ctr[0..6]");
+// counter slots: NDW <= 3 keeps {dchunk[0..2], efill} in one 16-B quad (one LDS read for the
+// sweep); more distance waves use ctr[0..NDW-1] + efill in ctr[7] (two quads)
+constexpr int DTW_CTR_EFILL = DTW_NDW <= 3 ? 3 : 7;
+constexpr int DTW_CTR_CPROG = DTW_NDW <= 3 ? 4 : 8;
+constexpr int DTW_CTR_PROG = DTW_NDW <= 3 ? 5 : 9;
+constexpr int DTW_CTR_RDY = DTW_NDW <= 3 ? 6 : 10;
 // Ring row stride in doubles.  A distance wave's lane l reads row t-l, so consecutive lanes sit
 // one stride apart; 12-dim rows padded to 14 doubles (112 B, 28 dwords: 16 distinct 4-dword bank
 // quads in every 16-lane group of ds_read_b128) make those reads conflict-free (96 B is 2-way).
@@ -386,18 +393,18 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   __shared__ __attribute__((aligned(16))) double oring[64][DTW_OROW];   // C of step t at [l][t % OQ]
   __shared__ __attribute__((aligned(16))) double eqa[DTW_EQ];           // C[64b][c] at slot c - 1
   __shared__ __attribute__((aligned(16))) double eqb[DTW_EQ];           // C[64b][c] at slot c
-  // ctr[0..2] dchunk (per distance wave: 1 + its last finished chunk), ctr[3] efill (edge columns
-  // in the rings), ctr[4] cprog (code steps done), ctr[5] prog (sweep steps done), ctr[6] rdy
-  // (highest ring block ready)
-  __shared__ __attribute__((aligned(16))) int ctr[8];
+  // dchunk[w] (per distance wave: 1 + its last finished chunk) in ctr[0..NDW-1], then efill (edge
+  // columns in the rings), cprog (code steps done), prog (sweep steps done), rdy (highest ring
+  // block ready) at the DTW_CTR_* slots
+  __shared__ __attribute__((aligned(16))) int ctr[16];
   __shared__ int64_t shb;
   __shared__ int shk;
 #define SONAR_LDS_LD(x) __hip_atomic_load(&(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
 #define SONAR_LDS_ST(x, v) __hip_atomic_store(&(x), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-  int& efill = ctr[3];
-  int& cprog = ctr[4];
-  int& prog = ctr[5];
-  int& rdy = ctr[6];
+  int& efill = ctr[DTW_CTR_EFILL];
+  int& cprog = ctr[DTW_CTR_CPROG];
+  int& prog = ctr[DTW_CTR_PROG];
+  int& rdy = ctr[DTW_CTR_RDY];
   // (wave is uniform: readfirstlane keeps it, and every address derived from it, in SGPRs)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const double inf = __builtin_inf();
@@ -414,7 +421,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     } else {
       shb = atomicAdd(&a_in.sync[0], 1);
     }
-    for (int k = 0; k < 8; ++k) ctr[k] = 0;
+    for (int k = 0; k < 16; ++k) ctr[k] = 0;
     rdy = -1;
   }
   if (threadIdx.x < 64) {        // steps -1 and -2: C[i][j] for j <= 0 is +Inf (column 0) / unset
@@ -656,9 +663,8 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
             *reinterpret_cast<double2*>(drow + u) = make_double2(buf[k][u], buf[k][u + 1]);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           if (lane == 0) {
-            SONAR_LDS_ST(ctr[0], (int)(c + 1));
-            SONAR_LDS_ST(ctr[1], (int)(c + 1));
-            SONAR_LDS_ST(ctr[2], (int)(c + 1));
+#pragma unroll
+            for (int k = 0; k < DTW_NDW; ++k) SONAR_LDS_ST(ctr[k], (int)(c + 1));
           }
           if (c + DTW_PF < nch) fetch(c + DTW_PF, buf[k]);
         }
@@ -766,20 +772,38 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   // and the code wave's progress (C-ring slots reused after DTW_OQ steps) are there.  32-bit
   // compares: nq + nr < 2^31 is checked on the host.
   const int nr32 = (int)nr;
-  auto ready = [&](int s0, int4 c03, int cp) -> bool {
+  // the counters the sweep reads: dchunk[0..NDW-1], efill, cprog (scalars, not an array, so
+  // nothing lands in scratch)
+  struct Ctrs { int d0, d1, d2, d3, d4, d5, d6, ef, cp; };
+  auto ready = [&](int s0, Ctrs k) -> bool {
     const int c = s0 / DTW_ECH, w = c % DTW_NDW;
-    const int dchk = w == 0 ? c03.x : (w == 1 ? c03.y : c03.z);
+    int dchk = k.d0;
+    if (DTW_NDW > 1 && w == 1) dchk = k.d1;
+    if (DTW_NDW > 2 && w == 2) dchk = k.d2;
+    if (DTW_NDW > 3 && w == 3) dchk = k.d3;
+    if (DTW_NDW > 4 && w == 4) dchk = k.d4;
+    if (DTW_NDW > 5 && w == 5) dchk = k.d5;
+    if (DTW_NDW > 6 && w == 6) dchk = k.d6;
     const int neede = s0 + DTW_ECH < nr32 ? s0 + DTW_ECH : nr32;
-    return dchk > c && (!Ein || c03.w >= neede) && cp >= s0 + DTW_ECH - DTW_OQ + 2;
+    return dchk > c && (!Ein || k.ef >= neede) && k.cp >= s0 + DTW_ECH - DTW_OQ + 2;
   };
-  // {dchunk[0..2], efill} as one 16-B volatile LDS read, cprog as one 4-B read
+  // {dchunk, efill} as one (NDW <= 3) or two 16-B volatile LDS reads, cprog as one 4-B read
   typedef int ctr4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) volatile ctr4 lds_ctr4;   // LDS, not flat
   typedef __attribute__((address_space(3))) volatile int lds_int;
-  auto load_ctr = [&](int4& c03, int& cp) {
+  auto load_ctr = [&]() -> Ctrs {
+    Ctrs k;
     const ctr4 x = *(lds_ctr4*)(&ctr[0]);
-    c03 = make_int4(x.x, x.y, x.z, x.w);
-    cp = *(lds_int*)(&ctr[4]);
+    k.d0 = x.x; k.d1 = x.y; k.d2 = x.z; k.d3 = x.w;
+    if constexpr (DTW_NDW > 3) {
+      const ctr4 y = *(lds_ctr4*)(&ctr[4]);
+      k.d4 = y.x; k.d5 = y.y; k.d6 = y.z; k.ef = y.w;
+    } else {
+      k.d4 = k.d5 = k.d6 = 0;
+      k.ef = x.w;
+    }
+    k.cp = *(lds_int*)(&ctr[DTW_CTR_CPROG]);
+    return k;
   };
   // raw loads only: the border selects come after the steps, so the loads' latency overlaps the
   // chunk instead of stalling its start
@@ -835,11 +859,9 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   };
 
   double dc[DTW_ECH], ech[DTW_ECH];
-  int4 c03;
-  int cp;
-  load_ctr(c03, cp);
-  if (!ready(0, c03, cp)) {
-    SONAR_SPIN_UNTIL((load_ctr(c03, cp), ready(0, c03, cp)));
+  Ctrs kc = load_ctr();
+  if (!ready(0, kc)) {
+    SONAR_SPIN_UNTIL((kc = load_ctr(), ready(0, kc)));
   }
   if (a.trace) t_first = __builtin_amdgcn_s_memrealtime();
   load_chunk(0, dc, ech);
@@ -849,7 +871,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     // next chunk: counters first, then its data (LDS completes a wave's requests in order)
     double dcn[DTW_ECH], echn[DTW_ECH];
     if (s1 < S) {
-      load_ctr(c03, cp);
+      kc = load_ctr();
       load_chunk(s1, dcn, echn);
     }
     if (s0 >= 63 && s1 <= nr) {
@@ -876,8 +898,8 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         __hip_atomic_store(Eout + je, __builtin_bit_cast(uint64_t, ev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (s1 >= S) break;
-    if (!ready((int)s1, c03, cp)) {                    // a producer is behind: wait, then reload
-      SONAR_SPIN_UNTIL((load_ctr(c03, cp), ready((int)s1, c03, cp)));
+    if (!ready((int)s1, kc)) {                         // a producer is behind: wait, then reload
+      SONAR_SPIN_UNTIL((kc = load_ctr(), ready((int)s1, kc)));
       load_chunk(s1, dcn, echn);
     }
     fix_edges(s1, echn);
