@@ -348,9 +348,17 @@ constexpr int DTW_EAHEAD = 64;    // the feeder fetches edge columns up to min(p
 #endif
 constexpr int DTW_WAVES = 4 + DTW_NDW;
 // wave roles: 0 sweep, 1..NDW distance, then the ring feeder, the code wave and the edge poller
-constexpr int DTW_FEEDER_WAVE = DTW_NDW + 1;
+// DTW_SWAP_FEEDER: the feeder takes wave 4 (the sweep's SIMD under the 0,2,1,3 order) and the
+// last distance wave moves to the feeder's slot (NDW >= 4 only; A/B knob)
+#ifndef DTW_SWAP_FEEDER
+#define DTW_SWAP_FEEDER 0
+#endif
+constexpr bool DTW_SWAP = DTW_SWAP_FEEDER && DTW_NDW >= 4;
+constexpr int DTW_FEEDER_WAVE = DTW_SWAP ? 4 : DTW_NDW + 1;
 constexpr int DTW_CODE_WAVE = DTW_NDW + 2;
 constexpr int DTW_EDGE_WAVE = DTW_NDW + 3;
+// distance-wave index of wave `wave` (1..NDW+1 minus the feeder)
+__device__ __forceinline__ int dtw_dist_index(int wave) { return DTW_SWAP && wave == DTW_NDW + 1 ? 3 : wave - 1; }
 static_assert(DTW_NDW >= 1 && DTW_NDW <= 7, "distance counters live in ctr[0..6]");
 // counter slots: NDW <= 3 keeps {dchunk[0..2], efill} in one 16-B quad (one LDS read for the
 // sweep); more distance waves use ctr[0..NDW-1] + efill in ctr[7] (two quads)
@@ -672,9 +680,9 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     }
     return;
   }
-  if (!PRE && wave >= 1) {
+  if (!PRE && wave >= 1) {   // (every other role returned above)
     // ---------------------------------------------------------- distance waves
-    const int w = wave - 1;
+    const int w = dtw_dist_index(wave);
     for (int64_t c = w; DTW_ECH * c < S; c += DTW_NDW) {
       const int64_t t0 = DTW_ECH * c;
       // ring slots of steps t0..t0+7 were last read by the sweep for steps t0-DQ..t0-DQ+7
