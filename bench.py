@@ -61,7 +61,8 @@ def parse():
     ap.add_argument("--c5-pairs", type=int, default=1000, help="C5 stream pairs in total (0 = skip)")
     ap.add_argument("--c5-seconds", type=float, default=60.0)
     ap.add_argument("--c5-max-lag", type=float, default=20.0, help="maxOffsetSeconds (lags are drawn in [0, 20) s)")
-    ap.add_argument("--c5-workers", type=int, default=16, help="concurrent contexts (HIP streams) per rank")
+    ap.add_argument("--c5-workers", type=int, default=128,
+                    help="pairs in flight per rank (sonar_align_pairs: 16 streams x batches of 8)")
     ap.add_argument("--c6-gallery", type=int, default=256, help="C3-sized fingerprints added (0 = skip row f1)")
     ap.add_argument("--c6-frames", type=int, default=51676)
     ap.add_argument("--c6-compare-gallery", type=int, default=65536)

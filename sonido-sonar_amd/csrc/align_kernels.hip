@@ -13,6 +13,7 @@
 //                           edge hand-off, lane = row, DPP neighbours, distance inline
 //                           (see the DTW section below for the layout)
 //       dtw_walk_kernel   : one wave walks the 2-bit direction codes from (N, M)
+#include <cstdint>
 #include <cstdlib>
 #include <type_traits>
 
@@ -261,6 +262,8 @@ struct DtwBatch {
   const int64_t* start;
   int n;
   int32_t* ticket;
+  const int2* map;   // nullable: ticket -> (DTW, band) in any order where a band's predecessor
+                     // has the smaller ticket; null: DTW-major through `start`
 };
 
 namespace {
@@ -419,13 +422,24 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   if (threadIdx.x == 0) {
     if constexpr (BATCH) {
       const int64_t t = atomicAdd(bt.ticket, 1);
-      int lo = 0, hi = bt.n;                          // start[lo] <= t < start[lo + 1]
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (bt.start[mid] <= t) lo = mid; else hi = mid;
+      if (bt.map) {
+        if (t < bt.start[bt.n]) {
+          const int2 pb = bt.map[t];
+          shk = pb.x;
+          shb = pb.y;
+        } else {
+          shk = 0;
+          shb = INT64_MAX;                            // past the last ticket: the block exits
+        }
+      } else {
+        int lo = 0, hi = bt.n;                        // start[lo] <= t < start[lo + 1]
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (bt.start[mid] <= t) lo = mid; else hi = mid;
+        }
+        shk = lo;
+        shb = t - bt.start[lo];                       // >= nb past the last DTW: the block exits
       }
-      shk = lo;
-      shb = t - bt.start[lo];                         // >= nb past the last DTW: the block exits
     } else {
       shb = atomicAdd(&a_in.sync[0], 1);
     }
@@ -1325,11 +1339,11 @@ int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const uint32_t* cod
 }
 
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
-                     int64_t max_cap, int32_t* ticket, hipStream_t s) {
+                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap) {
   if (n <= 0 || total_bands <= 0) return 0;
   if (total_bands > INT32_MAX) return -1;
   const DtwArgs none{};
-  const DtwBatch bt{dargs, dstart, n, ticket};
+  const DtwBatch bt{dargs, dstart, n, ticket, dmap};
   const bool pre = hargs[0].Dd != nullptr;
   if (pre) {
     for (int k = 0; k < n; ++k) {

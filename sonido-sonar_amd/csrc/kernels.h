@@ -180,8 +180,10 @@ struct DtwArgs {
 // round trip.  The caller zeroes each DTW's sync words and *ticket and fills each E with the
 // sentinel words 0x7FF00001 first; max_cap >= every nq + nr + 1.
 // (hargs: the same array on the host; every Dd set -> distances precomputed per DTW first)
+// dmap (nullable): ticket -> (DTW, band) order, e.g. band-major across the batch so a band waits
+// about one hand-off for its predecessor instead of b of them
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
-                     int64_t max_cap, int32_t* ticket, hipStream_t s);
+                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr);
 // sets *flag = 1 if any of the n values is not finite
 int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 

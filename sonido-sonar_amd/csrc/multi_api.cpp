@@ -151,7 +151,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     total_bands += p.g.nb;
   }
   const size_t stat_b = al256((size_t)n * 32 + 16), args_b = al256((size_t)n * sizeof(sonar::DtwArgs)),
-               start_b = al256((size_t)(n + 1) * 8);
+               start_b = al256((size_t)(n + 1) * 8), map_b = al256((size_t)total_bands * 8);
   char* chroma = (char*)dbuf(w, "pb.chroma", chroma_b);
   char* Cn = (char*)dbuf(w, "pb.Cn", cn_b);
   const bool pre = sonar::detail::dtw_pre_enabled(12);
@@ -162,7 +162,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* wst = (char*)dbuf(w, "pb.wstart", wst_b);
   char* path = (char*)dbuf(w, "pb.path", path_b);
   char* corr = (char*)dbuf(w, "pb.corr", corr_b);
-  char* small = (char*)dbuf(w, "pb.small", stat_b + args_b + start_b);
+  char* small = (char*)dbuf(w, "pb.small", stat_b + args_b + start_b + map_b);
   double* eq = (double*)dbuf(w, "pb.eq", (size_t)maxE * 8);
   double* er = (double*)dbuf(w, "pb.er", (size_t)maxE * 8);
   double* xa = (double*)dbuf(w, "ncc.xa", (size_t)maxE * 8);
@@ -170,7 +170,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   double* st = (double*)dbuf(w, "ncc.stats", 64);
   double* up_q = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.q", (size_t)maxn * 8);
   double* up_r = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.r", (size_t)maxn * 8);
-  char* h = (char*)sonar::detail::hbuf(w, "pb.host", stat_b + args_b + start_b + corr_b + path_b);
+  char* h = (char*)sonar::detail::hbuf(w, "pb.host", stat_b + args_b + start_b + map_b + corr_b + path_b);
   if (!chroma || !Cn || (pre && !Dd) || !Dn || !E || !codes || !wst || !path || !corr || !small || !eq || !er || !xa || !xb || !st ||
       (!device_ptrs && (!up_q || !up_r)) || !h)
     return fail(w, SONAR_ERR_NOMEM, "allocation failed (pair batch)");
@@ -181,7 +181,9 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* hstat = h;
   sonar::DtwArgs* hargs = (sonar::DtwArgs*)(h + stat_b);
   int64_t* hstart = (int64_t*)(h + stat_b + args_b);
-  char* hcorr = h + stat_b + args_b + start_b;
+  int2* hmap = (int2*)(h + stat_b + args_b + start_b);
+  int2* dmap = (int2*)(small + stat_b + args_b + start_b);
+  char* hcorr = h + stat_b + args_b + start_b + map_b;
   char* hpath = hcorr + corr_b;
   HIP_TRY(w, hipMemsetAsync(small, 0, stat_b, s));
   if (e_b) HIP_TRY(w, hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, e_b / 4, s));
@@ -217,8 +219,21 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     acc += p.g.nb;
   }
   hstart[n] = acc;
-  HIP_TRY(w, hipMemcpyAsync(dargs, hargs, args_b + start_b, hipMemcpyHostToDevice, s));
-  if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s) != 0)
+  // band-major tickets across the batch (SONAR_DTW_BAND_MAJOR=0: DTW-major): band b of every DTW
+  // before band b+1 of any, so a block waits about one hand-off for its predecessor band rather
+  // than b of them while holding its slot
+  const char* bm = std::getenv("SONAR_DTW_BAND_MAJOR");
+  const bool band_major = !(bm && std::atoi(bm) == 0);
+  if (band_major) {
+    int64_t t = 0, maxnb = 0;
+    for (const auto& p : pg) maxnb = std::max(maxnb, p.g.nb);
+    for (int64_t b = 0; b < maxnb; ++b)
+      for (int i = 0; i < n; ++i)
+        if (b < pg[i].g.nb) hmap[t++] = make_int2(i, (int)b);
+  }
+  HIP_TRY(w, hipMemcpyAsync(dargs, hargs, args_b + start_b + (band_major ? map_b : 0), hipMemcpyHostToDevice, s));
+  if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s,
+                              band_major ? dmap : nullptr) != 0)
     return fail(w, SONAR_ERR_DEVICE, "dtw batch launch failed");
   HIP_TRY(w, hipMemcpyAsync(hstat, small, (size_t)n * 32, hipMemcpyDeviceToHost, s));
   if (corr_b) HIP_TRY(w, hipMemcpyAsync(hcorr, corr, corr_b, hipMemcpyDeviceToHost, s));
@@ -264,7 +279,7 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
   if (npairs < 0 || (npairs > 0 && (!q_pcm || !nq || !r_pcm || !nr || !out)))
     return fail(c, SONAR_ERR_INVALID, "null pair arrays");
   if (npairs == 0) return SONAR_OK;
-  const int64_t inflight = workers > 0 ? workers : 16;
+  const int64_t inflight = workers > 0 ? workers : 128;   // pairs in flight (measured: C5 rises to ~128)
   std::atomic<int> first_err{SONAR_OK};
   auto note = [&](int r, int64_t k, sonar_ctx* w) {
     if (r == SONAR_OK) return;
@@ -275,8 +290,8 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
   const char* bev = std::getenv("SONAR_PAIR_BATCH");
   const bool batched = !(bev && std::atoi(bev) == 0);
   const char* sev = std::getenv("SONAR_PAIR_STREAMS");
-  const int nstreams = batched ? (int)std::max<int64_t>(1, std::min<int64_t>(sev ? std::atoi(sev) : 8, npairs))
-                               : (int)std::min<int64_t>(inflight, npairs);
+  const int nstreams = batched ? (int)std::max<int64_t>(1, std::min<int64_t>(sev ? std::atoi(sev) : 16, npairs))
+                               : (int)std::min<int64_t>(std::min<int64_t>(inflight, 16), npairs);
   int rc = SONAR_OK;
   std::vector<sonar_ctx*>& ws = workers_of(c, nstreams, &rc);
   if (rc != SONAR_OK) return fail(c, rc, "worker context creation failed");
@@ -298,7 +313,12 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
   // in-flight count split over the streams), cut further by a device-memory budget
   const int64_t per = std::max<int64_t>(1, (inflight + nstreams - 1) / nstreams);
   const char* mev = std::getenv("SONAR_PAIR_BATCH_GB");
-  const size_t budget = (size_t)((mev ? std::atof(mev) : 24.0) * (1ull << 30));
+  size_t budget = (size_t)((mev ? std::atof(mev) : 24.0) * (1ull << 30));
+  {   // every stream holds one batch: keep them within ~70 % of the device memory free now
+    size_t fr = 0, tot = 0;
+    if (hipSetDevice(c->device) == hipSuccess && hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0)
+      budget = std::min(budget, (size_t)(0.7 * (double)fr / (double)nstreams));
+  }
   const int64_t max_lag_samples = (int64_t)(max_lag_seconds * (double)sample_rate);   // alignment.go:104
   std::vector<PairGeo> geo;
   for (int64_t k = 0; k < npairs; ++k) {
