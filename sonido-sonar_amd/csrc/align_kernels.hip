@@ -334,7 +334,10 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 #endif
 constexpr int DTW_RROWS = DTW_RROWS_CFG;   // reference rows in the LDS ring
 constexpr int DTW_RBLK = 16;               // rows per ring refill
-constexpr int DTW_DQ = 32;                 // steps of distances held in LDS
+#ifndef DTW_DQ_CFG
+#define DTW_DQ_CFG 32
+#endif
+constexpr int DTW_DQ = DTW_DQ_CFG;         // steps of distances held in LDS (a power of two)
 constexpr int DTW_OQ = 32;                 // steps of C values held in LDS for the code wave
 constexpr int DTW_DROW = DTW_DQ + 2;       // doubles per lane row of the transposed rings: a
 constexpr int DTW_OROW = DTW_OQ + 2;       // multiple of 4 dwords plus 4 (mod 64 dwords)
@@ -577,6 +580,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     uint32_t* Db = a.Dn + ((b * a.SW) << 6) + lane;
     double* Cb = a.Cn + dtw_cn_off(b, S2, 0, lane);
     uint32_t dacc = 0;
+    double ckv = 0.0;                                  // the lane's C at the latest multiple-of-64 column
     for (int64_t s0 = 0; s0 < S; s0 += DTW_ECH) {
       const int need = (int)(s0 + DTW_ECH < S ? s0 + DTW_ECH : S);
       SONAR_SPIN_UNTIL(SONAR_LDS_LD(prog) >= need);
@@ -615,10 +619,26 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         dacc |= code << (2 * ((s0 & 8) + u));
       }
       // the chunk's C values: cv[2 + u] = step s0 + u, stored as pairs (Cn[b][s/2][l][s%2])
+      if (a.Cn) {
 #pragma unroll
-      for (int k = 0; k < DTW_ECH / 2; ++k)
-        if (s0 + 2 * k < S)
-          *reinterpret_cast<double2*>(Cb + ((s0 + 2 * k) << 6)) = make_double2(cv[2 + 2 * k], cv[3 + 2 * k]);
+        for (int k = 0; k < DTW_ECH / 2; ++k)
+          if (s0 + 2 * k < S)
+            *reinterpret_cast<double2*>(Cb + ((s0 + 2 * k) << 6)) = make_double2(cv[2 + 2 * k], cv[3 + 2 * k]);
+      } else {
+        // checkpoint columns only.  Lane l meets column J = 64m at step J + l - 1, so every lane
+        // has C[i][J] once the chunk holding step J + 62 is done (s0 % 64 == 56, J = s0 - 56):
+        // one coalesced 512-B store per 64 steps.  In that chunk lanes 57-63 take their value of
+        // column J and lane 0 already its value of column J + 64.
+        const int u = (int)((lane - 1 - s0) & 63);      // the chunk step at which the lane's column is 64m
+        // (one LDS read of the C ring, still holding the chunk, instead of a select over cv[])
+        const double cap = u < DTW_ECH ? oring[lane][(s0 + u) & (DTW_OQ - 1)] : ckv;
+        const int64_t J = s0 - 56;
+#ifndef DTW_DBG_NOCK   // A/B diagnostics: no checkpoint stores (wrong path costs; timing only)
+        if ((s0 & 63) == 56 && J >= 64 && J <= nr)
+          a.CK[((b * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = (u < DTW_ECH && lane != 0) ? cap : ckv;
+#endif
+        ckv = cap;
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) SONAR_LDS_ST(cprog, need);
       if ((s0 & 8) || s0 + DTW_ECH >= S) {             // steps 16w .. 16w+15 complete (or the last one)
@@ -935,7 +955,11 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     a.trace[8 * b + 0] = t_start;
     a.trace[8 * b + 1] = t_first;
     a.trace[8 * b + 2] = __builtin_amdgcn_s_memrealtime();
-    a.trace[8 * b + 3] = spins_total;
+    // spins (10 ns ticks, low 24 bits), XCC id (bits 24-31) and HW_ID (high word: SIMD bits 4-5,
+    // CU/SH/SE bits 8-15) of the sweep wave, so the probe can see which sweeps shared a SIMD
+    const uint64_t hw = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    const uint64_t xcc = (uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20); // HW_REG_XCC_ID
+    a.trace[8 * b + 3] = (spins_total & 0xFFFFFFull) | ((xcc & 0xFF) << 24) | (hw << 32);
     a.trace[8 * b + 4] = c_start;
     a.trace[8 * b + 5] = __builtin_amdgcn_s_memtime();
   }
@@ -1086,7 +1110,7 @@ __global__ __launch_bounds__(1024) void dtw_path_scan_kernel(const uint32_t* cod
   if constexpr (BATCH) {
     const DtwArgs a = load_args_uniform(args + blockIdx.x);
     codes = a.codes; P = *a.plen; nq = a.nq; nr = a.nr; wstart = a.wstart;
-    if (t == 0) *a.cnm = cn_at(a.Cn, a.S, nq, nr);
+    if (t == 0 && a.Cn) *a.cnm = cn_at(a.Cn, a.S, nq, nr);   // (CK mode: the tile pass writes it)
   }
   const int64_t nw = (P + 15) >> 4;
   const int64_t per = (nw + 1023) / 1024;
@@ -1144,7 +1168,7 @@ __global__ __launch_bounds__(256) void dtw_path_points_kernel(const uint32_t* co
   for (int k = 0; k < 16; ++k) {
     ii[k] = i; jj[k] = j;
     c[k] = 0.0;
-    if (k < n && i > 0 && j > 0) c[k] = __dsub_rn(cn_at(Cn, S, i, j), cn_at(Cn, S, i - 1, j - 1));
+    if (Cn && k < n && i > 0 && j > 0) c[k] = __dsub_rn(cn_at(Cn, S, i, j), cn_at(Cn, S, i - 1, j - 1));
     const uint32_t m = (x >> (2 * k)) & 3u;
     i -= m != 1u;
     j -= m != 0u;
@@ -1153,8 +1177,120 @@ __global__ __launch_bounds__(256) void dtw_path_points_kernel(const uint32_t* co
   for (int k = 0; k < 16; ++k) {
     if (k < n) {
       const int64_t f = P - 1 - (16 * w + k);
-      pq[f] = ii[k] - 1; pr[f] = jj[k] - 1; pc[f] = c[k];
+      pq[f] = ii[k] - 1; pr[f] = jj[k] - 1;
+      if (Cn || ii[k] == 0 || jj[k] == 0) pc[f] = c[k];   // (CK mode: the tile pass writes the rest)
     }
+  }
+}
+
+// ---------------------------------------------------------------- path tiles (CK mode)
+// Without the cost matrix, a path point's cost C[i][j] - C[i-1][j-1] (dtw.go:165-188) is
+// recomputed: the path visits at most nb + ceil(nr/64) tiles of 64 x 64 cells (tile (bi, bj) =
+// rows 64bi+1 .., columns 64bj+1 ..), and a tile's cells follow from its top row C[64bi][*] (the
+// band edge E of band bi-1, or row 0) and its left column C[*][64bj] (checkpoint CK, or column
+// 0), both written by the band kernel.  The recurrence, the distance (Go's sequential sum,
+// unfused, then a correctly rounded sqrt) and math.Min are the band kernel's, so every value is
+// bit-identical to the full store's.
+//  dtw_path_runs_kernel: thread per path point; a point whose tile differs from its
+//    predecessor's starts a run (the path is monotone, so a tile's points are contiguous); runs
+//    are appended through an atomic counter in any order.
+//  dtw_path_tile_kernel: one wave per run: the tile's distances into LDS (lane = row), the
+//    anti-diagonal recurrence in LDS (127 steps), then the run's costs (and C[nq][nr]).
+template <bool BATCH>
+__global__ __launch_bounds__(256) void dtw_path_runs_kernel(DtwArgs a_in, const DtwArgs* args) {
+  const DtwArgs a = BATCH ? load_args_uniform(args + blockIdx.y) : a_in;
+  const int64_t P = *a.plen;
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= P) return;
+  const int pi = a.pq[f], pj = a.pr[f];
+  if (pi < 0 || pj < 0) return;                      // border point: cost 0, written by the points pass
+  bool start = f == 0;
+  if (!start) {
+    const int qi = a.pq[f - 1], qj = a.pr[f - 1];
+    start = qi < 0 || qj < 0 || (qi >> 6) != (pi >> 6) || (qj >> 6) != (pj >> 6);
+  }
+  if (start) {
+    const int k = atomicAdd(&a.runs[0], 1);
+    a.runs[1 + k] = (int)f;
+  }
+}
+
+template <bool BATCH, int D>
+__global__ __launch_bounds__(64) void dtw_path_tile_kernel(DtwArgs a_in, const DtwArgs* args) {
+  __shared__ double T[65][66];                       // T[li][lj] = C[64bi + li][64bj + lj]
+  __shared__ double Dl[64][65];                      // local distance of cell (64bi+1+l, 64bj+1+c)
+  __shared__ __attribute__((aligned(16))) double Rt[D > 0 ? 64 * D : 2];   // D > 0: the tile's reference rows
+  const DtwArgs a = BATCH ? load_args_uniform(args + blockIdx.y) : a_in;
+  const int lane = threadIdx.x;
+  if ((int)blockIdx.x >= a.runs[0]) return;
+  const int64_t P = *a.plen, nq = a.nq, nr = a.nr;
+  const int f0 = a.runs[1 + blockIdx.x];
+  const int bi = a.pq[f0] >> 6, bj = a.pr[f0] >> 6;
+  const double inf = __builtin_inf();
+  const int64_t i = 64 * (int64_t)bi + 1 + lane;     // the lane's row
+  const int64_t jb = 64 * (int64_t)bj;               // column of the tile's left boundary
+  // top row (C[64bi][jb + c], c = 0 .. 64) and left column (C[i][jb])
+  for (int c = lane; c <= 64; c += 64) {
+    const int64_t j = jb + c;
+    double v = inf;
+    if (bi == 0) v = j == 0 ? 0.0 : inf;
+    else if (j >= 1 && j <= nr) v = __builtin_bit_cast(double, a.E[(int64_t)(bi - 1) * (nr + 1) + j]);
+    T[0][c] = v;
+  }
+  T[1 + lane][0] = bj == 0 ? inf : a.CK[(((int64_t)bi * (nr >> 6) + bj - 1) << 6) + lane];
+  // distances: lane = row, 64 columns (the reference row is the same for every lane)
+  const int dim = a.dim;
+  const double* qrow = a.q + (i <= nq ? i - 1 : 0) * dim;
+  if constexpr (D > 0) {
+    // the query row in registers, the 64 reference rows staged in LDS (broadcast reads)
+    double qv[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) qv[k] = qrow[k];
+    const int64_t jl = jb + 1 + lane;
+    const double* rrow = a.r + (jl <= nr ? jl - 1 : 0) * D;
+#pragma unroll
+    for (int k = 0; k < D; ++k) Rt[lane * D + k] = rrow[k];
+    __syncthreads();
+    for (int c = 0; c < 64; ++c) {
+      double sum = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const double df = qv[k] - Rt[c * D + k];
+        sum = sum + df * df;
+      }
+      Dl[lane][c] = sqrt(sum);
+    }
+  } else {
+    for (int c = 0; c < 64; ++c) {
+      const int64_t j = jb + 1 + c;
+      const double* rrow = a.r + (j <= nr ? j - 1 : 0) * dim;
+      double sum = 0.0;
+      for (int k = 0; k < dim; ++k) {
+        const double df = qrow[k] - rrow[k];
+        sum = sum + df * df;
+      }
+      Dl[lane][c] = sqrt(sum);
+    }
+  }
+  __syncthreads();
+  for (int st = 0; st < 127; ++st) {
+    const int c = st - lane;                         // column jb + 1 + c
+    if (c >= 0 && c < 64) {
+      const int64_t j = jb + 1 + c;
+      const double up = T[lane][c + 1], left = T[lane + 1][c], dg = T[lane][c];
+      double v = Dl[lane][c] + go_min(go_min(up, left), dg);
+      if (a.band > 0 && (i - j > a.band || j - i > a.band)) v = inf;   // outside the Sakoe-Chiba band
+      T[lane + 1][c + 1] = v;
+    }
+    __syncthreads();
+  }
+  // the run's points: at most 127 (a monotone path inside one tile), contiguous from f0
+  for (int64_t f = f0 + lane; f < P && f < f0 + 128; f += 64) {
+    const int pi = a.pq[f], pj = a.pr[f];
+    if (pi < 0 || pj < 0 || (pi >> 6) != bi || (pj >> 6) != bj) continue;
+    const int li = pi - 64 * bi + 1, lj = pj - 64 * bj + 1;
+    a.pc[f] = __dsub_rn(T[li][lj], T[li - 1][lj - 1]);
+    if (pi == nq - 1 && pj == nr - 1) *a.cnm = T[li][lj];
   }
 }
 
@@ -1255,6 +1391,8 @@ DtwGeom dtw_geom(int64_t nq, int64_t nr) {
 }
 size_t dtw_cn_bytes(const DtwGeom& g) { return (size_t)g.nb * ((g.S + 1) / 2) * 128 * 8; }
 size_t dtw_dn_bytes(const DtwGeom& g) { return (size_t)g.nb * g.SW * 64 * 4; }
+size_t dtw_ck_bytes(const DtwGeom& g) { return (size_t)g.nb * (g.nr >= 64 ? g.nr / 64 : 1) * 64 * 8; }
+int64_t dtw_run_words(const DtwGeom& g) { return g.nb + (g.nr + 63) / 64 + 2; }
 size_t dtw_edge_bytes(const DtwGeom& g) { return (size_t)(g.nb > 1 ? g.nb - 1 : 1) * (g.nr + 1) * 8; }
 int64_t dtw_cn_index(const DtwGeom& g, int64_t i, int64_t j) {
   const int64_t b = (i - 1) >> 6, l = (i - 1) & 63, s = j - 1 + l;
@@ -1268,11 +1406,13 @@ void launch_dtw_dist(const double* q, const double* r, const DtwGeom& g, double*
 
 int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, const DtwGeom& g, double* Cn,
                uint32_t* Dn, uint64_t* E, int32_t* sync_words, uint32_t* codes, int64_t* plen, uint64_t* trace,
-               hipStream_t s, hipEvent_t mid, double* Dd) {
+               hipStream_t s, hipEvent_t mid, double* Dd, double* CK) {
   if (hipMemsetAsync(sync_words, 0, 2 * sizeof(int32_t), s) != hipSuccess) return -5;
   if (g.nb > 1 && hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, dtw_edge_bytes(g) / 4, s) != hipSuccess) return -5;
   DtwArgs a{q, r, dim, band, g.nq, g.nr, g.nb, g.S, g.SW, Cn, Dn, reinterpret_cast<uint64_t*>(E), sync_words,
             trace};
+  a.CK = CK;
+  if (!Cn && !CK) return -1;
   const DtwBatch nob{};
   const bool pre = Dd && dim == 12;
   // SONAR_DTW_DBG_CONC=1 (timing experiment only, WRONG results): the distance kernel on a side
@@ -1338,6 +1478,21 @@ int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const uint32_t* cod
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s) {
+  if (P <= 0) return 0;
+  const DtwGeom g = dtw_geom(a.nq, a.nr);
+  if (hipMemsetAsync(a.runs, 0, 4, s) != hipSuccess) return -5;
+  hipLaunchKernelGGL(dtw_path_runs_kernel<false>, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, a,
+                     (const DtwArgs*)nullptr);
+  if (a.dim == 12)
+    hipLaunchKernelGGL((dtw_path_tile_kernel<false, 12>), dim3((unsigned)(dtw_run_words(g) - 2)), dim3(64), 0, s, a,
+                       (const DtwArgs*)nullptr);
+  else
+    hipLaunchKernelGGL((dtw_path_tile_kernel<false, 0>), dim3((unsigned)(dtw_run_words(g) - 2)), dim3(64), 0, s, a,
+                       (const DtwArgs*)nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
                      int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap) {
   if (n <= 0 || total_bands <= 0) return 0;
@@ -1363,6 +1518,17 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
   hipLaunchKernelGGL(dtw_path_points_kernel<true>, dim3((unsigned)((nw + 255) / 256), (unsigned)n), dim3(256), 0, s,
                      (const uint32_t*)nullptr, (const int2*)nullptr, (int64_t)0, (const double*)nullptr, (int64_t)0,
                      (int32_t*)nullptr, (int32_t*)nullptr, (double*)nullptr, dargs);
+  if (!hargs[0].Cn) {   // CK mode (every DTW of a batch alike): the path-tile pass; runs zeroed by the caller
+    int64_t max_tiles = 1;
+    for (int k = 0; k < n; ++k) {
+      const int64_t t = dtw_run_words(dtw_geom(hargs[k].nq, hargs[k].nr)) - 2;
+      max_tiles = t > max_tiles ? t : max_tiles;
+    }
+    hipLaunchKernelGGL(dtw_path_runs_kernel<true>, dim3((unsigned)((max_cap + 255) / 256), (unsigned)n), dim3(256), 0,
+                       s, none, dargs);
+    hipLaunchKernelGGL((dtw_path_tile_kernel<true, 12>), dim3((unsigned)max_tiles, (unsigned)n), dim3(64), 0, s, none,
+                       dargs);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "kernels.h"
+
 #include <map>
 #include <string>
 #include <utility>
@@ -98,6 +100,9 @@ struct DtwPending {
 int ncc_enqueue(sonar_ctx* c, const double* da, int64_t na, const double* db, int64_t nb, int32_t max_lag,
                 double** hcorr, int64_t* L);
 void ncc_metrics_host(const double* corr, int64_t L, int64_t na, int64_t nb, double* metrics);
+// the path-tile pass's arguments (launch_dtw_path_tiles) of one DTW in checkpoint mode
+sonar::DtwArgs tile_args(const double* q, const double* r, int dim, int band, const sonar::DtwGeom& g, uint64_t* E,
+                         double* CK, int32_t* runs, int32_t* pq, int32_t* pr, double* pc, int64_t* plen, double* cnm);
 int dtw_enqueue(sonar_ctx* c, const double* dq, int64_t nq, const double* dr, int64_t nr, int32_t dim, int32_t band,
                 DtwPending* p);
 int dtw_finish(sonar_ctx* c, DtwPending* p, const int32_t** hq, const int32_t** hr, const double** hc, int64_t* P,

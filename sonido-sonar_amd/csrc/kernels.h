@@ -145,8 +145,10 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
                uint32_t* codes /* walk moves, 2 bits each */, int64_t* plen,
                uint64_t* trace /* nullable, [nb][8] diagnostics */, hipStream_t s,
                hipEvent_t mid = nullptr /* recorded between the sweep and the walk */,
-               double* Dd = nullptr /* dim 12: dtw_cn_bytes of scratch -> precomputed distances */);
-// wstart: scratch of (P + 15) / 16 int2 (each code word's starting cell)
+               double* Dd = nullptr /* dim 12: dtw_cn_bytes of scratch -> precomputed distances */,
+               double* CK = nullptr /* Cn null: dtw_ck_bytes of checkpoint columns instead */);
+// wstart: scratch of (P + 15) / 16 int2 (each code word's starting cell).  Cn null: only the
+// points (and the zero cost of border points) are written; launch_dtw_path_tiles adds the costs
 int launch_dtw_path_cost(const double* Cn, const DtwGeom& g, const uint32_t* codes, int64_t P, int2* wstart,
                          int32_t* pq, int32_t* pr, double* pc, hipStream_t s);
 // costMatrix[1:] (nq x (nr+1), column 0 = +Inf) from the band-skewed store
@@ -172,7 +174,21 @@ struct DtwArgs {
   double* cnm;     // C[nq][nr]
   // precomputed local distances in Cn's layout (dtw_dist_kernel); null: computed inside the band kernel
   double* Dd;
+  // Cn null: the band kernel keeps only every 64th column of C (CK, dtw_ck_bytes), and the path
+  // costs are recomputed per 64 x 64 tile the path visits (launch_dtw_path_tiles); runs holds
+  // [0] the tile count, then each tile's first path index (dtw_run_words ints)
+  double* CK;
+  int32_t* runs;
 };
+// checkpoint columns C[64b+1 .. 64b+64][64c] (c = 1 .. nr/64) of every band, and the run words of
+// the path-tile pass
+size_t dtw_ck_bytes(const DtwGeom& g);
+int64_t dtw_run_words(const DtwGeom& g);
+// path costs and C[nq][nr] from CK + E (the band kernel's checkpoint columns and band edges), for
+// a path whose points (pq, pr) are already written: one wave per 64 x 64 tile the path visits
+// recomputes the tile's cells in the band kernel's arithmetic (bit-identical).  Needs a.q, r, dim,
+// band, nq, nr, nb, E, CK, pq, pr, pc, runs, cnm.
+int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s);
 // n DTWs of 12-dim finite sequences, unbanded (the chroma DTWs of sonar_align_pairs), from a
 // device array of DtwArgs: the band kernel over all of them (block tickets run through DTW k's
 // bands at dstart[k] .. dstart[k+1]-1; dstart[n] = total_bands), the walks (one block each), the

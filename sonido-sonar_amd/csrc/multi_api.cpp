@@ -111,12 +111,13 @@ struct PairGeo {
   int64_t k = 0, nq = 0, nr = 0, Fq = 0, Fr = 0, Eq = 0, Er = 0, L = 0, mlf = 0, cap = 0;
   bool corr = false;
   sonar::DtwGeom g{};
-  size_t chroma = 0, cn = 0, dn = 0, e = 0, codes = 0, wst = 0, path = 0, corr_off = 0;   // region offsets
+  size_t chroma = 0, cn = 0, ck = 0, runs = 0, dn = 0, e = 0, codes = 0, wst = 0, path = 0, corr_off = 0;   // region offsets
 };
 
-// device bytes one pair of a batch holds (chroma, the DTW stores, the path)
+// device bytes one pair of a batch holds (chroma, the DTW stores, the path; PRE: the distances)
 size_t pair_bytes(const PairGeo& p) {
-  return al256((size_t)(p.Fq + p.Fr) * 96) + 2 * al256(sonar::dtw_cn_bytes(p.g)) + al256(sonar::dtw_dn_bytes(p.g)) +
+  return al256((size_t)(p.Fq + p.Fr) * 96) + (sonar::detail::dtw_pre_enabled(12) ? al256(sonar::dtw_cn_bytes(p.g)) : 0) +
+         al256(sonar::dtw_ck_bytes(p.g)) + al256((size_t)sonar::dtw_run_words(p.g) * 4) + al256(sonar::dtw_dn_bytes(p.g)) +
          al256(sonar::dtw_edge_bytes(p.g)) + al256((size_t)((p.cap + 1023) / 1024) * 256) +
          al256((size_t)((p.cap + 15) / 16 + 1) * 8) + al256((size_t)p.cap * 16) + al256((size_t)(2 * p.L + 1) * 8);
 }
@@ -134,11 +135,14 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   HIP_TRY(w, hipSetDevice(w->device));
   hipStream_t s = w->stream;
   std::vector<PairGeo> pg = in;
-  size_t chroma_b = 0, cn_b = 0, dn_b = 0, e_b = 0, codes_b = 0, wst_b = 0, path_b = 0, corr_b = 0;
+  const bool pre = sonar::detail::dtw_pre_enabled(12);
+  size_t chroma_b = 0, cn_b = 0, ck_b = 0, runs_b = 0, dn_b = 0, e_b = 0, codes_b = 0, wst_b = 0, path_b = 0, corr_b = 0;
   int64_t maxE = 1, maxn = 1, max_cap = 1, total_bands = 0;
   for (auto& p : pg) {
     p.chroma = chroma_b; chroma_b += al256((size_t)(p.Fq + p.Fr) * 96);
-    p.cn = cn_b; cn_b += al256(sonar::dtw_cn_bytes(p.g));
+    if (pre) { p.cn = cn_b; cn_b += al256(sonar::dtw_cn_bytes(p.g)); }
+    p.ck = ck_b; ck_b += al256(sonar::dtw_ck_bytes(p.g));
+    p.runs = runs_b; runs_b += al256((size_t)sonar::dtw_run_words(p.g) * 4);
     p.dn = dn_b; dn_b += al256(sonar::dtw_dn_bytes(p.g));
     p.e = e_b; e_b += al256(sonar::dtw_edge_bytes(p.g));
     p.codes = codes_b; codes_b += al256((size_t)((p.cap + 1023) / 1024) * 256);
@@ -153,8 +157,8 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   const size_t stat_b = al256((size_t)n * 32 + 16), args_b = al256((size_t)n * sizeof(sonar::DtwArgs)),
                start_b = al256((size_t)(n + 1) * 8), map_b = al256((size_t)total_bands * 8);
   char* chroma = (char*)dbuf(w, "pb.chroma", chroma_b);
-  char* Cn = (char*)dbuf(w, "pb.Cn", cn_b);
-  const bool pre = sonar::detail::dtw_pre_enabled(12);
+  char* CK = (char*)dbuf(w, "pb.CK", ck_b);
+  char* runs = (char*)dbuf(w, "pb.runs", runs_b);
   char* Dd = pre ? (char*)dbuf(w, "pb.Dd", cn_b) : nullptr;
   char* Dn = (char*)dbuf(w, "pb.Dn", dn_b);
   char* E = (char*)dbuf(w, "pb.E", e_b);
@@ -171,7 +175,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   double* up_q = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.q", (size_t)maxn * 8);
   double* up_r = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.r", (size_t)maxn * 8);
   char* h = (char*)sonar::detail::hbuf(w, "pb.host", stat_b + args_b + start_b + map_b + corr_b + path_b);
-  if (!chroma || !Cn || (pre && !Dd) || !Dn || !E || !codes || !wst || !path || !corr || !small || !eq || !er || !xa || !xb || !st ||
+  if (!chroma || !CK || !runs || (pre && !Dd) || !Dn || !E || !codes || !wst || !path || !corr || !small || !eq || !er || !xa || !xb || !st ||
       (!device_ptrs && (!up_q || !up_r)) || !h)
     return fail(w, SONAR_ERR_NOMEM, "allocation failed (pair batch)");
   int32_t* dstat = (int32_t*)small;                 // per pair: [0..1] plen, [2..3] C[nq][nr], [4..7] sync
@@ -186,6 +190,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* hcorr = h + stat_b + args_b + start_b + map_b;
   char* hpath = hcorr + corr_b;
   HIP_TRY(w, hipMemsetAsync(small, 0, stat_b, s));
+  HIP_TRY(w, hipMemsetAsync(runs, 0, runs_b, s));
   if (e_b) HIP_TRY(w, hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, e_b / 4, s));
   int64_t acc = 0;
   for (int i = 0; i < n; ++i) {
@@ -210,7 +215,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     a = sonar::DtwArgs{};
     a.q = cq; a.r = cr; a.dim = 12; a.band = -1;
     a.nq = p.g.nq; a.nr = p.g.nr; a.nb = p.g.nb; a.S = p.g.S; a.SW = p.g.SW;
-    a.Cn = (double*)(Cn + p.cn); a.Dn = (uint32_t*)(Dn + p.dn); a.E = (uint64_t*)(E + p.e); a.sync = sync;
+    a.Cn = nullptr; a.CK = (double*)(CK + p.ck); a.runs = (int32_t*)(runs + p.runs); a.Dn = (uint32_t*)(Dn + p.dn); a.E = (uint64_t*)(E + p.e); a.sync = sync;
     a.codes = (uint32_t*)(codes + p.codes); a.plen = (int64_t*)(dstat + 8 * i); a.wstart = (int2*)(wst + p.wst);
     a.pc = (double*)(path + p.path); a.pq = (int32_t*)(a.pc + p.cap); a.pr = a.pq + p.cap;
     a.cnm = (double*)(dstat + 8 * i + 2);

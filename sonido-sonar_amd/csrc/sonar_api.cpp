@@ -772,14 +772,20 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
     dq = pq; dr = pr;
   }
   const sonar::DtwGeom g = sonar::dtw_geom(nq, nr);
-  double* Cn = (double*)dbuf(c, "dtw.Cn", sonar::dtw_cn_bytes(g));
+  // the full cost store only when the caller asks for the cost matrix; otherwise every 64th
+  // column (CK) and the path costs recomputed per visited tile
+  const bool full = cost != nullptr;
+  double* Cn = full ? (double*)dbuf(c, "dtw.Cn", sonar::dtw_cn_bytes(g)) : nullptr;
+  double* CK = full ? nullptr : (double*)dbuf(c, "dtw.CK", sonar::dtw_ck_bytes(g));
+  int32_t* runs = full ? nullptr : (int32_t*)dbuf(c, "dtw.runs", (size_t)sonar::dtw_run_words(g) * 4);
+  double* cnm_d = (double*)dbuf(c, "dtw.cnm", 8);
   uint32_t* Dn = (uint32_t*)dbuf(c, "dtw.Dn", sonar::dtw_dn_bytes(g));
   uint64_t* E = (uint64_t*)dbuf(c, "dtw.E", sonar::dtw_edge_bytes(g));
   int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", 16);
   const int64_t cap = nq + nr + 1;
   uint32_t* codes = (uint32_t*)dbuf(c, "dtw.codes", ((cap + 1023) / 1024) * 64 * 4);
   int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
-  if (!Cn || !Dn || !E || !sync || !codes || !pl)
+  if ((full ? !Cn : (!CK || !runs)) || !cnm_d || !Dn || !E || !sync || !codes || !pl)
     return fail(c, SONAR_ERR_NOMEM, "device allocation failed (cost matrix)");
   // math.Min's NaN / -Inf / -0 rules only matter when an input is not finite
   bool fast = true;
@@ -804,7 +810,7 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
   HIP_TRY(c, hipEventRecord(c->dtw_ev[0], s));
   double* Dd = sonar::detail::dtw_pre_enabled(dim) ? (double*)dbuf(c, "dtw.Dd", sonar::dtw_cn_bytes(g)) : nullptr;
   if (sonar::detail::dtw_pre_enabled(dim) && !Dd) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (distances)");
-  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, codes, pl, trace, s, c->dtw_ev[1], Dd) != 0)
+  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, codes, pl, trace, s, c->dtw_ev[1], Dd, CK) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
   HIP_TRY(c, hipEventRecord(c->dtw_ev[2], s));
   timed_end(c, s, tend);
@@ -829,11 +835,13 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
   }
   int2* wstart = (int2*)dbuf(c, "dtw.wstart", (size_t)((P + 15) / 16 + 1) * sizeof(int2));
   if (!wstart) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (path)");
-  if (sonar::launch_dtw_path_cost(Cn, g, codes, P, wstart, oq, orr, oc, s) != 0)
+  if (sonar::launch_dtw_path_cost(Cn, g, codes, P, wstart, oq, orr, oc, s) != 0 ||
+      (!full && sonar::launch_dtw_path_tiles(sonar::detail::tile_args(dq, dr, dim, band, g, E, CK, runs, oq, orr, oc,
+                                                                        pl, cnm_d), P, s) != 0))
     return fail(c, SONAR_ERR_DEVICE, "dtw path launch failed");
   HIP_TRY(c, hipEventRecord(c->dtw_ev[3], s));
   double cNM = 0;
-  HIP_TRY(c, hipMemcpyAsync(&cNM, Cn + sonar::dtw_cn_index(g, nq, nr), 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(&cNM, full ? Cn + sonar::dtw_cn_index(g, nq, nr) : cnm_d, 8, hipMemcpyDeviceToHost, s));
   double* cost_dev = cost;
   if (cost && !device_ptrs) {
     cost_dev = (double*)dbuf(c, "dtw.cost", (size_t)nq * (nr + 1) * 8);
@@ -863,6 +871,15 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
 // ============================================= deferred-sync pair pieces ====
 namespace sonar {
 namespace detail {
+
+sonar::DtwArgs tile_args(const double* q, const double* r, int dim, int band, const sonar::DtwGeom& g, uint64_t* E,
+                         double* CK, int32_t* runs, int32_t* pq, int32_t* pr, double* pc, int64_t* plen, double* cnm) {
+  sonar::DtwArgs a{};
+  a.q = q; a.r = r; a.dim = dim; a.band = band;
+  a.nq = g.nq; a.nr = g.nr; a.nb = g.nb; a.S = g.S; a.SW = g.SW;
+  a.E = E; a.CK = CK; a.runs = runs; a.pq = pq; a.pr = pr; a.pc = pc; a.plen = plen; a.cnm = cnm;
+  return a;
+}
 
 void ncc_metrics_host(const double* corr, int64_t L, int64_t na, int64_t nb, double* metrics) {
   const auto m = sonar::host::ncc_metrics(corr, 2 * L + 1, L, na, nb);
@@ -902,7 +919,7 @@ int dtw_enqueue(sonar_ctx* c, const double* dq, int64_t nq, const double* dr, in
   if (nq + nr > (int64_t)INT32_MAX) return fail(c, SONAR_ERR_UNSUPPORTED, "sequence too long");
   hipStream_t s = c->stream;
   const sonar::DtwGeom g = sonar::dtw_geom(nq, nr);
-  double* Cn = (double*)dbuf(c, "dtw.Cn", sonar::dtw_cn_bytes(g));
+  double* CK = (double*)dbuf(c, "dtw.CK", sonar::dtw_ck_bytes(g));
   uint32_t* Dn = (uint32_t*)dbuf(c, "dtw.Dn", sonar::dtw_dn_bytes(g));
   uint64_t* E = (uint64_t*)dbuf(c, "dtw.E", sonar::dtw_edge_bytes(g));
   int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", 16);
@@ -910,13 +927,13 @@ int dtw_enqueue(sonar_ctx* c, const double* dq, int64_t nq, const double* dr, in
   uint32_t* codes = (uint32_t*)dbuf(c, "dtw.codes", ((cap + 1023) / 1024) * 64 * 4);
   int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
   int64_t* st = (int64_t*)hbuf(c, "dtw.status", 32);
-  if (!Cn || !Dn || !E || !sync || !codes || !pl || !st) return fail(c, SONAR_ERR_NOMEM, "allocation failed (dtw)");
+  if (!CK || !Dn || !E || !sync || !codes || !pl || !st) return fail(c, SONAR_ERR_NOMEM, "allocation failed (dtw)");
   HIP_TRY(c, hipMemsetAsync(sync + 2, 0, 4, s));
   if (sonar::launch_nonfinite(dq, nq * dim, sync + 2, s) || sonar::launch_nonfinite(dr, nr * dim, sync + 2, s))
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
   double* Dd = sonar::detail::dtw_pre_enabled(dim) ? (double*)dbuf(c, "dtw.Dd", sonar::dtw_cn_bytes(g)) : nullptr;
   if (sonar::detail::dtw_pre_enabled(dim) && !Dd) return fail(c, SONAR_ERR_NOMEM, "allocation failed (dtw)");
-  if (sonar::launch_dtw(dq, dr, dim, band, true, g, Cn, Dn, E, sync, codes, pl, nullptr, s, nullptr, Dd) != 0)
+  if (sonar::launch_dtw(dq, dr, dim, band, true, g, nullptr, Dn, E, sync, codes, pl, nullptr, s, nullptr, Dd, CK) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
   HIP_TRY(c, hipMemcpyAsync(st, pl, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipMemcpyAsync(st + 1, sync, 12, hipMemcpyDeviceToHost, s));
@@ -930,17 +947,21 @@ int dtw_finish(sonar_ctx* c, DtwPending* p, const int32_t** hq, const int32_t** 
   hipStream_t s = c->stream;
   const sonar::DtwGeom g = sonar::dtw_geom(p->nq, p->nr);
   const int64_t cap = p->nq + p->nr + 1;
-  double* Cn = (double*)dbuf(c, "dtw.Cn", sonar::dtw_cn_bytes(g));
+  double* CK = (double*)dbuf(c, "dtw.CK", sonar::dtw_ck_bytes(g));
   uint32_t* Dn = (uint32_t*)dbuf(c, "dtw.Dn", sonar::dtw_dn_bytes(g));
   uint64_t* E = (uint64_t*)dbuf(c, "dtw.E", sonar::dtw_edge_bytes(g));
   int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", 16);
   uint32_t* codes = (uint32_t*)dbuf(c, "dtw.codes", ((cap + 1023) / 1024) * 64 * 4);
   int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
+  int32_t* runs = (int32_t*)dbuf(c, "dtw.runs", (size_t)sonar::dtw_run_words(g) * 4);
+  double* cnm_d = (double*)dbuf(c, "dtw.cnm", 8);
+  if (!runs || !cnm_d) return fail(c, SONAR_ERR_NOMEM, "allocation failed (dtw path)");
   int32_t nfw[3];
   std::memcpy(nfw, p->st + 1, 12);
   if (nfw[2] != 0) {                                              // non-finite input: exact math.Min rules
     double* Dd = sonar::detail::dtw_pre_enabled(p->dim) ? (double*)dbuf(c, "dtw.Dd", sonar::dtw_cn_bytes(g)) : nullptr;
-    if (sonar::launch_dtw(p->dq, p->dr, p->dim, p->band, false, g, Cn, Dn, E, sync, codes, pl, nullptr, s, nullptr, Dd))
+    if (sonar::launch_dtw(p->dq, p->dr, p->dim, p->band, false, g, nullptr, Dn, E, sync, codes, pl, nullptr, s, nullptr,
+                          Dd, CK))
       return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
     HIP_TRY(c, hipMemcpyAsync(p->st, pl, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipMemcpyAsync(p->st + 1, sync, 8, hipMemcpyDeviceToHost, s));
@@ -956,13 +977,15 @@ int dtw_finish(sonar_ctx* c, DtwPending* p, const int32_t** hq, const int32_t** 
   // one pinned block: cost(N,M), path costs, then the two index arrays
   char* h = (char*)hbuf(c, "dtw.path", 8 + (size_t)cap * 16);
   if (!oq || !orr || !oc || !wstart || !h) return fail(c, SONAR_ERR_NOMEM, "allocation failed (dtw path)");
-  if (sonar::launch_dtw_path_cost(Cn, g, codes, P, wstart, oq, orr, oc, s) != 0)
+  if (sonar::launch_dtw_path_cost(nullptr, g, codes, P, wstart, oq, orr, oc, s) != 0 ||
+      sonar::launch_dtw_path_tiles(tile_args(p->dq, p->dr, p->dim, p->band, g, E, CK, runs, oq, orr, oc, pl, cnm_d), P,
+                                   s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw path launch failed");
   double* hcnm = (double*)h;
   double* hcost = hcnm + 1;
   int32_t* hpq = (int32_t*)(hcost + cap);
   int32_t* hpr = hpq + cap;
-  HIP_TRY(c, hipMemcpyAsync(hcnm, Cn + sonar::dtw_cn_index(g, p->nq, p->nr), 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(hcnm, cnm_d, 8, hipMemcpyDeviceToHost, s));
   if (P > 0) {
     HIP_TRY(c, hipMemcpyAsync(hcost, oc, P * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipMemcpyAsync(hpq, oq, P * 4, hipMemcpyDeviceToHost, s));

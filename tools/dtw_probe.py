@@ -41,7 +41,11 @@ tp = os.environ.get("SONAR_DTW_TRACE")
 if tp and os.path.exists(tp):
     t = np.fromfile(tp, dtype=np.uint64).reshape(-1, 8).astype(np.float64)
     base = t[:, 0].min()
-    st, fe, en, sp = (t[:, 0] - base) / 100.0, (t[:, 1] - base) / 100.0, (t[:, 2] - base) / 100.0, t[:, 3] / 100.0
+    raw3 = np.fromfile(tp, dtype=np.uint64).reshape(-1, 8)[:, 3]
+    hw = (raw3 >> np.uint64(32)).astype(np.int64)
+    xcc = ((raw3 >> np.uint64(24)) & np.uint64(0xFF)).astype(np.int64)
+    sp_raw = (raw3 & np.uint64(0xFFFFFF)).astype(np.float64)
+    st, fe, en, sp = (t[:, 0] - base) / 100.0, (t[:, 1] - base) / 100.0, (t[:, 2] - base) / 100.0, sp_raw / 100.0
     S = n + 63
     dur = en - st
     nb = len(t)
@@ -57,3 +61,32 @@ if tp and os.path.exists(tp):
               f"  dist0 wait {t[k, 6] / 100.0:8.1f} code wait {t[k, 7] / 100.0:8.1f}")
     act = [(np.sum((st <= x) & (en > x))) for x in np.linspace(0, en.max(), 11)]
     print("active bands at 0,10..100% of the span:", act)
+    # which sweeps shared a CU / a SIMD: per band, the fraction of its lifetime during which another
+    # band's sweep ran on the same CU (same SIMD)
+    cu = (xcc << 8) | ((hw >> 8) & 0xFF)
+    simd = (hw >> 4) & 3
+    print("distinct CUs seen:", len(np.unique(cu)), " sweep SIMD histogram:", np.bincount(simd, minlength=4).tolist())
+    ov_cu, ov_simd = np.zeros(nb), np.zeros(nb)
+    order = np.argsort(cu, kind="stable")
+    for c in np.unique(cu):
+        ks = np.nonzero(cu == c)[0]
+        for k in ks:
+            for m in ks:
+                if m == k:
+                    continue
+                o = max(0.0, min(en[k], en[m]) - max(st[k], st[m]))
+                ov_cu[k] += o
+                if simd[m] == simd[k]:
+                    ov_simd[k] += o
+    fcu, fsimd = ov_cu / np.maximum(dur, 1e-9), ov_simd / np.maximum(dur, 1e-9)
+    nsps = dur / S * 1e3
+    print("co-resident sweep on the CU, fraction of band life: median %.2f; on the same SIMD: median %.2f mean %.2f"
+          % (np.median(fcu), np.median(fsimd), fsimd.mean()))
+    lo, hi = fsimd < 0.2, fsimd > 0.6
+    if lo.any() and hi.any():
+        print("ns/step, bands whose sweep shared its SIMD < 20%% of the time: median %.1f (n=%d); > 60%%: %.1f (n=%d)"
+              % (np.median(nsps[lo]), lo.sum(), np.median(nsps[hi]), hi.sum()))
+    lo, hi = fcu < 0.2, fcu > 0.6
+    if lo.any() and hi.any():
+        print("ns/step, bands alone on the CU > 80%% of the time: median %.1f (n=%d); shared > 60%%: %.1f (n=%d)"
+              % (np.median(nsps[lo]), lo.sum(), np.median(nsps[hi]), hi.sum()))
