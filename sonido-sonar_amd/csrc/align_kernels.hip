@@ -381,6 +381,24 @@ constexpr int dtw_ring_stride() { return D == 12 ? 14 : (D > 0 ? D : 1); }
 // never wrap and a lane addresses them as one base plus immediate offsets.
 constexpr int DTW_RMIR = DTW_ECH;
 
+// The Dn allocation (dtw_dn_bytes) holds, after the nb * SW * 64 direction words, the band exit
+// map Xm[nb][nr64] and its segment boundaries Xr[nb][nseg][64] (int32, dtw_exit_map_kernel), and
+// the band walk's meta words: ent[nb] (the column at which the path crosses the band's last valid
+// row), cnt[nb] (its moves inside the band) and off[nb] (moves of the later bands: where its
+// moves start in the walk's order).
+constexpr int DTW_XSEG = 1024;    // columns per exit-map segment (a multiple of 64)
+__host__ __device__ __forceinline__ int64_t dtw_nr64(int64_t nr) { return (nr + 63) & ~(int64_t)63; }
+__host__ __device__ __forceinline__ int64_t dtw_nseg(int64_t nr) { return (nr + DTW_XSEG - 1) / DTW_XSEG; }
+__device__ __forceinline__ int32_t* dtw_xmap(uint32_t* Dn, int64_t nb, int64_t SW) {
+  return reinterpret_cast<int32_t*>(Dn + ((nb * SW) << 6));
+}
+__device__ __forceinline__ int32_t* dtw_xbound(uint32_t* Dn, int64_t nb, int64_t SW, int64_t nr) {
+  return dtw_xmap(Dn, nb, SW) + nb * dtw_nr64(nr);
+}
+__device__ __forceinline__ int32_t* dtw_walk_meta(uint32_t* Dn, int64_t nb, int64_t SW, int64_t nr) {
+  return dtw_xbound(Dn, nb, SW, nr) + nb * dtw_nseg(nr) * 64;
+}
+
 // C[i][j] of band-step (b, s), lane l in the paired layout Cn[b][s/2][l][s%2]
 __device__ __forceinline__ int64_t dtw_cn_off(int64_t b, int64_t S2, int64_t s, int64_t l) {
   return ((b * S2 + (s >> 1)) << 7) + 2 * l + (s & 1);
@@ -978,6 +996,36 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
 // dynamic register indexing -- followed by scalar bit-field work.  The next band's window is
 // prefetched on band entry around the current column.
 #define DTW_WIN 16
+// The steps while the walk stays in its band, window slot K and the matrix interior (l >= 0,
+// s >= 16 * w, j >= 1), for window slot kw (uniform).  A move: 0 up (l-1, s-1), 1 left (j-1, s-1),
+// 2 diagonal (both, s-2), as arithmetic on the code: dl = 1 - (c & 1), dj = (c + 1) >> 1,
+// dbp = 2 + (c & 2).  The words of the current lane (wc) and of the lane above (wu) are held in
+// SGPRs; an up/diagonal move takes wu and fetches the next lane's word with a v_readlane whose
+// result is needed only a move later, so the readlane latency is off the move-to-move chain.
+// Uses win[], ll, bp, jj and emit() of the enclosing walk.
+#define DTW_STEP_SLOT(K)                                                              \
+    case K: {                                                                         \
+      uint32_t wc = __builtin_amdgcn_readlane(win[K], ll);                            \
+      uint32_t wu = __builtin_amdgcn_readlane(win[K], ll > 0 ? ll - 1 : 0);           \
+      do {                                                                            \
+        const uint32_t code = (wc >> bp) & 3u;                                        \
+        emit(code);                                                                   \
+        const int dl = 1 - (int)(code & 1u);                                          \
+        ll -= dl;                                                                     \
+        jj -= (int)((code + 1u) >> 1);                                                \
+        bp -= 2 + (int)(code & 2u);                                                   \
+        wc = dl ? wu : wc;                                                            \
+        wu = __builtin_amdgcn_readlane(win[K], ll > 0 ? ll - 1 : 0);                  \
+      } while ((ll | bp | (jj - 1)) >= 0);                                            \
+      break;                                                                          \
+    }
+#define DTW_WALK_SLOTS(kw)                                                                                     \
+  switch (kw) {                                                                                                \
+    DTW_STEP_SLOT(0) DTW_STEP_SLOT(1) DTW_STEP_SLOT(2) DTW_STEP_SLOT(3) DTW_STEP_SLOT(4) DTW_STEP_SLOT(5)       \
+    DTW_STEP_SLOT(6) DTW_STEP_SLOT(7) DTW_STEP_SLOT(8) DTW_STEP_SLOT(9) DTW_STEP_SLOT(10) DTW_STEP_SLOT(11)     \
+    DTW_STEP_SLOT(12) DTW_STEP_SLOT(13) DTW_STEP_SLOT(14) DTW_STEP_SLOT(15)                                     \
+    default: break;                                                                                            \
+  }
 __device__ __forceinline__ void dtw_walk_body(const uint32_t* Dn, int64_t nq, int64_t nr, int64_t SW,
                                               uint32_t* codes, int64_t* plen) {
   const int lane = threadIdx.x;
@@ -1031,33 +1079,7 @@ __device__ __forceinline__ void dtw_walk_body(const uint32_t* Dn, int64_t nq, in
     int ll = __builtin_amdgcn_readfirstlane(l);
     int bp = __builtin_amdgcn_readfirstlane(2 * (s & 15));          // bit position of step s
     int jj = __builtin_amdgcn_readfirstlane(j);
-    // a move: 0 up (l-1, s-1), 1 left (j-1, s-1), 2 diagonal (both, s-2), as arithmetic on the
-    // code: dl = 1 - (c & 1), dj = (c + 1) >> 1, dbp = 2 + (c & 2).  The words of the current
-    // lane (wc) and of the lane above (wu) are held in SGPRs; an up/diagonal move takes wu and
-    // fetches the next lane's word with a v_readlane whose result is needed only a move later,
-    // so the readlane latency is off the move-to-move chain.
-#define STEP_SLOT(K)                                                                  \
-    case K: {                                                                         \
-      uint32_t wc = __builtin_amdgcn_readlane(win[K], ll);                            \
-      uint32_t wu = __builtin_amdgcn_readlane(win[K], ll > 0 ? ll - 1 : 0);           \
-      do {                                                                            \
-        const uint32_t code = (wc >> bp) & 3u;                                        \
-        emit(code);                                                                   \
-        const int dl = 1 - (int)(code & 1u);                                          \
-        ll -= dl;                                                                     \
-        jj -= (int)((code + 1u) >> 1);                                                \
-        bp -= 2 + (int)(code & 2u);                                                   \
-        wc = dl ? wu : wc;                                                            \
-        wu = __builtin_amdgcn_readlane(win[K], ll > 0 ? ll - 1 : 0);                  \
-      } while ((ll | bp | (jj - 1)) >= 0);                                            \
-      break;                                                                          \
-    }
-    switch (kw) {
-      STEP_SLOT(0) STEP_SLOT(1) STEP_SLOT(2) STEP_SLOT(3) STEP_SLOT(4) STEP_SLOT(5) STEP_SLOT(6) STEP_SLOT(7)
-      STEP_SLOT(8) STEP_SLOT(9) STEP_SLOT(10) STEP_SLOT(11) STEP_SLOT(12) STEP_SLOT(13) STEP_SLOT(14) STEP_SLOT(15)
-      default: break;
-    }
-#undef STEP_SLOT
+    DTW_WALK_SLOTS(kw);
     i = 64 * bnd + ll + 1;
     j = jj;
   }
@@ -1082,6 +1104,197 @@ __global__ __launch_bounds__(64) void dtw_walk_kernel(const uint32_t* Dn, int64_
 __global__ __launch_bounds__(64) void dtw_walk_batch_kernel(const DtwArgs* args) {
   const DtwArgs a = load_args_uniform(args + blockIdx.x);
   dtw_walk_body(a.Dn, a.nq, a.nr, a.SW, a.codes, a.plen);
+}
+
+// ------------------------------------------------------- backtrack by bands ----
+// The serial walk above is a chain of nq + nr dependent moves (5.3 ms at 51,676^2).  With the
+// exit map Xm the chain shrinks to one dependent load per band, and the bands' own stretches of
+// the path are walked in parallel; the moves land in the same 2-bit stream, in the same order,
+// as the serial walk's (dtw.go:165-188):
+//  dtw_exit_map_kernel     Xm and the segment boundaries (above), every band and segment at once.
+//  dtw_walk_chain_kernel   one lane: ent[nb-1] = nr (the walk starts at (nq, nr)), then
+//                          ent[b-1] = Xm[b][ent[b] - 1] (0 stays 0; a segment symbol resolved).
+//  dtw_walk_band_kernel<false>  one wave per band: from (64b + lv + 1, ent[b]) until the path
+//                          reaches row 64b (band 0: to (0, 0), border moves included); cnt[b].
+//  dtw_walk_scan_kernel    off[b] = moves of the bands below b in the walk order (b' > b), the
+//                          total P, and the move words zeroed.
+//  dtw_walk_band_kernel<true>   the same walks again, ORing their moves into the stream at off[b].
+// (BATCH: blockIdx.y, or the block, is the DTW of a batch)
+// Exit map of band b (dtw_exit_map_kernel, grid (segment, band[, DTW])): X(l, j) = the column
+// at which the backtrack from cell (64b+1+l, j) reaches row 64b.  It follows the codes as C
+// follows the costs: X(l, j) = X(l-1, j) (up), X(l, j-1) (left), X(l-1, j-1) (diagonal), with
+// X(-1, j) = j (the edge row) and X(l, 0) = 0 (the path then runs up column 0), so one wave
+// sweeps a segment of DTW_XSEG columns in the band kernel's skew (lane = row, DPP from lane l-1),
+// reading the 2-bit codes 16 steps per word.  A segment does not wait for its left neighbour: its
+// left boundary X(l, J0-1) enters as the symbol -(l+1), and the chain resolves a symbol through
+// the neighbour's right boundary Xr[b][k-1][l] (a path crosses a segment's left edge before
+// reaching row 64b only within ~64 columns of it, so this is rare and one hop).
+template <bool BATCH>
+__global__ __launch_bounds__(64) void dtw_exit_map_kernel(DtwArgs a_in, const DtwArgs* args) {
+  const DtwArgs a = BATCH ? load_args_uniform(args + blockIdx.z) : a_in;
+  const int64_t b = blockIdx.y, k = blockIdx.x;
+  const int64_t nq = a.nq, nr = a.nr, nb = a.nb, SW = a.SW, nseg = dtw_nseg(nr);
+  if (b >= nb || k >= nseg) return;
+  const int lane = threadIdx.x;
+  const int64_t J0 = 1 + k * DTW_XSEG, J1 = J0 + DTW_XSEG < nr + 1 ? J0 + DTW_XSEG : nr + 1;   // columns [J0, J1)
+  const int lv = (int)(b == nb - 1 ? nq - 1 - 64 * b : 63);
+  const uint32_t* Db = a.Dn + ((b * SW) << 6) + lane;
+  int32_t* Xb = dtw_xmap(a.Dn, nb, SW) + b * dtw_nr64(nr);
+  const int T = (int)(J1 - J0) + lv;               // steps until row lv has reached column J1-1
+  const int64_t w0 = (J0 - 1) >> 4;                // the segment's first code word (J0-1 = 1024k)
+  const int nw = (T + 15) >> 4;
+  int x = k == 0 ? 0 : -(lane + 1);                // own X of the previous step (the left boundary)
+  int xdg = (int)(J0 - 1);                         // lane 0: X(-1, J0-1)
+  int xacc = 0;
+  constexpr int WB = 8;                            // code words per batch (128 steps)
+  uint32_t cur[WB], nxt[WB];
+#pragma unroll
+  for (int q = 0; q < WB; ++q) cur[q] = (q < nw && w0 + q < SW) ? Db[(w0 + q) << 6] : 0u;
+  for (int wb = 0; wb < nw; wb += WB) {
+#pragma unroll
+    for (int q = 0; q < WB; ++q) {
+      const int64_t w = w0 + wb + WB + q;
+      nxt[q] = (wb + WB + q < nw && w < SW) ? Db[w << 6] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < WB; ++q) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int t = (wb + q) * 16 + u;
+        const uint32_t code = (cur[q] >> (2 * u)) & 3u;
+        const int xup = __builtin_amdgcn_update_dpp((int)(J0 + t), x, 0x138, 0xf, 0xf, false);   // wave_shr:1
+        const int xn = code == 0u ? xup : (code == 1u ? x : xdg);
+        xdg = xup;
+        const int jl = t - lane;                   // the lane's column - J0
+        x = (jl >= 0 && jl < (int)(J1 - J0)) ? xn : x;
+        const int jv = t - lv;                     // row lv's column - J0 (uniform)
+        if (jv >= 0 && jv < (int)(J1 - J0)) {
+          const int64_t c = J0 - 1 + jv;           // Xm index of that column
+          xacc = lane == (int)(c & 63) ? __builtin_amdgcn_readlane(x, lv) : xacc;
+          if ((c & 63) == 63 || jv == (int)(J1 - J0) - 1) Xb[(c & ~(int64_t)63) + lane] = xacc;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < WB; ++q) cur[q] = nxt[q];
+  }
+  dtw_xbound(a.Dn, nb, SW, nr)[(b * nseg + k) * 64 + lane] = x;   // X(l, J1-1) (rows <= lv)
+}
+
+template <bool BATCH>
+__global__ __launch_bounds__(64) void dtw_walk_chain_kernel(DtwArgs a_in, const DtwArgs* args) {
+  const DtwArgs a = BATCH ? load_args_uniform(args + blockIdx.x) : a_in;
+  if (threadIdx.x != 0) return;
+  const int64_t nb = a.nb, nr64 = dtw_nr64(a.nr), nseg = dtw_nseg(a.nr);
+  const int32_t* X = dtw_xmap(a.Dn, nb, a.SW);
+  const int32_t* Xr = dtw_xbound(a.Dn, nb, a.SW, a.nr);
+  int32_t* ent = dtw_walk_meta(a.Dn, nb, a.SW, a.nr);
+  int e = (int)a.nr;
+  ent[nb - 1] = e;
+  for (int64_t b = nb - 1; b > 0; --b) {
+    if (e > 0) {
+      int v = X[b * nr64 + e - 1];
+      int64_t k = (e - 1) / DTW_XSEG;
+      while (v < 0 && k > 0) v = Xr[(b * nseg + --k) * 64 + (-v - 1)];   // a segment's left boundary
+      e = v < 0 ? 0 : v;
+    }
+    ent[b - 1] = e;
+  }
+}
+
+template <bool EMIT, bool BATCH>
+__global__ __launch_bounds__(64) void dtw_walk_band_kernel(DtwArgs a_in, const DtwArgs* args) {
+  const DtwArgs a = BATCH ? load_args_uniform(args + blockIdx.y) : a_in;
+  const int64_t nb = a.nb;
+  const int bnd = (int)blockIdx.x;
+  if (bnd >= nb) return;
+  const int lane = threadIdx.x;
+  const int64_t nq = a.nq, SW = a.SW;
+  const int sw = (int)SW;
+  int32_t* meta = dtw_walk_meta(a.Dn, nb, SW, a.nr);
+  const int lv = (int)(bnd == nb - 1 ? nq - 1 - 64 * (int64_t)bnd : 63);
+  const int ilo = 64 * bnd;
+  int i = ilo + lv + 1, j = __builtin_amdgcn_readfirstlane(meta[bnd]);
+  int64_t g = EMIT ? __builtin_amdgcn_readfirstlane(meta[2 * nb + bnd]) : 0;   // the next move's index
+  int P = 0;
+  uint32_t cacc = 0;
+  uint32_t* codes = a.codes;
+  auto emit = [&](uint32_t code) {
+    if constexpr (EMIT) {
+      cacc |= code << (2 * (g & 15));
+      ++g;
+      if ((g & 15) == 0) {                         // a word complete (shared with a neighbour band
+        if (lane == 0) atomicOr(&codes[(g >> 4) - 1], cacc);   // at the segment's ends: OR)
+        cacc = 0;
+      }
+    }
+    ++P;
+  };
+  const uint32_t* Db = a.Dn + (((int64_t)bnd * sw) << 6) + lane;
+  uint32_t win[DTW_WIN];
+  int wlo = -1;
+  while (i > ilo && j > 0) {
+    const int l = (i - 1) & 63;
+    const int s = j - 1 + l, w = s >> 4;
+    if (w < wlo || wlo < 0) {
+      wlo = w - (DTW_WIN - 1) > 0 ? w - (DTW_WIN - 1) : 0;
+#pragma unroll
+      for (int k = 0; k < DTW_WIN; ++k) win[k] = (wlo + k < sw) ? Db[(int64_t)(wlo + k) << 6] : 0u;
+    }
+    const int kw = __builtin_amdgcn_readfirstlane(w - wlo);
+    int ll = __builtin_amdgcn_readfirstlane(l);
+    int bp = __builtin_amdgcn_readfirstlane(2 * (s & 15));
+    int jj = __builtin_amdgcn_readfirstlane(j);
+    DTW_WALK_SLOTS(kw);
+    i = ilo + ll + 1;
+    j = jj;
+  }
+  if (bnd == 0) {
+    while (i > 0 || j > 0) {                       // findPreviousStep on the borders
+      emit(i == 0 ? 1u : 0u);
+      if (i == 0) --j; else --i;
+    }
+  } else {
+    while (i > ilo) { emit(0u); --i; }             // j == 0: up column 0 to the band's top
+  }
+  if constexpr (EMIT) {
+    if ((g & 15) && lane == 0) atomicOr(&codes[g >> 4], cacc);
+  } else {
+    if (lane == 0) meta[nb + bnd] = P;
+  }
+}
+
+template <bool BATCH>
+__global__ __launch_bounds__(1024) void dtw_walk_scan_kernel(DtwArgs a_in, const DtwArgs* args) {
+  __shared__ int64_t wsum[16];
+  const DtwArgs a = BATCH ? load_args_uniform(args + blockIdx.x) : a_in;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t nb = a.nb;
+  int32_t* meta = dtw_walk_meta(a.Dn, nb, a.SW, a.nr);
+  const int32_t* cnt = meta + nb;
+  int32_t* off = meta + 2 * nb;
+  // thread t owns bands in walk order k = nb-1-b over [k0, k1)
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t k0 = t * per < nb ? t * per : nb, k1 = (t + 1) * per < nb ? (t + 1) * per : nb;
+  int64_t sum = 0;
+  for (int64_t k = k0; k < k1; ++k) sum += cnt[nb - 1 - k];
+  int64_t inc = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int64_t base = 0, tot = 0;
+  for (int w = 0; w < 16; ++w) { base += w < wv ? wsum[w] : 0; tot += wsum[w]; }
+  int64_t o = base + inc - sum;
+  for (int64_t k = k0; k < k1; ++k) {
+    off[nb - 1 - k] = (int32_t)o;
+    o += cnt[nb - 1 - k];
+  }
+  const int64_t nw = (tot + 15) >> 4;
+  for (int64_t w = t; w < nw; w += 1024) a.codes[w] = 0u;
+  if (t == 0) *a.plen = tot;
 }
 
 namespace {
@@ -1194,8 +1407,8 @@ __global__ __launch_bounds__(256) void dtw_path_points_kernel(const uint32_t* co
 //  dtw_path_runs_kernel: thread per path point; a point whose tile differs from its
 //    predecessor's starts a run (the path is monotone, so a tile's points are contiguous); runs
 //    are appended through an atomic counter in any order.
-//  dtw_path_tile_kernel: one wave per run: the tile's distances into LDS (lane = row), the
-//    anti-diagonal recurrence in LDS (127 steps), then the run's costs (and C[nq][nr]).
+//  dtw_path_tile_kernel: one wave per run: the tile's anti-diagonal recurrence in registers
+//    (127 steps, lane = row, distances inline), each path point's cost taken at its own step.
 template <bool BATCH>
 __global__ __launch_bounds__(256) void dtw_path_runs_kernel(DtwArgs a_in, const DtwArgs* args) {
   const DtwArgs a = BATCH ? load_args_uniform(args + blockIdx.y) : a_in;
@@ -1217,9 +1430,13 @@ __global__ __launch_bounds__(256) void dtw_path_runs_kernel(DtwArgs a_in, const 
 
 template <bool BATCH, int D>
 __global__ __launch_bounds__(64) void dtw_path_tile_kernel(DtwArgs a_in, const DtwArgs* args) {
-  __shared__ double T[65][66];                       // T[li][lj] = C[64bi + li][64bj + lj]
-  __shared__ double Dl[64][65];                      // local distance of cell (64bi+1+l, 64bj+1+c)
+  // Registers only for the recurrence (the band kernel's sweep shape: lane = row, at step st lane l
+  // relaxes column c = st - l, C[i-1][j] by DPP from lane l-1, C[i-1][j-1] one step later, C[i][j-1]
+  // its own), so the block needs ~7 KB of LDS and co-resides with the band kernel's blocks (the
+  // earlier T/Dl tile arrays took 73 KB and waited for whole CUs to drain under C5's streams).
   __shared__ __attribute__((aligned(16))) double Rt[D > 0 ? 64 * D : 2];   // D > 0: the tile's reference rows
+  __shared__ double top[66];                         // C[64bi][jb + c], c = 0 .. 64
+  __shared__ int rlo[64], rhi[64], rf[64];           // the run's points in row li: columns, first index
   const DtwArgs a = BATCH ? load_args_uniform(args + blockIdx.y) : a_in;
   const int lane = threadIdx.x;
   if ((int)blockIdx.x >= a.runs[0]) return;
@@ -1229,68 +1446,73 @@ __global__ __launch_bounds__(64) void dtw_path_tile_kernel(DtwArgs a_in, const D
   const double inf = __builtin_inf();
   const int64_t i = 64 * (int64_t)bi + 1 + lane;     // the lane's row
   const int64_t jb = 64 * (int64_t)bj;               // column of the tile's left boundary
-  // top row (C[64bi][jb + c], c = 0 .. 64) and left column (C[i][jb])
   for (int c = lane; c <= 64; c += 64) {
     const int64_t j = jb + c;
     double v = inf;
     if (bi == 0) v = j == 0 ? 0.0 : inf;
     else if (j >= 1 && j <= nr) v = __builtin_bit_cast(double, a.E[(int64_t)(bi - 1) * (nr + 1) + j]);
-    T[0][c] = v;
+    top[c] = v;
   }
-  T[1 + lane][0] = bj == 0 ? inf : a.CK[(((int64_t)bi * (nr >> 6) + bj - 1) << 6) + lane];
-  // distances: lane = row, 64 columns (the reference row is the same for every lane)
+  const double leftc = bj == 0 ? inf : a.CK[(((int64_t)bi * (nr >> 6) + bj - 1) << 6) + lane];   // C[i][jb]
+  rlo[lane] = 64; rhi[lane] = -1; rf[lane] = INT32_MAX;
   const int dim = a.dim;
   const double* qrow = a.q + (i <= nq ? i - 1 : 0) * dim;
+  double qv[D > 0 ? D : 1];
   if constexpr (D > 0) {
-    // the query row in registers, the 64 reference rows staged in LDS (broadcast reads)
-    double qv[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) qv[k] = qrow[k];
     const int64_t jl = jb + 1 + lane;
     const double* rrow = a.r + (jl <= nr ? jl - 1 : 0) * D;
 #pragma unroll
     for (int k = 0; k < D; ++k) Rt[lane * D + k] = rrow[k];
-    __syncthreads();
-    for (int c = 0; c < 64; ++c) {
-      double sum = 0.0;
-#pragma unroll
-      for (int k = 0; k < D; ++k) {
-        const double df = qv[k] - Rt[c * D + k];
-        sum = sum + df * df;
-      }
-      Dl[lane][c] = sqrt(sum);
-    }
-  } else {
-    for (int c = 0; c < 64; ++c) {
-      const int64_t j = jb + 1 + c;
-      const double* rrow = a.r + (j <= nr ? j - 1 : 0) * dim;
-      double sum = 0.0;
-      for (int k = 0; k < dim; ++k) {
-        const double df = qrow[k] - rrow[k];
-        sum = sum + df * df;
-      }
-      Dl[lane][c] = sqrt(sum);
-    }
   }
   __syncthreads();
-  for (int st = 0; st < 127; ++st) {
-    const int c = st - lane;                         // column jb + 1 + c
-    if (c >= 0 && c < 64) {
-      const int64_t j = jb + 1 + c;
-      const double up = T[lane][c + 1], left = T[lane + 1][c], dg = T[lane][c];
-      double v = Dl[lane][c] + go_min(go_min(up, left), dg);
-      if (a.band > 0 && (i - j > a.band || j - i > a.band)) v = inf;   // outside the Sakoe-Chiba band
-      T[lane + 1][c + 1] = v;
-    }
-    __syncthreads();
-  }
-  // the run's points: at most 127 (a monotone path inside one tile), contiguous from f0
+  // the run's points: at most 127 (a monotone path inside one tile), contiguous from f0; a row's
+  // points are consecutive columns at consecutive indices
   for (int64_t f = f0 + lane; f < P && f < f0 + 128; f += 64) {
     const int pi = a.pq[f], pj = a.pr[f];
     if (pi < 0 || pj < 0 || (pi >> 6) != bi || (pj >> 6) != bj) continue;
-    const int li = pi - 64 * bi + 1, lj = pj - 64 * bj + 1;
-    a.pc[f] = __dsub_rn(T[li][lj], T[li - 1][lj - 1]);
-    if (pi == nq - 1 && pj == nr - 1) *a.cnm = T[li][lj];
+    const int li = pi - 64 * bi, lj = pj - 64 * bj;
+    atomicMin(&rlo[li], lj);
+    atomicMax(&rhi[li], lj);
+    atomicMin(&rf[li], (int)f);
+  }
+  __syncthreads();
+  const int mlo = rlo[lane], mhi = rhi[lane], mf = rf[lane];
+  // own C of the previous step (before the lane's first column: C[i][jb], which its lower
+  // neighbour takes as the diagonal of ITS first cell), and the previous step's up
+  double v = leftc, upp = top[0];
+  for (int st = 0; st < 127; ++st) {
+    const int c = st - lane;                         // column jb + 1 + c
+    const double up = shr1(v, top[st + 1 < 65 ? st + 1 : 64]);   // lane 0: the top row
+    const double dg = upp;
+    upp = up;
+    if (c >= 0 && c < 64) {
+      const int64_t j = jb + 1 + c;
+      const double left = v;
+      double sum = 0.0;
+      if constexpr (D > 0) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const double df = qv[k] - Rt[c * D + k];
+          sum = sum + df * df;
+        }
+      } else {
+        const double* rrow = a.r + (j <= nr ? j - 1 : 0) * dim;
+        for (int k = 0; k < dim; ++k) {
+          const double df = qrow[k] - rrow[k];
+          sum = sum + df * df;
+        }
+      }
+      double nv = sqrt(sum) + go_min(go_min(up, left), dg);
+      if (a.band > 0 && (i - j > a.band || j - i > a.band)) nv = inf;   // outside the Sakoe-Chiba band
+      v = nv;
+      if (c >= mlo && c <= mhi) {
+        const int64_t f = mf + (c - mlo);
+        a.pc[f] = __dsub_rn(nv, dg);
+        if (i == nq && j == nr) *a.cnm = nv;
+      }
+    }
   }
 }
 
@@ -1381,6 +1603,12 @@ __global__ void nonfinite_kernel(const double* x, int64_t n, int32_t* flag) {
     if (!__builtin_isfinite(x[k])) *flag = 1;
 }
 
+// SONAR_DTW_SERIAL_WALK=1: the one-wave serial backtrack instead of the backtrack by bands (A/B)
+static bool dtw_serial_walk() {
+  const char* e = std::getenv("SONAR_DTW_SERIAL_WALK");
+  return e && e[0] == '1';
+}
+
 DtwGeom dtw_geom(int64_t nq, int64_t nr) {
   DtwGeom g;
   g.nq = nq; g.nr = nr;
@@ -1390,7 +1618,10 @@ DtwGeom dtw_geom(int64_t nq, int64_t nr) {
   return g;
 }
 size_t dtw_cn_bytes(const DtwGeom& g) { return (size_t)g.nb * ((g.S + 1) / 2) * 128 * 8; }
-size_t dtw_dn_bytes(const DtwGeom& g) { return (size_t)g.nb * g.SW * 64 * 4; }
+size_t dtw_dn_bytes(const DtwGeom& g) {   // direction words + exit map + walk meta (dtw_walk_meta)
+  return ((size_t)g.nb * g.SW * 64 + (size_t)g.nb * dtw_nr64(g.nr) + (size_t)g.nb * dtw_nseg(g.nr) * 64 +
+          3 * (size_t)g.nb + 3) / 4 * 16;
+}
 size_t dtw_ck_bytes(const DtwGeom& g) { return (size_t)g.nb * (g.nr >= 64 ? g.nr / 64 : 1) * 64 * 8; }
 int64_t dtw_run_words(const DtwGeom& g) { return g.nb + (g.nr + 63) / 64 + 2; }
 size_t dtw_edge_bytes(const DtwGeom& g) { return (size_t)(g.nb > 1 ? g.nb - 1 : 1) * (g.nr + 1) * 8; }
@@ -1463,7 +1694,19 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
 #undef SONAR_DTW_LAUNCH
   if (mid) hipEventRecord(mid, s);
   if (conc) hipStreamWaitEvent(s, ev_b, 0);
-  hipLaunchKernelGGL(dtw_walk_kernel, dim3(1), dim3(64), 0, s, Dn, g.nq, g.nr, g.SW, codes, plen);
+  if (dtw_serial_walk()) {
+    hipLaunchKernelGGL(dtw_walk_kernel, dim3(1), dim3(64), 0, s, Dn, g.nq, g.nr, g.SW, codes, plen);
+  } else {
+    a.codes = codes;
+    a.plen = plen;
+    const DtwArgs* none = nullptr;
+    hipLaunchKernelGGL(dtw_exit_map_kernel<false>, dim3((unsigned)dtw_nseg(g.nr), (unsigned)g.nb), dim3(64), 0, s, a,
+                       none);
+    hipLaunchKernelGGL(dtw_walk_chain_kernel<false>, dim3(1), dim3(64), 0, s, a, none);
+    hipLaunchKernelGGL((dtw_walk_band_kernel<false, false>), dim3((unsigned)g.nb), dim3(64), 0, s, a, none);
+    hipLaunchKernelGGL(dtw_walk_scan_kernel<false>, dim3(1), dim3(1024), 0, s, a, none);
+    hipLaunchKernelGGL((dtw_walk_band_kernel<true, false>), dim3((unsigned)g.nb), dim3(64), 0, s, a, none);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -1511,7 +1754,22 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
     hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
                        0, s, none, bt);
   }
-  hipLaunchKernelGGL(dtw_walk_batch_kernel, dim3((unsigned)n), dim3(64), 0, s, dargs);
+  if (dtw_serial_walk()) {
+    hipLaunchKernelGGL(dtw_walk_batch_kernel, dim3((unsigned)n), dim3(64), 0, s, dargs);
+  } else {
+    int64_t max_nb = 1;
+    for (int k = 0; k < n; ++k) max_nb = hargs[k].nb > max_nb ? hargs[k].nb : max_nb;
+    int64_t max_seg = 1;
+    for (int k = 0; k < n; ++k) max_seg = dtw_nseg(hargs[k].nr) > max_seg ? dtw_nseg(hargs[k].nr) : max_seg;
+    hipLaunchKernelGGL(dtw_exit_map_kernel<true>, dim3((unsigned)max_seg, (unsigned)max_nb, (unsigned)n), dim3(64), 0,
+                       s, none, dargs);
+    hipLaunchKernelGGL(dtw_walk_chain_kernel<true>, dim3((unsigned)n), dim3(64), 0, s, none, dargs);
+    hipLaunchKernelGGL((dtw_walk_band_kernel<false, true>), dim3((unsigned)max_nb, (unsigned)n), dim3(64), 0, s, none,
+                       dargs);
+    hipLaunchKernelGGL(dtw_walk_scan_kernel<true>, dim3((unsigned)n), dim3(1024), 0, s, none, dargs);
+    hipLaunchKernelGGL((dtw_walk_band_kernel<true, true>), dim3((unsigned)max_nb, (unsigned)n), dim3(64), 0, s, none,
+                       dargs);
+  }
   hipLaunchKernelGGL(dtw_path_scan_kernel<true>, dim3((unsigned)n), dim3(1024), 0, s, (const uint32_t*)nullptr,
                      (int64_t)0, (int64_t)0, (int64_t)0, (int2*)nullptr, dargs);
   const int64_t nw = (max_cap + 15) >> 4;
