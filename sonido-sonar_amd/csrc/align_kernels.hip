@@ -1129,6 +1129,33 @@ __global__ __launch_bounds__(64) void dtw_walk_batch_kernel(const DtwArgs* args)
 // left boundary X(l, J0-1) enters as the symbol -(l+1), and the chain resolves a symbol through
 // the neighbour's right boundary Xr[b][k-1][l] (a path crosses a segment's left edge before
 // reaching row 64b only within ~64 columns of it, so this is rare and one hop).
+// 64 steps of the exit-map recurrence (4 code words); row lv's X after step t0 + u -> hrow[u]
+template <bool GUARD>
+__device__ __forceinline__ void dtw_xm_block(const uint32_t (&cw)[4], int t0, int J0, int ncol, int lane, int lv,
+                                             int& x, int& xdg, int* hrow) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int hist[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int t = t0 + 16 * q + u;
+      // code 0 up, 1 left, 2 diagonal as two sign-extended bit masks and two bit-selects
+      const int mleft = (int)(cw[q] << (31 - 2 * u)) >> 31, mdiag = (int)(cw[q] << (30 - 2 * u)) >> 31;
+      const int xup = __builtin_amdgcn_update_dpp(J0 + t, x, 0x138, 0xf, 0xf, false);   // wave_shr:1
+      const int xud = (mdiag & xdg) | (~mdiag & xup);
+      const int xn = (mleft & x) | (~mleft & xud);
+      xdg = xup;
+      if constexpr (GUARD) x = (unsigned)(t - lane) < (unsigned)ncol ? xn : x;
+      else x = xn;
+      hist[u] = x;
+    }
+    if (lane == lv) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) hrow[16 * q + u] = hist[u];
+    }
+  }
+}
+
 template <bool BATCH>
 __global__ __launch_bounds__(64) void dtw_exit_map_kernel(DtwArgs a_in, const DtwArgs* args) {
   const DtwArgs a = BATCH ? load_args_uniform(args + blockIdx.z) : a_in;
@@ -1140,43 +1167,36 @@ __global__ __launch_bounds__(64) void dtw_exit_map_kernel(DtwArgs a_in, const Dt
   const int lv = (int)(b == nb - 1 ? nq - 1 - 64 * b : 63);
   const uint32_t* Db = a.Dn + ((b * SW) << 6) + lane;
   int32_t* Xb = dtw_xmap(a.Dn, nb, SW) + b * dtw_nr64(nr);
-  const int T = (int)(J1 - J0) + lv;               // steps until row lv has reached column J1-1
+  const int ncol = (int)(J1 - J0);
+  const int T = ncol + lv;                         // steps until row lv has reached column J1-1
   const int64_t w0 = (J0 - 1) >> 4;                // the segment's first code word (J0-1 = 1024k)
-  const int nw = (T + 15) >> 4;
+  const int nblk = (T + 63) >> 6;                  // 64-step blocks (4 code words each)
+  __shared__ int hrow[64];                         // row lv's X over a block's 64 steps
   int x = k == 0 ? 0 : -(lane + 1);                // own X of the previous step (the left boundary)
   int xdg = (int)(J0 - 1);                         // lane 0: X(-1, J0-1)
-  int xacc = 0;
-  constexpr int WB = 8;                            // code words per batch (128 steps)
-  uint32_t cur[WB], nxt[WB];
+  auto ldw = [&](int q) -> uint32_t {
+    const int64_t w = w0 + q;
+    return (q < 4 * nblk && w < SW) ? Db[w << 6] : 0u;
+  };
+  // code words two blocks ahead of the recurrence (HBM latency is a few blocks of steps)
+  uint32_t cur[4], nx1[4], nx2[4];
 #pragma unroll
-  for (int q = 0; q < WB; ++q) cur[q] = (q < nw && w0 + q < SW) ? Db[(w0 + q) << 6] : 0u;
-  for (int wb = 0; wb < nw; wb += WB) {
+  for (int q = 0; q < 4; ++q) { cur[q] = ldw(q); nx1[q] = ldw(4 + q); }
+  for (int blk = 0; blk < nblk; ++blk) {
 #pragma unroll
-    for (int q = 0; q < WB; ++q) {
-      const int64_t w = w0 + wb + WB + q;
-      nxt[q] = (wb + WB + q < nw && w < SW) ? Db[w << 6] : 0u;
-    }
+    for (int q = 0; q < 4; ++q) nx2[q] = ldw(4 * (blk + 2) + q);
+    const int t0 = 64 * blk;
+    // the guards (a lane before its first or past its last column keeps its X) only where the
+    // block crosses the skewed start or end
+    if (t0 < 64 || t0 + 64 > ncol) dtw_xm_block<true>(cur, t0, (int)J0, ncol, lane, lv, x, xdg, hrow);
+    else dtw_xm_block<false>(cur, t0, (int)J0, ncol, lane, lv, x, xdg, hrow);
+    // row lv's 64 values (steps t0 .. t0+63 = Xm columns J0-1+t0-lv+u) -> one coalesced store
+    __syncthreads();
+    const int tu = t0 + lane - lv;
+    if (tu >= 0 && tu < ncol) Xb[J0 - 1 + tu] = hrow[lane];
+    __syncthreads();
 #pragma unroll
-    for (int q = 0; q < WB; ++q) {
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int t = (wb + q) * 16 + u;
-        const uint32_t code = (cur[q] >> (2 * u)) & 3u;
-        const int xup = __builtin_amdgcn_update_dpp((int)(J0 + t), x, 0x138, 0xf, 0xf, false);   // wave_shr:1
-        const int xn = code == 0u ? xup : (code == 1u ? x : xdg);
-        xdg = xup;
-        const int jl = t - lane;                   // the lane's column - J0
-        x = (jl >= 0 && jl < (int)(J1 - J0)) ? xn : x;
-        const int jv = t - lv;                     // row lv's column - J0 (uniform)
-        if (jv >= 0 && jv < (int)(J1 - J0)) {
-          const int64_t c = J0 - 1 + jv;           // Xm index of that column
-          xacc = lane == (int)(c & 63) ? __builtin_amdgcn_readlane(x, lv) : xacc;
-          if ((c & 63) == 63 || jv == (int)(J1 - J0) - 1) Xb[(c & ~(int64_t)63) + lane] = xacc;
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < WB; ++q) cur[q] = nxt[q];
+    for (int q = 0; q < 4; ++q) { cur[q] = nx1[q]; nx1[q] = nx2[q]; }
   }
   dtw_xbound(a.Dn, nb, SW, nr)[(b * nseg + k) * 64 + lane] = x;   // X(l, J1-1) (rows <= lv)
 }
