@@ -85,9 +85,17 @@ def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0 over gloo (RCCL
+    # refuses two ranks on one device); the driver's multi-GPU runs use neither override
+    if os.environ.get("SONAR_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("SONAR_BENCH_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
     return world, rank, local
