@@ -60,6 +60,10 @@ struct sonar_ctx {
   double dtw_ms[3] = {0.0, 0.0, 0.0};
   IngestState* ingest = nullptr;
   std::vector<sonar_ctx*> workers;   // sonar_align_pairs' worker contexts (multi_api.cpp)
+  // a second stream for the NCC while the chroma DTW runs on `stream` (align_impl), and the two
+  // events that order it: features done -> side, NCC done -> stream
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev[2] = {nullptr, nullptr};
 };
 
 struct sonar_result {

@@ -604,9 +604,30 @@ int align_impl(sonar_ctx* c, const double* qe, int64_t nqe, const double* re, in
   if (dev) {
     HIP_TRY(c, hipSetDevice(c->device));
     int st = SONAR_OK;
-    if (want_corr) st = sonar::detail::ncc_enqueue(c, qe, nqe, re, nre, (int32_t)mlf, &hcorr, &hL);
-    if (st == SONAR_OK && want_dtw) st = sonar::detail::dtw_enqueue(c, qc, nqc, rc_, nrc, 12, -1, &pend);
-    if (st != SONAR_OK) return st;
+    if (want_corr && want_dtw) {
+      // the NCC (energies) and the DTW (chroma) are independent: the NCC runs on the side stream
+      // beside the band kernel (which leaves LDS and wave slots free on every CU), and the main
+      // stream waits for it, so the one synchronisation below still covers both
+      if (!c->side) {
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        for (auto& e : c->side_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      }
+      HIP_TRY(c, hipEventRecord(c->side_ev[0], c->stream));
+      HIP_TRY(c, hipStreamWaitEvent(c->side, c->side_ev[0], 0));
+      hipStream_t main_stream = c->stream;
+      c->stream = c->side;
+      st = sonar::detail::ncc_enqueue(c, qe, nqe, re, nre, (int32_t)mlf, &hcorr, &hL);
+      c->stream = main_stream;
+      if (st != SONAR_OK) return st;
+      HIP_TRY(c, hipEventRecord(c->side_ev[1], c->side));
+      st = sonar::detail::dtw_enqueue(c, qc, nqc, rc_, nrc, 12, -1, &pend);
+      if (st != SONAR_OK) return st;
+      HIP_TRY(c, hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
+    } else {
+      if (want_corr) st = sonar::detail::ncc_enqueue(c, qe, nqe, re, nre, (int32_t)mlf, &hcorr, &hL);
+      if (st == SONAR_OK && want_dtw) st = sonar::detail::dtw_enqueue(c, qc, nqc, rc_, nrc, 12, -1, &pend);
+      if (st != SONAR_OK) return st;
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
   sonar::detail::AlignIn in;

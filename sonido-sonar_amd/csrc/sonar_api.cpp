@@ -254,6 +254,9 @@ void sonar_destroy(sonar_ctx* c) {
   if (c->ev1) hipEventDestroy(c->ev1);
   for (auto& e : c->dtw_ev)
     if (e) hipEventDestroy(e);
+  for (auto& e : c->side_ev)
+    if (e) hipEventDestroy(e);
+  if (c->side) hipStreamDestroy(c->side);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
