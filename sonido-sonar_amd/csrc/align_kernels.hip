@@ -958,9 +958,21 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         __hip_atomic_store(Eout + je, __builtin_bit_cast(uint64_t, ev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (s1 >= S) break;
-    if (!ready((int)s1, kc)) {                         // a producer is behind: wait, then reload
-      SONAR_SPIN_UNTIL((kc = load_ctr(), ready((int)s1, kc)));
+    if (!ready((int)s1, kc)) {
+      // the counters read at the chunk's start were stale.  When the band is gated by its
+      // predecessor's edge (every chunk, once it has caught up) the data usually arrived during
+      // the chunk, so the fresh counters and the chunk's data are read back to back (LDS
+      // completes a wave's requests in order: data read after a count that covers it is valid),
+      // one LDS round trip instead of two; only a still-missing producer spins.
+#ifndef DTW_NOREREAD
+      kc = load_ctr();
       load_chunk(s1, dcn, echn);
+      if (!ready((int)s1, kc))
+#endif
+      {
+        SONAR_SPIN_UNTIL((kc = load_ctr(), ready((int)s1, kc)));
+        load_chunk(s1, dcn, echn);
+      }
     }
     fix_edges(s1, echn);
 #pragma unroll

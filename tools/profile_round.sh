@@ -9,6 +9,7 @@ OUT="$R/gpurun_out/prof_$TAG"; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 "$R/bench.py" > "$OUT/bench_traced.log" 2>&1 || { echo "trace pass failed"; exit 1; }
+rm -f "$OUT"/trace/*_kernel_trace.csv   # per-dispatch rows: tens of MB, the stats CSV is the summary
 echo "trace done"
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/$c" -o run -- \
