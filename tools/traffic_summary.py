@@ -16,8 +16,13 @@ stats = glob.glob(f"{src}/trace/**/*kernel_stats.csv", recursive=True)
 shutil.copy(stats[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
 trace = glob.glob(f"{src}/trace/**/*kernel_trace.csv", recursive=True)
 durs = collections.defaultdict(list)
-for r in csv.DictReader(open(trace[0])):
-    durs[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+if trace:
+    for r in csv.DictReader(open(trace[0])):
+        durs[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+else:   # the per-dispatch CSV is dropped on the box (size): average and count from the stats summary
+    for r in csv.DictReader(open(stats[0])):
+        n = int(r["Calls"])
+        durs[r["Name"]] = [float(r["AverageNs"]) / 1e6] * n
 
 per = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
