@@ -1635,6 +1635,15 @@ __global__ void nonfinite_kernel(const double* x, int64_t n, int32_t* flag) {
     if (!__builtin_isfinite(x[k])) *flag = 1;
 }
 
+// the probe over both sequences of every DTW of a batch (blockIdx.y = the DTW): one launch per
+// batch instead of two per pair on the batch's stream
+__global__ void nonfinite_batch_kernel(const DtwArgs* args) {
+  const DtwArgs a = load_args_uniform(args + blockIdx.y);
+  const int64_t nqe = a.nq * a.dim, n = nqe + a.nr * a.dim;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+    if (!__builtin_isfinite(k < nqe ? a.q[k] : a.r[k - nqe])) a.sync[2] = 1;
+}
+
 // SONAR_DTW_SERIAL_WALK=1: the one-wave serial backtrack instead of the backtrack by bands (A/B)
 static bool dtw_serial_walk() {
   const char* e = std::getenv("SONAR_DTW_SERIAL_WALK");
@@ -1825,6 +1834,14 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
 int launch_dtw_cost_rowmajor(const double* Cn, const DtwGeom& g, double* out, hipStream_t s) {
   const dim3 grid((unsigned)((g.nr + 63) / 64), (unsigned)g.nb);
   hipLaunchKernelGGL(dtw_cost_rowmajor_kernel, grid, dim3(256), 0, s, Cn, g.nq, g.nr, g.S, out);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int launch_nonfinite_batch(const DtwArgs* dargs, int n, int64_t max_elems, hipStream_t s) {
+  if (n <= 0 || max_elems <= 0) return 0;
+  int64_t blocks = (max_elems + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(nonfinite_batch_kernel, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, dargs);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

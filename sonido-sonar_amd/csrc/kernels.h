@@ -202,6 +202,9 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
                      int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr);
 // sets *flag = 1 if any of the n values is not finite
 int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
+// the same probe over q and r of every DTW of a batch (sets args[k].sync[2]); max_elems >= every
+// (nq + nr) * dim
+int launch_nonfinite_batch(const DtwArgs* dargs, int n, int64_t max_elems, hipStream_t s);
 
 // LPC formants (lpc_kernels.hip): one block per frame; out is sonar_formant_frame[frames]
 int launch_formants(const double* pcm, int64_t frames, int64_t hop, int W, int p, int sr, int frame_ok_len,

@@ -209,8 +209,6 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     if (p.corr && sonar::launch_ncc(eq, p.Eq, er, p.Er, p.L, xa, xb, st, (double*)(corr + p.corr_off), s) != 0)
       return fail(w, SONAR_ERR_DEVICE, "ncc launch failed");
     int32_t* sync = dstat + 8 * i + 4;
-    if (sonar::launch_nonfinite(cq, p.Fq * 12, sync + 2, s) || sonar::launch_nonfinite(cr, p.Fr * 12, sync + 2, s))
-      return fail(w, SONAR_ERR_DEVICE, "dtw launch failed");
     sonar::DtwArgs& a = hargs[i];
     a = sonar::DtwArgs{};
     a.q = cq; a.r = cr; a.dim = 12; a.band = -1;
@@ -237,6 +235,10 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
         if (b < pg[i].g.nb) hmap[t++] = make_int2(i, (int)b);
   }
   HIP_TRY(w, hipMemcpyAsync(dargs, hargs, args_b + start_b + (band_major ? map_b : 0), hipMemcpyHostToDevice, s));
+  // the non-finite probe of every pair's chroma in one launch (flags in each pair's sync[2])
+  int64_t max_el = 0;
+  for (const auto& p : pg) max_el = std::max(max_el, (p.Fq + p.Fr) * 12);
+  if (sonar::launch_nonfinite_batch(dargs, n, max_el, s) != 0) return fail(w, SONAR_ERR_DEVICE, "dtw launch failed");
   if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s,
                               band_major ? dmap : nullptr) != 0)
     return fail(w, SONAR_ERR_DEVICE, "dtw batch launch failed");
