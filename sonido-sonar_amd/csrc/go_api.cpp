@@ -429,10 +429,14 @@ int sonar_generate_fingerprint(sonar_ctx* c, const double* pcm, int64_t n, int32
 }
 
 // ------------------------------------------ AlignmentExtractor --------------
-// MusicFeatureExtractor energy + chroma (music.go:245-259, :327-376, :460-466)
-int sonar_music_alignment_features(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, int32_t stft_w,
-                                   int32_t stft_h, int32_t fw, int32_t fh, double* energy, double* chroma,
-                                   int32_t device_ptrs) {
+}  // extern "C"
+
+namespace {
+// MusicFeatureExtractor energy + chroma (music.go:245-259, :327-376, :460-466) on c->stream; `tag`
+// names this call's scratch, so two calls on different streams do not share it
+int music_features_impl(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, int32_t stft_w, int32_t stft_h,
+                        int32_t fw, int32_t fh, double* energy, double* chroma, int32_t device_ptrs,
+                        const std::string& tag) {
   if (!c) return SONAR_ERR_INVALID;
   if (!pcm || n <= 0) return fail(c, SONAR_ERR_INVALID, "invalid input data");        // music.go:179-181
   if (stft_w <= 0 || stft_h <= 0) return fail(c, SONAR_ERR_INVALID, "window and hop size must be positive");
@@ -443,23 +447,23 @@ int sonar_music_alignment_features(sonar_ctx* c, const double* pcm, int64_t n, i
   hipStream_t s = c->stream;
   const double* dp = pcm;
   if (!device_ptrs) {
-    void* b = dbuf(c, "mf.pcm", n * 8);
+    void* b = dbuf(c, "mf.pcm" + tag, n * 8);
     if (!b) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
     HIP_TRY(c, hipMemcpyAsync(b, pcm, n * 8, hipMemcpyHostToDevice, s));
     dp = (const double*)b;
   }
-  double* y = (double*)dbuf(c, "mf.pre", n * 8);                 // processedPCM
+  double* y = (double*)dbuf(c, "mf.pre" + tag, n * 8);           // processedPCM
   if (!y) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
-  double* dcs = (double*)dbuf(c, "mf.dcscratch", sonar::dc_preemph_scratch_bytes(n));
+  double* dcs = (double*)dbuf(c, "mf.dcscratch" + tag, sonar::dc_preemph_scratch_bytes(n));
   if (!dcs) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
   if (sonar::launch_dc_preemph(dp, n, 0.995, 0.95, y, dcs, s) != 0) return fail(c, SONAR_ERR_DEVICE, "dc launch failed");
   const int64_t Fe = sonar_energy_frames(n, fw, fh);
-  double* de = device_ptrs ? energy : (double*)dbuf(c, "mf.energy", std::max<int64_t>(Fe, 1) * 8);
+  double* de = device_ptrs ? energy : (double*)dbuf(c, "mf.energy" + tag, std::max<int64_t>(Fe, 1) * 8);
   // ShortTimeEnergy of the already pre-emphasised signal: alpha 0 makes the kernel's
   // pre-emphasis the identity (x - 0 * x[n-1] == x exactly)
   if (Fe > 0 && sonar::launch_energy(y, 1, n, Fe, fw, fh, 0.0, de, 1, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "energy launch failed");
-  double* dc = device_ptrs ? chroma : (double*)dbuf(c, "mf.chroma", F * 12 * 8);
+  double* dc = device_ptrs ? chroma : (double*)dbuf(c, "mf.chroma" + tag, F * 12 * 8);
   if (!de || !dc) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
   const int rc = sonar_chroma_stft(c, y, n, F, fh, sr, 0, dc, 1);
   if (rc != SONAR_OK) return rc;
@@ -469,6 +473,15 @@ int sonar_music_alignment_features(sonar_ctx* c, const double* pcm, int64_t n, i
     HIP_TRY(c, hipStreamSynchronize(s));
   }
   return SONAR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int sonar_music_alignment_features(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, int32_t stft_w,
+                                   int32_t stft_h, int32_t fw, int32_t fh, double* energy, double* chroma,
+                                   int32_t device_ptrs) {
+  return music_features_impl(c, pcm, n, sr, stft_w, stft_h, fw, fh, energy, chroma, device_ptrs, "");
 }
 
 }  // extern "C"
@@ -694,10 +707,23 @@ int sonar_align_pair_device(sonar_ctx* c, const double* q_pcm, int64_t nq, const
   double* qc = (double*)dbuf(c, "ap.qc", Fq * 12 * 8);
   double* rc = (double*)dbuf(c, "ap.rc", Fr * 12 * 8);
   if (!qe || !re || !qc || !rc) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
-  int st = sonar_music_alignment_features(c, q_pcm, nq, sample_rate, stft_window, hop, feature_window, hop, qe, qc, 1);
-  if (st == SONAR_OK)
-    st = sonar_music_alignment_features(c, r_pcm, nr, sample_rate, stft_window, hop, feature_window, hop, re, rc, 1);
+  // the two streams' features are independent: r's on the side stream (its own scratch) beside q's
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->side) {
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    for (auto& e : c->side_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  HIP_TRY(c, hipEventRecord(c->side_ev[0], c->stream));        // the caller's PCM is ready on c->stream
+  HIP_TRY(c, hipStreamWaitEvent(c->side, c->side_ev[0], 0));
+  int st = music_features_impl(c, q_pcm, nq, sample_rate, stft_window, hop, feature_window, hop, qe, qc, 1, "");
   if (st != SONAR_OK) return st;
+  hipStream_t main_stream = c->stream;
+  c->stream = c->side;
+  st = music_features_impl(c, r_pcm, nr, sample_rate, stft_window, hop, feature_window, hop, re, rc, 1, ".r");
+  c->stream = main_stream;
+  if (st != SONAR_OK) return st;
+  HIP_TRY(c, hipEventRecord(c->side_ev[1], c->side));
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, c->side_ev[1], 0));
   return align_impl(c, Eq > 0 ? qe : nullptr, Eq, Er > 0 ? re : nullptr, Er, qc, Fq, rc, Fr, nq, nr, sample_rate,
                     sample_rate, hop, feature_window, max_lag_seconds, 1, out);
 }
