@@ -65,7 +65,8 @@ int d2h(sonar_ctx* c, std::vector<T>& v, const void* d, size_t n) {
 }
 
 double percentile10_threshold(std::vector<double> e) {            // speech.go:594-604 (bubble sort)
-  std::sort(e.begin(), e.end());
+  // the element at index n/10 of the sorted order; a selection gives the same value in O(n)
+  std::nth_element(e.begin(), e.begin() + e.size() / 10, e.end());
   return e[e.size() / 10];
 }
 
@@ -205,7 +206,7 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   HIP_TRY(c, hipStreamSynchronize(s));
 
   auto* res = new sonar_result();
-  if (fc->enable_mfcc) res->put("mfcc", mfcc, F, nm);
+  if (fc->enable_mfcc) res->put("mfcc", std::move(mfcc), F, nm);
   static const char* spec_names[9] = {"spectral_centroid", "spectral_rolloff", "spectral_bandwidth",
                                       "spectral_flatness", "spectral_crest", "spectral_slope", "spectral_flux",
                                       "", ""};
@@ -214,7 +215,7 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     if (d == 6 && F <= 1) continue;                               // flux only when TimeFrames > 1 (:362-365)
     res->put(spec_names[d], std::vector<double>(spec.begin() + d * Fz, spec.begin() + d * Fz + cnt), cnt, 1);
   }
-  res->vec("zero_crossing_rate", zcr);
+  res->put("zero_crossing_rate", std::move(zcr), (int64_t)Fz, 1);
 
   // whole-signal stats: partials reduced in block order
   double peak = 0, sabs = 0, ssq = 0, cross = 0;
@@ -226,6 +227,12 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   // ---- speech features (extractSpeechFeatures :272-313) -------------------------
   sonar::host::YinTracker tracker;
   bool is_speech = false;
+  double thr10 = 0.0;                                             // percentile10_threshold(energy), once
+  bool have_thr10 = false;
+  auto energy_thr10 = [&]() {
+    if (!have_thr10) { thr10 = percentile10_threshold(energy); have_thr10 = true; }
+    return thr10;
+  };
   if (fc->enable_speech_features) {
     // detectSpeech (speech_analysis.go:105-132), sample rate = FeatureConfig.SampleRate
     bool sp = !(n < (int64_t)(csr / 4));
@@ -275,7 +282,7 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
       const double dur = (double)n / (double)csr;
       double sil = 0.0;
       if (!energy.empty()) {
-        const double thr = percentile10_threshold(energy);
+        const double thr = energy_thr10();
         int64_t k = 0;
         for (double e : energy) if (e <= thr) k++;
         sil = (double)k / (double)energy.size();
@@ -296,7 +303,7 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
       // extractPauseDurations (:587-637)
       std::vector<double> pauses;
       if (!energy.empty()) {
-        const double thr = percentile10_threshold(energy);
+        const double thr = energy_thr10();
         const double fts = (double)fc->hop_size / (double)csr;
         bool in = false; int64_t st = 0;
         for (int64_t i = 0; i < (int64_t)energy.size(); i++) {
@@ -316,7 +323,7 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     res->scalar("dynamic_range", lrange);
     double sil = 0.0;
     if (!energy.empty()) {                                        // calculateSilenceRatio (:639-665)
-      const double thr = percentile10_threshold(energy);
+      const double thr = energy_thr10();
       int64_t k = 0;
       for (double e : energy) if (e <= thr) k++;
       sil = (double)k / (double)energy.size();
