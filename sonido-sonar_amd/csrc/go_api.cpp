@@ -168,14 +168,24 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   fo.centroid = dspec; fo.rolloff = dspec + Fz; fo.bandwidth = dspec + 2 * Fz; fo.flatness = dspec + 3 * Fz;
   fo.crest = dspec + 4 * Fz; fo.slope = dspec + 5 * Fz; fo.flux = dspec + 6 * Fz; fo.low_ratio = dspec + 7 * Fz;
   fo.high_ratio = dspec + 8 * Fz; fo.zcr = dzcr; fo.energy = Fe > 0 ? den : nullptr;
-  int rc = sonar_fingerprint(c, dpcm, n, &cfg, &fo);
-  if (rc != SONAR_OK) return rc;
-
   // ---- YIN raw results on the pre-emphasised PCM (extractHarmonicFeatures :464) ---
+  // on the side stream, beside the fused STFT kernel (both only read the PCM); the main stream
+  // waits for it before the copies back
   double* dpit = (double*)dbuf(c, "sx.pitch", std::max<int64_t>(Fp, 1) * 8);
   double* dcon = (double*)dbuf(c, "sx.conf", std::max<int64_t>(Fp, 1) * 8);
   if (!dpit || !dcon) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (pitch)");
-  if (sonar::launch_yin(dy, n, Fp, 512, csr, dpit, dcon, nullptr, s) != 0) return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
+  if (!c->side) {
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    for (auto& e : c->side_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  HIP_TRY(c, hipEventRecord(c->side_ev[0], s));                  // dy is written
+  HIP_TRY(c, hipStreamWaitEvent(c->side, c->side_ev[0], 0));
+  if (sonar::launch_yin(dy, n, Fp, 512, csr, dpit, dcon, nullptr, c->side) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
+  HIP_TRY(c, hipEventRecord(c->side_ev[1], c->side));
+  int rc = sonar_fingerprint(c, dpcm, n, &cfg, &fo);
+  if (rc != SONAR_OK) return rc;
+  HIP_TRY(c, hipStreamWaitEvent(s, c->side_ev[1], 0));
   // whole-signal statistics of the pre-emphasised PCM
   const int SB = 256;
   double* dpart = (double*)dbuf(c, "sx.stats", SB * 4 * 8);
