@@ -251,6 +251,9 @@ constexpr int DTW_ECH = 8;                          // edge values polled per ch
 #endif
 constexpr uint64_t DTW_SENT = 0x7FF000017FF00001ull;  // signalling NaN: never an arithmetic result
 constexpr int DTW_SPIN_LIMIT = 1 << 22;
+#ifndef DTW_SPIN_SLEEP
+#define DTW_SPIN_SLEEP 4                            // s_sleep between LDS counter polls (A/B 0,1,4,8,16: 4-8 best)
+#endif
 
 static_assert(sizeof(DtwArgs) % 4 == 0, "read as dwords");
 
@@ -495,7 +498,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     if (!(cond)) {                                                                    \
       const uint64_t w0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;            \
       while (!(cond)) {                                                               \
-        __builtin_amdgcn_s_sleep(1);                                                  \
+        __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);                                     \
         if (++sp_ > (uint64_t)DTW_SPIN_LIMIT * 4) { if (lane == 0) atomicOr(&a.sync[1], 2); break; } \
       }                                                                               \
       if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - w0_;             \
