@@ -23,6 +23,7 @@ import math
 import os
 import sys
 import time
+import traceback
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "sonido-sonar_amd")]
@@ -276,8 +277,27 @@ def cpu_baseline(seconds_hint, gpu_mfcc, seconds_total, gpu_mfcc64=None):
     return base, parity, parity64
 
 
-DTW_BYTES_PER_CELL = 8.25     # C store (8 B, the reference's CostMatrix) + 2-bit direction code
+# Algorithmic HBM bytes per cell of the band kernel in checkpoint mode (the default: the cost matrix
+# is not stored unless the caller asks for it): 2-bit direction codes 0.25 B, every 64th column of
+# C 8 B / 64 = 0.125 B, the band's bottom edge row 8 B / 64 rows = 0.125 B written and read back
+# by the band below 0.125 B.  The inputs (12 doubles per row) are read once: ~0 per cell.
+DTW_BYTES_PER_CELL = 0.625
+DTW_BYTES_BREAKDOWN = {"direction_codes": 0.25, "checkpoint_columns": 0.125, "edge_store": 0.125, "edge_load": 0.125}
 FP64_PEAK_TFS = 78.6          # MI355X FP64 vector (AMD spec)
+
+
+def load_pmc_bytes(pattern, kernel_prefix):
+    """FETCH_SIZE x2 (gfx950 half count) + WRITE_SIZE per launch, bytes, of the first kernel whose
+    name starts with `kernel_prefix` in the newest committed profiles/<pattern> PMC summary."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        for name, k in d.get("kernels", {}).items():
+            if name.startswith(kernel_prefix) and "FETCH_SIZE" in k and "WRITE_SIZE" in k:
+                return {"bytes_per_launch": (2 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0,
+                        "fetch_bytes": 2 * k["FETCH_SIZE"] * 1024.0, "write_bytes": k["WRITE_SIZE"] * 1024.0,
+                        "kernel": name, "source": os.path.relpath(path, ROOT)}
+    return None
 
 
 def bench_dtw(ctx, n, steps, parity=False):
@@ -288,7 +308,14 @@ def bench_dtw(ctx, n, steps, parity=False):
     q = rng.random((n, 12))
     r = np.roll(q, 37, axis=0) + 0.01 * rng.random((n, 12))
     ctx.dtw(q[:256], r[:256])       # warm-up / allocation of small buffers
-    ctx.dtw(q, r)                   # allocation of the (n+1)^2 cost matrix
+    ctx.dtw(q, r)                   # warm-up at full size (codes, checkpoint columns, edges)
+    # one band alone (64 query rows against all n reference rows): the isolated step time of the
+    # sweep, which prices the wavefront's dependency chain below
+    band0 = []
+    for _ in range(3):
+        ctx.dtw(q[:64], r)
+        band0.append(ctx.dtw_last_timing()[0])
+    step_ns = float(np.median(band0)) * 1e6 / (n + 63)
     torch.cuda.synchronize()
     walls, parts = [], []
     for _ in range(steps):
@@ -299,25 +326,44 @@ def bench_dtw(ctx, n, steps, parity=False):
     dt = float(np.median(walls))
     band_ms, walk_ms, dec_ms = (float(v) for v in np.median(np.array(parts), axis=0))
     cells = n * n
+    nb = (n + 63) // 64
+    chain_steps = (n + 63) + 64 * (nb - 1)      # band nb-1's last step: every band's 64-step lag, then its sweep
+    floor_ms = chain_steps * step_ns * 1e-6
+    traffic = load_pmc_bytes("*dtw_pmc*.json", "dtw_band_kernel<12, true, false, false")
+    hbm_gbs = cells * DTW_BYTES_PER_CELL / (band_ms * 1e-3) / 1e9
     out = {"dtw_cells_per_s": cells / dt, "dtw_ms": dt * 1e3, "dtw_ms_spread": [min(walls) * 1e3, max(walls) * 1e3],
            "dtw_n": n, "dtw_dim": 12, "dtw_path_len": int(len(res["path_q"])), "dtw_reps": steps,
            "dtw_kernel_ms": {"band_sweep": band_ms, "walk": walk_ms, "path_decode": dec_ms},
-           "dtw_roofline": {"bound": "hbm", "kernel": "dtw_band_kernel",
-                            "achieved": cells * DTW_BYTES_PER_CELL / (band_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": cells * DTW_BYTES_PER_CELL / (band_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                            "algorithmic_bytes_per_cell": DTW_BYTES_PER_CELL,
+           # the binding limit is the wavefront's dependency chain, not a roof: band b starts 64 steps
+           # after band b-1, so the last band ends after (n + 63) + 64 (nb - 1) steps at the sweep's
+           # isolated step time (one band alone, measured above); frac = that floor / the band kernel
+           "dtw_roofline": {"bound": "wavefront", "kernel": "dtw_band_kernel", "achieved": band_ms,
+                            "peak": floor_ms, "unit": "ms", "frac": floor_ms / band_ms,
+                            "chain_steps": chain_steps, "step_ns_one_band": step_ns,
                             "sweep_cells_per_s": cells / (band_ms * 1e-3),
-                            "fp64_tflops": cells * 40 / (band_ms * 1e-3) / 1e12,
-                            "fp64_frac": cells * 40 / (band_ms * 1e-3) / 1e12 / FP64_PEAK_TFS,
-                            "note": "40 flop/cell (12-dim Euclidean + min + add, SURVEY.md 8(d)); the sweep is a "
-                                    "wavefront of nq + nr dependent steps, latency-bound below both roofs"}}
+                            "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": hbm_gbs / HBM_PEAK_GBS,
+                                    "algorithmic_bytes_per_cell": DTW_BYTES_PER_CELL,
+                                    "algorithmic_bytes_breakdown": DTW_BYTES_BREAKDOWN,
+                                    "algorithmic_bytes_per_launch": cells * DTW_BYTES_PER_CELL,
+                                    "traffic": traffic["bytes_per_launch"] if traffic else None,
+                                    "traffic_detail": traffic},
+                            "fp64": {"achieved": cells * 40 / (band_ms * 1e-3) / 1e12, "peak": FP64_PEAK_TFS,
+                                     "unit": "TFLOP/s", "frac": cells * 40 / (band_ms * 1e-3) / 1e12 / FP64_PEAK_TFS},
+                            "note": "40 flop/cell (12-dim Euclidean + min + add, SURVEY.md 8(d)); 0.625 B/cell "
+                                    "algorithmic (checkpoint mode); the sweep is bound by the wavefront's "
+                                    "dependency chain, below both the HBM and the FP64 roofs"},
+           "dtw_counters": ctx.dtw_counters(reset=True)}
     if parity:
         O = oracle_module()
         threads = cpu_threads()
         with pinned(threads):
-            t0 = time.perf_counter()
-            ref = O.dtw_full(q, r, nthreads=threads)
-            dtc = time.perf_counter() - t0
+            dts = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                ref = O.dtw_full(q, r, nthreads=threads)
+                dts.append(time.perf_counter() - t0)
+            dtc = float(np.median(dts))
         out["dtw_parity"] = {"cells": cells, "path_equal": bool(np.array_equal(res["path_q"], ref["path_q"]) and
                                                                np.array_equal(res["path_r"], ref["path_r"])),
                              "path_cost_equal": bool(np.array_equal(res["path_cost"], ref["path_cost"])),
@@ -325,7 +371,8 @@ def bench_dtw(ctx, n, steps, parity=False):
                              "oracle": "dtw_oracle.c stripe wavefront (same cells and order as or_dtw)"}
         out["dtw_cpu_baseline"] = {"value": cells / dtc, "unit": "cells/s", "cores": threads, "kind": "port",
                                    "sample": f"the same {n} x {n} 12-dim DTW, oracle stripe wavefront over "
-                                             f"{threads} threads (the Go reference fills serially), one run"}
+                                             f"{threads} threads (the Go reference fills serially), median of 3",
+                                   "spread_cells_per_s": [cells / max(dts), cells / min(dts)]}
     return out
 
 
@@ -351,14 +398,21 @@ def bench_c5(args, world, rank, dev, ctx):
     run([0])                                   # warm-up: worker contexts, tables, buffers
     run(list(range(min(len(data), args.c5_workers))))
     torch.cuda.synchronize()
-    dts = []
+    ctx.dtw_counters(reset=True)
+    dts, errs, recd = [], [], None
     for _ in range(args.reps):
         barrier(world)
         t0 = time.perf_counter()
-        recd = run(list(range(len(data))))
+        try:                                   # a failed call must not skip this rank's collectives
+            recd = run(list(range(len(data))))
+        except sonar.SonarError as e:
+            errs.append(str(e))
         torch.cuda.synchronize()
         barrier(world)
         dts.append(max_over_ranks(time.perf_counter() - t0, world))
+    counters = ctx.dtw_counters(reset=True)
+    if recd is None:
+        raise RuntimeError(f"every C5 repetition failed: {errs[0]}")
     dt = float(np.median(dts))
     recs = np.stack([recd[f] for f in sonar.PAIR_FIELDS] + [np.array([lag for _, _, lag in data])], axis=1)
     allrec = pairs.gather_records(torch.tensor(recs, dtype=torch.float64, device=dev), world, counts).cpu().numpy()
@@ -371,7 +425,9 @@ def bench_c5(args, world, rank, dev, ctx):
             "c5_frames_per_s": 2 * P * F / dt, "c5_frames_note": "both streams' STFT frames of every pair (BASELINE configs[4])",
             "c5_pairs": P, "c5_seconds_per_stream": args.c5_seconds,
             "c5_max_lag_s": args.c5_max_lag, "c5_workers_per_rank": args.c5_workers, "c5_entry": "sonar_align_pairs",
-            "c5_lag_recovered": float(ok.mean()), "c5_dtw_cells_per_pair": F * F}
+            "c5_lag_recovered": float(ok.mean()), "c5_dtw_cells_per_pair": F * F,
+            "c5_dtw_counters_rank0": counters, "c5_failed_reps": len(errs),
+            **({"c5_error": errs[0]} if errs else {})}
 
 
 def bench_c3(args, ctx, dev):
@@ -747,35 +803,56 @@ def main():
         f0 = sum(counts[:rank])
         assert torch.equal(timeline[f0:f0 + F], out)
 
-    extra = {}
+    # every leg after the headline is wrapped: its exception is recorded as "<leg>_error" in the
+    # line (which is still printed) and the process exits non-zero.  Legs with collectives (C5)
+    # catch their own errors inside, so the ranks' collective sequences stay aligned.
+    extra, errors = {}, {}
+
+    def leg(name, fn):
+        try:
+            r_ = fn()
+            if r_:
+                extra.update(r_)
+        except Exception as e:  # noqa: BLE001 -- recorded in the line, exit status non-zero
+            errors[f"{name}_error"] = f"{type(e).__name__}: {e}"
+            traceback.print_exc(file=sys.stderr)
+
     out64 = None
     if not args.no_f64:
-        extra["headline_f64"], out64 = bench_headline_f64(args, ctx, pcm, F, dev)
-    if args.dtw_len > 0:
-        extra.update(bench_dtw(ctx, args.dtw_len, args.dtw_steps,
-                               parity=rank == 0 and world == 1 and not args.no_cpu_baseline))
-    if args.ingest_reps > 0:
-        extra.update(bench_ingest(args, ctx, pcm, cfg, F))
-    if args.c5_pairs > 0:
-        extra.update(bench_c5(args, world, rank, dev, ctx))
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            extra["c5_cpu_baseline"] = c5_cpu_baseline(args)
-    if args.c3_seconds > 0:
-        extra.update(bench_c3(args, ctx, dev))
-    if args.c4_seconds > 0:
-        extra.update(bench_c4(args, ctx))
-    if args.c6_gallery > 0:
-        extra.update(bench_c6(args, ctx, dev))
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            extra["c6_cpu_baseline"] = c6_cpu_baseline(args)
-    if args.c7_seconds > 0:
-        extra.update(bench_c7(args, ctx))
-
+        def f64_leg():
+            nonlocal out64
+            res, out64 = bench_headline_f64(args, ctx, pcm, F, dev)
+            return {"headline_f64": res}
+        leg("headline_f64", f64_leg)
     cpu, parity = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, parity, parity64 = cpu_baseline(args.cpu_seconds, out.cpu().numpy(), args.seconds, out64)
-        if parity64 is not None:
-            extra["headline_f64"]["parity"] = parity64
+        def cpu_leg():
+            nonlocal cpu, parity
+            cpu, parity, parity64 = cpu_baseline(args.cpu_seconds, out.cpu().numpy(), args.seconds, out64)
+            if parity64 is not None and "headline_f64" in extra:
+                extra["headline_f64"]["parity"] = parity64
+        leg("cpu_baseline", cpu_leg)
+    if args.dtw_len > 0:
+        leg("dtw", lambda: bench_dtw(ctx, args.dtw_len, args.dtw_steps,
+                                     parity=rank == 0 and world == 1 and not args.no_cpu_baseline))
+    if args.ingest_reps > 0:
+        leg("ingest", lambda: bench_ingest(args, ctx, pcm, cfg, F))
+    if args.c5_pairs > 0:
+        leg("c5", lambda: bench_c5(args, world, rank, dev, ctx))
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            leg("c5_cpu_baseline", lambda: {"c5_cpu_baseline": c5_cpu_baseline(args)})
+    if args.c3_seconds > 0:
+        leg("c3", lambda: bench_c3(args, ctx, dev))
+    if args.c4_seconds > 0:
+        leg("c4", lambda: bench_c4(args, ctx))
+    if args.c6_gallery > 0:
+        leg("c6", lambda: bench_c6(args, ctx, dev))
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            leg("c6_cpu_baseline", lambda: {"c6_cpu_baseline": c6_cpu_baseline(args)})
+    if args.c7_seconds > 0:
+        leg("c7", lambda: bench_c7(args, ctx))
+    if "c5_error" in extra:
+        errors["c5_error"] = extra["c5_error"]
 
     achieved_gbs = F * BYTES_PER_FRAME / (kernel_ms * 1e-3) / 1e9
     achieved_tfs = F * FLOPS_PER_FRAME / (kernel_ms * 1e-3) / 1e12
@@ -812,11 +889,14 @@ def main():
         line["allgather_ms"] = gather_ms
         line["allgather_bytes"] = F_total * N_MFCC * 4
     line.update(extra)
+    line.update(errors)
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+    if errors:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -119,6 +119,14 @@ const char* sonar_last_fp_kernel(sonar_ctx* ctx);
  * context: ms3[0] the band sweep (dtw_band_kernel), ms3[1] the backtrack walk,
  * ms3[2] the path decode -- diagnostics and the bench's DTW roofline. */
 int sonar_dtw_last_timing(sonar_ctx* ctx, double* ms3);
+/* Liveness counters of the DTW band pipeline accumulated on this context (and
+ * the worker contexts of sonar_align_pairs) since the last reset: out4[0]
+ * edge-poll refresh fences (an agent-scope acquire issued after 1 ms without
+ * a new value from the band above), out4[1] those after which the next poll
+ * found new values, out4[2] DTWs whose pipeline timed out (the call returned
+ * SONAR_ERR_DEVICE with a diagnostic text in sonar_last_error), out4[3] waves
+ * that timed out.  reset != 0 zeroes them after reading -- diagnostics. */
+int sonar_dtw_counters(sonar_ctx* ctx, int64_t* out4, int32_t reset);
 
 /* ---- sizes (same integer rules as the Go code) ------------------------ */
 /* (n - W)/H + 1, Go truncating division; <= 0 -> SONAR_ERR_TOO_SHORT

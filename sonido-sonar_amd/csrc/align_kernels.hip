@@ -250,7 +250,20 @@ constexpr int DTW_ECH = 8;                          // edge values polled per ch
 #define DTW_G 4                                     // steps per scheduling group in the sweep
 #endif
 constexpr uint64_t DTW_SENT = 0x7FF000017FF00001ull;  // signalling NaN: never an arithmetic result
-constexpr int DTW_SPIN_LIMIT = 1 << 22;
+// Liveness bound of every wait in the band kernel: a wait gives up when it has seen no progress
+// for DTW_STALL_TICKS of s_memrealtime (100 MHz) AND has polled at least DTW_STALL_POLLS times (a
+// wave that was switched out does not time out on wall time alone).  The first wave to give up
+// writes the DTW's diagnostic record (DtwArgs::diag) and raises the block's LDS abort word, which
+// every other wait of the block checks; the edge poller also watches the DTW's global error word,
+// so the bands below a failed one stop within milliseconds instead of each running out its bound.
+#ifndef DTW_STALL_MS
+#define DTW_STALL_MS 1000
+#endif
+constexpr uint64_t DTW_STALL_TICKS = (uint64_t)DTW_STALL_MS * 100000ull;
+constexpr uint32_t DTW_STALL_POLLS = 1u << 18;
+// the edge poller's refresh: after 1 ms without a new edge value it issues one agent-scope acquire
+// (buffer_inv sc1) and counts it in diag[13] (diag[14] when the next poll found new values)
+constexpr uint64_t DTW_REFRESH_TICKS = 100000ull;
 #ifndef DTW_SPIN_SLEEP
 #define DTW_SPIN_SLEEP 4                            // s_sleep between LDS counter polls (A/B 0,1,4,8,16: 4-8 best)
 #endif
@@ -375,6 +388,8 @@ constexpr int DTW_CTR_EFILL = DTW_NDW <= 3 ? 3 : 7;
 constexpr int DTW_CTR_CPROG = DTW_NDW <= 3 ? 4 : 8;
 constexpr int DTW_CTR_PROG = DTW_NDW <= 3 ? 5 : 9;
 constexpr int DTW_CTR_RDY = DTW_NDW <= 3 ? 6 : 10;
+constexpr int DTW_CTR_ABORT = 12;   // set by the first wave of the block that gives up
+constexpr int DTW_CTR_TICKET = 13;  // the block's ticket (diagnostics)
 // Ring row stride in doubles.  A distance wave's lane l reads row t-l, so consecutive lanes sit
 // one stride apart; 12-dim rows padded to 14 doubles (112 B, 28 dwords: 16 distinct 4-dword bank
 // quads in every 16-lane group of ds_read_b128) make those reads conflict-free (96 B is 2-way).
@@ -405,6 +420,81 @@ __device__ __forceinline__ int32_t* dtw_walk_meta(uint32_t* Dn, int64_t nb, int6
 // C[i][j] of band-step (b, s), lane l in the paired layout Cn[b][s/2][l][s%2]
 __device__ __forceinline__ int64_t dtw_cn_off(int64_t b, int64_t S2, int64_t s, int64_t l) {
   return ((b * S2 + (s >> 1)) << 7) + 2 * l + (s & 1);
+}
+
+// A wait of the band kernel gave up (called by the whole wave, uniformly): raise the block's abort
+// word and the DTW's error bit for this role, and, if this is the DTW's first such wave, write its
+// diagnostic record (layout at DtwArgs::diag).  The record re-reads the band above's edge word at
+// the first column this band lacks in four ways -- sc1 load, sc1 load after an agent acquire,
+// system-scope load, atomic fetch_or(0) at agent and system scope -- so a value that never left the
+// producer can be told apart from one the consumer's caches did not show, and scans that edge row
+// for the first column still holding the sentinel (how far the producer got).
+#ifdef DTW_STALL_INLINE   // A/B knob
+__device__ __forceinline__ void dtw_stall(
+#else
+__device__ __attribute__((noinline)) void dtw_stall(
+#endif
+    int32_t* sync, uint64_t* diag, int role, int64_t b, int* ctr,
+                                                     const uint64_t* Ein, int64_t nr, uint32_t polls, uint64_t t0) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t now = __builtin_amdgcn_s_memrealtime();
+  const int prog = __hip_atomic_load(&ctr[DTW_CTR_PROG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int cprog = __hip_atomic_load(&ctr[DTW_CTR_CPROG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int efill = __hip_atomic_load(&ctr[DTW_CTR_EFILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int rdy = __hip_atomic_load(&ctr[DTW_CTR_RDY], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int ticket = __hip_atomic_load(&ctr[DTW_CTR_TICKET], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  uint64_t dch = 0;
+#pragma unroll
+  for (int w = 0; w < 4 && w < DTW_NDW; ++w)
+    dch |= (uint64_t)(uint16_t)__hip_atomic_load(&ctr[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) << (16 * w);
+  int claimed = 0;
+  if (lane == 0) {
+    __hip_atomic_store(&ctr[DTW_CTR_ABORT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    atomicOr(&sync[1], 1 << (role - 1));
+    if (diag) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&diag[15]), 1ull);
+      const uint64_t hdr = (1ull << 63) | ((uint64_t)role << 56) | ((uint64_t)(ticket & 0xFFFFFF) << 32) |
+                           (uint64_t)(uint32_t)b;
+      claimed = atomicCAS(reinterpret_cast<unsigned long long*>(&diag[0]), 0ull, (unsigned long long)hdr) == 0;
+    }
+  }
+  claimed = __builtin_amdgcn_readfirstlane(claimed);
+  if (!claimed) return;
+  const int64_t lo = prog < cprog ? prog : cprog;
+  const int64_t want = lo + DTW_EAHEAD < nr ? lo + DTW_EAHEAD : nr;
+  uint64_t e[5] = {0, 0, 0, 0, 0};
+  int64_t first = -1;
+  if (Ein) {
+    uint64_t* E = const_cast<uint64_t*>(Ein);
+    const int64_t col = efill + 1 <= nr ? efill + 1 : nr;
+    if (lane == 0) e[0] = __hip_atomic_load(E + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (lane == 0) {
+      e[1] = __hip_atomic_load(E + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      e[2] = __hip_atomic_load(E + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      e[3] = __hip_atomic_fetch_or(E + col, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      e[4] = __hip_atomic_fetch_or(E + col, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    for (int64_t c0 = 1; c0 <= nr; c0 += 64) {
+      const int64_t j = c0 + lane;
+      const uint64_t v = j <= nr ? __hip_atomic_load(E + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(j <= nr && v == DTW_SENT);
+      if (m) { first = c0 + (int64_t)__builtin_ctzll(m); break; }
+    }
+  }
+  if (lane == 0) {
+    uint64_t* d = diag;
+    d[1] = (uint32_t)prog | ((uint64_t)(uint32_t)cprog << 32);
+    d[2] = (uint32_t)efill | ((uint64_t)(uint32_t)rdy << 32);
+    d[3] = dch;
+    d[4] = (uint32_t)want | ((uint64_t)(uint32_t)nr << 32);
+    for (int k = 0; k < 5; ++k) d[5 + k] = e[k];
+    d[10] = (uint64_t)first;
+    d[11] = ((now - t0) & 0xFFFFFFFFFFull) | ((uint64_t)(polls >> 10) << 40);
+    const uint64_t hw = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    const uint64_t xcc = (uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20); // HW_REG_XCC_ID
+    d[12] = (xcc & 0xFF) | (hw << 32);
+  }
 }
 
 // PRE: the local distances come precomputed from dtw_dist_kernel (a.Dd), so the block is only
@@ -444,8 +534,10 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const double inf = __builtin_inf();
   if (threadIdx.x == 0) {
+    for (int k = 0; k < 16; ++k) ctr[k] = 0;
     if constexpr (BATCH) {
       const int64_t t = atomicAdd(bt.ticket, 1);
+      ctr[DTW_CTR_TICKET] = (int)t;
       if (bt.map) {
         if (t < bt.start[bt.n]) {
           const int2 pb = bt.map[t];
@@ -466,8 +558,8 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
       }
     } else {
       shb = atomicAdd(&a_in.sync[0], 1);
+      ctr[DTW_CTR_TICKET] = (int)shb;
     }
-    for (int k = 0; k < 16; ++k) ctr[k] = 0;
     rdy = -1;
   }
   if (threadIdx.x < 64) {        // steps -1 and -2: C[i][j] for j <= 0 is +Inf (column 0) / unset
@@ -491,17 +583,28 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   const bool row_ok = i <= nq;
   const int64_t qrow = row_ok ? i - 1 : 0;
   uint64_t spins_total = 0;
-  // spin (LDS only) until `cond` holds; bounded, flags the error word instead of hanging
-#define SONAR_SPIN_UNTIL(cond)                                                        \
+  // spin (LDS only) until `cond` holds.  Bounded (DTW_STALL_TICKS and DTW_STALL_POLLS without
+  // `cond`): the wave then reports through dtw_stall and the whole block returns; it also returns
+  // as soon as another wave of the block has given up (the LDS abort word, checked every 64 polls)
+#define SONAR_SPIN_UNTIL(role, cond)                                                  \
   do {                                                                                \
-    uint64_t sp_ = 0;                                                                 \
     if (!(cond)) {                                                                    \
-      const uint64_t w0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;            \
+      const uint64_t tr0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;           \
+      uint64_t w0_ = 0;                                                               \
+      uint32_t sp_ = 0;                                                               \
       while (!(cond)) {                                                               \
         __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);                                     \
-        if (++sp_ > (uint64_t)DTW_SPIN_LIMIT * 4) { if (lane == 0) atomicOr(&a.sync[1], 2); break; } \
+        if ((++sp_ & 63) == 0) {                                                      \
+          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) return;                               \
+          const uint64_t now_ = __builtin_amdgcn_s_memrealtime();                     \
+          if (sp_ == 64) w0_ = now_;                                                  \
+          else if (sp_ >= DTW_STALL_POLLS && now_ - w0_ > DTW_STALL_TICKS) {          \
+            dtw_stall(a.sync, a.diag, (role), b, ctr, Ein, nr, sp_, w0_);            \
+            return;                                                                   \
+          }                                                                           \
+        }                                                                             \
       }                                                                               \
-      if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - w0_;             \
+      if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - tr0_;            \
     }                                                                                 \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
   } while (0)
@@ -511,7 +614,11 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     // two waves, so the edge poll's global-load latency never delays a ring refill
     const bool do_ring = !PRE && wave == FEEDER_WAVE;
     int64_t nextblk = 0, have = 0;
-    uint64_t idle = 0;
+    // polls without work since the last one that found work, the realtime of the 64th of them,
+    // and the edge poller's refresh state
+    uint32_t idle = 0;
+    uint64_t t_idle = 0, t_fence = 0;
+    bool fenced = false;
     const int64_t ecols = Ein ? nr : 0;
     // block nextblk's rows are loaded into registers as soon as the previous block is written
     // (lanes < RBLK, one row each), so the global-load latency is off the distance waves' path
@@ -524,7 +631,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     if constexpr (D > 0 && !PRE) prefetch(0);
     while (true) {
       const int64_t p = SONAR_LDS_LD(prog), cp = SONAR_LDS_LD(cprog);
-      bool work = false;
+      bool work = false, wait_edge = false;
       if (D > 0 && !PRE && do_ring) {
         // block m overwrites rows up to r = RBLK*m - RROWS + RBLK - 1, which distance chunks up to
         // index (r + 63) / ECH read (chunk t0 reads rows t0-63 .. t0+7): all of them are done once
@@ -564,6 +671,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         const int64_t lo = p < cp ? p : cp;
         const int64_t want = lo + DTW_EAHEAD < ecols ? lo + DTW_EAHEAD : ecols;
         if (have < want) {
+          wait_edge = true;
           const int64_t jj = have + 1 + lane;
           uint64_t v = INF_BITS;
           if (jj <= want) v = __hip_atomic_load(Ein + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -583,11 +691,35 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         }
       }
       if (do_ring ? (D == 0 || nextblk >= nblk) : have >= ecols) break;
-      if (!work) {
+      if (work) {
+        if (fenced) {
+          fenced = false;
+          if (lane == 0 && a.diag) atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[14]), 1ull);
+        }
+        idle = 0;
+      } else {
         __builtin_amdgcn_s_sleep(1);
-        if (++idle > (uint64_t)DTW_SPIN_LIMIT * 4) {   // producer band never arrived: flag, release the rest
-          if (lane == 0) { atomicOr(&a.sync[1], 1); SONAR_LDS_ST(efill, (int)ecols); SONAR_LDS_ST(rdy, (int)nblk); }
-          break;
+        if ((++idle & 63) == 0) {
+          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) return;
+          const uint64_t now = __builtin_amdgcn_s_memrealtime();
+          if (idle == 64) t_idle = now;
+          if (wait_edge) {
+            // another band of this DTW gave up: its edge (and so this band's) will never come
+            if (__hip_atomic_load(&a.sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+              if (lane == 0) SONAR_LDS_ST(ctr[DTW_CTR_ABORT], 1);
+              return;
+            }
+            if (now - t_idle > DTW_REFRESH_TICKS && now - t_fence > DTW_REFRESH_TICKS) {
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+              t_fence = now;
+              fenced = true;
+              if (lane == 0 && a.diag) atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[13]), 1ull);
+            }
+          }
+          if (idle >= DTW_STALL_POLLS && now - t_idle > DTW_STALL_TICKS) {
+            dtw_stall(a.sync, a.diag, do_ring ? DTW_ROLE_FEEDER : DTW_ROLE_EDGE, b, ctr, Ein, nr, idle, t_idle);
+            return;
+          }
         }
       }
     }
@@ -604,7 +736,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     double ckv = 0.0;                                  // the lane's C at the latest multiple-of-64 column
     for (int64_t s0 = 0; s0 < S; s0 += DTW_ECH) {
       const int need = (int)(s0 + DTW_ECH < S ? s0 + DTW_ECH : S);
-      SONAR_SPIN_UNTIL(SONAR_LDS_LD(prog) >= need);
+      SONAR_SPIN_UNTIL(DTW_ROLE_CODE, SONAR_LDS_LD(prog) >= need);
       // steps s0-2 .. s0+7 as 5 pairs (the last value unused); lane 0's neighbour pairs are the
       // edge columns (t+2, t+3) at eqb slots (t+2, t+3) (per-lane addresses, no divergence)
       double cv[DTW_ECH + 2], nv[DTW_ECH + 2];
@@ -719,7 +851,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         const int64_t c = c0 + k;
         if (c < nch) {
           const int64_t t0 = DTW_ECH * c;
-          SONAR_SPIN_UNTIL(SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW_DQ);
+          SONAR_SPIN_UNTIL(DTW_ROLE_LOADER, SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW_DQ);
           double* drow = &dring[lane][t0 & (DTW_DQ - 1)];
 #pragma unroll
           for (int u = 0; u < DTW_ECH; u += 2)
@@ -741,12 +873,12 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     for (int64_t c = w; DTW_ECH * c < S; c += DTW_NDW) {
       const int64_t t0 = DTW_ECH * c;
       // ring slots of steps t0..t0+7 were last read by the sweep for steps t0-DQ..t0-DQ+7
-      SONAR_SPIN_UNTIL(SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW_DQ);
+      SONAR_SPIN_UNTIL(DTW_ROLE_DIST, SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW_DQ);
       double dv[DTW_ECH];
       if constexpr (D > 0) {
         const int64_t need = (t0 + DTW_ECH - 1) / DTW_RBLK;             // rows up to t0+7
         const int64_t needc = need < nblk - 1 ? need : nblk - 1;
-        SONAR_SPIN_UNTIL(SONAR_LDS_LD(rdy) >= needc);
+        SONAR_SPIN_UNTIL(DTW_ROLE_DIST, SONAR_LDS_LD(rdy) >= needc);
 #ifdef DTW_DBG_NODIST   // A/B diagnostics: the distance waves only signal
 #pragma unroll
         for (int u = 0; u < DTW_ECH; ++u) dv[u] = 0.0;
@@ -869,14 +1001,22 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     return k;
   };
   // raw loads only: the border selects come after the steps, so the loads' latency overlaps the
-  // chunk instead of stalling its start
+  // chunk instead of stalling its start.  Volatile like the counter loads: the compiler keeps them
+  // behind the counter read that covers them (LDS returns one wave's requests in order), with no
+  // wait between the two
+  typedef double d2v __attribute__((ext_vector_type(2)));
+#ifdef DTW_NOVOL   // A/B knob: plain loads
+  typedef __attribute__((address_space(3))) d2v lds_d2;
+#else
+  typedef __attribute__((address_space(3))) volatile d2v lds_d2;
+#endif
   auto load_chunk = [&](int64_t s0, double (&dc)[DTW_ECH], double (&ech)[DTW_ECH]) {
     const double* dr = &dring[lane][s0 & (DTW_DQ - 1)];
     const double* er = &eqa[s0 & (DTW_EQ - 1)];        // columns s0+1 .. s0+8
 #pragma unroll
     for (int u = 0; u < DTW_ECH; u += 2) {
-      const double2 d2 = *reinterpret_cast<const double2*>(dr + u);
-      const double2 e2 = *reinterpret_cast<const double2*>(er + u);
+      const d2v d2 = *(lds_d2*)(dr + u);
+      const d2v e2 = *(lds_d2*)(er + u);
       dc[u] = d2.x; dc[u + 1] = d2.y;
       ech[u] = e2.x; ech[u + 1] = e2.y;
     }
@@ -924,7 +1064,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   double dc[DTW_ECH], ech[DTW_ECH];
   Ctrs kc = load_ctr();
   if (!ready(0, kc)) {
-    SONAR_SPIN_UNTIL((kc = load_ctr(), ready(0, kc)));
+    SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready(0, kc)));
   }
   if (a.trace) t_first = __builtin_amdgcn_s_memrealtime();
   load_chunk(0, dc, ech);
@@ -973,7 +1113,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
       if (!ready((int)s1, kc))
 #endif
       {
-        SONAR_SPIN_UNTIL((kc = load_ctr(), ready((int)s1, kc)));
+        SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready((int)s1, kc)));
         load_chunk(s1, dcn, echn);
       }
     }
@@ -1682,11 +1822,15 @@ void launch_dtw_dist(const double* q, const double* r, const DtwGeom& g, double*
 int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, const DtwGeom& g, double* Cn,
                uint32_t* Dn, uint64_t* E, int32_t* sync_words, uint32_t* codes, int64_t* plen, uint64_t* trace,
                hipStream_t s, hipEvent_t mid, double* Dd, double* CK) {
+  // sync_words: [0] ticket, [1] error bits, [2] non-finite flag (set by the caller's probe), [3]
+  // unused, then the DTW_DIAG_WORDS-word diagnostic record at byte 16 (DTW_SYNC_BYTES in all)
   if (hipMemsetAsync(sync_words, 0, 2 * sizeof(int32_t), s) != hipSuccess) return -5;
+  if (hipMemsetAsync(sync_words + 4, 0, DTW_DIAG_WORDS * 8, s) != hipSuccess) return -5;
   if (g.nb > 1 && hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, dtw_edge_bytes(g) / 4, s) != hipSuccess) return -5;
   DtwArgs a{q, r, dim, band, g.nq, g.nr, g.nb, g.S, g.SW, Cn, Dn, reinterpret_cast<uint64_t*>(E), sync_words,
             trace};
   a.CK = CK;
+  a.diag = reinterpret_cast<uint64_t*>(sync_words + 4);
   if (!Cn && !CK) return -1;
   const DtwBatch nob{};
   const bool pre = Dd && dim == 12;

@@ -64,6 +64,9 @@ struct sonar_ctx {
   // events that order it: features done -> side, NCC done -> stream
   hipStream_t side = nullptr;
   hipEvent_t side_ev[2] = {nullptr, nullptr};
+  // band-kernel liveness counters (sonar_dtw_counters): edge refresh fences, those followed by new
+  // edge values, DTWs that timed out, waves that timed out
+  long long dtw_ctr[4] = {0, 0, 0, 0};
 };
 
 struct sonar_result {
@@ -107,6 +110,9 @@ void ncc_metrics_host(const double* corr, int64_t L, int64_t na, int64_t nb, dou
 // the path-tile pass's arguments (launch_dtw_path_tiles) of one DTW in checkpoint mode
 sonar::DtwArgs tile_args(const double* q, const double* r, int dim, int band, const sonar::DtwGeom& g, uint64_t* E,
                          double* CK, int32_t* runs, int32_t* pq, int32_t* pr, double* pc, int64_t* plen, double* cnm);
+// the band kernel's status block of one DTW (int32 sync[4] + the DtwArgs::diag record): adds its
+// counters to c->dtw_ctr and, when the DTW timed out, returns the failure text with the record
+std::string dtw_status(sonar_ctx* c, const void* sync_block);
 int dtw_enqueue(sonar_ctx* c, const double* dq, int64_t nq, const double* dr, int64_t nr, int32_t dim, int32_t band,
                 DtwPending* p);
 int dtw_finish(sonar_ctx* c, DtwPending* p, const int32_t** hq, const int32_t** hr, const double** hc, int64_t* P,

@@ -179,7 +179,27 @@ struct DtwArgs {
   // [0] the tile count, then each tile's first path index (dtw_run_words ints)
   double* CK;
   int32_t* runs;
+  // nullable: the DTW's 16-word diagnostic record (zeroed before the launch).  The first band-kernel
+  // wave of this DTW whose wait makes no progress for DTW_STALL_TICKS writes it:
+  //  [0]  bit 63 valid, bits 56-62 role (DtwRole), bits 32-55 block ticket, bits 0-31 band
+  //  [1]  prog | cprog << 32        [2] efill | rdy << 32        [3] dchunk[0..3], 16 bits each
+  //  [4]  edge target column (min(prog, cprog) + 64, <= nr) | nr << 32
+  //  [5]  E[efill+1] of the band above by an agent-scope (sc1) load, [6] the same after an
+  //       agent-scope acquire (buffer_inv sc1), [7] by a system-scope load, [8] by an agent-scope
+  //       atomic fetch_or(0), [9] by a system-scope fetch_or(0)
+  //  [10] the first column of that E row still holding the sentinel (sc1 scan; -1: none)
+  //  [11] s_memrealtime ticks (10 ns) of the failed wait (low 40 bits) | polls / 1024 << 40
+  //  [12] XCC id | HW_ID << 32 of the reporting wave
+  //  [13] edge-poll refresh fences issued by any band of this DTW (an agent acquire after 1 ms
+  //       without a new edge value), [14] those after which the next poll found new values,
+  //  [15] waves of this DTW that timed out
+  uint64_t* diag;
 };
+constexpr int DTW_DIAG_WORDS = 16;
+// bytes of a single DTW's sync block (launch_dtw): 4 status words + the diagnostic record
+constexpr int DTW_SYNC_BYTES = 16 + 8 * DTW_DIAG_WORDS;
+enum DtwRole : int { DTW_ROLE_EDGE = 1, DTW_ROLE_FEEDER = 2, DTW_ROLE_SWEEP = 3, DTW_ROLE_CODE = 4,
+                     DTW_ROLE_DIST = 5, DTW_ROLE_LOADER = 6 };
 // checkpoint columns C[64b+1 .. 64b+64][64c] (c = 1 .. nr/64) of every band, and the run words of
 // the path-tile pass
 size_t dtw_ck_bytes(const DtwGeom& g);

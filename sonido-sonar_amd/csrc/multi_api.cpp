@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -129,7 +130,7 @@ size_t pair_bytes(const PairGeo& p) {
 // align_one (exact math.Min rules); their indices are appended to `redo`.
 int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* const* q_pcm, const double* const* r_pcm,
                 int32_t sr, int32_t sw, int32_t hop, int32_t fw, int32_t device_ptrs, sonar_pair_record* out,
-                std::vector<int64_t>* redo) {
+                std::vector<int64_t>* redo, std::vector<std::pair<int64_t, std::string>>* errs) {
   const int n = (int)in.size();
   if (n == 0) return SONAR_OK;
   HIP_TRY(w, hipSetDevice(w->device));
@@ -154,8 +155,12 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     max_cap = std::max(max_cap, p.cap);
     total_bands += p.g.nb;
   }
-  const size_t stat_b = al256((size_t)n * 32 + 16), args_b = al256((size_t)n * sizeof(sonar::DtwArgs)),
-               start_b = al256((size_t)(n + 1) * 8), map_b = al256((size_t)total_bands * 8);
+  // small (device) and the head of h (pinned host) share one layout: per-pair status words + the
+  // batch ticket, the per-pair band-kernel diagnostic records, then the DTW arguments, ticket
+  // starts and the band-major ticket map
+  const size_t stat_b = al256((size_t)n * 32 + 16), diag_b = al256((size_t)n * 8 * sonar::DTW_DIAG_WORDS),
+               args_b = al256((size_t)n * sizeof(sonar::DtwArgs)), start_b = al256((size_t)(n + 1) * 8),
+               map_b = al256((size_t)total_bands * 8);
   char* chroma = (char*)dbuf(w, "pb.chroma", chroma_b);
   char* CK = (char*)dbuf(w, "pb.CK", ck_b);
   char* runs = (char*)dbuf(w, "pb.runs", runs_b);
@@ -166,7 +171,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* wst = (char*)dbuf(w, "pb.wstart", wst_b);
   char* path = (char*)dbuf(w, "pb.path", path_b);
   char* corr = (char*)dbuf(w, "pb.corr", corr_b);
-  char* small = (char*)dbuf(w, "pb.small", stat_b + args_b + start_b + map_b);
+  char* small = (char*)dbuf(w, "pb.small", stat_b + diag_b + args_b + start_b + map_b);
   double* eq = (double*)dbuf(w, "pb.eq", (size_t)maxE * 8);
   double* er = (double*)dbuf(w, "pb.er", (size_t)maxE * 8);
   double* xa = (double*)dbuf(w, "ncc.xa", (size_t)maxE * 8);
@@ -174,22 +179,25 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   double* st = (double*)dbuf(w, "ncc.stats", 64);
   double* up_q = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.q", (size_t)maxn * 8);
   double* up_r = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.r", (size_t)maxn * 8);
-  char* h = (char*)sonar::detail::hbuf(w, "pb.host", stat_b + args_b + start_b + map_b + corr_b + path_b);
+  char* h = (char*)sonar::detail::hbuf(w, "pb.host", stat_b + diag_b + args_b + start_b + map_b + corr_b + path_b);
   if (!chroma || !CK || !runs || (pre && !Dd) || !Dn || !E || !codes || !wst || !path || !corr || !small || !eq || !er || !xa || !xb || !st ||
       (!device_ptrs && (!up_q || !up_r)) || !h)
     return fail(w, SONAR_ERR_NOMEM, "allocation failed (pair batch)");
   int32_t* dstat = (int32_t*)small;                 // per pair: [0..1] plen, [2..3] C[nq][nr], [4..7] sync
   int32_t* ticket = (int32_t*)(small + (size_t)n * 32);
-  sonar::DtwArgs* dargs = (sonar::DtwArgs*)(small + stat_b);
-  int64_t* dstart = (int64_t*)(small + stat_b + args_b);
+  uint64_t* ddiag = (uint64_t*)(small + stat_b);
+  const size_t ab = stat_b + diag_b;                 // where the arguments start
+  sonar::DtwArgs* dargs = (sonar::DtwArgs*)(small + ab);
+  int64_t* dstart = (int64_t*)(small + ab + args_b);
   char* hstat = h;
-  sonar::DtwArgs* hargs = (sonar::DtwArgs*)(h + stat_b);
-  int64_t* hstart = (int64_t*)(h + stat_b + args_b);
-  int2* hmap = (int2*)(h + stat_b + args_b + start_b);
-  int2* dmap = (int2*)(small + stat_b + args_b + start_b);
-  char* hcorr = h + stat_b + args_b + start_b + map_b;
+  const uint64_t* hdiag = (const uint64_t*)(h + stat_b);
+  sonar::DtwArgs* hargs = (sonar::DtwArgs*)(h + ab);
+  int64_t* hstart = (int64_t*)(h + ab + args_b);
+  int2* hmap = (int2*)(h + ab + args_b + start_b);
+  int2* dmap = (int2*)(small + ab + args_b + start_b);
+  char* hcorr = h + ab + args_b + start_b + map_b;
   char* hpath = hcorr + corr_b;
-  HIP_TRY(w, hipMemsetAsync(small, 0, stat_b, s));
+  HIP_TRY(w, hipMemsetAsync(small, 0, stat_b + diag_b, s));
   HIP_TRY(w, hipMemsetAsync(runs, 0, runs_b, s));
   if (e_b) HIP_TRY(w, hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, e_b / 4, s));
   int64_t acc = 0;
@@ -218,6 +226,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     a.pc = (double*)(path + p.path); a.pq = (int32_t*)(a.pc + p.cap); a.pr = a.pq + p.cap;
     a.cnm = (double*)(dstat + 8 * i + 2);
     a.Dd = pre ? (double*)(Dd + p.cn) : nullptr;
+    a.diag = ddiag + (size_t)i * sonar::DTW_DIAG_WORDS;
     hstart[i] = acc;
     acc += p.g.nb;
   }
@@ -242,7 +251,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s,
                               band_major ? dmap : nullptr) != 0)
     return fail(w, SONAR_ERR_DEVICE, "dtw batch launch failed");
-  HIP_TRY(w, hipMemcpyAsync(hstat, small, (size_t)n * 32, hipMemcpyDeviceToHost, s));
+  HIP_TRY(w, hipMemcpyAsync(hstat, small, stat_b + diag_b, hipMemcpyDeviceToHost, s));
   if (corr_b) HIP_TRY(w, hipMemcpyAsync(hcorr, corr, corr_b, hipMemcpyDeviceToHost, s));
   HIP_TRY(w, hipMemcpyAsync(hpath, path, path_b, hipMemcpyDeviceToHost, s));
   HIP_TRY(w, hipStreamSynchronize(s));
@@ -257,10 +266,29 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     std::memcpy(sync, ps + 16, 16);
     sonar_pair_record* rec = &out[p.k];
     if (sync[2]) { redo->push_back(p.k); continue; }
-    if (sync[1]) {
+    alignas(8) char sblk[sonar::DTW_SYNC_BYTES];
+    std::memcpy(sblk, sync, 16);
+    std::memcpy(sblk + 16, hdiag + (size_t)i * sonar::DTW_DIAG_WORDS, 8 * sonar::DTW_DIAG_WORDS);
+    const std::string why = sonar::detail::dtw_status(w, sblk);
+    if (!why.empty()) {
       std::memset(rec, 0, sizeof(*rec));
-      rec->status = fail(w, SONAR_ERR_DEVICE, "dtw band pipeline timed out");
+      rec->status = fail(w, SONAR_ERR_DEVICE, why);
+      errs->emplace_back(p.k, why);
       continue;
+    }
+    if (const char* dump = std::getenv("SONAR_PAIR_DUMP")) {
+      // tests only: the batched DTW's raw outputs of pair k (path length, C[nq][nr], path costs,
+      // query and reference indices) into <dump>/pair_<k>.bin, to be checked against the oracle
+      const double* pc = (const double*)(hpath + p.path);
+      const std::string fn = std::string(dump) + "/pair_" + std::to_string(p.k) + ".bin";
+      if (FILE* f = std::fopen(fn.c_str(), "wb")) {
+        std::fwrite(&P, 8, 1, f);
+        std::fwrite(&cnm, 8, 1, f);
+        std::fwrite(pc, 8, (size_t)P, f);
+        std::fwrite(pc + p.cap, 4, (size_t)P, f);
+        std::fwrite((const int32_t*)(pc + p.cap) + p.cap, 4, (size_t)P, f);
+        std::fclose(f);
+      }
     }
     sonar::detail::AlignIn ai;
     ai.q_pcm_len = p.nq; ai.r_pcm_len = p.nr; ai.sample_rate = sr; ai.hop = hop;
@@ -366,12 +394,13 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
   }
   std::atomic<size_t> next{0};
   std::vector<std::vector<int64_t>> redo(nstreams);
+  std::vector<std::vector<std::pair<int64_t, std::string>>> errs(nstreams);
   for (int t = 0; t < nstreams; ++t) {
     th.emplace_back([&, t] {
       sonar_ctx* w = ws[t];
       for (size_t bi = next.fetch_add(1); bi < batches.size(); bi = next.fetch_add(1)) {
         const int r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window,
-                                  device_ptrs, out, &redo[t]);
+                                  device_ptrs, out, &redo[t], &errs[t]);
         if (r != SONAR_OK)
           for (const auto& p : batches[bi]) { out[p.k].status = r; note(r, p.k, w); }
       }
@@ -381,11 +410,17 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
     });
   }
   for (auto& x : th) x.join();
-  for (int64_t k = 0; k < npairs && first_err.load() == SONAR_OK; ++k)   // per-pair device flags
-    if (out[k].status != SONAR_OK) {
-      first_err = out[k].status;
-      c->err = std::string("pair ") + std::to_string(k) + ": dtw band pipeline timed out";
-    }
+  for (sonar_ctx* w : ws)                            // band-kernel liveness counters to the caller's ctx
+    for (int k = 0; k < 4; ++k) { c->dtw_ctr[k] += w->dtw_ctr[k]; w->dtw_ctr[k] = 0; }
+  // per-pair device failures (the band pipeline's diagnostic text), lowest pair first
+  std::vector<std::pair<int64_t, std::string>> all;
+  for (auto& e : errs) all.insert(all.end(), e.begin(), e.end());
+  if (!all.empty() && first_err.load() == SONAR_OK) {
+    std::sort(all.begin(), all.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    first_err = out[all[0].first].status;
+    c->err = "pair " + std::to_string(all[0].first) + ": " + all[0].second;
+    if (all.size() > 1) c->err += " (" + std::to_string(all.size() - 1) + " more pairs failed)";
+  }
   return first_err.load();
 }
 

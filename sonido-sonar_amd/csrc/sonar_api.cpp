@@ -284,6 +284,21 @@ int sonar_enable_kernel_timing(sonar_ctx* c, int on) {
 
 const char* sonar_last_fp_kernel(sonar_ctx* c) { return c ? c->last_fp_kernel : ""; }
 
+int sonar_dtw_counters(sonar_ctx* c, int64_t* out4, int32_t reset) {
+  if (!c || !out4) return SONAR_ERR_INVALID;
+  for (int k = 0; k < 4; ++k) {
+    long long v = c->dtw_ctr[k];
+    for (sonar_ctx* w : c->workers) v += w->dtw_ctr[k];
+    out4[k] = v;
+  }
+  if (reset) {
+    for (int k = 0; k < 4; ++k) c->dtw_ctr[k] = 0;
+    for (sonar_ctx* w : c->workers)
+      for (int k = 0; k < 4; ++k) w->dtw_ctr[k] = 0;
+  }
+  return SONAR_OK;
+}
+
 int sonar_dtw_last_timing(sonar_ctx* c, double* ms3) {
   if (!c || !ms3) return SONAR_ERR_INVALID;
   for (int k = 0; k < 3; ++k) ms3[k] = c->dtw_ms[k];
@@ -784,7 +799,7 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
   double* cnm_d = (double*)dbuf(c, "dtw.cnm", 8);
   uint32_t* Dn = (uint32_t*)dbuf(c, "dtw.Dn", sonar::dtw_dn_bytes(g));
   uint64_t* E = (uint64_t*)dbuf(c, "dtw.E", sonar::dtw_edge_bytes(g));
-  int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", 16);
+  int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", sonar::DTW_SYNC_BYTES);
   const int64_t cap = nq + nr + 1;
   uint32_t* codes = (uint32_t*)dbuf(c, "dtw.codes", ((cap + 1023) / 1024) * 64 * 4);
   int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
@@ -824,11 +839,14 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
     if (FILE* f = std::fopen(trace_path, "wb")) { std::fwrite(t.data(), 8, t.size(), f); std::fclose(f); }
   }
   int64_t P = 0;
-  int32_t flags[2] = {0, 0};
+  alignas(8) char sblk[sonar::DTW_SYNC_BYTES];
   HIP_TRY(c, hipMemcpyAsync(&P, pl, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(c, hipMemcpyAsync(flags, sync, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(sblk, sync, sizeof(sblk), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
-  if (flags[1]) return fail(c, SONAR_ERR_DEVICE, "dtw band pipeline timed out");
+  {
+    const std::string why = sonar::detail::dtw_status(c, sblk);
+    if (!why.empty()) return fail(c, SONAR_ERR_DEVICE, why);
+  }
   int32_t* oq = path_q; int32_t* orr = path_r; double* oc = path_cost;
   if (!device_ptrs) {
     oq = (int32_t*)dbuf(c, "dtw.pq", cap * 4);
@@ -874,6 +892,44 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
 // ============================================= deferred-sync pair pieces ====
 namespace sonar {
 namespace detail {
+
+std::string dtw_status(sonar_ctx* c, const void* sync_block) {
+  int32_t sync[4];
+  uint64_t d[sonar::DTW_DIAG_WORDS];
+  std::memcpy(sync, sync_block, 16);
+  std::memcpy(d, static_cast<const char*>(sync_block) + 16, sizeof(d));
+  c->dtw_ctr[0] += (long long)d[13];
+  c->dtw_ctr[1] += (long long)d[14];
+  c->dtw_ctr[3] += (long long)d[15];
+  if (!sync[1]) return std::string();
+  c->dtw_ctr[2] += 1;
+  static const char* roles[] = {"?", "edge", "feeder", "sweep", "code", "distance", "loader"};
+  std::string roles_hit;
+  for (int k = 0; k < 6; ++k)
+    if (sync[1] & (1 << k)) roles_hit += std::string(roles_hit.empty() ? "" : "+") + roles[k + 1];
+  char buf[768];
+  if (!(d[0] >> 63)) {
+    std::snprintf(buf, sizeof(buf), "dtw band pipeline timed out (roles %s; no diagnostic record)", roles_hit.c_str());
+    return buf;
+  }
+  const int role = (int)((d[0] >> 56) & 0x7F);
+  const uint64_t ticks = d[11] & 0xFFFFFFFFFFull;
+  std::snprintf(buf, sizeof(buf),
+                "dtw band pipeline timed out (roles %s): first %s wave, band %u ticket %u, no progress for %.3f s "
+                "(%llu k polls); prog %u cprog %u efill %u rdy %d dchunk %u/%u/%u/%u edge target %u of %u; "
+                "E[efill+1] sc1 %016llx after-acquire %016llx system %016llx rmw-agent %016llx rmw-system %016llx; "
+                "first sentinel column %lld; xcc %u hw_id %08x; waves timed out %llu; refresh fences %llu (%llu hit)",
+                roles_hit.c_str(), roles[role >= 1 && role <= 6 ? role : 0], (unsigned)(d[0] & 0xFFFFFFFF),
+                (unsigned)((d[0] >> 32) & 0xFFFFFF), ticks * 1e-8, (unsigned long long)(d[11] >> 40),
+                (unsigned)(d[1] & 0xFFFFFFFF), (unsigned)(d[1] >> 32), (unsigned)(d[2] & 0xFFFFFFFF),
+                (int)(int32_t)(d[2] >> 32), (unsigned)(d[3] & 0xFFFF), (unsigned)((d[3] >> 16) & 0xFFFF),
+                (unsigned)((d[3] >> 32) & 0xFFFF), (unsigned)((d[3] >> 48) & 0xFFFF), (unsigned)(d[4] & 0xFFFFFFFF),
+                (unsigned)(d[4] >> 32), (unsigned long long)d[5], (unsigned long long)d[6], (unsigned long long)d[7],
+                (unsigned long long)d[8], (unsigned long long)d[9], (long long)(int64_t)d[10], (unsigned)(d[12] & 0xFF),
+                (unsigned)(d[12] >> 32), (unsigned long long)d[15], (unsigned long long)d[13],
+                (unsigned long long)d[14]);
+  return buf;
+}
 
 sonar::DtwArgs tile_args(const double* q, const double* r, int dim, int band, const sonar::DtwGeom& g, uint64_t* E,
                          double* CK, int32_t* runs, int32_t* pq, int32_t* pr, double* pc, int64_t* plen, double* cnm) {
@@ -925,11 +981,11 @@ int dtw_enqueue(sonar_ctx* c, const double* dq, int64_t nq, const double* dr, in
   double* CK = (double*)dbuf(c, "dtw.CK", sonar::dtw_ck_bytes(g));
   uint32_t* Dn = (uint32_t*)dbuf(c, "dtw.Dn", sonar::dtw_dn_bytes(g));
   uint64_t* E = (uint64_t*)dbuf(c, "dtw.E", sonar::dtw_edge_bytes(g));
-  int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", 16);
+  int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", sonar::DTW_SYNC_BYTES);
   const int64_t cap = nq + nr + 1;
   uint32_t* codes = (uint32_t*)dbuf(c, "dtw.codes", ((cap + 1023) / 1024) * 64 * 4);
   int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
-  int64_t* st = (int64_t*)hbuf(c, "dtw.status", 32);
+  int64_t* st = (int64_t*)hbuf(c, "dtw.status", 8 + sonar::DTW_SYNC_BYTES);
   if (!CK || !Dn || !E || !sync || !codes || !pl || !st) return fail(c, SONAR_ERR_NOMEM, "allocation failed (dtw)");
   HIP_TRY(c, hipMemsetAsync(sync + 2, 0, 4, s));
   if (sonar::launch_nonfinite(dq, nq * dim, sync + 2, s) || sonar::launch_nonfinite(dr, nr * dim, sync + 2, s))
@@ -939,7 +995,7 @@ int dtw_enqueue(sonar_ctx* c, const double* dq, int64_t nq, const double* dr, in
   if (sonar::launch_dtw(dq, dr, dim, band, true, g, nullptr, Dn, E, sync, codes, pl, nullptr, s, nullptr, Dd, CK) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
   HIP_TRY(c, hipMemcpyAsync(st, pl, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(c, hipMemcpyAsync(st + 1, sync, 12, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(st + 1, sync, sonar::DTW_SYNC_BYTES, hipMemcpyDeviceToHost, s));
   *p = DtwPending{dq, dr, nq, nr, dim, band, st};
   return SONAR_OK;
 }
@@ -953,7 +1009,7 @@ int dtw_finish(sonar_ctx* c, DtwPending* p, const int32_t** hq, const int32_t** 
   double* CK = (double*)dbuf(c, "dtw.CK", sonar::dtw_ck_bytes(g));
   uint32_t* Dn = (uint32_t*)dbuf(c, "dtw.Dn", sonar::dtw_dn_bytes(g));
   uint64_t* E = (uint64_t*)dbuf(c, "dtw.E", sonar::dtw_edge_bytes(g));
-  int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", 16);
+  int32_t* sync = (int32_t*)dbuf(c, "dtw.sync", sonar::DTW_SYNC_BYTES);
   uint32_t* codes = (uint32_t*)dbuf(c, "dtw.codes", ((cap + 1023) / 1024) * 64 * 4);
   int64_t* pl = (int64_t*)dbuf(c, "dtw.plen", 16);
   int32_t* runs = (int32_t*)dbuf(c, "dtw.runs", (size_t)sonar::dtw_run_words(g) * 4);
@@ -967,11 +1023,14 @@ int dtw_finish(sonar_ctx* c, DtwPending* p, const int32_t** hq, const int32_t** 
                           Dd, CK))
       return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
     HIP_TRY(c, hipMemcpyAsync(p->st, pl, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipMemcpyAsync(p->st + 1, sync, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(p->st + 1, sync, sonar::DTW_SYNC_BYTES, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     std::memcpy(nfw, p->st + 1, 8);
   }
-  if (nfw[1]) return fail(c, SONAR_ERR_DEVICE, "dtw band pipeline timed out");
+  {
+    const std::string why = dtw_status(c, p->st + 1);
+    if (!why.empty()) return fail(c, SONAR_ERR_DEVICE, why);
+  }
   const int64_t P = p->st[0];
   int32_t* oq = (int32_t*)dbuf(c, "dtw.pq", cap * 4);
   int32_t* orr = (int32_t*)dbuf(c, "dtw.pr", cap * 4);

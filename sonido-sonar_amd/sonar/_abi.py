@@ -182,6 +182,8 @@ def lib():
     L.sonar_last_kernel_ms.argtypes = [_vp, _d]
     L.sonar_enable_kernel_timing.argtypes = [_vp, C.c_int]
     L.sonar_dtw_last_timing.argtypes = [_vp, C.POINTER(C.c_double)]
+    if hasattr(L, "sonar_dtw_counters"):      # (absent from A/B builds of earlier rounds)
+        L.sonar_dtw_counters.argtypes = [_vp, C.POINTER(C.c_int64), C.c_int32]
     L.sonar_last_fp_kernel.argtypes = [_vp]
     L.sonar_last_fp_kernel.restype = C.c_char_p
     for f in ("sonar_stft_frames", "sonar_energy_frames"):
@@ -371,6 +373,14 @@ class Context:
         v = (C.c_double * 3)()
         self._check(self._L.sonar_dtw_last_timing(self._h, v))
         return tuple(v)
+
+    def dtw_counters(self, reset=False):
+        """Band-pipeline liveness counters since the last reset (sonar_dtw_counters): edge refresh
+        fences, fences followed by new edge values, timed-out DTWs, timed-out waves."""
+        v = (C.c_int64 * 4)()
+        self._check(self._L.sonar_dtw_counters(self._h, v, int(bool(reset))))
+        return {"edge_refresh_fences": v[0], "edge_refresh_hits": v[1], "dtw_timeouts": v[2],
+                "waves_timed_out": v[3]}
 
     def last_fp_kernel(self):
         """Name of the fused kernel the last fingerprint call launched (diagnostics)."""

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Alternating A/B of library builds on C5 (tools/c5_stress.py) and the C3-size DTW band kernel.
+# Usage: bash tools/scratch/ab_stress.sh <reps per C5 run> <tag>...  (default = sonido-sonar_amd/lib)
+set -o pipefail
+mkdir -p gpurun_out
+REPS=$1; shift
+for t in "$@"; do
+  if [ $t = default ]; then L=sonido-sonar_amd/lib/libsonar_gpu.so; else L=sonido-sonar_amd/lib_$t/libsonar_gpu.so; fi
+  SONAR_LIB=$PWD/$L timeout -k 10 120 python tools/scratch/dtw_band_ms.py 51676 5 || { echo "dtw fail $t"; exit 1; }
+  SONAR_LIB=$PWD/$L timeout -k 10 200 python tools/c5_stress.py --reps $REPS > gpurun_out/abs_$t.jsonl 2>gpurun_out/abs_$t.err || { echo "c5 fail $t"; exit 1; }
+  python3 -c "
+import json, numpy as np
+L=[json.loads(l) for l in open('gpurun_out/abs_$t.jsonl')]
+v=np.array([x['pairs_per_s'] for x in L if 'rep' in x]); s=L[-1]
+print('$t', 'c5 median', np.median(v), 'min', v.min(), 'max', v.max(), 'failed', s['failed_reps'], {k: s[k] for k in s if k not in ('summary','reps','failed_reps')})"
+done
