@@ -381,12 +381,16 @@ typedef struct {
 } sonar_pair_record;
 
 /* sonar_align_pair_device over npairs pairs: q_pcm[k] / r_pcm[k] float64 streams of nq[k] / nr[k]
- * samples (device pointers on ctx's device if device_ptrs, else host arrays).  `workers` (<= 0:
- * 16) worker contexts on ctx's device, one HIP stream and one host thread each, take pairs in
- * order, so the pairs' latency-bound kernels (the DC-removal scan, the Go-order NCC sums, the DTW
- * band pipeline and walk) overlap on the GPU.  HIP maps a process's streams onto
- * GPU_MAX_HW_QUEUES hardware queues (4 by default): set it to >= workers in the environment before
- * the first HIP call.  out[k] is filled for every pair; the return is SONAR_OK or the first error. */
+ * samples (device pointers on ctx's device if device_ptrs, else host arrays).  `workers` is the
+ * number of pairs in flight (<= 0: 128).  They are split over SONAR_PAIR_STREAMS worker contexts
+ * (environment, default 16; each one HIP stream and one host thread) in batches of
+ * ceil(workers / streams) pairs, each batch's chroma DTWs in ONE band-kernel launch, so the pairs'
+ * latency-bound kernels (the DC-removal scan, the Go-order NCC sums, the DTW band pipeline and
+ * walk) overlap on the GPU.  HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues
+ * (4 by default, at most 32): set GPU_MAX_HW_QUEUES >= SONAR_PAIR_STREAMS in the environment
+ * before the first HIP call of the process, or the streams share queues and serialise.  out[k] is
+ * filled for every pair; the return is SONAR_OK or the first error (a band pipeline that timed
+ * out names the pair and carries its diagnostic record in sonar_last_error). */
 int sonar_align_pairs(sonar_ctx* ctx, int64_t npairs, const double* const* q_pcm, const int64_t* nq,
                       const double* const* r_pcm, const int64_t* nr, int32_t sample_rate, int32_t stft_window,
                       int32_t hop, int32_t feature_window, double max_lag_seconds, int32_t workers,
@@ -424,7 +428,7 @@ int sonar_fingerprint_multi_gather(sonar_multi* m, const void* const* pcm_dev, i
                                    void* const* mfcc_dev);
 
 /* sonar_align_pairs with the pairs split into contiguous ranges over the devices (host PCM; each
- * device aligns its range with `workers` worker streams); the per-device records are then
+ * device aligns its range as sonar_align_pairs, `workers` pairs in flight); the per-device records are then
  * all-gathered over RCCL and device 0's gathered copy is returned in out[npairs]. */
 int sonar_align_pairs_multi(sonar_multi* m, int64_t npairs, const double* const* q_pcm, const int64_t* nq,
                             const double* const* r_pcm, const int64_t* nr, int32_t sample_rate,

@@ -1138,6 +1138,578 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   }
 }
 
+// ------------------------------------------------------- DTW: two 64-row sub-bands per block ----
+// dtw_band2_kernel: the band kernel over 128-row bands.  Lane l owns TWO rows, 128B+1+l (the top
+// sub-band = 64-band 2B) and 128B+65+l (the bottom sub-band = 64-band 2B+1).  At step s the top
+// row relaxes column s-l+1 and the bottom row column s-l-63, i.e. the bottom sub-band runs the
+// top's sweep 64 steps later, and its lane 0 takes its upper neighbour C[128B+64][j] from the top
+// sub-band's lane 63 one step earlier: a DPP wave_ror:1 of the top values used as the `old` operand
+// of the bottom's wave_shr:1, so the 64-row hand-off inside the 128-row band is one extra DPP off
+// the dependency chain instead of a global edge (dtw.go:106-135).  The two
+// cells of a step read only the previous step, so the sweep issues two independent min-add chains
+// per step in the latency of one: twice the cells per sweep step, half the global hand-offs and
+// half the bands (a 51,676-row problem is 404 bands: all resident at two blocks per CU).
+// Everything written keeps dtw_band_kernel's 64-row-band layouts (Dn, CK, E per 64-band; the
+// bottom sub-band at its own step s-64), so the walk, exit map, path decode and path-tile kernels
+// are shared.  Block = 8 waves as in dtw_band_kernel: sweep, 4 distance waves (waves 1-2 the top
+// sub-band's chunks, even / odd; 3-4 the bottom's), ring feeder, code wave, edge poller.
+// LDS 77.7 KB (2 blocks per CU): a 192-row reference ring (rows t0-127 .. t0+7 of every chunk in
+// flight), and 24-step distance and C rings per sub-band (slot = step mod 24: three 8-step chunks,
+// so a chunk or a step pair never wraps).
+constexpr int DTW2_RROWS = 192;
+constexpr int DTW2_Q = 24;                 // steps per ring (distance and C rings), 3 chunks
+constexpr int DTW2_ROW = DTW2_Q + 2;       // doubles per lane row: 52 dwords = 52 mod 64 (b128 conflict-free)
+__device__ __forceinline__ double ror1(double v) {      // lane l <- lane l-1, lane 0 <- lane 63
+  const int2 a = __builtin_bit_cast(int2, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, a.x, 0x13C, 0xf, 0xf, false);   // wave_ror:1
+  const int hi = __builtin_amdgcn_update_dpp(0, a.y, 0x13C, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, make_int2(lo, hi));
+}
+
+template <int D, bool FAST, bool BANDED, bool BATCH>
+__global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel(DtwArgs a_in, DtwBatch bt) {
+  static_assert(DTW_NDW == 4, "two distance waves per sub-band");
+  constexpr int DR = D > 0 ? D : 1;
+  constexpr int DS = dtw_ring_stride<D>();
+  __shared__ __attribute__((aligned(16))) double ring[(DTW2_RROWS + DTW_RMIR) * DS];
+  __shared__ __attribute__((aligned(16))) double dring[2][64][DTW2_ROW];   // distance of step t at [h][l][t % Q]
+  __shared__ __attribute__((aligned(16))) double oring[2][64][DTW2_ROW];   // C of step t at [h][l][t % Q]
+  __shared__ __attribute__((aligned(16))) double eqa[DTW_EQ];              // C[128B][c] at slot c - 1
+  __shared__ __attribute__((aligned(16))) double eqb[DTW_EQ];              // C[128B][c] at slot c
+  __shared__ __attribute__((aligned(16))) int ctr[16];
+  __shared__ int64_t shb;
+  __shared__ int shk;
+#define SONAR_LDS_LD(x) __hip_atomic_load(&(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#define SONAR_LDS_ST(x, v) __hip_atomic_store(&(x), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+  int& efill = ctr[DTW_CTR_EFILL];
+  int& cprog = ctr[DTW_CTR_CPROG];
+  int& prog = ctr[DTW_CTR_PROG];
+  int& rdy = ctr[DTW_CTR_RDY];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const double inf = __builtin_inf();
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 16; ++k) ctr[k] = 0;
+    if constexpr (BATCH) {
+      const int64_t t = atomicAdd(bt.ticket, 1);
+      ctr[DTW_CTR_TICKET] = (int)t;
+      if (t >= bt.start[bt.n]) {
+        shk = 0;
+        shb = INT64_MAX;                               // past the last ticket: the block exits
+      } else if (bt.map) {                             // ticket -> (DTW, 128-row band)
+        const int2 pb = bt.map[t];
+        shk = pb.x;
+        shb = pb.y;
+      } else {                                         // DTW-major: start[k] <= t < start[k + 1]
+        int lo = 0, hi = bt.n;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (bt.start[mid] <= t) lo = mid; else hi = mid;
+        }
+        shk = lo;
+        shb = t - bt.start[lo];
+      }
+    } else {
+      shb = atomicAdd(&a_in.sync[0], 1);
+      ctr[DTW_CTR_TICKET] = (int)shb;
+    }
+    rdy = -1;
+  }
+  if (threadIdx.x < 64) {        // steps -1 and -2 of both sub-bands: C[i][j <= 0] = +Inf
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      oring[h][lane][DTW2_Q - 1] = inf;
+      oring[h][lane][DTW2_Q - 2] = inf;
+    }
+  }
+  if (threadIdx.x < DTW_EQ) {    // the top edge rings start at +Inf (what a band without one reads)
+    eqa[threadIdx.x] = inf;
+    eqb[threadIdx.x] = inf;
+  }
+  __syncthreads();
+  const int64_t B = shb;
+  const DtwArgs a = BATCH ? load_args_uniform(bt.args + __builtin_amdgcn_readfirstlane(shk)) : a_in;
+  const int64_t nq = a.nq, nr = a.nr, nb = a.nb;
+  if (2 * B >= nb) return;
+  const int64_t b0 = 2 * B, b1 = 2 * B + 1;            // the two 64-row bands (b1 may be absent)
+  const bool has_b1 = b1 < nb;
+  const int64_t S64 = a.S, S2 = (a.S + 1) >> 1;        // steps of one 64-row band: nr + 63
+  const int64_t S = has_b1 ? S64 + 64 : S64;           // steps of this block's sweep
+  const int64_t b = b0;                                // (diagnostics: the top sub-band)
+  constexpr uint64_t INF_BITS = 0x7FF0000000000000ull;
+  const uint64_t* Ein = B > 0 ? a.E + (b0 - 1) * (nr + 1) : nullptr;      // C[128B][j] at index j
+  const int64_t nblk = (nr + DTW_RBLK - 1) / DTW_RBLK;
+  const int64_t i_t = 64 * b0 + 1 + lane, i_b = i_t + 64;
+  const bool ok_t = i_t <= nq, ok_b = i_b <= nq;
+  uint64_t spins_total = 0;
+  // DtwArgs::state (diagnostics, nullable): each wave's exit as one word at [8B + wave]: bits
+  // 60-63 how (1 finished, 2 saw the block's abort word, 3 timed out, 4 saw the DTW's error word),
+  // bits 32-59 its position (sweep / code: chunk step, distance: chunk, feeder: ring block, edge:
+  // columns in the rings), bits 0-31 prog, then efill at the moment of exit (16 bits each)
+  int64_t dpos = 0;
+  auto dtw_exit = [&](uint64_t how) {
+    if (a.state && lane == 0) {
+      const uint64_t p = (uint64_t)(uint16_t)SONAR_LDS_LD(prog), e = (uint64_t)(uint16_t)SONAR_LDS_LD(efill);
+      a.state[8 * B + wave] = (how << 60) | ((uint64_t)(dpos & 0xFFFFFFF) << 32) | (p << 16) | e;
+    }
+  };
+#define SONAR_SPIN_UNTIL(role, cond)                                                  \
+  do {                                                                                \
+    if (!(cond)) {                                                                    \
+      uint64_t w0_ = 0;                                                               \
+      uint32_t sp_ = 0;                                                               \
+      while (!(cond)) {                                                               \
+        __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);                                     \
+        if ((++sp_ & 63) == 0) {                                                      \
+          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) { dtw_exit(2); return; }             \
+          const uint64_t now_ = __builtin_amdgcn_s_memrealtime();                     \
+          if (sp_ == 64) w0_ = now_;                                                  \
+          else if (sp_ >= DTW_STALL_POLLS && now_ - w0_ > DTW_STALL_TICKS) {          \
+            dtw_stall(a.sync, a.diag, (role), b, ctr, Ein, nr, sp_, w0_);            \
+            dtw_exit(3);                                                              \
+            return;                                                                   \
+          }                                                                           \
+        }                                                                             \
+      }                                                                               \
+    }                                                                                 \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
+  } while (0)
+
+  if (wave == DTW_FEEDER_WAVE || wave == DTW_EDGE_WAVE) {
+    // ------------------------------------------------ ring feeder / edge poller (as dtw_band_kernel)
+    const bool do_ring = wave == DTW_FEEDER_WAVE;
+    int64_t nextblk = 0, have = 0;
+    uint32_t idle = 0;
+    uint64_t t_idle = 0, t_fence = 0;
+    bool fenced = false;
+    const int64_t ecols = Ein ? nr : 0;
+    double pv[DR];
+    auto prefetch = [&](int64_t blk) {
+      const int64_t row = DTW_RBLK * blk + lane;
+#pragma unroll
+      for (int k = 0; k < DR; ++k) pv[k] = (lane < DTW_RBLK && row < nr) ? a.r[row * D + k] : 0.0;
+    };
+    if (do_ring) prefetch(0);
+    while (true) {
+      const int64_t p = SONAR_LDS_LD(prog), cp = SONAR_LDS_LD(cprog);
+      bool work = false, wait_edge = false;
+      if (do_ring) {
+        // block m overwrites rows 16m - RROWS .., read by distance chunks t0 <= 16m - RROWS + 15 + 127
+        int mind = SONAR_LDS_LD(ctr[0]);
+#pragma unroll
+        for (int w = 1; w < DTW_NDW; ++w) {
+          const int x = SONAR_LDS_LD(ctr[w]);
+          mind = x < mind ? x : mind;
+        }
+        if (nextblk < nblk &&
+            (nextblk < DTW2_RROWS / DTW_RBLK ||
+             (int64_t)mind > (DTW_RBLK * nextblk - DTW2_RROWS + DTW_RBLK - 1 + 127) / DTW_ECH)) {
+          if (lane < DTW_RBLK) {
+            const int64_t row = DTW_RBLK * nextblk + lane;
+            const int slot = (int)(row % DTW2_RROWS);
+            double* dst = ring + slot * DS;
+            double* mir = ring + (DTW2_RROWS + slot) * DS;
+#pragma unroll
+            for (int k = 0; k < DR; ++k) dst[k] = pv[k];
+            if (slot < DTW_RMIR) {
+#pragma unroll
+              for (int k = 0; k < DR; ++k) mir[k] = pv[k];
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) SONAR_LDS_ST(rdy, (int)nextblk);
+          ++nextblk;
+          if (nextblk < nblk) prefetch(nextblk);
+          work = true;
+        }
+      }
+      if (!do_ring && have < ecols) {
+        const int64_t lo = p < cp ? p : cp;
+        const int64_t want = lo + DTW_EAHEAD < ecols ? lo + DTW_EAHEAD : ecols;
+        if (have < want) {
+          wait_edge = true;
+          const int64_t jj = have + 1 + lane;
+          uint64_t v = INF_BITS;
+          if (jj <= want) v = __hip_atomic_load(Ein + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t bad = __builtin_amdgcn_ballot_w64(jj <= want && v == DTW_SENT);
+          const int64_t lim = want - have < 64 ? want - have : 64;
+          const int64_t got = bad ? (int64_t)__builtin_ctzll(bad) : lim;
+          if (lane < got) {
+            eqa[(jj - 1) & (DTW_EQ - 1)] = __builtin_bit_cast(double, v);
+            eqb[jj & (DTW_EQ - 1)] = __builtin_bit_cast(double, v);
+          }
+          if (got > 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            have += got;
+            if (lane == 0) SONAR_LDS_ST(efill, (int)have);
+            work = true;
+          }
+        }
+      }
+      if (do_ring ? nextblk >= nblk : have >= ecols) break;
+      if (work) {
+        if (fenced) {
+          fenced = false;
+          if (lane == 0 && a.diag) atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[14]), 1ull);
+        }
+        idle = 0;
+      } else {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++idle & 63) == 0) {
+          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) { dpos = do_ring ? nextblk : have; dtw_exit(2); return; }
+          const uint64_t now = __builtin_amdgcn_s_memrealtime();
+          if (idle == 64) t_idle = now;
+          if (wait_edge) {
+            if (__hip_atomic_load(&a.sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+              if (lane == 0) SONAR_LDS_ST(ctr[DTW_CTR_ABORT], 1);
+              dpos = have;
+              dtw_exit(4);
+              return;
+            }
+            if (now - t_idle > DTW_REFRESH_TICKS && now - t_fence > DTW_REFRESH_TICKS) {
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+              t_fence = now;
+              fenced = true;
+              if (lane == 0 && a.diag) atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[13]), 1ull);
+            }
+          }
+          if (idle >= DTW_STALL_POLLS && now - t_idle > DTW_STALL_TICKS) {
+            dtw_stall(a.sync, a.diag, do_ring ? DTW_ROLE_FEEDER : DTW_ROLE_EDGE, b, ctr, Ein, nr, idle, t_idle);
+            dpos = do_ring ? nextblk : have;
+            dtw_exit(3);
+            return;
+          }
+        }
+      }
+    }
+    dpos = do_ring ? nextblk : have;
+    dtw_exit(1);
+    return;
+  }
+
+  if (wave == DTW_CODE_WAVE) {
+    // --------------------------------------------------------------- code wave
+    // findPreviousStep's code (dtw.go:191-217) of both sub-bands' cells, the 64th-column
+    // checkpoints, in each 64-band's own layout (the bottom sub-band at step s - 64).  Lane 0's
+    // neighbours: the top edge C[128B][*] (eqb) for the top sub-band, the top sub-band's lane 63
+    // C values for the bottom one.
+    uint32_t dacc[2] = {0u, 0u};
+    double ckv[2] = {0.0, 0.0};
+    const int S32 = (int)S, S64i = (int)S64, nr32 = (int)nr;
+    int sb = 0;                                        // ring slot of the chunk's first step
+    for (int s0 = 0; s0 < S32; s0 += DTW_ECH, sb = sb == 2 * DTW_ECH ? 0 : sb + DTW_ECH) {
+      const int need = s0 + DTW_ECH < S32 ? s0 + DTW_ECH : S32;
+      dpos = s0;
+      SONAR_SPIN_UNTIL(DTW_ROLE_CODE, SONAR_LDS_LD(prog) >= need);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int sh = s0 - 64 * h;                    // this sub-band's own step of the chunk
+        if (sh < 0 || (h == 1 && !has_b1) || sh >= S64i) continue;
+        const int64_t bb = b0 + h;
+        double cv[DTW_ECH + 2], nv[DTW_ECH + 2];
+#pragma unroll
+        for (int k = 0; k < DTW_ECH / 2 + 1; ++k) {
+          const int t = s0 - 2 + 2 * k;
+          const int sl = k == 0 ? (sb == 0 ? DTW2_Q - 2 : sb - 2) : sb - 2 + 2 * k;
+          const double2 o = *reinterpret_cast<const double2*>(&oring[h][lane][sl]);
+          double2 n;
+          if (lane > 0) n = *reinterpret_cast<const double2*>(&oring[h][lane - 1][sl]);
+          else if (h == 1) n = *reinterpret_cast<const double2*>(&oring[0][63][sl]);
+          else n = *reinterpret_cast<const double2*>(&eqb[(t + 2) & (DTW_EQ - 1)]);
+          cv[2 * k] = o.x; cv[2 * k + 1] = o.y;
+          nv[2 * k] = n.x; nv[2 * k + 1] = n.y;
+        }
+        if (lane == 0 && h == 0) {
+#pragma unroll
+          for (int u = 0; u < DTW_ECH + 1; ++u) {
+            const int c = s0 + u;                        // nv[u] = C[128B][c]
+            nv[u] = (c == 0 || !Ein || c > nr32) ? ((c == 0 && B == 0) ? 0.0 : inf) : nv[u];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < DTW_ECH; ++u) {
+          const double up = nv[u + 1], left = cv[u + 1], dg = nv[u];
+          uint32_t code;
+          if constexpr (FAST) {
+            const double best = vmin_f64(up, vmin_f64(left, dg));
+            code = best == up ? 0u : (best == left ? 1u : 2u);
+          } else {
+            double best = up;
+            code = 0;
+            if (left < best) { code = 1; best = left; }
+            if (dg < best) code = 2;
+          }
+          dacc[h] |= code << (2 * ((sh & 8) + u));
+        }
+        // checkpoint columns (as dtw_band_kernel's code wave, in the sub-band's own steps)
+        const int u = (lane - 1 - sh) & 63;
+        const double cap = u < DTW_ECH ? oring[h][lane][sb + u] : ckv[h];
+        const int J = sh - 56;
+        if ((sh & 63) == 56 && J >= 64 && J <= nr32)
+          a.CK[((bb * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = (u < DTW_ECH && lane != 0) ? cap : ckv[h];
+        ckv[h] = cap;
+        if ((sh & 8) || sh + DTW_ECH >= S64i) {           // steps 16w .. 16w+15 of this sub-band complete
+          a.Dn[((bb * a.SW + (sh >> 4)) << 6) + lane] = dacc[h];
+          dacc[h] = 0;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) SONAR_LDS_ST(cprog, need);
+    }
+    dpos = S;
+    dtw_exit(1);
+    return;
+  }
+
+  if (wave >= 1) {   // (feeder, edge and code returned above)
+    // ---------------------------------------------------------- distance waves
+    // wave 1 + 2h + e: sub-band h, chunks c = e mod 2
+    const int w = wave - 1, h = w >> 1;
+    if (h == 1 && !has_b1) {                           // no bottom sub-band: its chunks are never read
+      if (lane == 0) SONAR_LDS_ST(ctr[w], 1 << 30);
+      dtw_exit(1);
+      return;
+    }
+    double qv[DR];
+    {
+      const int64_t qrow = (h ? ok_b : ok_t) ? (h ? i_b : i_t) - 1 : 0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) qv[k] = a.q[qrow * D + k];
+    }
+    const int roff = 64 * h;                           // the sub-band's reference rows lag by 64
+    const int S32 = (int)S, nblk32 = (int)nblk;
+    // the wave's chunks c = e, e+2, ...: ring slot (8c mod 24) and the lane's first reference row
+    // (8c - l - roff mod RROWS), both advanced per chunk
+    int sl = 8 * (w & 1);
+    int rrow = ((8 * (w & 1) - lane - roff) % DTW2_RROWS + DTW2_RROWS) % DTW2_RROWS;
+    for (int c = w & 1; DTW_ECH * c < S32; c += 2) {
+      const int t0 = DTW_ECH * c;
+      dpos = c;
+      SONAR_SPIN_UNTIL(DTW_ROLE_DIST, SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW2_Q);
+      const int need = (t0 + DTW_ECH - 1) / DTW_RBLK;
+      const int needc = need < nblk32 - 1 ? need : nblk32 - 1;
+      SONAR_SPIN_UNTIL(DTW_ROLE_DIST, SONAR_LDS_LD(rdy) >= needc);
+      double dv[DTW_ECH];
+      // rows t0-l-roff .. +7 (mirror: never wraps); rows outside [0, nr) give values never stored
+      const double* rw0 = ring + rrow * DS;
+#pragma unroll
+      for (int g0 = 0; g0 < DTW_ECH; g0 += DTW_DG) {
+        double sum[DTW_DG];
+#pragma unroll
+        for (int k = 0; k < D; k += 2) {
+          double2 rv[DTW_DG];
+#pragma unroll
+          for (int u = 0; u < DTW_DG; ++u) rv[u] = *reinterpret_cast<const double2*>(rw0 + (g0 + u) * DS + k);
+#pragma unroll
+          for (int u = 0; u < DTW_DG; ++u) {
+            const double d0 = qv[k] - rv[u].x;
+            sum[u] = k == 0 ? d0 * d0 : sum[u] + d0 * d0;
+            const double d1 = qv[k + 1] - rv[u].y;
+            sum[u] = sum[u] + d1 * d1;
+          }
+        }
+        if constexpr (FAST) {
+          double mn = sum[0];
+#pragma unroll
+          for (int u = 1; u < DTW_DG; ++u) mn = vmin_f64(mn, sum[u]);
+          if (__builtin_amdgcn_ballot_w64(!(mn >= DTW_SQRT_MIN)) == 0) {
+#pragma unroll
+            for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt_normal(sum[u]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt(sum[u]);
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt(sum[u]);
+        }
+      }
+      double* drow = &dring[h][lane][sl];
+#pragma unroll
+      for (int u = 0; u < DTW_ECH; u += 2)
+        *reinterpret_cast<double2*>(drow + u) = make_double2(dv[u], dv[u + 1]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) SONAR_LDS_ST(ctr[w], c + 1);
+      sl = sl == 0 ? 2 * DTW_ECH : sl - DTW_ECH;       // + 16 mod 24
+      rrow += 2 * DTW_ECH;
+      if (rrow >= DTW2_RROWS) rrow -= DTW2_RROWS;
+    }
+    dpos = 1 << 27;
+    dtw_exit(1);
+    return;
+  }
+
+  // ---------------------------------------------------------------- sweep wave
+#ifndef DTW_NOPRIO
+  __builtin_amdgcn_s_setprio(3);
+#endif
+  uint64_t* Eout_t = has_b1 ? a.E + b0 * (nr + 1) : nullptr;              // C[128B+64][j]
+  uint64_t* Eout_b = (b1 + 1 < nb) ? a.E + b1 * (nr + 1) : nullptr;       // C[128B+128][j]
+  double out_t = inf, out_b = inf;                     // C[i][j-1]
+  double upp_t = (lane == 0 && B == 0) ? 0.0 : inf;    // C[i-1][j-1]
+  double upp_b = inf;
+  const int64_t band = a.band;
+  // 32-bit steps (nq + nr < 2^31 is checked on the host); sb = the ring slot of the chunk's first
+  // step (s0 mod 24), advanced per chunk instead of divided
+  const int nr32 = (int)nr, S32 = (int)S;
+  struct Ctrs { int d0, d1, d2, d3, ef, cp; };
+  auto ready = [&](int s0, Ctrs k) -> bool {
+    const int c = s0 >> 3;
+    const int dt = (c & 1) ? k.d1 : k.d0, db = (c & 1) ? k.d3 : k.d2;
+    const int neede = s0 + DTW_ECH < nr32 ? s0 + DTW_ECH : nr32;
+    return dt > c && db > c && (!Ein || k.ef >= neede) && k.cp >= s0 + DTW_ECH - DTW2_Q + 2;
+  };
+  typedef int ctr4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) volatile ctr4 lds_ctr4;
+  typedef __attribute__((address_space(3))) volatile int lds_int;
+  auto load_ctr = [&]() -> Ctrs {
+    Ctrs k;
+    const ctr4 x = *(lds_ctr4*)(&ctr[0]);
+    k.d0 = x.x; k.d1 = x.y; k.d2 = x.z; k.d3 = x.w;
+    const int ef = *(lds_int*)(&ctr[DTW_CTR_EFILL]);
+    const int cp = *(lds_int*)(&ctr[DTW_CTR_CPROG]);
+    k.ef = ef;
+    k.cp = cp;
+    return k;
+  };
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) volatile d2v lds_d2;
+  // steps [s0 + u0, s0 + u0 + n) of the chunk at slot sl: both sub-bands' distances and the top
+  // edge (eqa is pre-filled with +Inf, so a band without an edge reads +Inf)
+  auto load_part = [&](int s0, int sl, int u0, int n, double (&dt)[DTW_ECH], double (&db)[DTW_ECH],
+                       double (&ech)[DTW_ECH]) {
+    const double* drt = &dring[0][lane][sl];
+    const double* drb = &dring[1][lane][sl];
+    const double* er = &eqa[s0 & (DTW_EQ - 1)];          // columns s0+1 .. s0+8
+#pragma unroll
+    for (int u = u0; u < u0 + n; u += 2) {
+      const d2v x = *(lds_d2*)(drt + u);
+      const d2v y = *(lds_d2*)(drb + u);
+      const d2v e2 = *(lds_d2*)(er + u);
+      dt[u] = x.x; dt[u + 1] = x.y;
+      db[u] = y.x; db[u + 1] = y.y;
+      ech[u] = e2.x; ech[u + 1] = e2.y;
+    }
+  };
+  // columns past nr (their slots hold older columns) are +Inf; the values are uniform (broadcast
+  // reads), so they move to SGPRs
+  auto fix_edges = [&](int s0, double (&ech)[DTW_ECH]) {
+#pragma unroll
+    for (int u = 0; u < DTW_ECH; ++u) {
+      const double e = s0 + 1 + u > nr32 ? inf : ech[u];
+      const int2 e2 = __builtin_bit_cast(int2, e);
+      ech[u] = __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readfirstlane(e2.x),
+                                                    __builtin_amdgcn_readfirstlane(e2.y)));
+    }
+  };
+  // one step of both sub-bands: the top lane l at column s-l+1 (lane 0's up = the top edge l0up),
+  // the bottom lane l at column s-l-63 (lane 0's up = the top sub-band's lane 63, previous step).
+  // FULL: every lane's columns are in [1, nr] in both sub-bands (rows past nq compute values nobody
+  // reads).
+  auto step = [&](auto full_tag, int s, double l0up, double dt, double db) {
+    constexpr bool FULL = decltype(full_tag)::value;
+    const double up_t = shr1(out_t, l0up);
+    const double up_b = shr1(out_b, ror1(out_t));
+    double bt_, bb_;
+    if constexpr (FAST) {
+      bt_ = vmin_f64(up_t, vmin_f64(out_t, upp_t));
+      bb_ = vmin_f64(up_b, vmin_f64(out_b, upp_b));
+    } else {
+      bt_ = go_min(go_min(up_t, out_t), upp_t);
+      bb_ = go_min(go_min(up_b, out_b), upp_b);
+    }
+    double vt = dt + bt_, vb = db + bb_;
+    const int jt = s - lane + 1, jb = jt - 64;
+    if constexpr (BANDED) {
+      if (i_t - jt > band || jt - i_t > band) vt = inf;
+      if (i_b - jb > band || jb - i_b > band) vb = inf;
+    }
+    if constexpr (FULL) {
+      out_t = vt;
+      out_b = vb;
+    } else {
+      if (ok_t && jt >= 1 && jt <= nr32) out_t = vt;
+      if (ok_b && jb >= 1 && jb <= nr32) out_b = vb;
+    }
+    upp_t = up_t;
+    upp_b = up_b;
+  };
+  auto pair = [&](auto full_tag, int s, int sl, double e0, double e1, double dt0, double dt1, double db0,
+                  double db1) {
+    step(full_tag, s, e0, dt0, db0);
+    const double ot = out_t, ob = out_b;
+    step(full_tag, s + 1, e1, dt1, db1);
+    *reinterpret_cast<double2*>(&oring[0][lane][sl]) = make_double2(ot, out_t);
+    *reinterpret_cast<double2*>(&oring[1][lane][sl]) = make_double2(ob, out_b);
+  };
+
+  double dt[DTW_ECH], db[DTW_ECH], ech[DTW_ECH];
+  Ctrs kc = load_ctr();
+  if (!ready(0, kc)) {
+    SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready(0, kc)));
+  }
+  load_part(0, 0, 0, DTW_ECH, dt, db, ech);
+  fix_edges(0, ech);
+  int sb = 0;
+  for (int s0 = 0; s0 < S32; s0 += DTW_ECH) {
+    const int s1 = s0 + DTW_ECH;
+    const int sbn = sb == 2 * DTW_ECH ? 0 : sb + DTW_ECH;
+    dpos = s1;
+    // the next chunk's counters and its first half at the chunk's start, its second half once the
+    // first half of this chunk is done (its registers are free then): one chunk of data in flight
+    // (past the last chunk the loads read slots nobody uses)
+    double dtn[DTW_ECH], dbn[DTW_ECH], echn[DTW_ECH];
+    kc = load_ctr();
+    load_part(s1, sbn, 0, DTW_ECH / 2, dtn, dbn, echn);
+    if (s0 >= 127 && s1 <= nr32) {
+#pragma unroll
+      for (int u = 0; u < DTW_ECH; u += 2) {
+        if (u == DTW_ECH / 2) load_part(s1, sbn, DTW_ECH / 2, DTW_ECH / 2, dtn, dbn, echn);
+        pair(std::true_type{}, s0 + u, sb + u, ech[u], ech[u + 1], dt[u], dt[u + 1], db[u], db[u + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < DTW_ECH; u += 2) {
+        if (u == DTW_ECH / 2) load_part(s1, sbn, DTW_ECH / 2, DTW_ECH / 2, dtn, dbn, echn);
+        if (s0 + u < S32)
+          pair(std::false_type{}, s0 + u, sb + u, ech[u], ech[u + 1], dt[u], dt[u + 1], db[u], db[u + 1]);
+      }
+    }
+    // the chunk's 8 edge values of each sub-band's last row (lane 63): lanes 0-7 the top's
+    // (-> E[b0], column s0+u-62), lanes 8-15 the bottom's (-> E[b1], column s0+u-126)
+    const int ue = lane & (DTW_ECH - 1);
+    const double ev = oring[lane < DTW_ECH ? 0 : 1][63][sb + ue];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) SONAR_LDS_ST(prog, s1 < S32 ? s1 : S32);
+    {
+      const bool top = lane < DTW_ECH;
+      uint64_t* Eo = top ? Eout_t : Eout_b;
+      const int je = s0 + ue - (top ? 62 : 126);
+      if (lane < 2 * DTW_ECH && Eo && je >= 1 && je <= nr32)
+        __hip_atomic_store(Eo + je, __builtin_bit_cast(uint64_t, ev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (s1 >= S32) break;
+    if (!ready(s1, kc)) {
+      kc = load_ctr();
+      load_part(s1, sbn, 0, DTW_ECH, dtn, dbn, echn);
+      if (!ready(s1, kc)) {
+        SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready(s1, kc)));
+        load_part(s1, sbn, 0, DTW_ECH, dtn, dbn, echn);
+      }
+    }
+    fix_edges(s1, echn);
+#pragma unroll
+    for (int u = 0; u < DTW_ECH; ++u) { dt[u] = dtn[u]; db[u] = dbn[u]; ech[u] = echn[u]; }
+    sb = sbn;
+  }
+  dpos = S;
+  dtw_exit(1);
+  (void)spins_total;
+  (void)S2;
+#undef SONAR_SPIN_UNTIL
+#undef SONAR_LDS_LD
+#undef SONAR_LDS_ST
+}
+
 // Single wave: backtrack (dtw.go:165-188) over the 2-bit direction codes.  The walk is
 // inherently sequential, so it only emits its own moves (2 bits per step, 16 per word, stored
 // 64 words at a time); dtw_path_decode_kernel turns them into points and costs in parallel.
@@ -1787,6 +2359,16 @@ __global__ void nonfinite_batch_kernel(const DtwArgs* args) {
     if (!__builtin_isfinite(k < nqe ? a.q[k] : a.r[k - nqe])) a.sync[2] = 1;
 }
 
+// SONAR_DTW_BAND2=1: dtw_band2_kernel (128-row bands) for 12-dim DTWs (opt-in while it is measured;
+// default: the 64-row dtw_band_kernel)
+bool dtw_band2_enabled(int dim) {
+  static const bool on = [] {
+    const char* e = std::getenv("SONAR_DTW_BAND2");
+    return e && e[0] == '1';
+  }();
+  return on && dim == 12;
+}
+
 // SONAR_DTW_SERIAL_WALK=1: the one-wave serial backtrack instead of the backtrack by bands (A/B)
 static bool dtw_serial_walk() {
   const char* e = std::getenv("SONAR_DTW_SERIAL_WALK");
@@ -1876,6 +2458,17 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
       else hipLaunchKernelGGL((dtw_band_kernel<12, false, false, false, true>), grid, pblock, 0, s, a, nob);
     }
   }
+  else if (dim == 12 && !Cn && dtw_band2_enabled(dim)) {
+    // 128-row bands (dtw_band2_kernel): ceil(nb / 2) blocks
+    const dim3 grid2((unsigned)((g.nb + 1) / 2));
+    if (band > 0) {
+      if (fast) hipLaunchKernelGGL((dtw_band2_kernel<12, true, true, false>), grid2, block, 0, s, a, nob);
+      else hipLaunchKernelGGL((dtw_band2_kernel<12, false, true, false>), grid2, block, 0, s, a, nob);
+    } else {
+      if (fast) hipLaunchKernelGGL((dtw_band2_kernel<12, true, false, false>), grid2, block, 0, s, a, nob);
+      else hipLaunchKernelGGL((dtw_band2_kernel<12, false, false, false>), grid2, block, 0, s, a, nob);
+    }
+  }
   else if (dim == 12) SONAR_DTW_LAUNCH(12);
   else if (dim == 1) SONAR_DTW_LAUNCH(1);
   else SONAR_DTW_LAUNCH(0);
@@ -1938,6 +2531,9 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
     }
     hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true, true>), dim3((unsigned)total_bands),
                        dim3(64 * dtw_block_waves(true)), 0, s, none, bt);
+  } else if (dtw_band2_enabled(12)) {   // tickets are 128-row bands (the caller's map and starts)
+    hipLaunchKernelGGL((dtw_band2_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
+                       0, s, none, bt);
   } else {
     hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
                        0, s, none, bt);

@@ -194,6 +194,9 @@ struct DtwArgs {
   //       without a new edge value), [14] those after which the next poll found new values,
   //  [15] waves of this DTW that timed out
   uint64_t* diag;
+  // nullable (diagnostics, SONAR_DTW_STATE): how and where every wave of every band-kernel block
+  // ended, 8 words per block (dtw_band2_kernel)
+  uint64_t* state;
 };
 constexpr int DTW_DIAG_WORDS = 16;
 // bytes of a single DTW's sync block (launch_dtw): 4 status words + the diagnostic record
@@ -218,6 +221,10 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s);
 // (hargs: the same array on the host; every Dd set -> distances precomputed per DTW first)
 // dmap (nullable): ticket -> (DTW, band) order, e.g. band-major across the batch so a band waits
 // about one hand-off for its predecessor instead of b of them
+// the 128-row band kernel (dtw_band2_kernel: two 64-row sub-bands per block) runs every 12-dim
+// DTW in checkpoint mode when SONAR_DTW_BAND2=1; launch_dtw_batch's tickets are then 128-row
+// bands: per DTW ceil(nb / 2) of them, and dmap / dstart count those
+bool dtw_band2_enabled(int dim);
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
                      int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr);
 // sets *flag = 1 if any of the n values is not finite

@@ -137,6 +137,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   hipStream_t s = w->stream;
   std::vector<PairGeo> pg = in;
   const bool pre = sonar::detail::dtw_pre_enabled(12);
+  const bool band2 = !pre && sonar::dtw_band2_enabled(12);   // tickets over 128-row bands
   size_t chroma_b = 0, cn_b = 0, ck_b = 0, runs_b = 0, dn_b = 0, e_b = 0, codes_b = 0, wst_b = 0, path_b = 0, corr_b = 0;
   int64_t maxE = 1, maxn = 1, max_cap = 1, total_bands = 0;
   for (auto& p : pg) {
@@ -153,7 +154,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     maxE = std::max({maxE, p.Eq, p.Er});
     maxn = std::max({maxn, p.nq, p.nr});
     max_cap = std::max(max_cap, p.cap);
-    total_bands += p.g.nb;
+    total_bands += band2 ? (p.g.nb + 1) / 2 : p.g.nb;   // band-kernel tickets
   }
   // small (device) and the head of h (pinned host) share one layout: per-pair status words + the
   // batch ticket, the per-pair band-kernel diagnostic records, then the DTW arguments, ticket
@@ -198,6 +199,18 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* hcorr = h + ab + args_b + start_b + map_b;
   char* hpath = hcorr + corr_b;
   HIP_TRY(w, hipMemsetAsync(small, 0, stat_b + diag_b, s));
+  // SONAR_DTW_STATE=<dir> (diagnostics): every band-kernel block's per-wave exit words
+  // (DtwArgs::state), written to <dir>/state_pair<k>.bin for each pair whose pipeline timed out
+  const char* state_dir = std::getenv("SONAR_DTW_STATE");
+  std::vector<size_t> state_off(n, 0);
+  char* dstate = nullptr;
+  if (state_dir) {
+    size_t sb = 0;
+    for (int i = 0; i < n; ++i) { state_off[i] = sb; sb += al256((size_t)(pg[i].g.nb + 1) * 64); }
+    dstate = (char*)dbuf(w, "pb.state", sb);
+    if (!dstate) return fail(w, SONAR_ERR_NOMEM, "allocation failed (state)");
+    HIP_TRY(w, hipMemsetAsync(dstate, 0, sb, s));
+  }
   HIP_TRY(w, hipMemsetAsync(runs, 0, runs_b, s));
   if (e_b) HIP_TRY(w, hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, e_b / 4, s));
   int64_t acc = 0;
@@ -227,8 +240,9 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     a.cnm = (double*)(dstat + 8 * i + 2);
     a.Dd = pre ? (double*)(Dd + p.cn) : nullptr;
     a.diag = ddiag + (size_t)i * sonar::DTW_DIAG_WORDS;
+    a.state = dstate ? (uint64_t*)(dstate + state_off[i]) : nullptr;
     hstart[i] = acc;
-    acc += p.g.nb;
+    acc += band2 ? (p.g.nb + 1) / 2 : p.g.nb;
   }
   hstart[n] = acc;
   // band-major tickets across the batch (SONAR_DTW_BAND_MAJOR=0: DTW-major): band b of every DTW
@@ -238,10 +252,11 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   const bool band_major = !(bm && std::atoi(bm) == 0);
   if (band_major) {
     int64_t t = 0, maxnb = 0;
-    for (const auto& p : pg) maxnb = std::max(maxnb, p.g.nb);
+    auto blocks = [&](const PairGeo& p) { return band2 ? (p.g.nb + 1) / 2 : p.g.nb; };
+    for (const auto& p : pg) maxnb = std::max(maxnb, blocks(p));
     for (int64_t b = 0; b < maxnb; ++b)
       for (int i = 0; i < n; ++i)
-        if (b < pg[i].g.nb) hmap[t++] = make_int2(i, (int)b);
+        if (b < blocks(pg[i])) hmap[t++] = make_int2(i, (int)b);
   }
   HIP_TRY(w, hipMemcpyAsync(dargs, hargs, args_b + start_b + (band_major ? map_b : 0), hipMemcpyHostToDevice, s));
   // the non-finite probe of every pair's chroma in one launch (flags in each pair's sync[2])
@@ -271,6 +286,13 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     std::memcpy(sblk + 16, hdiag + (size_t)i * sonar::DTW_DIAG_WORDS, 8 * sonar::DTW_DIAG_WORDS);
     const std::string why = sonar::detail::dtw_status(w, sblk);
     if (!why.empty()) {
+      if (dstate) {
+        std::vector<uint64_t> st((size_t)(p.g.nb + 1) * 8);
+        if (hipMemcpy(st.data(), dstate + state_off[i], st.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+          const std::string fn = std::string(state_dir) + "/state_pair" + std::to_string(p.k) + ".bin";
+          if (FILE* f = std::fopen(fn.c_str(), "wb")) { std::fwrite(st.data(), 8, st.size(), f); std::fclose(f); }
+        }
+      }
       std::memset(rec, 0, sizeof(*rec));
       rec->status = fail(w, SONAR_ERR_DEVICE, why);
       errs->emplace_back(p.k, why);

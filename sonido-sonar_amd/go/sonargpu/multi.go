@@ -11,9 +11,10 @@ package sonargpu
 //
 // The pair entries take arrays of stream pointers.  cgo forbids storing Go pointers in C memory
 // unless they are pinned, so the slices are pinned with runtime.Pinner (Go 1.21) for the call.
-// HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default): set it to
-// at least the library's pair streams (SONAR_PAIR_STREAMS, default 8) in the environment before
-// the first call into the library.
+// HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default, at most 32):
+// set it to at least the library's pair streams (SONAR_PAIR_STREAMS, default 16) in the
+// environment before the first call into the library.  `workers` is the number of pairs in flight
+// (<= 0: 128, i.e. 16 streams x batches of 8).
 
 /*
 #include <stdlib.h>

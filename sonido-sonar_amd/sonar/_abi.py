@@ -500,8 +500,8 @@ class Context:
         return self._result(h)
 
     def align_pairs(self, qs, rs, nq=None, nr=None, sample_rate=44100, stft_window=1024, hop=256,
-                    feature_window=1024, max_lag_seconds=20.0, workers=16, device_ptrs=False):
-        """sonar_align_pairs: records of many pairs.  qs / rs: lists of host arrays, or of device
+                    feature_window=1024, max_lag_seconds=20.0, workers=128, device_ptrs=False):
+        """sonar_align_pairs: records of many pairs (workers = pairs in flight).  qs / rs: lists of host arrays, or of device
         pointers (ints) with device_ptrs=True and the lengths in nq / nr."""
         n = len(qs)
         qp, rp, keep = _pair_arrays(qs, rs)
@@ -750,7 +750,7 @@ class Multi:
         self._check(self._L.sonar_fingerprint_multi_gather(self._h, pp, n, C.byref(cfg), mp))
 
     def align_pairs(self, qs, rs, sample_rate=44100, stft_window=1024, hop=256, feature_window=1024,
-                    max_lag_seconds=20.0, workers=16):
+                    max_lag_seconds=20.0, workers=128):
         """sonar_align_pairs_multi: host streams, pair ranges per device, records all-gathered over RCCL."""
         n = len(qs)
         qp, rp, keep = _pair_arrays(qs, rs)

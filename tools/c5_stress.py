@@ -46,7 +46,10 @@ def main():
         except AttributeError:               # an A/B build of an earlier round
             return {}
 
-    run()
+    try:
+        run()
+    except sonar.SonarError as e:
+        print(json.dumps({"warmup_error": str(e)}), flush=True)
     counters()
     fails, tot = 0, {}
     for i in range(a.reps):
