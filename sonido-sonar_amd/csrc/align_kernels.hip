@@ -250,6 +250,36 @@ constexpr int DTW_ECH = 8;                          // edge values polled per ch
 #define DTW_G 4                                     // steps per scheduling group in the sweep
 #endif
 constexpr uint64_t DTW_SENT = 0x7FF000017FF00001ull;  // signalling NaN: never an arithmetic result
+// Every inter-workgroup access of the band pipeline is a GLOBAL instruction.  The batched band
+// kernels read their DtwArgs through readfirstlane, so the compiler cannot prove that E and the
+// sync words are global and emitted FLAT accesses for them: a flat_load_dwordx2 sc1 edge poll was
+// measured to keep returning the sentinel for milliseconds after the producer's store (every
+// agent-scope acquire issued after 1 ms without progress was followed by new values: 20,027 of
+// 20,053 in four C5 repetitions), which is what timed out the round-2 C5 runs.  The single-DTW
+// kernels got global_load sc1 and never stalled.  MI355X_MICROARCH.md: "global_/buffer_ sc1 loads
+// to registers (never flat_)".
+typedef __attribute__((address_space(1))) uint64_t dtw_gu64;
+typedef __attribute__((address_space(1))) int32_t dtw_gi32;
+__device__ __forceinline__ uint64_t g_load_agent(const uint64_t* p) {
+  return __hip_atomic_load((const dtw_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t g_load_system(const uint64_t* p) {
+  return __hip_atomic_load((const dtw_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ int32_t g_load_agent(const int32_t* p) {
+  return __hip_atomic_load((const dtw_gi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void g_store_agent(uint64_t* p, uint64_t v) {
+  __hip_atomic_store((dtw_gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a plain access through a pointer known to address global memory (global_* instead of flat_*;
+// a flat access also counts against lgkmcnt, so the LDS waits of the role would wait for it)
+#define DTW_GLOBAL(p) ((__attribute__((address_space(1))) std::remove_pointer_t<decltype(p)>*)(p))
+typedef double dtw_d2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void g_add_agent(uint64_t* p, uint64_t v) {
+  __hip_atomic_fetch_add((dtw_gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Liveness bound of every wait in the band kernel: a wait gives up when it has seen no progress
 // for DTW_STALL_TICKS of s_memrealtime (100 MHz) AND has polled at least DTW_STALL_POLLS times (a
 // wave that was switched out does not time out on wall time alone).  The first wave to give up
@@ -283,7 +313,10 @@ struct DtwBatch {
 };
 
 namespace {
-// a DtwArgs at a wave-uniform address into SGPRs (every field read through readfirstlane)
+
+// a DtwArgs at a wave-uniform address into SGPRs (every field read through readfirstlane).  The
+// compiler cannot tell that its pointers address global memory: accesses through them that matter
+// go through DTW_GLOBAL / g_load_agent / g_store_agent (global_* instead of flat_*)
 __device__ __forceinline__ DtwArgs load_args_uniform(const DtwArgs* p) {
   DtwArgs r;
   const int* src = reinterpret_cast<const int*>(p);
@@ -450,7 +483,7 @@ __device__ __attribute__((noinline)) void dtw_stall(
   int claimed = 0;
   if (lane == 0) {
     __hip_atomic_store(&ctr[DTW_CTR_ABORT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    atomicOr(&sync[1], 1 << (role - 1));
+    __hip_atomic_fetch_or((dtw_gi32*)&sync[1], 1 << (role - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (diag) {
       atomicAdd(reinterpret_cast<unsigned long long*>(&diag[15]), 1ull);
       const uint64_t hdr = (1ull << 63) | ((uint64_t)role << 56) | ((uint64_t)(ticket & 0xFFFFFF) << 32) |
@@ -459,6 +492,9 @@ __device__ __attribute__((noinline)) void dtw_stall(
     }
   }
   claimed = __builtin_amdgcn_readfirstlane(claimed);
+#ifdef DTW_STALL_LITE   // A/B knob: no diagnostic record beyond the header
+  claimed = 0;
+#endif
   if (!claimed) return;
   const int64_t lo = prog < cprog ? prog : cprog;
   const int64_t want = lo + DTW_EAHEAD < nr ? lo + DTW_EAHEAD : nr;
@@ -467,17 +503,17 @@ __device__ __attribute__((noinline)) void dtw_stall(
   if (Ein) {
     uint64_t* E = const_cast<uint64_t*>(Ein);
     const int64_t col = efill + 1 <= nr ? efill + 1 : nr;
-    if (lane == 0) e[0] = __hip_atomic_load(E + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) e[0] = g_load_agent(E + col);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (lane == 0) {
-      e[1] = __hip_atomic_load(E + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      e[2] = __hip_atomic_load(E + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      e[3] = __hip_atomic_fetch_or(E + col, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      e[4] = __hip_atomic_fetch_or(E + col, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      e[1] = g_load_agent(E + col);
+      e[2] = g_load_system(E + col);
+      e[3] = __hip_atomic_fetch_or((dtw_gu64*)(E + col), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      e[4] = __hip_atomic_fetch_or((dtw_gu64*)(E + col), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     for (int64_t c0 = 1; c0 <= nr; c0 += 64) {
       const int64_t j = c0 + lane;
-      const uint64_t v = j <= nr ? __hip_atomic_load(E + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+      const uint64_t v = j <= nr ? g_load_agent(E + j) : 0ull;
       const uint64_t m = __builtin_amdgcn_ballot_w64(j <= nr && v == DTW_SENT);
       if (m) { first = c0 + (int64_t)__builtin_ctzll(m); break; }
     }
@@ -495,6 +531,24 @@ __device__ __attribute__((noinline)) void dtw_stall(
     const uint64_t xcc = (uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20); // HW_REG_XCC_ID
     d[12] = (xcc & 0xFF) | (hw << 32);
   }
+}
+
+// The slow path of a bounded LDS wait, run every DTW_SPIN_CHECK polls (out of line, so the poll
+// loop stays as small as an unbounded one): returns the wait's start time (s_memrealtime; w0 on
+// the first call), or 0 when the wave must give up -- the block's abort word is set, or the wait
+// has seen no progress for DTW_STALL_TICKS (then it reports through dtw_stall first).
+constexpr uint32_t DTW_SPIN_CHECK = 1u << 14;
+__device__ __attribute__((noinline)) uint64_t dtw_spin_check(int32_t* sync, uint64_t* diag, int role, int64_t b,
+                                                             int* ctr, const uint64_t* Ein, int64_t nr,
+                                                             uint64_t w0, uint32_t rounds) {
+  if (__hip_atomic_load(&ctr[DTW_CTR_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return 0;
+  const uint64_t now = __builtin_amdgcn_s_memrealtime();
+  if (!w0) return now;
+  if (now - w0 > DTW_STALL_TICKS && rounds >= 64) {   // (and >= 2^20 polls: a wave switched out
+    dtw_stall(sync, diag, role, b, ctr, Ein, nr, rounds * DTW_SPIN_CHECK, w0);   //  does not time out)
+    return 0;
+  }
+  return w0;
 }
 
 // PRE: the local distances come precomputed from dtw_dist_kernel (a.Dd), so the block is only
@@ -586,28 +640,40 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   // spin (LDS only) until `cond` holds.  Bounded (DTW_STALL_TICKS and DTW_STALL_POLLS without
   // `cond`): the wave then reports through dtw_stall and the whole block returns; it also returns
   // as soon as another wave of the block has given up (the LDS abort word, checked every 64 polls)
+#ifdef DTW_OLD_SPIN   // A/B knob: round 2's wait (poll-count bound, no abort word)
+#define SONAR_SPIN_UNTIL(role, cond)                                                  \
+  do {                                                                                \
+    uint64_t sp_ = 0;                                                                 \
+    if (!(cond)) {                                                                    \
+      const uint64_t w0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;            \
+      while (!(cond)) {                                                               \
+        __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);                                     \
+        if (++sp_ > (uint64_t)(1 << 24)) { if (lane == 0) atomicOr(&a.sync[1], 2); break; } \
+      }                                                                               \
+      if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - w0_;             \
+    }                                                                                 \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
+  } while (0)
+#else
 #define SONAR_SPIN_UNTIL(role, cond)                                                  \
   do {                                                                                \
     if (!(cond)) {                                                                    \
       const uint64_t tr0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;           \
       uint64_t w0_ = 0;                                                               \
-      uint32_t sp_ = 0;                                                               \
+      uint32_t sp_ = 0, rounds_ = 0;                                                  \
       while (!(cond)) {                                                               \
         __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);                                     \
-        if ((++sp_ & 63) == 0) {                                                      \
-          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) return;                               \
-          const uint64_t now_ = __builtin_amdgcn_s_memrealtime();                     \
-          if (sp_ == 64) w0_ = now_;                                                  \
-          else if (sp_ >= DTW_STALL_POLLS && now_ - w0_ > DTW_STALL_TICKS) {          \
-            dtw_stall(a.sync, a.diag, (role), b, ctr, Ein, nr, sp_, w0_);            \
-            return;                                                                   \
-          }                                                                           \
+        if (++sp_ == DTW_SPIN_CHECK) {                                                \
+          sp_ = 0;                                                                    \
+          w0_ = dtw_spin_check(a.sync, a.diag, (role), b, ctr, Ein, nr, w0_, ++rounds_); \
+          if (!w0_) { return; }                                    \
         }                                                                             \
       }                                                                               \
       if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - tr0_;            \
     }                                                                                 \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
   } while (0)
+#endif
 
   if (wave == FEEDER_WAVE || wave == EDGE_WAVE) {
     // ------------------------------------------------ ring feeder / edge poller
@@ -626,7 +692,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     auto prefetch = [&](int64_t blk) {
       const int64_t row = DTW_RBLK * blk + lane;
 #pragma unroll
-      for (int k = 0; k < DR; ++k) pv[k] = (lane < DTW_RBLK && row < nr) ? a.r[row * D + k] : 0.0;
+      for (int k = 0; k < DR; ++k) pv[k] = (lane < DTW_RBLK && row < nr) ? DTW_GLOBAL(a.r)[row * D + k] : 0.0;
     };
     if constexpr (D > 0 && !PRE) prefetch(0);
     while (true) {
@@ -674,7 +740,11 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
           wait_edge = true;
           const int64_t jj = have + 1 + lane;
           uint64_t v = INF_BITS;
+#ifdef DTW_FLAT_EDGE     // A/B knob: the generic-pointer poll (flat_load ... sc1 in the batched kernel)
           if (jj <= want) v = __hip_atomic_load(Ein + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+          if (jj <= want) v = g_load_agent(Ein + jj);
+#endif
           const uint64_t bad = __builtin_amdgcn_ballot_w64(jj <= want && v == DTW_SENT);
           const int64_t lim = want - have < 64 ? want - have : 64;
           const int64_t got = bad ? (int64_t)__builtin_ctzll(bad) : lim;   // contiguous ready prefix
@@ -690,14 +760,26 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
           }
         }
       }
+#ifdef DTW_OLD_EDGE   // A/B knob: round 2's idle handling (cumulative poll bound)
+      if (do_ring ? (D == 0 || nextblk >= nblk) : have >= ecols) break;
+      (void)wait_edge; (void)fenced; (void)t_fence; (void)t_idle;
+      if (!work) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++idle > (1u << 24)) {
+          if (lane == 0) { atomicOr(&a.sync[1], 1); SONAR_LDS_ST(efill, (int)ecols); SONAR_LDS_ST(rdy, (int)nblk); }
+          break;
+        }
+      }
+    }
+#else
       if (do_ring ? (D == 0 || nextblk >= nblk) : have >= ecols) break;
       if (work) {
-        if (fenced) {
-          fenced = false;
-          if (lane == 0 && a.diag) atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[14]), 1ull);
-        }
+        // diag[14]: the first poll after a refresh found new values
+        if (fenced && lane == 0 && a.diag) g_add_agent(&a.diag[14], 1ull);
+        fenced = false;
         idle = 0;
       } else {
+        fenced = false;
         __builtin_amdgcn_s_sleep(1);
         if ((++idle & 63) == 0) {
           if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) return;
@@ -705,7 +787,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
           if (idle == 64) t_idle = now;
           if (wait_edge) {
             // another band of this DTW gave up: its edge (and so this band's) will never come
-            if (__hip_atomic_load(&a.sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            if (g_load_agent(&a.sync[1])) {
               if (lane == 0) SONAR_LDS_ST(ctr[DTW_CTR_ABORT], 1);
               return;
             }
@@ -713,7 +795,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
               __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
               t_fence = now;
               fenced = true;
-              if (lane == 0 && a.diag) atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[13]), 1ull);
+              if (lane == 0 && a.diag) g_add_agent(&a.diag[13], 1ull);
             }
           }
           if (idle >= DTW_STALL_POLLS && now - t_idle > DTW_STALL_TICKS) {
@@ -723,6 +805,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         }
       }
     }
+#endif
     return;
   }
 
@@ -730,8 +813,8 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     // --------------------------------------------------------------- code wave
     // step s, lane l: up = C of lane l-1 at step s-1, left = own at s-1, diag = lane l-1 at s-2;
     // lane 0's left neighbour is the band's top edge: C[64b][s+1] / C[64b][s]
-    uint32_t* Db = a.Dn + ((b * a.SW) << 6) + lane;
-    double* Cb = a.Cn + dtw_cn_off(b, S2, 0, lane);
+    __attribute__((address_space(1))) uint32_t* Db = DTW_GLOBAL(a.Dn) + ((b * a.SW) << 6) + lane;
+    __attribute__((address_space(1))) double* Cb = DTW_GLOBAL(a.Cn) + dtw_cn_off(b, S2, 0, lane);
     uint32_t dacc = 0;
     double ckv = 0.0;                                  // the lane's C at the latest multiple-of-64 column
     for (int64_t s0 = 0; s0 < S; s0 += DTW_ECH) {
@@ -776,7 +859,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
 #pragma unroll
         for (int k = 0; k < DTW_ECH / 2; ++k)
           if (s0 + 2 * k < S)
-            *reinterpret_cast<double2*>(Cb + ((s0 + 2 * k) << 6)) = make_double2(cv[2 + 2 * k], cv[3 + 2 * k]);
+            *(__attribute__((address_space(1))) dtw_d2*)(Cb + ((s0 + 2 * k) << 6)) = dtw_d2{cv[2 + 2 * k], cv[3 + 2 * k]};
       } else {
         // checkpoint columns only.  Lane l meets column J = 64m at step J + l - 1, so every lane
         // has C[i][J] once the chunk holding step J + 62 is done (s0 % 64 == 56, J = s0 - 56):
@@ -788,7 +871,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         const int64_t J = s0 - 56;
 #ifndef DTW_DBG_NOCK   // A/B diagnostics: no checkpoint stores (wrong path costs; timing only)
         if ((s0 & 63) == 56 && J >= 64 && J <= nr)
-          a.CK[((b * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = (u < DTW_ECH && lane != 0) ? cap : ckv;
+          DTW_GLOBAL(a.CK)[((b * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = (u < DTW_ECH && lane != 0) ? cap : ckv;
 #endif
         ckv = cap;
       }
@@ -799,14 +882,14 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         dacc = 0;
       }
     }
-    if (a.trace && lane == 0) a.trace[8 * b + 7] = spins_total;   // code wave's waits
+    if (a.trace && lane == 0) DTW_GLOBAL(a.trace)[8 * b + 7] = spins_total;   // code wave's waits
     return;
   }
 
   double qv[DR];
   if constexpr (D > 0 && !PRE) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) qv[k] = a.q[qrow * D + k];
+    for (int k = 0; k < D; ++k) qv[k] = DTW_GLOBAL(a.q)[qrow * D + k];
   }
   // local distance of the lane's cell at step t for a runtime dimension (D == 0), from global
   // memory (EuclideanDistanceFunc order, unfused)
@@ -829,7 +912,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     // chunk c = steps 8c .. 8c+7: four 16-B loads per lane (its pairs of steps in Dd), DTW_PF
     // chunks ahead in registers; written to the distance ring once the sweep has freed the slots
     // (the same rule as the distance waves), then every dchunk counter is set to c + 1
-    const double* Db = a.Dd + dtw_cn_off(b, S2, 0, lane);
+    const __attribute__((address_space(1))) double* Db = DTW_GLOBAL(a.Dd) + dtw_cn_off(b, S2, 0, lane);
     const int64_t nch = (S + DTW_ECH - 1) / DTW_ECH;
     double buf[DTW_PF][DTW_ECH];
     auto fetch = [&](int64_t c, double (&v)[DTW_ECH]) {
@@ -837,7 +920,10 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
 #pragma unroll
       for (int u = 0; u < DTW_ECH / 2; ++u) {
         double2 x = make_double2(0.0, 0.0);
-        if (p0 + u < S2) x = *reinterpret_cast<const double2*>(Db + ((p0 + u) << 7));
+        if (p0 + u < S2) {
+          const dtw_d2 y = *(const __attribute__((address_space(1))) dtw_d2*)(Db + ((p0 + u) << 7));
+          x = make_double2(y.x, y.y);
+        }
         v[2 * u] = x.x;
         v[2 * u + 1] = x.y;
       }
@@ -945,7 +1031,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) SONAR_LDS_ST(ctr[w], (int)(c + 1));
     }
-    if (a.trace && lane == 0 && w == 0) a.trace[8 * b + 6] = spins_total;   // distance wave 0's waits
+    if (a.trace && lane == 0 && w == 0) DTW_GLOBAL(a.trace)[8 * b + 6] = spins_total;   // distance wave 0's waits
     return;
   }
 
@@ -1071,6 +1157,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   fix_edges(0, ech);
   for (int64_t s0 = 0; s0 < S; s0 += DTW_ECH) {
     const int64_t s1 = s0 + DTW_ECH;
+    if (b == a.dbg_stall && s0 >= 1024) return;        // fault injection (tests only)
     // next chunk: counters first, then its data (LDS completes a wave's requests in order)
     double dcn[DTW_ECH], echn[DTW_ECH];
     if (s1 < S) {
@@ -1098,7 +1185,11 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     if (Eout) {                                        // one sc1 store of the chunk's 8 edge values
       const int64_t je = s0 + lane - 62;               // lane 63's column at step s0 + lane
       if (lane < DTW_ECH && je >= 1 && je <= nr)
+#ifdef DTW_FLAT_EDGE
         __hip_atomic_store(Eout + je, __builtin_bit_cast(uint64_t, ev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+        g_store_agent(Eout + je, __builtin_bit_cast(uint64_t, ev));
+#endif
     }
     if (s1 >= S) break;
     if (!ready((int)s1, kc)) {
@@ -1125,16 +1216,17 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
 #undef SONAR_LDS_LD
 #undef SONAR_LDS_ST
   if (a.trace && lane == 0) {
-    a.trace[8 * b + 0] = t_start;
-    a.trace[8 * b + 1] = t_first;
-    a.trace[8 * b + 2] = __builtin_amdgcn_s_memrealtime();
+    auto* tr = DTW_GLOBAL(a.trace);
+    tr[8 * b + 0] = t_start;
+    tr[8 * b + 1] = t_first;
+    tr[8 * b + 2] = __builtin_amdgcn_s_memrealtime();
     // spins (10 ns ticks, low 24 bits), XCC id (bits 24-31) and HW_ID (high word: SIMD bits 4-5,
     // CU/SH/SE bits 8-15) of the sweep wave, so the probe can see which sweeps shared a SIMD
     const uint64_t hw = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
     const uint64_t xcc = (uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20); // HW_REG_XCC_ID
-    a.trace[8 * b + 3] = (spins_total & 0xFFFFFFull) | ((xcc & 0xFF) << 24) | (hw << 32);
-    a.trace[8 * b + 4] = c_start;
-    a.trace[8 * b + 5] = __builtin_amdgcn_s_memtime();
+    tr[8 * b + 3] = (spins_total & 0xFFFFFFull) | ((xcc & 0xFF) << 24) | (hw << 32);
+    tr[8 * b + 4] = c_start;
+    tr[8 * b + 5] = __builtin_amdgcn_s_memtime();
   }
 }
 
@@ -1249,25 +1341,20 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
   auto dtw_exit = [&](uint64_t how) {
     if (a.state && lane == 0) {
       const uint64_t p = (uint64_t)(uint16_t)SONAR_LDS_LD(prog), e = (uint64_t)(uint16_t)SONAR_LDS_LD(efill);
-      a.state[8 * B + wave] = (how << 60) | ((uint64_t)(dpos & 0xFFFFFFF) << 32) | (p << 16) | e;
+      DTW_GLOBAL(a.state)[8 * B + wave] = (how << 60) | ((uint64_t)(dpos & 0xFFFFFFF) << 32) | (p << 16) | e;
     }
   };
 #define SONAR_SPIN_UNTIL(role, cond)                                                  \
   do {                                                                                \
     if (!(cond)) {                                                                    \
       uint64_t w0_ = 0;                                                               \
-      uint32_t sp_ = 0;                                                               \
+      uint32_t sp_ = 0, rounds_ = 0;                                                  \
       while (!(cond)) {                                                               \
         __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);                                     \
-        if ((++sp_ & 63) == 0) {                                                      \
-          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) { dtw_exit(2); return; }             \
-          const uint64_t now_ = __builtin_amdgcn_s_memrealtime();                     \
-          if (sp_ == 64) w0_ = now_;                                                  \
-          else if (sp_ >= DTW_STALL_POLLS && now_ - w0_ > DTW_STALL_TICKS) {          \
-            dtw_stall(a.sync, a.diag, (role), b, ctr, Ein, nr, sp_, w0_);            \
-            dtw_exit(3);                                                              \
-            return;                                                                   \
-          }                                                                           \
+        if (++sp_ == DTW_SPIN_CHECK) {                                                \
+          sp_ = 0;                                                                    \
+          w0_ = dtw_spin_check(a.sync, a.diag, (role), b, ctr, Ein, nr, w0_, ++rounds_); \
+          if (!w0_) { dtw_exit(2); return; }                                    \
         }                                                                             \
       }                                                                               \
     }                                                                                 \
@@ -1286,7 +1373,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
     auto prefetch = [&](int64_t blk) {
       const int64_t row = DTW_RBLK * blk + lane;
 #pragma unroll
-      for (int k = 0; k < DR; ++k) pv[k] = (lane < DTW_RBLK && row < nr) ? a.r[row * D + k] : 0.0;
+      for (int k = 0; k < DR; ++k) pv[k] = (lane < DTW_RBLK && row < nr) ? DTW_GLOBAL(a.r)[row * D + k] : 0.0;
     };
     if (do_ring) prefetch(0);
     while (true) {
@@ -1329,7 +1416,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
           wait_edge = true;
           const int64_t jj = have + 1 + lane;
           uint64_t v = INF_BITS;
-          if (jj <= want) v = __hip_atomic_load(Ein + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (jj <= want) v = g_load_agent(Ein + jj);
           const uint64_t bad = __builtin_amdgcn_ballot_w64(jj <= want && v == DTW_SENT);
           const int64_t lim = want - have < 64 ? want - have : 64;
           const int64_t got = bad ? (int64_t)__builtin_ctzll(bad) : lim;
@@ -1347,19 +1434,19 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
       }
       if (do_ring ? nextblk >= nblk : have >= ecols) break;
       if (work) {
-        if (fenced) {
-          fenced = false;
-          if (lane == 0 && a.diag) atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[14]), 1ull);
-        }
+        // diag[14]: the first poll after a refresh found new values
+        if (fenced && lane == 0 && a.diag) g_add_agent(&a.diag[14], 1ull);
+        fenced = false;
         idle = 0;
       } else {
+        fenced = false;
         __builtin_amdgcn_s_sleep(1);
         if ((++idle & 63) == 0) {
           if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) { dpos = do_ring ? nextblk : have; dtw_exit(2); return; }
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
           if (idle == 64) t_idle = now;
           if (wait_edge) {
-            if (__hip_atomic_load(&a.sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            if (g_load_agent(&a.sync[1])) {
               if (lane == 0) SONAR_LDS_ST(ctr[DTW_CTR_ABORT], 1);
               dpos = have;
               dtw_exit(4);
@@ -1369,7 +1456,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
               __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
               t_fence = now;
               fenced = true;
-              if (lane == 0 && a.diag) atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[13]), 1ull);
+              if (lane == 0 && a.diag) g_add_agent(&a.diag[13], 1ull);
             }
           }
           if (idle >= DTW_STALL_POLLS && now - t_idle > DTW_STALL_TICKS) {
@@ -1445,10 +1532,10 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
         const double cap = u < DTW_ECH ? oring[h][lane][sb + u] : ckv[h];
         const int J = sh - 56;
         if ((sh & 63) == 56 && J >= 64 && J <= nr32)
-          a.CK[((bb * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = (u < DTW_ECH && lane != 0) ? cap : ckv[h];
+          DTW_GLOBAL(a.CK)[((bb * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = (u < DTW_ECH && lane != 0) ? cap : ckv[h];
         ckv[h] = cap;
         if ((sh & 8) || sh + DTW_ECH >= S64i) {           // steps 16w .. 16w+15 of this sub-band complete
-          a.Dn[((bb * a.SW + (sh >> 4)) << 6) + lane] = dacc[h];
+          DTW_GLOBAL(a.Dn)[((bb * a.SW + (sh >> 4)) << 6) + lane] = dacc[h];
           dacc[h] = 0;
         }
       }
@@ -1473,7 +1560,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
     {
       const int64_t qrow = (h ? ok_b : ok_t) ? (h ? i_b : i_t) - 1 : 0;
 #pragma unroll
-      for (int k = 0; k < D; ++k) qv[k] = a.q[qrow * D + k];
+      for (int k = 0; k < D; ++k) qv[k] = DTW_GLOBAL(a.q)[qrow * D + k];
     }
     const int roff = 64 * h;                           // the sub-band's reference rows lag by 64
     const int S32 = (int)S, nblk32 = (int)nblk;
@@ -1654,6 +1741,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
     const int s1 = s0 + DTW_ECH;
     const int sbn = sb == 2 * DTW_ECH ? 0 : sb + DTW_ECH;
     dpos = s1;
+    if ((b0 == a.dbg_stall || b1 == a.dbg_stall) && s0 >= 1024) return;   // fault injection (tests only)
     // the next chunk's counters and its first half at the chunk's start, its second half once the
     // first half of this chunk is done (its registers are free then): one chunk of data in flight
     // (past the last chunk the loads read slots nobody uses)
@@ -1685,7 +1773,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
       uint64_t* Eo = top ? Eout_t : Eout_b;
       const int je = s0 + ue - (top ? 62 : 126);
       if (lane < 2 * DTW_ECH && Eo && je >= 1 && je <= nr32)
-        __hip_atomic_store(Eo + je, __builtin_bit_cast(uint64_t, ev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g_store_agent(Eo + je, __builtin_bit_cast(uint64_t, ev));
     }
     if (s1 >= S32) break;
     if (!ready(s1, kc)) {
@@ -2359,14 +2447,17 @@ __global__ void nonfinite_batch_kernel(const DtwArgs* args) {
     if (!__builtin_isfinite(k < nqe ? a.q[k] : a.r[k - nqe])) a.sync[2] = 1;
 }
 
+// SONAR_DTW_DBG_STALL=<band> (tests only): fault injection, see DtwArgs::dbg_stall
+int32_t dtw_dbg_stall_band() {
+  const char* e = std::getenv("SONAR_DTW_DBG_STALL");
+  return e ? (int32_t)std::atoi(e) : -1;
+}
+
 // SONAR_DTW_BAND2=1: dtw_band2_kernel (128-row bands) for 12-dim DTWs (opt-in while it is measured;
 // default: the 64-row dtw_band_kernel)
 bool dtw_band2_enabled(int dim) {
-  static const bool on = [] {
-    const char* e = std::getenv("SONAR_DTW_BAND2");
-    return e && e[0] == '1';
-  }();
-  return on && dim == 12;
+  const char* e = std::getenv("SONAR_DTW_BAND2");
+  return e && e[0] == '1' && dim == 12;
 }
 
 // SONAR_DTW_SERIAL_WALK=1: the one-wave serial backtrack instead of the backtrack by bands (A/B)
@@ -2413,6 +2504,7 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
             trace};
   a.CK = CK;
   a.diag = reinterpret_cast<uint64_t*>(sync_words + 4);
+  a.dbg_stall = dtw_dbg_stall_band();
   if (!Cn && !CK) return -1;
   const DtwBatch nob{};
   const bool pre = Dd && dim == 12;

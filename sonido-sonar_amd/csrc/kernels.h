@@ -197,6 +197,11 @@ struct DtwArgs {
   // nullable (diagnostics, SONAR_DTW_STATE): how and where every wave of every band-kernel block
   // ended, 8 words per block (dtw_band2_kernel)
   uint64_t* state;
+  // tests only (SONAR_DTW_DBG_STALL=<band>): the sweep of that 64-row band (band kernel) or of the
+  // 128-row band holding it (band2) stops after 1,024 steps without publishing more, so the
+  // pipeline's bounded waits and its diagnostic record can be exercised; -1: off
+  int32_t dbg_stall = -1;
+  int32_t pad_;
 };
 constexpr int DTW_DIAG_WORDS = 16;
 // bytes of a single DTW's sync block (launch_dtw): 4 status words + the diagnostic record
@@ -225,6 +230,7 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s);
 // DTW in checkpoint mode when SONAR_DTW_BAND2=1; launch_dtw_batch's tickets are then 128-row
 // bands: per DTW ceil(nb / 2) of them, and dmap / dstart count those
 bool dtw_band2_enabled(int dim);
+int32_t dtw_dbg_stall_band();   // SONAR_DTW_DBG_STALL (tests only), -1 when unset
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
                      int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr);
 // sets *flag = 1 if any of the n values is not finite

@@ -241,6 +241,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     a.Dd = pre ? (double*)(Dd + p.cn) : nullptr;
     a.diag = ddiag + (size_t)i * sonar::DTW_DIAG_WORDS;
     a.state = dstate ? (uint64_t*)(dstate + state_off[i]) : nullptr;
+    a.dbg_stall = sonar::dtw_dbg_stall_band();
     hstart[i] = acc;
     acc += band2 ? (p.g.nb + 1) / 2 : p.g.nb;
   }
