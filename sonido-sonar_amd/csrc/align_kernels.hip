@@ -526,29 +526,37 @@ __device__ __attribute__((noinline)) void dtw_stall(
     d[4] = (uint32_t)want | ((uint64_t)(uint32_t)nr << 32);
     for (int k = 0; k < 5; ++k) d[5 + k] = e[k];
     d[10] = (uint64_t)first;
-    d[11] = ((now - t0) & 0xFFFFFFFFFFull) | ((uint64_t)(polls >> 10) << 40);
+    // (a wait of another wave of the block, reported here by the edge poller: the bound itself)
+    d[11] = ((t0 ? now - t0 : DTW_STALL_TICKS) & 0xFFFFFFFFFFull) | ((uint64_t)(polls >> 10) << 40);
     const uint64_t hw = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
     const uint64_t xcc = (uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20); // HW_REG_XCC_ID
     d[12] = (xcc & 0xFF) | (hw << 32);
   }
 }
 
-// The slow path of a bounded LDS wait, run every DTW_SPIN_CHECK polls (out of line, so the poll
-// loop stays as small as an unbounded one): returns the wait's start time (s_memrealtime; w0 on
-// the first call), or 0 when the wave must give up -- the block's abort word is set, or the wait
-// has seen no progress for DTW_STALL_TICKS (then it reports through dtw_stall first).
-constexpr uint32_t DTW_SPIN_CHECK = 1u << 14;
-__device__ __attribute__((noinline)) uint64_t dtw_spin_check(int32_t* sync, uint64_t* diag, int role, int64_t b,
-                                                             int* ctr, const uint64_t* Ein, int64_t nr,
-                                                             uint64_t w0, uint32_t rounds) {
-  if (__hip_atomic_load(&ctr[DTW_CTR_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return 0;
-  const uint64_t now = __builtin_amdgcn_s_memrealtime();
-  if (!w0) return now;
-  if (now - w0 > DTW_STALL_TICKS && rounds >= 64) {   // (and >= 2^20 polls: a wave switched out
-    dtw_stall(sync, diag, role, b, ctr, Ein, nr, rounds * DTW_SPIN_CHECK, w0);   //  does not time out)
-    return 0;
+// A bounded LDS wait (SONAR_SPIN_UNTIL) checks the block's abort word and the clock every
+// DTW_SPIN_CHECK polls (~10 ms); after DTW_STALL_TICKS without progress (and >= 16 checks, so a wave
+// that was switched out does not time out on wall time alone) it gives up: it records its role in
+// the block's LDS stall word, raises the abort word and its bit of the DTW's error word, and
+// stops waiting: it sets the wave's dead_ flag, which ends this and every later wait at once, so the
+// wave runs out its loop on stale LDS data (in-bounds: every index comes from loop counters) and
+// its DTW is reported failed.  Neither a call nor a `return` inside the wait loops: a call costs the
+// sweep's, code wave's and distance waves' loops their register allocation (C5 -10 %), and a
+// `return` is a divergent exit from those loops (the abort word is an LDS load), which turns their
+// uniform loop state into per-lane values (sweep 87 -> 128 VGPRs, C5 -15 %).  The edge poller (or
+// the ring feeder), whose loop already holds the call, sees the abort word and writes the DTW's
+// diagnostic record for the stalled role (dtw_stall).
+constexpr uint32_t DTW_SPIN_CHECK = 1u << 16;
+constexpr int DTW_CTR_STALLED = 14;   // role of the block's first wave that timed out (0: none)
+__device__ __forceinline__ void dtw_local_stall(int role, int32_t* sync, int* ctr, int lane) {
+  if (lane == 0) {
+    int expect = 0;
+    __hip_atomic_compare_exchange_strong(&ctr[DTW_CTR_STALLED], &expect, role, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&ctr[DTW_CTR_ABORT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or((__attribute__((address_space(1))) int32_t*)&sync[1], 1 << (role - 1), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
   }
-  return w0;
 }
 
 // PRE: the local distances come precomputed from dtw_dist_kernel (a.Dd), so the block is only
@@ -637,9 +645,9 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   const bool row_ok = i <= nq;
   const int64_t qrow = row_ok ? i - 1 : 0;
   uint64_t spins_total = 0;
-  // spin (LDS only) until `cond` holds.  Bounded (DTW_STALL_TICKS and DTW_STALL_POLLS without
-  // `cond`): the wave then reports through dtw_stall and the whole block returns; it also returns
-  // as soon as another wave of the block has given up (the LDS abort word, checked every 64 polls)
+  uint32_t dead_ = 0;
+  // spin (LDS only) until `cond` holds; bounded, see DTW_SPIN_CHECK.  A wave that gives up, or sees
+  // the block's abort word, sets dead_ and runs out its loop without waiting again.
 #ifdef DTW_OLD_SPIN   // A/B knob: round 2's wait (poll-count bound, no abort word)
 #define SONAR_SPIN_UNTIL(role, cond)                                                  \
   do {                                                                                \
@@ -657,16 +665,21 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
 #else
 #define SONAR_SPIN_UNTIL(role, cond)                                                  \
   do {                                                                                \
-    if (!(cond)) {                                                                    \
+    if (!dead_ && !(cond)) {                                                          \
       const uint64_t tr0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;           \
       uint64_t w0_ = 0;                                                               \
       uint32_t sp_ = 0, rounds_ = 0;                                                  \
       while (!(cond)) {                                                               \
         __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);                                     \
-        if (++sp_ == DTW_SPIN_CHECK) {                                                \
+        if (++sp_ > DTW_SPIN_CHECK) {                                                 \
           sp_ = 0;                                                                    \
-          w0_ = dtw_spin_check(a.sync, a.diag, (role), b, ctr, Ein, nr, w0_, ++rounds_); \
-          if (!w0_) { return; }                                    \
+          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) { dead_ = 1; break; }                 \
+          const uint64_t now_ = __builtin_amdgcn_s_memrealtime();                     \
+          if (!w0_) w0_ = now_;                                                       \
+          else if (++rounds_ >= 16 && now_ - w0_ > DTW_STALL_TICKS) {                 \
+            dtw_local_stall((role), a.sync, ctr, lane);                               \
+            dead_ = 1; break;                                                         \
+          }                                                                           \
         }                                                                             \
       }                                                                               \
       if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - tr0_;            \
@@ -782,7 +795,12 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         fenced = false;
         __builtin_amdgcn_s_sleep(1);
         if ((++idle & 63) == 0) {
-          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) return;
+          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) {
+            // a wave of this block timed out (SONAR_SPIN_UNTIL): write its diagnostic record here
+            const int st = SONAR_LDS_LD(ctr[DTW_CTR_STALLED]);
+            if (st) dtw_stall(a.sync, a.diag, st, b, ctr, Ein, nr, 0, 0);
+            return;
+          }
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
           if (idle == 64) t_idle = now;
           if (wait_edge) {
@@ -1333,6 +1351,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
   const int64_t i_t = 64 * b0 + 1 + lane, i_b = i_t + 64;
   const bool ok_t = i_t <= nq, ok_b = i_b <= nq;
   uint64_t spins_total = 0;
+  uint32_t dead_ = 0;   // a bounded wait gave up: the wave runs out its loop without waiting
   // DtwArgs::state (diagnostics, nullable): each wave's exit as one word at [8B + wave]: bits
   // 60-63 how (1 finished, 2 saw the block's abort word, 3 timed out, 4 saw the DTW's error word),
   // bits 32-59 its position (sweep / code: chunk step, distance: chunk, feeder: ring block, edge:
@@ -1346,17 +1365,24 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
   };
 #define SONAR_SPIN_UNTIL(role, cond)                                                  \
   do {                                                                                \
-    if (!(cond)) {                                                                    \
+    if (!dead_ && !(cond)) {                                                          \
+      const uint64_t tr0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;           \
       uint64_t w0_ = 0;                                                               \
       uint32_t sp_ = 0, rounds_ = 0;                                                  \
       while (!(cond)) {                                                               \
         __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);                                     \
-        if (++sp_ == DTW_SPIN_CHECK) {                                                \
+        if (++sp_ > DTW_SPIN_CHECK) {                                                 \
           sp_ = 0;                                                                    \
-          w0_ = dtw_spin_check(a.sync, a.diag, (role), b, ctr, Ein, nr, w0_, ++rounds_); \
-          if (!w0_) { dtw_exit(2); return; }                                    \
+          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) { dead_ = 1; break; }                 \
+          const uint64_t now_ = __builtin_amdgcn_s_memrealtime();                     \
+          if (!w0_) w0_ = now_;                                                       \
+          else if (++rounds_ >= 16 && now_ - w0_ > DTW_STALL_TICKS) {                 \
+            dtw_local_stall((role), a.sync, ctr, lane);                               \
+            dead_ = 1; break;                                                         \
+          }                                                                           \
         }                                                                             \
       }                                                                               \
+      if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - tr0_;            \
     }                                                                                 \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
   } while (0)
@@ -1442,7 +1468,13 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
         fenced = false;
         __builtin_amdgcn_s_sleep(1);
         if ((++idle & 63) == 0) {
-          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) { dpos = do_ring ? nextblk : have; dtw_exit(2); return; }
+          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) {
+            const int st = SONAR_LDS_LD(ctr[DTW_CTR_STALLED]);
+            if (st) dtw_stall(a.sync, a.diag, st, b, ctr, Ein, nr, 0, 0);
+            dpos = do_ring ? nextblk : have;
+            dtw_exit(2);
+            return;
+          }
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
           if (idle == 64) t_idle = now;
           if (wait_edge) {
@@ -1469,7 +1501,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
       }
     }
     dpos = do_ring ? nextblk : have;
-    dtw_exit(1);
+    dtw_exit(dead_ ? 2 : 1);
     return;
   }
 
@@ -1542,8 +1574,9 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) SONAR_LDS_ST(cprog, need);
     }
+    if (a.trace && lane == 0) DTW_GLOBAL(a.trace)[8 * B + 6] = spins_total;
     dpos = S;
-    dtw_exit(1);
+    dtw_exit(dead_ ? 2 : 1);
     return;
   }
 
@@ -1553,7 +1586,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
     const int w = wave - 1, h = w >> 1;
     if (h == 1 && !has_b1) {                           // no bottom sub-band: its chunks are never read
       if (lane == 0) SONAR_LDS_ST(ctr[w], 1 << 30);
-      dtw_exit(1);
+      dtw_exit(dead_ ? 2 : 1);
       return;
     }
     double qv[DR];
@@ -1620,8 +1653,9 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
       rrow += 2 * DTW_ECH;
       if (rrow >= DTW2_RROWS) rrow -= DTW2_RROWS;
     }
+    if (a.trace && lane == 0 && w == 0) DTW_GLOBAL(a.trace)[8 * B + 7] = spins_total;
     dpos = 1 << 27;
-    dtw_exit(1);
+    dtw_exit(dead_ ? 2 : 1);
     return;
   }
 
@@ -1729,11 +1763,27 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
     *reinterpret_cast<double2*>(&oring[1][lane][sl]) = make_double2(ob, out_b);
   };
 
+  // SONAR_DTW_TRACE (a.trace, diagnostics): per 128-row band [8B + 0..7]: start, first chunk ready,
+  // end (s_memrealtime, 10 ns), then the sweep's wait ticks by the first missing input: distances,
+  // top edge, code wave; [6] the code wave's and [7] distance wave 0's wait ticks
+  uint64_t tw_[3] = {0, 0, 0};
+  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto why = [&](int s0, Ctrs k) -> int {
+    const int c = s0 >> 3;
+    const int dt_ = (c & 1) ? k.d1 : k.d0, db_ = (c & 1) ? k.d3 : k.d2;
+    if (!(dt_ > c && db_ > c)) return 0;
+    const int neede = s0 + DTW_ECH < nr32 ? s0 + DTW_ECH : nr32;
+    return (Ein && k.ef < neede) ? 1 : 2;
+  };
   double dt[DTW_ECH], db[DTW_ECH], ech[DTW_ECH];
   Ctrs kc = load_ctr();
   if (!ready(0, kc)) {
+    const int w_ = why(0, kc);
+    const uint64_t t0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
     SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready(0, kc)));
+    if (a.trace) tw_[w_] += __builtin_amdgcn_s_memrealtime() - t0_;
   }
+  const uint64_t t_first = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
   load_part(0, 0, 0, DTW_ECH, dt, db, ech);
   fix_edges(0, ech);
   int sb = 0;
@@ -1780,7 +1830,10 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
       kc = load_ctr();
       load_part(s1, sbn, 0, DTW_ECH, dtn, dbn, echn);
       if (!ready(s1, kc)) {
+        const int w_ = why(s1, kc);
+        const uint64_t t0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
         SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready(s1, kc)));
+        if (a.trace) tw_[w_] += __builtin_amdgcn_s_memrealtime() - t0_;
         load_part(s1, sbn, 0, DTW_ECH, dtn, dbn, echn);
       }
     }
@@ -1789,8 +1842,17 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
     for (int u = 0; u < DTW_ECH; ++u) { dt[u] = dtn[u]; db[u] = dbn[u]; ech[u] = echn[u]; }
     sb = sbn;
   }
+  if (a.trace && lane == 0) {
+    auto* tr = DTW_GLOBAL(a.trace);
+    tr[8 * B + 0] = t_start;
+    tr[8 * B + 1] = t_first;
+    tr[8 * B + 2] = __builtin_amdgcn_s_memrealtime();
+    tr[8 * B + 3] = tw_[0];
+    tr[8 * B + 4] = tw_[1];
+    tr[8 * B + 5] = tw_[2];
+  }
   dpos = S;
-  dtw_exit(1);
+  dtw_exit(dead_ ? 2 : 1);
   (void)spins_total;
   (void)S2;
 #undef SONAR_SPIN_UNTIL
