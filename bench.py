@@ -303,7 +303,9 @@ def load_pmc_bytes(pattern, kernel_prefix):
 def bench_dtw(ctx, n, steps, parity=False):
     """C3-size DTW (51,676 x 51,676, 12-dim) through the sonar_dtw host entry (H2D of the inputs,
     D2H of the path): cells/s end to end, per-kernel HIP-event times (band sweep, walk, path
-    decode) and the band sweep's roofline: 8.25 B/cell of HBM writes (C + direction codes)."""
+    decode) and the band sweep's roofline: bound by the wavefront's dependency chain (chain steps x
+    the isolated step time of one band), with the HBM roof beside it at the checkpoint mode's
+    0.625 algorithmic B/cell and the PMC bytes of the newest profiles/*dtw_pmc*.json."""
     rng = np.random.default_rng(7)
     q = rng.random((n, 12))
     r = np.roll(q, 37, axis=0) + 0.01 * rng.random((n, 12))

@@ -1860,6 +1860,306 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
 #undef SONAR_LDS_ST
 }
 
+// ------------------------------------------------------------------ one wave per band ----
+// dtw_wave_kernel: the same cells, the same arithmetic in the same order and the same outputs as
+// dtw_band_kernel<12, FAST, !BANDED> in checkpoint mode (Dn direction words, CK checkpoint
+// columns, E bottom edges), with every role of that kernel's 8-wave block folded into ONE wave per
+// 64-row band: lane l = row 64b+1+l computes its own local distances (reference rows from a
+// 128-row LDS ring the wave refills itself, 16 rows two chunks ahead), the min-chain (DPP
+// wave_shr:1), findPreviousStep's 2-bit code (dtw.go:191-217) from the same up / left / diagonal
+// values, its checkpoint value, and polls the band above's edge row from E itself (sc1 global
+// loads two chunks ahead).  No LDS counters, no hand-offs inside a band.
+//  * Why: in the 8-wave block the CU's issue slots go to waves that mostly wait (C5: ~196 ns per
+//    band step with two blocks per CU, ~40 % VALU busy), and 52 KB of LDS per band leaves 512 of a
+//    51,676-row DTW's 808 bands resident.  Here a band costs 15 KB and 1 wave: every band of C3 is
+//    resident, and under C5 the distances of one wave fill the latency of another's chain.
+//  * Pipelining inside the wave: iteration c sweeps chunk c (8 steps) with distances computed in
+//    iteration c-1 and computes chunk c+1's sums in the same basic block, so the independent sums
+//    fill the min-chain's latency.
+constexpr int DTWW_RROWS = 128;            // reference rows in the LDS ring (+ DTWW_CH mirrored)
+constexpr int DTWW_DS = 14;                // doubles per ring row: 112 B, b128 reads conflict-free
+constexpr int DTWW_CH = 8;                 // steps per chunk
+#ifndef DTWW_EAHEAD
+#define DTWW_EAHEAD 1                      // chunks between an edge poll and its use (A/B 1-3: 1 best)
+#endif
+
+// lane 0 <- lane u of v (DPP row_shl:u; lanes 1..63 get values nobody reads)
+template <int U>
+__device__ __forceinline__ double from_lane(double v) {
+  if constexpr (U == 0) {
+    return v;
+  } else {
+    const int2 a = __builtin_bit_cast(int2, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, a.x, 0x100 + U, 0xf, 0xf, true);    // row_shl:U
+    const int hi = __builtin_amdgcn_update_dpp(0, a.y, 0x100 + U, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, make_int2(lo, hi));
+  }
+}
+
+// LDS written by one lane and read by another of the same wave: the hardware keeps a wave's LDS
+// requests in order, so only the compiler has to be kept from moving accesses across this point
+__device__ __forceinline__ void dtw_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// waves per SIMD the register allocation aims at: the single DTW (C3: about one band per SIMD)
+// takes the latency-optimal schedule, a batch of many DTWs several waves per SIMD
+#ifndef DTWW_MINW_BATCH
+#define DTWW_MINW_BATCH 1
+#endif
+#ifndef DTWW_MINW_ONE
+#define DTWW_MINW_ONE 1
+#endif
+template <bool BATCH>
+__global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
+  __shared__ __attribute__((aligned(16))) double ring[(DTWW_RROWS + DTWW_CH) * DTWW_DS];
+  __shared__ __attribute__((aligned(16))) double ebuf[2][DTWW_CH];   // lane 63's C of a chunk (parity)
+  __shared__ __attribute__((aligned(16))) int ctr[16];               // dtw_stall's counter layout
+  const int lane = threadIdx.x;
+  const double inf = __builtin_inf();
+  // ---- ticket -> (DTW, band): taken at the block's start, so every band with a smaller ticket
+  // (this band's predecessor among them) is already running
+  int64_t tb = 0;
+  int tk = 0, tt = 0;
+  if (lane == 0) {
+    if constexpr (BATCH) {
+      const int t = atomicAdd(bt.ticket, 1);
+      tt = t;
+      if (bt.map) {
+        if (t < bt.start[bt.n]) {
+          const int2 pb = bt.map[t];
+          tk = pb.x;
+          tb = pb.y;
+        } else {
+          tb = INT64_MAX;
+        }
+      } else {
+        int lo = 0, hi = bt.n;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (bt.start[mid] <= t) lo = mid; else hi = mid;
+        }
+        tk = lo;
+        tb = t - bt.start[lo];
+      }
+    } else {
+      tb = atomicAdd(&a_in.sync[0], 1);
+      tt = (int)tb;
+    }
+  }
+  const int64_t b = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(tb >> 32)) << 32) |
+                              (uint32_t)__builtin_amdgcn_readfirstlane((int)tb));
+  const DtwArgs a = BATCH ? load_args_uniform(bt.args + __builtin_amdgcn_readfirstlane(tk)) : a_in;
+  if (b >= a.nb) return;
+  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  const int64_t nq = a.nq, nr = a.nr, S = a.S;
+  const int nr32 = (int)nr;
+  const uint64_t* Ein = b > 0 ? a.E + (b - 1) * (nr + 1) : nullptr;        // C[64b][j] at index j
+  uint64_t* Eout = (b + 1 < a.nb) ? a.E + b * (nr + 1) : nullptr;         // C[64b+64][j]
+  const int64_t i = 64 * b + 1 + lane;
+  const bool row_ok = i <= nq;
+  const int64_t qrow = row_ok ? i - 1 : 0;
+  double qv[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) qv[k] = DTW_GLOBAL(a.q)[qrow * 12 + k];
+  // the ring starts zeroed (rows before column 1 are read for cells nobody keeps)
+  for (int k = lane; k < (DTWW_RROWS + DTWW_CH) * DTWW_DS / 2; k += 64)
+    *reinterpret_cast<double2*>(&ring[2 * k]) = make_double2(0.0, 0.0);
+  if (lane < 16) ctr[lane] = lane == DTW_CTR_TICKET ? __builtin_amdgcn_readfirstlane(tt) : 0;
+  dtw_wave_sync();
+  // reference rows in blocks of 16 (192 doubles: 3 per lane), rows past nr as zeros
+  auto fetch = [&](int64_t k, double (&v)[3]) {
+    const int64_t row = 16 * k + (lane >> 2);
+    if (row < nr) {
+      const auto* p = DTW_GLOBAL(a.r) + row * 12 + 3 * (lane & 3);
+      v[0] = p[0]; v[1] = p[1]; v[2] = p[2];
+    } else {
+      v[0] = v[1] = v[2] = 0.0;
+    }
+  };
+  auto put = [&](int64_t k, const double (&v)[3]) {
+    const int slot = (int)((16 * k + (lane >> 2)) & (DTWW_RROWS - 1));
+    double* d = ring + slot * DTWW_DS + 3 * (lane & 3);
+    d[0] = v[0]; d[1] = v[1]; d[2] = v[2];
+    if (slot < DTWW_CH) {
+      d += DTWW_RROWS * DTWW_DS;
+      d[0] = v[0]; d[1] = v[1]; d[2] = v[2];
+    }
+  };
+  // the 8 cells of one chunk: sums in Go's order (distance.go:29-36, unfused), interleaved
+#ifndef DTWW_DG
+#define DTWW_DG 8                          // cells interleaved per pass of the sums
+#endif
+  auto sums = [&](int64_t t0, double (&sm)[DTWW_CH]) {
+    const double* rw0 = ring + (int)((t0 - lane) & (DTWW_RROWS - 1)) * DTWW_DS;
+#pragma unroll
+    for (int g = 0; g < DTWW_CH; g += DTWW_DG) {
+#pragma unroll
+      for (int k = 0; k < 12; k += 2) {
+        double2 rv[DTWW_DG];
+#pragma unroll
+        for (int u = 0; u < DTWW_DG; ++u) rv[u] = *reinterpret_cast<const double2*>(rw0 + (g + u) * DTWW_DS + k);
+#pragma unroll
+        for (int u = 0; u < DTWW_DG; ++u) {
+          const double d0 = qv[k] - rv[u].x;
+          sm[g + u] = k == 0 ? d0 * d0 : sm[g + u] + d0 * d0;   // 0.0 + x == x for x >= +0 or NaN
+          const double d1 = qv[k + 1] - rv[u].y;
+          sm[g + u] = sm[g + u] + d1 * d1;
+        }
+      }
+    }
+  };
+  auto roots = [&](const double (&sm)[DTWW_CH], double (&dv)[DTWW_CH]) {
+    double mn = sm[0];
+#pragma unroll
+    for (int u = 1; u < DTWW_CH; ++u) mn = vmin_f64(mn, sm[u]);
+    if (__builtin_amdgcn_ballot_w64(!(mn >= DTW_SQRT_MIN)) == 0) {
+#pragma unroll
+      for (int u = 0; u < DTWW_CH; ++u) dv[u] = sqrt_normal(sm[u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < DTWW_CH; ++u) dv[u] = sqrt(sm[u]);
+    }
+  };
+  // top edge of chunk c (columns 8c+1 .. 8c+8) in lanes 0..7, raw words (sentinel = not yet)
+  auto poll = [&](int64_t c) -> uint64_t {
+    const int64_t col = DTWW_CH * c + 1 + lane;
+    return (Ein && lane < DTWW_CH && col <= nr) ? g_load_agent(Ein + col) : 0ull;
+  };
+  auto missing = [&](int64_t c, uint64_t raw) -> uint64_t {
+    const int64_t col = DTWW_CH * c + 1 + lane;
+    return __builtin_amdgcn_ballot_w64(Ein && lane < DTWW_CH && col <= nr && raw == DTW_SENT);
+  };
+
+  double blk[3];
+  fetch(0, blk);
+  put(0, blk);
+  dtw_wave_sync();
+  fetch(1, blk);
+  const int64_t nch = (S + DTWW_CH - 1) / DTWW_CH;
+  uint64_t ewq[DTWW_EAHEAD];                          // polls of chunks c .. c+EAHEAD-1
+#pragma unroll
+  for (int k = 0; k < DTWW_EAHEAD; ++k) ewq[k] = k < nch ? poll(k) : 0ull;
+  double sm[DTWW_CH], dv[DTWW_CH];
+  sums(0, sm);
+  roots(sm, dv);
+  double out = inf;                                   // C[i][j-1]; C[i][0] = +Inf
+  double up_prev = (lane == 0 && b == 0) ? 0.0 : inf; // C[i-1][j-1]; C[0][0] = 0
+  double ckv = 0.0;                                   // the lane's C at its latest multiple-of-64 column
+  uint32_t dacc = 0;
+  uint64_t spins = 0, t_first = 0;
+  __attribute__((address_space(1))) uint32_t* Db = DTW_GLOBAL(a.Dn) + ((b * a.SW) << 6) + lane;
+  for (int64_t c = 0; c < nch; ++c) {
+    const int64_t s0 = DTWW_CH * c, s1 = s0 + DTWW_CH;
+    if (b == a.dbg_stall && s0 >= 1024) return;        // fault injection (tests only)
+    // reference rows: block m+1 into the ring and block m+2 requested at chunk 2m (block m+1's
+    // slots were last read by chunk 2m-5; it is first read by chunk 2m+1's distances)
+    if ((c & 1) == 0) {
+      put((c >> 1) + 1, blk);
+      dtw_wave_sync();
+      fetch((c >> 1) + 2, blk);
+    }
+    // this chunk's top edge (polled two chunks ago), then the poll of chunk c+2
+    uint64_t ew = ewq[0];
+    uint64_t miss = missing(c, ew);
+    if (miss) {
+      const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t polls = 0;
+      do {
+        __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);
+        if (ew == DTW_SENT) ew = poll(c);
+        miss = missing(c, ew);
+        if (miss && (++polls & 63) == 0) {
+          if (__builtin_amdgcn_readfirstlane(g_load_agent(&a.sync[1]))) return;   // another band gave up
+          const uint64_t now = __builtin_amdgcn_s_memrealtime();
+          if (polls >= DTW_STALL_POLLS && now - w0 > DTW_STALL_TICKS) {
+            if (lane == 0) {
+              ctr[DTW_CTR_PROG] = (int)s0;
+              ctr[DTW_CTR_CPROG] = (int)s0;
+              ctr[DTW_CTR_EFILL] = (int)s0 + __builtin_ctzll(miss);
+              ctr[DTW_CTR_RDY] = (int)((s0 + 15) >> 4);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            dtw_stall(a.sync, a.diag, DTW_ROLE_EDGE, b, ctr, Ein, nr, polls, w0);
+            return;
+          }
+        }
+      } while (miss);
+      spins += __builtin_amdgcn_s_memrealtime() - w0;
+    }
+    if (a.trace && c == 0) t_first = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+    for (int k = 0; k + 1 < DTWW_EAHEAD; ++k) ewq[k] = ewq[k + 1];
+    ewq[DTWW_EAHEAD - 1] = c + DTWW_EAHEAD < nch ? poll(c + DTWW_EAHEAD) : 0ull;
+    const int64_t colc = s0 + 1 + lane;                // lanes 0..7: C[64b][colc]
+    const double e = (Ein && colc <= nr) ? __builtin_bit_cast(double, ew) : inf;
+    // next chunk's sums, in the same basic block as this chunk's steps (no branch between them):
+    // the independent sums fill the min-chain's latency.  Past the last chunk they read rows nobody
+    // keeps.
+    double smn[DTWW_CH];
+    sums(s1, smn);
+    // ---- the chunk's steps.  A lane keeps C[i][j] only for its row <= nq and j in [1, nr] (rows
+    // past nq stay +Inf: nothing reads them; dtw_band_kernel also fills them in full chunks)
+    const int jm1 = row_ok ? (int)s0 - lane : INT32_MIN;   // j - 1 at the chunk's first step
+    double o[DTWW_CH];
+    auto step = [&](auto u_tag, double d) {
+      constexpr int u = decltype(u_tag)::value;
+      const int64_t s = s0 + u;
+      const double up = shr1(out, from_lane<u>(e));      // C[i-1][j]; lane 0: C[64b][s+1]
+      const double left = out, dg = up_prev;
+      const double best = vmin_f64(up, vmin_f64(left, dg));
+      const uint32_t code = best == up ? 0u : (best == left ? 1u : 2u);
+      dacc |= code << (2 * ((s0 & 8) + u));
+      const double v = d + best;
+      if ((uint32_t)(jm1 + u) < (uint32_t)nr32) out = v;
+      up_prev = up;
+      if ((((int)s + 1 - lane) & 63) == 0) ckv = out;  // column j = s - l + 1 is a multiple of 64
+      o[u] = out;
+      if constexpr (u == 6) {
+        // every lane holds C[i][J] for J = s0 - 56 (lanes 57-63 met it in this chunk, lane 0
+        // meets J + 64 at step 7): one coalesced 512-B checkpoint store per 64 steps
+        const int64_t J = s0 - 56;
+        if ((s0 & 63) == 56 && J >= 64 && J <= nr)
+          DTW_GLOBAL(a.CK)[((b * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = ckv;
+      }
+    };
+    step(std::integral_constant<int, 0>{}, dv[0]);
+    step(std::integral_constant<int, 1>{}, dv[1]);
+    step(std::integral_constant<int, 2>{}, dv[2]);
+    step(std::integral_constant<int, 3>{}, dv[3]);
+    step(std::integral_constant<int, 4>{}, dv[4]);
+    step(std::integral_constant<int, 5>{}, dv[5]);
+    step(std::integral_constant<int, 6>{}, dv[6]);
+    step(std::integral_constant<int, 7>{}, dv[7]);
+    // direction words: steps 16w .. 16w+15 (or the last ones)
+    if ((s0 & 8) || s1 >= S) {
+      Db[(s0 >> 4) << 6] = dacc;
+      dacc = 0;
+    }
+    // bottom edge: lane 63's C of the chunk's steps -> lanes 0..7 -> one sc1 store each
+    if (Eout) {
+      double* eb = ebuf[c & 1];
+      if (lane == 63) {
+#pragma unroll
+        for (int u = 0; u < DTWW_CH; u += 2) *reinterpret_cast<double2*>(eb + u) = make_double2(o[u], o[u + 1]);
+      }
+      dtw_wave_sync();
+      const int64_t je = s0 + lane - 62;               // lane 63's column at step s0 + lane
+      if (lane < DTWW_CH && je >= 1 && je <= nr) g_store_agent(Eout + je, __builtin_bit_cast(uint64_t, eb[lane]));
+    }
+    roots(smn, dv);
+  }
+  if (a.trace && lane == 0) {
+    auto* tr = DTW_GLOBAL(a.trace);
+    tr[8 * b + 0] = t_start;
+    tr[8 * b + 1] = t_first;
+    tr[8 * b + 2] = __builtin_amdgcn_s_memrealtime();
+    tr[8 * b + 3] = spins;
+  }
+  (void)nr32;
+}
+
 // Single wave: backtrack (dtw.go:165-188) over the 2-bit direction codes.  The walk is
 // inherently sequential, so it only emits its own moves (2 bits per step, 16 per word, stored
 // 64 words at a time); dtw_path_decode_kernel turns them into points and costs in parallel.
@@ -2522,6 +2822,19 @@ bool dtw_band2_enabled(int dim) {
   return e && e[0] == '1' && dim == 12;
 }
 
+// SONAR_DTW_WAVE=0: the 8-wave dtw_band_kernel instead of the one-wave dtw_wave_kernel for 12-dim
+// FAST checkpoint-mode DTWs (A/B)
+static bool dtw_wave_enabled() {
+  const char* e = std::getenv("SONAR_DTW_WAVE");
+  return !(e && e[0] == '0');
+}
+// the single DTW (one chain of bands, latency-bound) keeps the 8-wave band kernel unless
+// SONAR_DTW_WAVE=1 asks for the one-wave kernel there too
+static bool dtw_wave_one_enabled() {
+  const char* e = std::getenv("SONAR_DTW_WAVE");
+  return e && e[0] == '1';
+}
+
 // SONAR_DTW_SERIAL_WALK=1: the one-wave serial backtrack instead of the backtrack by bands (A/B)
 static bool dtw_serial_walk() {
   const char* e = std::getenv("SONAR_DTW_SERIAL_WALK");
@@ -2623,6 +2936,8 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
       else hipLaunchKernelGGL((dtw_band2_kernel<12, false, false, false>), grid2, block, 0, s, a, nob);
     }
   }
+  else if (dim == 12 && !Cn && fast && band <= 0 && dtw_wave_one_enabled())
+    hipLaunchKernelGGL(dtw_wave_kernel<false>, grid, dim3(64), 0, s, a, nob);
   else if (dim == 12) SONAR_DTW_LAUNCH(12);
   else if (dim == 1) SONAR_DTW_LAUNCH(1);
   else SONAR_DTW_LAUNCH(0);
@@ -2688,6 +3003,8 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
   } else if (dtw_band2_enabled(12)) {   // tickets are 128-row bands (the caller's map and starts)
     hipLaunchKernelGGL((dtw_band2_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
                        0, s, none, bt);
+  } else if (!hargs[0].Cn && dtw_wave_enabled()) {
+    hipLaunchKernelGGL(dtw_wave_kernel<true>, dim3((unsigned)total_bands), dim3(64), 0, s, none, bt);
   } else {
     hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
                        0, s, none, bt);

@@ -77,6 +77,7 @@ struct MfccPairParams {
   int pow2;             // F5: MFCC.Compute fed |X|^2 -> filterbank of |X|^4
   float* out;           // [F][n_mfcc]
   int lds_src, lds_dct, lds_wave0, lds_bytes;
+  int waves_per_block;  // 4: mfcc_pair_kernel; 8: mfcc_pair2_kernel (two pairs per wave at a time)
 };
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s);
 int mfcc_pair_wave_bytes();

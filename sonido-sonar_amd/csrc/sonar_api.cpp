@@ -514,18 +514,25 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
       q.lds_src = al(64 * t.JS * 8);
       q.lds_dct = q.lds_src + 64 * 16 * 2;
       q.lds_wave0 = q.lds_dct + al(16 * (t.NMP + 4) * 4);
-      q.lds_bytes = q.lds_wave0 + 4 * sonar::mfcc_pair_wave_bytes();
+      // mfcc_pair_kernel (4 waves, 3 blocks per CU); SONAR_MFCC_PAIR2=1: mfcc_pair2_kernel (8 waves x
+      // two pairs each, one block per CU; measured 3-6 % slower, DESIGN.md Kernel 1a) when its 16
+      // wave regions fit next to the tables
+      const char* p2env = std::getenv("SONAR_MFCC_PAIR2");
+      const bool two = p2env && p2env[0] == '1' && q.lds_wave0 + 16 * sonar::mfcc_pair_wave_bytes() <= 160 * 1024;
+      q.waves_per_block = two ? 8 : 4;
+      q.lds_bytes = q.lds_wave0 + (two ? 16 : 4) * sonar::mfcc_pair_wave_bytes();
       int dev_cus = 256;
       hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
-      const int64_t NP = (F + 1) / 2, target_waves = (int64_t)dev_cus * 12;
+      const int64_t NP = (F + 1) / 2, target_waves = (int64_t)dev_cus * (two ? 8 : 12);
       q.pairs_per_wave = std::max<int64_t>(1, (NP + target_waves - 1) / target_waves);
+      if (two) q.pairs_per_wave += q.pairs_per_wave & 1;   // whole iterations of two pairs
       if (std::getenv("SONAR_DEBUG_SYNC")) hipDeviceSynchronize();
       hipEvent_t tend = timed_begin(c, s);
       if (sonar::launch_mfcc_pair(q, s) != 0)
         return fail(c, SONAR_ERR_DEVICE, std::string("mfcc kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
       timed_end(c, s, tend);
       pair_done = true;
-      c->last_fp_kernel = "mfcc_pair_kernel";
+      c->last_fp_kernel = two ? "mfcc_pair2_kernel" : "mfcc_pair_kernel";
     }
   }
   if (need_fft && !generic && !pair_done) {

@@ -4,6 +4,9 @@ of analyzers/spectral.go:385-545 + spectral/mfcc.go:113-245) on the configuratio
 route to it (f32 PCM, f32 output, MFCC only, W = 1024), and against the general fused
 kernel (SONAR_FP_GENERIC) on the same input.
 
+Both headline kernels are covered: mfcc_pair_kernel (the default) and mfcc_pair2_kernel (two
+pairs per wave, SONAR_MFCC_PAIR2=1).
+
 Tolerance (north_star: float features within 1e-4 relative): 1e-4 of the frame's MFCC
 L2 norm -- the near-zero coefficients c1..c12 carry rounding of the large c0, so a
 per-coefficient relative bound is not meaningful in f32."""
@@ -29,9 +32,21 @@ def _ref(x, H=256, sr=44100, nm=40, nc=13, power=False, win="hann"):
     return O.mfcc_frames(mag ** 2 if power else mag, sr, n_coef=nc, n_mels=nm)
 
 
-def _fp(ctx, x, cfg, kernel="mfcc_pair_kernel"):
+_EXPECT = {"kernel": "mfcc_pair_kernel"}
+
+
+@pytest.fixture(params=["mfcc_pair_kernel", "mfcc_pair2_kernel"], autouse=True)
+def pair_kernel(request, monkeypatch):
+    """every test runs on both headline kernels: the one-pair default and the two-pairs-per-wave
+    variant (SONAR_MFCC_PAIR2=1)"""
+    monkeypatch.setenv("SONAR_MFCC_PAIR2", "1" if request.param == "mfcc_pair2_kernel" else "0")
+    _EXPECT["kernel"] = request.param
+    return request.param
+
+
+def _fp(ctx, x, cfg, kernel=None):
     out = ctx.fingerprint(x, cfg)["mfcc"]
-    assert ctx.last_fp_kernel() == kernel
+    assert ctx.last_fp_kernel() == (kernel or _EXPECT["kernel"])
     again = ctx.fingerprint(x, cfg)["mfcc"]
     assert np.array_equal(out, again, equal_nan=True), "nondeterministic: " + str(
         np.nonzero(np.any(out != again, axis=1))[0][:16].tolist())
@@ -81,7 +96,7 @@ def test_filterbank_shapes(ctx, sr, nm, nc):
     x = synth.c2_hour(seconds=2.0)
     # 64 mels at 48 kHz needs > 64 filterbank chunks: served by the general kernel
     got = _fp(ctx, x, _cfg(ctx, sample_rate=sr, n_filters=nm, n_mfcc=nc),
-              "fp_wave_kernel" if nm == 64 else "mfcc_pair_kernel")
+              "fp_wave_kernel" if nm == 64 else None)
     ref = _ref(x, sr=sr, nm=nm, nc=nc)
     assert _err(got, ref) < 1e-4
 

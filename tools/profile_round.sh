@@ -18,7 +18,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
   echo "$c done"
 done
 # per-launch HBM bytes -> profiles/<tag>_traffic.json (read by bench.py's roofline.traffic)
-(cd "$R" && python3 tools/traffic_summary.py "$OUT" "$TAG" mfcc_pair_kernel > "$OUT/traffic_summary.log") \
+(cd "$R" && python3 tools/traffic_summary.py "$OUT" "$TAG" mfcc_pair > "$OUT/traffic_summary.log") \
     || { echo "traffic summary failed"; exit 1; }
 timeout -k 10 600 python3 "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; exit 1; }
 cat "$OUT/bench.json"

@@ -8,6 +8,7 @@ for t in "$@"; do
   EV=""
   if [ $t = default ]; then L=sonido-sonar_amd/lib/libsonar_gpu.so;
   elif [ $t = b2 ]; then L=sonido-sonar_amd/lib/libsonar_gpu.so; EV="SONAR_DTW_BAND2=1";   # 128-row band kernel
+  elif [ $t = band ]; then L=sonido-sonar_amd/lib/libsonar_gpu.so; EV="SONAR_DTW_WAVE=0";   # 8-wave band kernel
   else L=sonido-sonar_amd/lib_$t/libsonar_gpu.so; fi
   env $EV SONAR_LIB=$PWD/$L timeout -k 10 120 python tools/scratch/dtw_band_ms.py 51676 5 || { echo "dtw fail $t"; exit 1; }
   env $EV SONAR_LIB=$PWD/$L timeout -k 10 200 python tools/c5_stress.py --reps $REPS > gpurun_out/abs_$t.jsonl 2>gpurun_out/abs_$t.err || { echo "c5 fail $t"; exit 1; }

@@ -1,7 +1,7 @@
 """Micro-benchmark of the fused path-A kernel variants on 1 h of C2 PCM (device resident).
 Prints one line per variant: average kernel ms from HIP events over N launches."""
 import os, sys, json
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "sonido-sonar_amd"), ROOT]
 import torch, sonar
 from sonar import shard
