@@ -127,6 +127,12 @@ int sonar_dtw_last_timing(sonar_ctx* ctx, double* ms3);
  * SONAR_ERR_DEVICE with a diagnostic text in sonar_last_error), out4[3] waves
  * that timed out.  reset != 0 zeroes them after reading -- diagnostics. */
 int sonar_dtw_counters(sonar_ctx* ctx, int64_t* out4, int32_t reset);
+/* Frees the device and pinned host buffers this context (and its sonar_align_pairs
+ * worker contexts) cache between calls; the tables and streams stay.  The next call
+ * allocates what it needs again.  sonar_align_pairs' workers keep up to ~70 % of the
+ * device memory that was free when it ran: trim releases it.  No Go counterpart
+ * (memory management of this library). */
+int sonar_trim(sonar_ctx* ctx);
 
 /* ---- sizes (same integer rules as the Go code) ------------------------ */
 /* (n - W)/H + 1, Go truncating division; <= 0 -> SONAR_ERR_TOO_SHORT

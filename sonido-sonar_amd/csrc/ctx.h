@@ -89,6 +89,8 @@ namespace sonar {
 namespace detail {
 int fail(sonar_ctx* c, int code, const std::string& msg);
 void* dbuf(sonar_ctx* c, const std::string& name, size_t bytes);
+// frees every cached device / pinned host buffer of c (sonar_trim; the batch path's NOMEM retry)
+void trim_buffers(sonar_ctx* c);
 void* hbuf(sonar_ctx* c, const std::string& name, size_t bytes);
 // DTW with the local distances precomputed (dtw_dist_kernel + the 4-wave band kernel) for this
 // feature dimension; opt-in with SONAR_DTW_PRE=1 (the distance waves inside the band kernel are

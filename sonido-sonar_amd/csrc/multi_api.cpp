@@ -422,8 +422,22 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
     th.emplace_back([&, t] {
       sonar_ctx* w = ws[t];
       for (size_t bi = next.fetch_add(1); bi < batches.size(); bi = next.fetch_add(1)) {
-        const int r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window,
-                                  device_ptrs, out, &redo[t], &errs[t]);
+        int r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window,
+                            device_ptrs, out, &redo[t], &errs[t]);
+        if (r == SONAR_ERR_NOMEM) {
+          // the worker's cached buffers are sized by earlier batches, name by name: release them
+          // and retry the batch once; then pair by pair on the unbatched path
+          sonar::detail::trim_buffers(w);
+          r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window, device_ptrs,
+                          out, &redo[t], &errs[t]);
+          if (r == SONAR_ERR_NOMEM) {
+            sonar::detail::trim_buffers(w);
+            r = SONAR_OK;
+            for (const auto& p : batches[bi])
+              note(align_one(w, q_pcm[p.k], nq[p.k], r_pcm[p.k], nr[p.k], sample_rate, stft_window, hop,
+                             feature_window, max_lag_seconds, device_ptrs, &out[p.k]), p.k, w);
+          }
+        }
         if (r != SONAR_OK)
           for (const auto& p : batches[bi]) { out[p.k].status = r; note(r, p.k, w); }
       }

@@ -81,6 +81,15 @@ void timed_end(sonar_ctx* c, hipStream_t s, hipEvent_t end) {
   c->ev_used++;
 }
 
+// the cached buffers of one context (not its workers')
+void trim_buffers(sonar_ctx* c) {
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  for (auto& kv : c->bufs) if (kv.second.ptr) hipFree(kv.second.ptr);
+  for (auto& kv : c->hbufs) if (kv.second.ptr) hipHostFree(kv.second.ptr);
+  c->bufs.clear();
+  c->hbufs.clear();
+}
 }  // namespace detail
 }  // namespace sonar
 
@@ -283,6 +292,14 @@ int sonar_enable_kernel_timing(sonar_ctx* c, int on) {
 }
 
 const char* sonar_last_fp_kernel(sonar_ctx* c) { return c ? c->last_fp_kernel : ""; }
+
+
+int sonar_trim(sonar_ctx* c) {
+  if (!c) return SONAR_ERR_INVALID;
+  for (sonar_ctx* w : c->workers) sonar::detail::trim_buffers(w);
+  sonar::detail::trim_buffers(c);
+  return SONAR_OK;
+}
 
 int sonar_dtw_counters(sonar_ctx* c, int64_t* out4, int32_t reset) {
   if (!c || !out4) return SONAR_ERR_INVALID;

@@ -71,6 +71,13 @@ func (x *Context) Close() {
 	}
 }
 
+// Trim frees the device and pinned host buffers the context (and the worker
+// contexts of AlignPairs) cache between calls (sonar_trim); the next call
+// allocates again.
+func (x *Context) Trim() error {
+	return x.err(C.sonar_trim(x.c))
+}
+
 // err maps a return code to a Go error carrying the C side's message, which uses
 // the reference's own error text ("empty signal", "signal too short for given
 // window size and hop size", "empty sequences provided", ...).

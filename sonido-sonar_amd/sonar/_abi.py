@@ -184,6 +184,8 @@ def lib():
     L.sonar_dtw_last_timing.argtypes = [_vp, C.POINTER(C.c_double)]
     if hasattr(L, "sonar_dtw_counters"):      # (absent from A/B builds of earlier rounds)
         L.sonar_dtw_counters.argtypes = [_vp, C.POINTER(C.c_int64), C.c_int32]
+    if hasattr(L, "sonar_trim"):
+        L.sonar_trim.argtypes = [_vp]
     L.sonar_last_fp_kernel.argtypes = [_vp]
     L.sonar_last_fp_kernel.restype = C.c_char_p
     for f in ("sonar_stft_frames", "sonar_energy_frames"):
@@ -381,6 +383,11 @@ class Context:
         self._check(self._L.sonar_dtw_counters(self._h, v, int(bool(reset))))
         return {"edge_refresh_fences": v[0], "edge_refresh_hits": v[1], "dtw_timeouts": v[2],
                 "waves_timed_out": v[3]}
+
+    def trim(self):
+        """Free the device / pinned host buffers this context and its pair workers cache
+        (sonar_trim); the next call allocates again."""
+        self._check(self._L.sonar_trim(self._h))
 
     def last_fp_kernel(self):
         """Name of the fused kernel the last fingerprint call launched (diagnostics)."""

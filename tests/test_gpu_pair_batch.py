@@ -1,7 +1,8 @@
 """The batched pair path of sonar_align_pairs (one band-kernel launch over a batch's chroma DTWs,
 batched walk / path decode, one host sync per batch) against the unbatched path
 (SONAR_PAIR_BATCH=0: one sonar_align_pair_device per pair), and the opt-in precomputed-distance
-DTW (SONAR_DTW_PRE=1: dtw_dist_kernel + the 4-wave band kernel) against the default band kernel.
+DTW (SONAR_DTW_PRE=1: dtw_dist_kernel + the 4-wave band kernel) against the default band kernel,
+and the DTW kernel variants (one-wave batch default, 8-wave band, 128-row) against each other.
 Pairs are independent and both paths run the same arithmetic, so records must be identical
 (NaN-aware), for pairs of different lengths, any batch cut, and a pair whose chroma is not finite
 (the batch redoes it through the exact math.Min path)."""
@@ -90,5 +91,44 @@ def test_precomputed_distance_pairs(ctx, monkeypatch, mixed_pairs):
     qs, rs = mixed_pairs
     ref = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2)
     got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2, SONAR_DTW_PRE=1)
+    for f in sonar.PAIR_FIELDS:
+        assert _same(got[f], ref[f]), f
+
+
+@pytest.mark.parametrize("env", [dict(SONAR_DTW_WAVE=0), dict(SONAR_DTW_BAND2=1)])
+def test_batch_dtw_kernels_agree(ctx, monkeypatch, mixed_pairs, env):
+    """The batch's default one-wave DTW kernel (dtw_wave_kernel) against the 8-wave band kernel
+    (SONAR_DTW_WAVE=0) and the 128-row kernel (SONAR_DTW_BAND2=1): identical records."""
+    qs, rs = mixed_pairs
+    ref = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2)
+    got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2, **env)
+    assert np.all(ref["status"] == 0) and np.all(got["status"] == 0)
+    for f in sonar.PAIR_FIELDS:
+        assert _same(got[f], ref[f]), f
+
+
+@pytest.mark.parametrize("nq,nr", [(1000, 1000), (700, 1333), (63, 65), (4100, 3900), (64, 5000), (3000, 64)])
+def test_wave_kernel_single_dtw_bit_exact(ctx, monkeypatch, nq, nr):
+    """dtw_wave_kernel on a single DTW (SONAR_DTW_WAVE=1) against the band kernel: path, path
+    costs and distance bit-exact, ragged last bands and one-band / one-chunk shapes included."""
+    rng = np.random.default_rng(3 * nq + nr)
+    q = rng.random((nq, 12))
+    r = np.roll(rng.random((nr, 12)), 5, axis=0)
+    ref = ctx.dtw(q, r)
+    monkeypatch.setenv("SONAR_DTW_WAVE", "1")
+    got = ctx.dtw(q, r)
+    monkeypatch.delenv("SONAR_DTW_WAVE")
+    assert got["distance"] == ref["distance"]
+    for k in ("path_q", "path_r", "path_cost"):
+        assert np.array_equal(got[k], ref[k]), k
+
+
+def test_trim_releases_and_reallocates(ctx, monkeypatch, mixed_pairs):
+    """sonar_trim frees the cached buffers of the context and its pair workers; the next call
+    allocates again and gives the same records."""
+    qs, rs = mixed_pairs
+    ref = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2)
+    ctx.trim()
+    got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2)
     for f in sonar.PAIR_FIELDS:
         assert _same(got[f], ref[f]), f
