@@ -1918,8 +1918,11 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
   __shared__ __attribute__((aligned(16))) int ctr[16];               // dtw_stall's counter layout
   const int lane = threadIdx.x;
   const double inf = __builtin_inf();
-  // ---- ticket -> (DTW, band): taken at the block's start, so every band with a smaller ticket
-  // (this band's predecessor among them) is already running
+  // ---- tickets -> (DTW, band).  BATCH: the wave is persistent and takes one ticket after
+  // another (grid = the batch's wave budget, launch_dtw_batch): a band starts only when a wave
+  // is free, so its predecessor (a smaller ticket, taken by a running wave) is usually well ahead
+  // and no wave holds a slot waiting down a chain.  Single DTW: one band per block.
+  for (;;) {
   int64_t tb = 0;
   int tk = 0, tt = 0;
   if (lane == 0) {
@@ -1952,6 +1955,8 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
                               (uint32_t)__builtin_amdgcn_readfirstlane((int)tb));
   const DtwArgs a = BATCH ? load_args_uniform(bt.args + __builtin_amdgcn_readfirstlane(tk)) : a_in;
   if (b >= a.nb) return;
+  [&]() {   // one band; a `return` in it ends the band, not the wave
+  dtw_wave_sync();   // the previous band's LDS reads are behind the ring reset below
   const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
   const int64_t nq = a.nq, nr = a.nr, S = a.S;
   const int nr32 = (int)nr;
@@ -1991,10 +1996,44 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
 #ifndef DTWW_DG
 #define DTWW_DG 8                          // cells interleaved per pass of the sums
 #endif
-  auto sums = [&](int64_t t0, double (&sm)[DTWW_CH]) {
+// DTWW_SCHED: keep each dimension pair's LDS reads behind the previous pair's arithmetic (VALU and
+// SALU may still move across, so the min-chain interleaves): fewer reads hoisted, fewer registers
+#ifdef DTWW_SCHED
+#define DTWW_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0x0006)
+#else
+#define DTWW_SCHED_FENCE() ((void)0)
+#endif
+  auto sums = [&](int64_t t0, double (&sm)[DTWW_CH], int glo = 0, int ghi = DTWW_CH) {
     const double* rw0 = ring + (int)((t0 - lane) & (DTWW_RROWS - 1)) * DTWW_DS;
+#ifdef DTWW_PIPE
+    // one dimension pair's reads in flight ahead of the arithmetic: the empty asm "rewrites" the
+    // sums and clobbers memory, so the reads of pair k+2 cannot be hoisted above pair k's
+    // arithmetic (without it the scheduler issues all 48 reads first: 192 VGPRs)
+    (void)glo; (void)ghi;
+    double2 rv[2][DTWW_CH];
 #pragma unroll
-    for (int g = 0; g < DTWW_CH; g += DTWW_DG) {
+    for (int u = 0; u < DTWW_CH; ++u) rv[0][u] = *reinterpret_cast<const double2*>(rw0 + u * DTWW_DS);
+#pragma unroll
+    for (int k = 0; k < 12; k += 2) {
+      const int cur = (k >> 1) & 1;
+      if (k + 2 < 12) {
+#pragma unroll
+        for (int u = 0; u < DTWW_CH; ++u) rv[cur ^ 1][u] = *reinterpret_cast<const double2*>(rw0 + u * DTWW_DS + k + 2);
+      }
+#pragma unroll
+      for (int u = 0; u < DTWW_CH; ++u) {
+        const double d0 = qv[k] - rv[cur][u].x;
+        sm[u] = k == 0 ? d0 * d0 : sm[u] + d0 * d0;
+        const double d1 = qv[k + 1] - rv[cur][u].y;
+        sm[u] = sm[u] + d1 * d1;
+      }
+      asm volatile("" : "+v"(sm[0]), "+v"(sm[1]), "+v"(sm[2]), "+v"(sm[3]), "+v"(sm[4]), "+v"(sm[5]), "+v"(sm[6]),
+                   "+v"(sm[7]) :: "memory");
+    }
+    return;
+#endif
+#pragma unroll
+    for (int g = glo; g < ghi; g += DTWW_DG) {
 #pragma unroll
       for (int k = 0; k < 12; k += 2) {
         double2 rv[DTWW_DG];
@@ -2007,6 +2046,7 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
           const double d1 = qv[k + 1] - rv[u].y;
           sm[g + u] = sm[g + u] + d1 * d1;
         }
+        DTWW_SCHED_FENCE();
       }
     }
   };
@@ -2050,6 +2090,9 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
   uint32_t dacc = 0;
   uint64_t spins = 0, t_first = 0;
   __attribute__((address_space(1))) uint32_t* Db = DTW_GLOBAL(a.Dn) + ((b * a.SW) << 6) + lane;
+  int64_t st_s0 = -1;                                  // a wait gave up at this chunk (-1: none)
+  uint32_t st_polls = 0;
+  uint64_t st_w0 = 0, st_miss = 0;
   for (int64_t c = 0; c < nch; ++c) {
     const int64_t s0 = DTWW_CH * c, s1 = s0 + DTWW_CH;
     if (b == a.dbg_stall && s0 >= 1024) return;        // fault injection (tests only)
@@ -2074,18 +2117,14 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
           if (__builtin_amdgcn_readfirstlane(g_load_agent(&a.sync[1]))) return;   // another band gave up
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
           if (polls >= DTW_STALL_POLLS && now - w0 > DTW_STALL_TICKS) {
-            if (lane == 0) {
-              ctr[DTW_CTR_PROG] = (int)s0;
-              ctr[DTW_CTR_CPROG] = (int)s0;
-              ctr[DTW_CTR_EFILL] = (int)s0 + __builtin_ctzll(miss);
-              ctr[DTW_CTR_RDY] = (int)((s0 + 15) >> 4);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            dtw_stall(a.sync, a.diag, DTW_ROLE_EDGE, b, ctr, Ein, nr, polls, w0);
-            return;
+            // give up: the record is written after the chunk loop (a call inside the loop
+            // would cost the loop its register allocation)
+            st_s0 = s0; st_polls = polls; st_w0 = w0; st_miss = miss;
+            break;
           }
         }
       } while (miss);
+      if (st_s0 >= 0) break;
       spins += __builtin_amdgcn_s_memrealtime() - w0;
     }
     if (a.trace && c == 0) t_first = __builtin_amdgcn_s_memrealtime();
@@ -2098,7 +2137,11 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
     // the independent sums fill the min-chain's latency.  Past the last chunk they read rows nobody
     // keeps.
     double smn[DTWW_CH];
+#ifndef DTWW_SPLIT
     sums(s1, smn);
+#else
+    sums(s1, smn, 0, DTWW_CH / 2);
+#endif
     // ---- the chunk's steps.  A lane keeps C[i][j] only for its row <= nq and j in [1, nr] (rows
     // past nq stay +Inf: nothing reads them; dtw_band_kernel also fills them in full chunks)
     const int jm1 = row_ok ? (int)s0 - lane : INT32_MIN;   // j - 1 at the chunk's first step
@@ -2128,6 +2171,10 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
     step(std::integral_constant<int, 1>{}, dv[1]);
     step(std::integral_constant<int, 2>{}, dv[2]);
     step(std::integral_constant<int, 3>{}, dv[3]);
+#ifdef DTWW_SPLIT   // the second half of the next chunk's sums beside the second half of the steps
+    __builtin_amdgcn_sched_barrier(0);
+    sums(s1, smn, DTWW_CH / 2, DTWW_CH);
+#endif
     step(std::integral_constant<int, 4>{}, dv[4]);
     step(std::integral_constant<int, 5>{}, dv[5]);
     step(std::integral_constant<int, 6>{}, dv[6]);
@@ -2150,6 +2197,17 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
     }
     roots(smn, dv);
   }
+  if (st_s0 >= 0) {
+    if (lane == 0) {
+      ctr[DTW_CTR_PROG] = (int)st_s0;
+      ctr[DTW_CTR_CPROG] = (int)st_s0;
+      ctr[DTW_CTR_EFILL] = (int)st_s0 + __builtin_ctzll(st_miss);
+      ctr[DTW_CTR_RDY] = (int)((st_s0 + 15) >> 4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    dtw_stall(a.sync, a.diag, DTW_ROLE_EDGE, b, ctr, Ein, nr, st_polls, st_w0);
+    return;
+  }
   if (a.trace && lane == 0) {
     auto* tr = DTW_GLOBAL(a.trace);
     tr[8 * b + 0] = t_start;
@@ -2158,6 +2216,9 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
     tr[8 * b + 3] = spins;
   }
   (void)nr32;
+  }();
+  if constexpr (!BATCH) return;
+  }
 }
 
 // Single wave: backtrack (dtw.go:165-188) over the 2-bit direction codes.  The walk is
@@ -2830,6 +2891,7 @@ static bool dtw_wave_enabled() {
 }
 // the single DTW (one chain of bands, latency-bound) keeps the 8-wave band kernel unless
 // SONAR_DTW_WAVE=1 asks for the one-wave kernel there too
+bool dtw_wave_batch_enabled() { return dtw_wave_enabled(); }
 static bool dtw_wave_one_enabled() {
   const char* e = std::getenv("SONAR_DTW_WAVE");
   return e && e[0] == '1';
@@ -2987,7 +3049,7 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s) {
 }
 
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
-                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap) {
+                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap, int waves) {
   if (n <= 0 || total_bands <= 0) return 0;
   if (total_bands > INT32_MAX) return -1;
   const DtwArgs none{};
@@ -3003,8 +3065,9 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
   } else if (dtw_band2_enabled(12)) {   // tickets are 128-row bands (the caller's map and starts)
     hipLaunchKernelGGL((dtw_band2_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
                        0, s, none, bt);
-  } else if (!hargs[0].Cn && dtw_wave_enabled()) {
-    hipLaunchKernelGGL(dtw_wave_kernel<true>, dim3((unsigned)total_bands), dim3(64), 0, s, none, bt);
+  } else if (!hargs[0].Cn && dtw_wave_batch_enabled()) {
+    const int64_t grid = waves > 0 && waves < total_bands ? waves : total_bands;   // persistent waves
+    hipLaunchKernelGGL(dtw_wave_kernel<true>, dim3((unsigned)grid), dim3(64), 0, s, none, bt);
   } else {
     hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
                        0, s, none, bt);

@@ -231,9 +231,13 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s);
 // DTW in checkpoint mode when SONAR_DTW_BAND2=1; launch_dtw_batch's tickets are then 128-row
 // bands: per DTW ceil(nb / 2) of them, and dmap / dstart count those
 bool dtw_band2_enabled(int dim);
+// otherwise (default; SONAR_DTW_WAVE=0: the 8-wave band kernel) the one-wave kernel
+// (dtw_wave_kernel) runs the batch as `waves` persistent waves taking tickets in order (<= 0: one
+// block per ticket)
+bool dtw_wave_batch_enabled();
 int32_t dtw_dbg_stall_band();   // SONAR_DTW_DBG_STALL (tests only), -1 when unset
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
-                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr);
+                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr, int waves = 0);
 // sets *flag = 1 if any of the n values is not finite
 int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 // the same probe over q and r of every DTW of a batch (sets args[k].sync[2]); max_elems >= every

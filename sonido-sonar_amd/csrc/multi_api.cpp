@@ -130,7 +130,7 @@ size_t pair_bytes(const PairGeo& p) {
 // align_one (exact math.Min rules); their indices are appended to `redo`.
 int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* const* q_pcm, const double* const* r_pcm,
                 int32_t sr, int32_t sw, int32_t hop, int32_t fw, int32_t device_ptrs, sonar_pair_record* out,
-                std::vector<int64_t>* redo, std::vector<std::pair<int64_t, std::string>>* errs) {
+                std::vector<int64_t>* redo, std::vector<std::pair<int64_t, std::string>>* errs, int nstreams) {
   const int n = (int)in.size();
   if (n == 0) return SONAR_OK;
   HIP_TRY(w, hipSetDevice(w->device));
@@ -264,8 +264,19 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   int64_t max_el = 0;
   for (const auto& p : pg) max_el = std::max(max_el, (p.Fq + p.Fr) * 12);
   if (sonar::launch_nonfinite_batch(dargs, n, max_el, s) != 0) return fail(w, SONAR_ERR_DEVICE, "dtw launch failed");
+  // the one-wave DTW kernel: one block per ticket (its waves keep taking tickets while any are
+  // left, so a block launched after the last ticket exits at once).  SONAR_DTW_WAVES=<n> caps the
+  // grid at n persistent waves instead -- measured slower for every n tried (32-160 per stream,
+  // profiles/r03s5_c5_persistent_ab.log): a batch's DTW then cannot take the slots that the other
+  // streams' feature phases leave free
+  int waves = 0;
+  if (!pre && !band2 && sonar::dtw_wave_batch_enabled()) {
+    const char* wev = std::getenv("SONAR_DTW_WAVES");
+    waves = wev ? std::atoi(wev) : 0;
+  }
+  (void)nstreams;
   if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s,
-                              band_major ? dmap : nullptr) != 0)
+                              band_major ? dmap : nullptr, waves) != 0)
     return fail(w, SONAR_ERR_DEVICE, "dtw batch launch failed");
   HIP_TRY(w, hipMemcpyAsync(hstat, small, stat_b + diag_b, hipMemcpyDeviceToHost, s));
   if (corr_b) HIP_TRY(w, hipMemcpyAsync(hcorr, corr, corr_b, hipMemcpyDeviceToHost, s));
@@ -423,13 +434,13 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
       sonar_ctx* w = ws[t];
       for (size_t bi = next.fetch_add(1); bi < batches.size(); bi = next.fetch_add(1)) {
         int r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window,
-                            device_ptrs, out, &redo[t], &errs[t]);
+                            device_ptrs, out, &redo[t], &errs[t], nstreams);
         if (r == SONAR_ERR_NOMEM) {
           // the worker's cached buffers are sized by earlier batches, name by name: release them
           // and retry the batch once; then pair by pair on the unbatched path
           sonar::detail::trim_buffers(w);
           r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window, device_ptrs,
-                          out, &redo[t], &errs[t]);
+                          out, &redo[t], &errs[t], nstreams);
           if (r == SONAR_ERR_NOMEM) {
             sonar::detail::trim_buffers(w);
             r = SONAR_OK;
