@@ -1876,7 +1876,22 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel
 //  * Pipelining inside the wave: iteration c sweeps chunk c (8 steps) with distances computed in
 //    iteration c-1 and computes chunk c+1's sums in the same basic block, so the independent sums
 //    fill the min-chain's latency.
-constexpr int DTWW_RROWS = 128;            // reference rows in the LDS ring (+ DTWW_CH mirrored)
+#ifndef DTWW_RROWS_CFG
+#define DTWW_RROWS_CFG 128
+#endif
+// reference rows in the LDS ring (+ DTWW_CH mirrored).  A chunk reads rows 8c-63 .. 8c+7 and the
+// refill writes the block 16-31 rows past the chunk's rows, so 96 rows suffice (13.6 KB per wave:
+// 11 waves per CU instead of 10); 128 makes the slot a mask
+constexpr int DTWW_RROWS = DTWW_RROWS_CFG;
+static_assert(DTWW_RROWS == 128 || DTWW_RROWS == 96, "ring rows");
+__device__ __forceinline__ int dtww_slot(int64_t row) {
+  if constexpr (DTWW_RROWS == 128) {
+    return (int)(row & 127);
+  } else {
+    const int r = (int)(row % DTWW_RROWS);   // row > -DTWW_RROWS
+    return r < 0 ? r + DTWW_RROWS : r;
+  }
+}
 constexpr int DTWW_DS = 14;                // doubles per ring row: 112 B, b128 reads conflict-free
 constexpr int DTWW_CH = 8;                 // steps per chunk
 #ifndef DTWW_EAHEAD
@@ -1911,8 +1926,24 @@ __device__ __forceinline__ void dtw_wave_sync() {
 #ifndef DTWW_MINW_ONE
 #define DTWW_MINW_ONE 1
 #endif
-template <bool BATCH>
-__global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
+// LEAN (batches only, SONAR_DTW_LEAN): no cross-chunk pipelining inside the wave -- a chunk's
+// distances are computed at its start, fenced off from its steps -- so the register file holds
+// one chunk's state and DTWW_MINW_LEAN waves share a SIMD: the latency one wave cannot fill with its
+// own independent sums is filled by the other waves' work
+#ifndef DTWW_MINW_LEAN
+#define DTWW_MINW_LEAN 2
+#endif
+// MODE 2 (DTWW_IL, opt-in SONAR_DTW_IL=1; measured slower): the next chunk's sums are cut into the six dimension
+// pairs and the two halves of the square roots, and each piece is fenced (sched_barrier) together
+// with ONE step of this chunk, its LDS reads issued one piece ahead.  Without the fences the
+// scheduler hoists all 48 reads and sums above the steps (256 VGPRs + 58 AGPRs) and the steps' DPP /
+// min / add chain then runs alone, its latency exposed; fenced, each step's chain hides behind
+// ~48 independent f64 operations.
+constexpr int DTWW_PIPE_MODE = 0, DTWW_LEAN_MODE = 1, DTWW_IL_MODE = 2;
+template <bool BATCH, int MODE = DTWW_PIPE_MODE>
+__global__ __launch_bounds__(64, MODE == DTWW_LEAN_MODE ? DTWW_MINW_LEAN : (BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE))
+void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
+  constexpr bool LEAN = MODE == DTWW_LEAN_MODE, IL = MODE == DTWW_IL_MODE;
   __shared__ __attribute__((aligned(16))) double ring[(DTWW_RROWS + DTWW_CH) * DTWW_DS];
   __shared__ __attribute__((aligned(16))) double ebuf[2][DTWW_CH];   // lane 63's C of a chunk (parity)
   __shared__ __attribute__((aligned(16))) int ctr[16];               // dtw_stall's counter layout
@@ -1984,7 +2015,7 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
     }
   };
   auto put = [&](int64_t k, const double (&v)[3]) {
-    const int slot = (int)((16 * k + (lane >> 2)) & (DTWW_RROWS - 1));
+    const int slot = dtww_slot(16 * k + (lane >> 2));
     double* d = ring + slot * DTWW_DS + 3 * (lane & 3);
     d[0] = v[0]; d[1] = v[1]; d[2] = v[2];
     if (slot < DTWW_CH) {
@@ -2004,7 +2035,7 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
 #define DTWW_SCHED_FENCE() ((void)0)
 #endif
   auto sums = [&](int64_t t0, double (&sm)[DTWW_CH], int glo = 0, int ghi = DTWW_CH) {
-    const double* rw0 = ring + (int)((t0 - lane) & (DTWW_RROWS - 1)) * DTWW_DS;
+    const double* rw0 = ring + dtww_slot(t0 - lane) * DTWW_DS;
 #ifdef DTWW_PIPE
     // one dimension pair's reads in flight ahead of the arithmetic: the empty asm "rewrites" the
     // sums and clobbers memory, so the reads of pair k+2 cannot be hoisted above pair k's
@@ -2082,8 +2113,10 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
 #pragma unroll
   for (int k = 0; k < DTWW_EAHEAD; ++k) ewq[k] = k < nch ? poll(k) : 0ull;
   double sm[DTWW_CH], dv[DTWW_CH];
-  sums(0, sm);
-  roots(sm, dv);
+  if constexpr (!LEAN) {
+    sums(0, sm);
+    roots(sm, dv);
+  }
   double out = inf;                                   // C[i][j-1]; C[i][0] = +Inf
   double up_prev = (lane == 0 && b == 0) ? 0.0 : inf; // C[i-1][j-1]; C[0][0] = 0
   double ckv = 0.0;                                   // the lane's C at its latest multiple-of-64 column
@@ -2137,11 +2170,20 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
     // the independent sums fill the min-chain's latency.  Past the last chunk they read rows nobody
     // keeps.
     double smn[DTWW_CH];
+    if constexpr (LEAN) {
+      (void)s1;
+      sums(s0, sm);
+      roots(sm, dv);
+      __builtin_amdgcn_sched_barrier(0);
+    } else if constexpr (IL) {
+      // the pieces are interleaved with the steps below
+    } else {
 #ifndef DTWW_SPLIT
-    sums(s1, smn);
+      sums(s1, smn);
 #else
-    sums(s1, smn, 0, DTWW_CH / 2);
+      sums(s1, smn, 0, DTWW_CH / 2);
 #endif
+    }
     // ---- the chunk's steps.  A lane keeps C[i][j] only for its row <= nq and j in [1, nr] (rows
     // past nq stay +Inf: nothing reads them; dtw_band_kernel also fills them in full chunks)
     const int jm1 = row_ok ? (int)s0 - lane : INT32_MIN;   // j - 1 at the chunk's first step
@@ -2167,18 +2209,76 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
           DTW_GLOBAL(a.CK)[((b * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = ckv;
       }
     };
+    if constexpr (IL) {
+      // piece k (k = 0, 2, .., 10): dimensions k, k+1 of the next chunk's 8 cells, in Go's order
+      // (distance.go:29-36, unfused; 0.0 + x == x for the first square)
+      const double* rw0 = ring + dtww_slot(s1 - lane) * DTWW_DS;
+      double2 rva[DTWW_CH], rvb[DTWW_CH];
+      auto rd = [&](double2 (&rv)[DTWW_CH], int k) {
+#pragma unroll
+        for (int u = 0; u < DTWW_CH; ++u) rv[u] = *reinterpret_cast<const double2*>(rw0 + u * DTWW_DS + k);
+      };
+      auto ar = [&](const double2 (&rv)[DTWW_CH], int k) {
+#pragma unroll
+        for (int u = 0; u < DTWW_CH; ++u) {
+          const double d0 = qv[k] - rv[u].x;
+          smn[u] = k == 0 ? d0 * d0 : smn[u] + d0 * d0;
+          const double d1 = qv[k + 1] - rv[u].y;
+          smn[u] = smn[u] + d1 * d1;
+        }
+      };
+      double dvn[DTWW_CH];
+      // the fence keeps the machine scheduler from moving work across; the empty asm "redefines" the
+      // values a piece produced, so earlier passes cannot sink its arithmetic into a later piece
+#define DTWW_PIN(v) asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), \
+                                         "+v"(v[6]), "+v"(v[7]))
+#define DTWW_FENCE() __builtin_amdgcn_sched_barrier(0)
+      rd(rva, 0);
+      DTWW_FENCE();
+      rd(rvb, 2);  step(std::integral_constant<int, 0>{}, dv[0]);  ar(rva, 0);  DTWW_PIN(smn);  DTWW_FENCE();
+      rd(rva, 4);  step(std::integral_constant<int, 1>{}, dv[1]);  ar(rvb, 2);  DTWW_PIN(smn);  DTWW_FENCE();
+      rd(rvb, 6);  step(std::integral_constant<int, 2>{}, dv[2]);  ar(rva, 4);  DTWW_PIN(smn);  DTWW_FENCE();
+      rd(rva, 8);  step(std::integral_constant<int, 3>{}, dv[3]);  ar(rvb, 6);  DTWW_PIN(smn);  DTWW_FENCE();
+      rd(rvb, 10); step(std::integral_constant<int, 4>{}, dv[4]);  ar(rva, 8);  DTWW_PIN(smn);  DTWW_FENCE();
+      step(std::integral_constant<int, 5>{}, dv[5]);  ar(rvb, 10);  DTWW_PIN(smn);  DTWW_FENCE();
+      step(std::integral_constant<int, 6>{}, dv[6]);
+#pragma unroll
+      for (int u = 0; u < DTWW_CH / 2; ++u) dvn[u] = sqrt_normal(smn[u]);
+      asm volatile("" : "+v"(dvn[0]), "+v"(dvn[1]), "+v"(dvn[2]), "+v"(dvn[3]));
+      DTWW_FENCE();
+      step(std::integral_constant<int, 7>{}, dv[7]);
+#pragma unroll
+      for (int u = DTWW_CH / 2; u < DTWW_CH; ++u) dvn[u] = sqrt_normal(smn[u]);
+      asm volatile("" : "+v"(dvn[4]), "+v"(dvn[5]), "+v"(dvn[6]), "+v"(dvn[7]));
+      DTWW_FENCE();
+#undef DTWW_FENCE
+#undef DTWW_PIN
+      // sqrt_normal holds for sums in [2^-767, Inf) only; otherwise the full sqrt (same bits)
+      double mn = smn[0];
+#pragma unroll
+      for (int u = 1; u < DTWW_CH; ++u) mn = vmin_f64(mn, smn[u]);
+      if (__builtin_amdgcn_ballot_w64(!(mn >= DTW_SQRT_MIN)) != 0) {
+#pragma unroll
+        for (int u = 0; u < DTWW_CH; ++u) dvn[u] = sqrt(smn[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < DTWW_CH; ++u) dv[u] = dvn[u];
+    } else {
     step(std::integral_constant<int, 0>{}, dv[0]);
     step(std::integral_constant<int, 1>{}, dv[1]);
     step(std::integral_constant<int, 2>{}, dv[2]);
     step(std::integral_constant<int, 3>{}, dv[3]);
 #ifdef DTWW_SPLIT   // the second half of the next chunk's sums beside the second half of the steps
-    __builtin_amdgcn_sched_barrier(0);
-    sums(s1, smn, DTWW_CH / 2, DTWW_CH);
+    if constexpr (!LEAN) {
+      __builtin_amdgcn_sched_barrier(0);
+      sums(s1, smn, DTWW_CH / 2, DTWW_CH);
+    }
 #endif
     step(std::integral_constant<int, 4>{}, dv[4]);
     step(std::integral_constant<int, 5>{}, dv[5]);
     step(std::integral_constant<int, 6>{}, dv[6]);
     step(std::integral_constant<int, 7>{}, dv[7]);
+    }
     // direction words: steps 16w .. 16w+15 (or the last ones)
     if ((s0 & 8) || s1 >= S) {
       Db[(s0 >> 4) << 6] = dacc;
@@ -2195,7 +2295,7 @@ __global__ __launch_bounds__(64, BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE) void d
       const int64_t je = s0 + lane - 62;               // lane 63's column at step s0 + lane
       if (lane < DTWW_CH && je >= 1 && je <= nr) g_store_agent(Eout + je, __builtin_bit_cast(uint64_t, eb[lane]));
     }
-    roots(smn, dv);
+    if constexpr (!LEAN && !IL) roots(smn, dv);
   }
   if (st_s0 >= 0) {
     if (lane == 0) {
@@ -2892,6 +2992,15 @@ static bool dtw_wave_enabled() {
 // the single DTW (one chain of bands, latency-bound) keeps the 8-wave band kernel unless
 // SONAR_DTW_WAVE=1 asks for the one-wave kernel there too
 bool dtw_wave_batch_enabled() { return dtw_wave_enabled(); }
+// the batched one-wave kernel's schedule (A/B; both measured slower on C5, DESIGN Kernel 6):
+// SONAR_DTW_LEAN=1 no cross-chunk pipelining (several waves per SIMD), SONAR_DTW_IL=1 the next
+// chunk's sums fenced piece by piece between the steps; default the unfenced pipelined schedule
+static int dtw_wave_mode() {
+  const char* l = std::getenv("SONAR_DTW_LEAN");
+  if (l && l[0] == '1') return DTWW_LEAN_MODE;
+  const char* i = std::getenv("SONAR_DTW_IL");
+  return (i && i[0] == '1') ? DTWW_IL_MODE : DTWW_PIPE_MODE;
+}
 static bool dtw_wave_one_enabled() {
   const char* e = std::getenv("SONAR_DTW_WAVE");
   return e && e[0] == '1';
@@ -3067,7 +3176,13 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
                        0, s, none, bt);
   } else if (!hargs[0].Cn && dtw_wave_batch_enabled()) {
     const int64_t grid = waves > 0 && waves < total_bands ? waves : total_bands;   // persistent waves
-    hipLaunchKernelGGL(dtw_wave_kernel<true>, dim3((unsigned)grid), dim3(64), 0, s, none, bt);
+    const int mode = dtw_wave_mode();
+    if (mode == DTWW_LEAN_MODE)
+      hipLaunchKernelGGL((dtw_wave_kernel<true, DTWW_LEAN_MODE>), dim3((unsigned)grid), dim3(64), 0, s, none, bt);
+    else if (mode == DTWW_IL_MODE)
+      hipLaunchKernelGGL((dtw_wave_kernel<true, DTWW_IL_MODE>), dim3((unsigned)grid), dim3(64), 0, s, none, bt);
+    else
+      hipLaunchKernelGGL((dtw_wave_kernel<true, DTWW_PIPE_MODE>), dim3((unsigned)grid), dim3(64), 0, s, none, bt);
   } else {
     hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
                        0, s, none, bt);

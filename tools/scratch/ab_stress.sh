@@ -10,6 +10,10 @@ for t in "$@"; do
   elif [ $t = b2 ]; then L=sonido-sonar_amd/lib/libsonar_gpu.so; EV="SONAR_DTW_BAND2=1";   # 128-row band kernel
   elif [ ${t:0:1} = n ]; then L=sonido-sonar_amd/lib/libsonar_gpu.so; EV="SONAR_DTW_WAVES=${t:1}";   # persistent waves per batch
   elif [ ${t:0:1} = p ]; then L=sonido-sonar_amd/lib_pipe/libsonar_gpu.so; EV="SONAR_DTW_WAVES=${t:1}";   # DTWW_PIPE build
+  elif [ $t = lean ]; then L=sonido-sonar_amd/lib/libsonar_gpu.so; EV="SONAR_DTW_LEAN=1";   # LEAN one-wave kernel
+  elif [ $t = lean96 ]; then L=sonido-sonar_amd/lib_r96/libsonar_gpu.so; EV="SONAR_DTW_LEAN=1";   # LEAN + 96-row ring
+  elif [ ${t:0:1} = l ] && [ $t != lean ] && [ $t != lean96 ]; then L=sonido-sonar_amd/lib_r96/libsonar_gpu.so; EV="SONAR_DTW_LEAN=1 SONAR_DTW_WAVES=${t:1}";   # LEAN + r96 + persistent waves per batch
+  elif [ $t = il ]; then L=sonido-sonar_amd/lib/libsonar_gpu.so; EV="SONAR_DTW_IL=1";   # fenced interleaved wave kernel
   elif [ $t = band ]; then L=sonido-sonar_amd/lib/libsonar_gpu.so; EV="SONAR_DTW_WAVE=0";   # 8-wave band kernel
   else L=sonido-sonar_amd/lib_$t/libsonar_gpu.so; fi
   env $EV SONAR_LIB=$PWD/$L timeout -k 10 120 python tools/scratch/dtw_band_ms.py 51676 5 || { echo "dtw fail $t"; exit 1; }
