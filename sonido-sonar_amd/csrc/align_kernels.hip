@@ -66,6 +66,7 @@ __device__ __forceinline__ double lane_bcast(double v, int j) {
 
 __global__ __launch_bounds__(64) void ncc_stats_kernel(const double* a, int64_t na, const double* b, int64_t nb,
                                                        double* stats) {
+  SONAR_FEAT_PRIO();
   const int w = blockIdx.x;
   const int lane = threadIdx.x;
   const double* s = w ? b : a;
@@ -112,6 +113,7 @@ __global__ __launch_bounds__(64) void ncc_stats_kernel(const double* a, int64_t 
 
 __global__ void ncc_norm_kernel(const double* a, int64_t na, const double* b, int64_t nb, const double* stats,
                                 double* xa, double* xb) {
+  SONAR_FEAT_PRIO();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < na) {
     const double d = __dsub_rn(a[i], stats[0]);
@@ -130,6 +132,7 @@ __global__ void ncc_norm_kernel(const double* a, int64_t na, const double* b, in
 constexpr int kNccTile = 1024;
 __global__ __launch_bounds__(256) void ncc_lag_kernel(const double* x, int64_t na, const double* y, int64_t nb,
                                                       int64_t L, double* corr) {
+  SONAR_FEAT_PRIO();
   __shared__ double xs[kNccTile + 256], ys[kNccTile + 256];
   __shared__ int64_t ovmax_s;
   const int64_t nl = 2 * L + 1;
@@ -2158,7 +2161,7 @@ void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
         }
       } while (miss);
       if (st_s0 >= 0) break;
-      spins += __builtin_amdgcn_s_memrealtime() - w0;
+      if (c > 0) spins += __builtin_amdgcn_s_memrealtime() - w0;   // chunk 0's wait: t_first
     }
     if (a.trace && c == 0) t_first = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
@@ -2622,17 +2625,20 @@ __global__ __launch_bounds__(64) void dtw_walk_band_kernel(DtwArgs a_in, const D
   }
 }
 
+// any block of 64..1024 threads (a multiple of 64).  Batches launch 256: a 1024-thread block needs
+// 4 waves on every SIMD of one CU at once, which a CU that also holds a DTW wave (320 registers of
+// 512) cannot give, so under C5 the block waited for a CU to drain (4.1 ms average in the r03c trace)
 template <bool BATCH>
 __global__ __launch_bounds__(1024) void dtw_walk_scan_kernel(DtwArgs a_in, const DtwArgs* args) {
   __shared__ int64_t wsum[16];
   const DtwArgs a = BATCH ? load_args_uniform(args + blockIdx.x) : a_in;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, NT = (int)blockDim.x, NWV = NT >> 6;
   const int64_t nb = a.nb;
   int32_t* meta = dtw_walk_meta(a.Dn, nb, a.SW, a.nr);
   const int32_t* cnt = meta + nb;
   int32_t* off = meta + 2 * nb;
   // thread t owns bands in walk order k = nb-1-b over [k0, k1)
-  const int64_t per = (nb + 1023) / 1024;
+  const int64_t per = (nb + NT - 1) / NT;
   const int64_t k0 = t * per < nb ? t * per : nb, k1 = (t + 1) * per < nb ? (t + 1) * per : nb;
   int64_t sum = 0;
   for (int64_t k = k0; k < k1; ++k) sum += cnt[nb - 1 - k];
@@ -2644,14 +2650,14 @@ __global__ __launch_bounds__(1024) void dtw_walk_scan_kernel(DtwArgs a_in, const
   if (lane == 63) wsum[wv] = inc;
   __syncthreads();
   int64_t base = 0, tot = 0;
-  for (int w = 0; w < 16; ++w) { base += w < wv ? wsum[w] : 0; tot += wsum[w]; }
+  for (int w = 0; w < NWV; ++w) { base += w < wv ? wsum[w] : 0; tot += wsum[w]; }
   int64_t o = base + inc - sum;
   for (int64_t k = k0; k < k1; ++k) {
     off[nb - 1 - k] = (int32_t)o;
     o += cnt[nb - 1 - k];
   }
   const int64_t nw = (tot + 15) >> 4;
-  for (int64_t w = t; w < nw; w += 1024) a.codes[w] = 0u;
+  for (int64_t w = t; w < nw; w += NT) a.codes[w] = 0u;
   if (t == 0) *a.plen = tot;
 }
 
@@ -2677,14 +2683,14 @@ template <bool BATCH>
 __global__ __launch_bounds__(1024) void dtw_path_scan_kernel(const uint32_t* codes, int64_t P, int64_t nq,
                                                              int64_t nr, int2* wstart, const DtwArgs* args) {
   __shared__ int64_t wsum[2][16];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, NT = (int)blockDim.x;   // 64..1024 (see walk scan)
   if constexpr (BATCH) {
     const DtwArgs a = load_args_uniform(args + blockIdx.x);
     codes = a.codes; P = *a.plen; nq = a.nq; nr = a.nr; wstart = a.wstart;
     if (t == 0 && a.Cn) *a.cnm = cn_at(a.Cn, a.S, nq, nr);   // (CK mode: the tile pass writes it)
   }
   const int64_t nw = (P + 15) >> 4;
-  const int64_t per = (nw + 1023) / 1024;
+  const int64_t per = (nw + NT - 1) / NT;
   const int64_t w0 = t * per < nw ? t * per : nw, w1 = (t + 1) * per < nw ? (t + 1) * per : nw;
   auto counts = [&](int64_t w, int64_t& di, int64_t& dj) {
     const uint32_t x = codes[w];
@@ -3006,6 +3012,14 @@ static bool dtw_wave_one_enabled() {
   return e && e[0] == '1';
 }
 
+// threads of the batched walk / path scans (one block per DTW): 256 by default so the block fits
+// beside the DTW waves of other batches; SONAR_SCAN_THREADS=1024 (A/B) the single-DTW shape
+static unsigned dtw_batch_scan_threads() {
+  const char* e = std::getenv("SONAR_SCAN_THREADS");
+  const int v = e ? std::atoi(e) : 256;
+  return (v >= 64 && v <= 1024 && v % 64 == 0) ? (unsigned)v : 256u;
+}
+
 // SONAR_DTW_SERIAL_WALK=1: the one-wave serial backtrack instead of the backtrack by bands (A/B)
 static bool dtw_serial_walk() {
   const char* e = std::getenv("SONAR_DTW_SERIAL_WALK");
@@ -3199,11 +3213,11 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
     hipLaunchKernelGGL(dtw_walk_chain_kernel<true>, dim3((unsigned)n), dim3(64), 0, s, none, dargs);
     hipLaunchKernelGGL((dtw_walk_band_kernel<false, true>), dim3((unsigned)max_nb, (unsigned)n), dim3(64), 0, s, none,
                        dargs);
-    hipLaunchKernelGGL(dtw_walk_scan_kernel<true>, dim3((unsigned)n), dim3(1024), 0, s, none, dargs);
+    hipLaunchKernelGGL(dtw_walk_scan_kernel<true>, dim3((unsigned)n), dim3(dtw_batch_scan_threads()), 0, s, none, dargs);
     hipLaunchKernelGGL((dtw_walk_band_kernel<true, true>), dim3((unsigned)max_nb, (unsigned)n), dim3(64), 0, s, none,
                        dargs);
   }
-  hipLaunchKernelGGL(dtw_path_scan_kernel<true>, dim3((unsigned)n), dim3(1024), 0, s, (const uint32_t*)nullptr,
+  hipLaunchKernelGGL(dtw_path_scan_kernel<true>, dim3((unsigned)n), dim3(dtw_batch_scan_threads()), 0, s, (const uint32_t*)nullptr,
                      (int64_t)0, (int64_t)0, (int64_t)0, (int2*)nullptr, dargs);
   const int64_t nw = (max_cap + 15) >> 4;
   hipLaunchKernelGGL(dtw_path_points_kernel<true>, dim3((unsigned)((nw + 255) / 256), (unsigned)n), dim3(256), 0, s,

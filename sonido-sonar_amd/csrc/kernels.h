@@ -9,6 +9,18 @@
 
 namespace sonar {
 
+// Issue priority of the latency-bound kernels of a pair's feature phase (DC / pre-emphasis passes,
+// energy, chroma, NCC) against the DTW waves sharing their SIMDs in a batched C5 run
+// (-DSONAR_FEAT_PRIO=<0..3>, A/B knob; 0 = the hardware default, no instruction)
+#ifndef SONAR_FEAT_PRIO_LEVEL
+#define SONAR_FEAT_PRIO_LEVEL 0
+#endif
+#if SONAR_FEAT_PRIO_LEVEL > 0
+#define SONAR_FEAT_PRIO() __builtin_amdgcn_s_setprio(SONAR_FEAT_PRIO_LEVEL)
+#else
+#define SONAR_FEAT_PRIO() ((void)0)
+#endif
+
 // Fused per-frame kernel (fp_kernel.hip).  Every wave owns a contiguous range
 // of STFT frames and processes it in batches of NB frames: whole-frame FFTs
 // (W = 128 * R real points as a 64*R-point complex FFT + real split) into

@@ -64,6 +64,7 @@ __global__ __launch_bounds__(256) void zcr_kernel(const void* pcm, int pcm_f64, 
 // block span does not fit the LDS budget of energy_lds_kernel below.
 __global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H,
                                                      double alpha, void* out, int out_f64) {
+  SONAR_FEAT_PRIO();
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= Fe) return;
   const int64_t s = t * H;
@@ -104,6 +105,7 @@ __device__ __forceinline__ int en_slot(int i) { return i + (i >> 8); }
 
 __global__ __launch_bounds__(256) void energy_lds_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W,
                                                          int H, double alpha, void* out, int out_f64) {
+  SONAR_FEAT_PRIO();
   extern __shared__ double xs[];
   const int64_t t0 = (int64_t)blockIdx.x * kEnFpb;
   const int nf = (int)min((int64_t)kEnFpb, Fe - t0);
@@ -295,6 +297,7 @@ template <int PPL>
 __global__ __launch_bounds__(256) void chroma_wave_kernel(const double* y, int64_t n, int64_t frames, int hop,
                                                           const double* win, const double* trig_g, const int* cls,
                                                           double* out) {
+  SONAR_FEAT_PRIO();
   constexpr int FS = 64 * PPL, K = FS / 2 + 1;
   constexpr int LG = PPL == 4 ? 8 : (PPL == 8 ? 9 : (PPL == 16 ? 10 : 11));
   static_assert((1 << LG) == FS, "power-of-two frame");
@@ -637,6 +640,7 @@ __device__ __forceinline__ int dc_slot(int i) { return i + (i >> 8); }
 template <bool WRITE>
 __global__ __launch_bounds__(256) void dc_pass_kernel(const double* x, int64_t n, double R, double alpha,
                                                       const double* ystart, double* ends, double* z) {
+  SONAR_FEAT_PRIO();
   __shared__ double xs[kDcSpan + (kDcSpan >> 8) + 1];
   const int64_t c0 = (int64_t)blockIdx.x * kDcCpb;
   const int64_t base = c0 * kDcChunk - 1;
@@ -660,6 +664,7 @@ __global__ __launch_bounds__(256) void dc_pass_kernel(const double* x, int64_t n
 // instead of 10,336 dependent steps.  Rounding differs from the serial chain by a few ulp of the
 // carry, which the DC filter then decays by R per sample.
 __global__ __launch_bounds__(64) void dc_carry_kernel(const double* ends, int64_t T, double RC, double* ystart) {
+  SONAR_FEAT_PRIO();
   const int lane = threadIdx.x;
   double Yin = 0.0;
   for (int64_t i = 0; i < T; i += 64) {

@@ -211,6 +211,18 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     if (!dstate) return fail(w, SONAR_ERR_NOMEM, "allocation failed (state)");
     HIP_TRY(w, hipMemsetAsync(dstate, 0, sb, s));
   }
+  // SONAR_DTW_BATCH_TRACE=1 (diagnostics): every band's start / first-edge / end / edge-wait ticks
+  // (dtw_wave_kernel's trace words), summed per batch into a line on stderr
+  const bool btrace = [] { const char* e = std::getenv("SONAR_DTW_BATCH_TRACE"); return e && e[0] == '1'; }();
+  std::vector<size_t> trace_off(n, 0);
+  uint64_t* dtrace = nullptr;
+  size_t trace_b = 0;
+  if (btrace) {
+    for (int i = 0; i < n; ++i) { trace_off[i] = trace_b; trace_b += (size_t)pg[i].g.nb * 8; }
+    dtrace = (uint64_t*)dbuf(w, "pb.trace", trace_b * 8);
+    if (!dtrace) return fail(w, SONAR_ERR_NOMEM, "allocation failed (trace)");
+    HIP_TRY(w, hipMemsetAsync(dtrace, 0, trace_b * 8, s));
+  }
   HIP_TRY(w, hipMemsetAsync(runs, 0, runs_b, s));
   if (e_b) HIP_TRY(w, hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, e_b / 4, s));
   int64_t acc = 0;
@@ -241,6 +253,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     a.Dd = pre ? (double*)(Dd + p.cn) : nullptr;
     a.diag = ddiag + (size_t)i * sonar::DTW_DIAG_WORDS;
     a.state = dstate ? (uint64_t*)(dstate + state_off[i]) : nullptr;
+    a.trace = dtrace ? dtrace + trace_off[i] : nullptr;
     a.dbg_stall = sonar::dtw_dbg_stall_band();
     hstart[i] = acc;
     acc += band2 ? (p.g.nb + 1) / 2 : p.g.nb;
@@ -282,6 +295,27 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   if (corr_b) HIP_TRY(w, hipMemcpyAsync(hcorr, corr, corr_b, hipMemcpyDeviceToHost, s));
   HIP_TRY(w, hipMemcpyAsync(hpath, path, path_b, hipMemcpyDeviceToHost, s));
   HIP_TRY(w, hipStreamSynchronize(s));
+  if (dtrace) {
+    // ticks of s_memrealtime (100 MHz): band-time = end - start, of which first-edge wait =
+    // first - start and later edge waits = the sweep's spin ticks; steps = S per band
+    std::vector<uint64_t> tr(trace_b);
+    if (hipMemcpy(tr.data(), dtrace, trace_b * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      double busy = 0, first = 0, spin = 0, steps = 0;
+      uint64_t t0 = UINT64_MAX, t1 = 0;
+      for (int i = 0; i < n; ++i)
+        for (int64_t b = 0; b < pg[i].g.nb; ++b) {
+          const uint64_t* r = tr.data() + trace_off[i] + 8 * b;
+          if (!r[2]) continue;
+          busy += (double)(r[2] - r[0]); first += (double)(r[1] - r[0]); spin += (double)r[3];
+          steps += (double)pg[i].g.S;
+          t0 = std::min(t0, r[0]); t1 = std::max(t1, r[2]);
+        }
+      std::fprintf(stderr, "{\"dtw_batch_trace\": {\"pairs\": %d, \"band_us\": %.1f, \"first_wait_us\": %.1f, "
+                   "\"spin_us\": %.1f, \"steps\": %.0f, \"ns_per_step_busy\": %.2f, \"ns_per_step_compute\": %.2f, \"span_us\": %.1f}}\n",
+                   n, busy / 100.0, first / 100.0, spin / 100.0, steps, busy * 10.0 / steps,
+                   (busy - first - spin) * 10.0 / steps, (double)(t1 - t0) / 100.0);
+    }
+  }
   for (int i = 0; i < n; ++i) {
     const PairGeo& p = pg[i];
     const char* ps = hstat + (size_t)i * 32;
