@@ -64,9 +64,27 @@ __device__ __forceinline__ double lane_bcast(double v, int j) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// a batched launch's job (blockIdx.y) into SGPRs
+template <class J>
+__device__ __forceinline__ J load_job(const J* p) {
+  static_assert(sizeof(J) % 4 == 0, "read as dwords");
+  J r;
+  const int* src = reinterpret_cast<const int*>(p);
+  int* dst = reinterpret_cast<int*>(&r);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(J) / 4); ++k) dst[k] = __builtin_amdgcn_readfirstlane(src[k]);
+  return r;
+}
+
+// BJ (this and the two NCC kernels below): one pair per blockIdx.y, its arguments from jobs[]
+template <bool BJ = false>
 __global__ __launch_bounds__(64) void ncc_stats_kernel(const double* a, int64_t na, const double* b, int64_t nb,
-                                                       double* stats) {
+                                                       double* stats, const NccJob* jobs) {
   SONAR_FEAT_PRIO();
+  if constexpr (BJ) {
+    const NccJob j = load_job(jobs + blockIdx.y);
+    a = j.a; na = j.na; b = j.b; nb = j.nb; stats = j.stats;
+  }
   const int w = blockIdx.x;
   const int lane = threadIdx.x;
   const double* s = w ? b : a;
@@ -111,9 +129,14 @@ __global__ __launch_bounds__(64) void ncc_stats_kernel(const double* a, int64_t 
   }
 }
 
+template <bool BJ = false>
 __global__ void ncc_norm_kernel(const double* a, int64_t na, const double* b, int64_t nb, const double* stats,
-                                double* xa, double* xb) {
+                                double* xa, double* xb, const NccJob* jobs) {
   SONAR_FEAT_PRIO();
+  if constexpr (BJ) {
+    const NccJob j = load_job(jobs + blockIdx.y);
+    a = j.a; na = j.na; b = j.b; nb = j.nb; stats = j.stats; xa = j.xa; xb = j.xb;
+  }
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < na) {
     const double d = __dsub_rn(a[i], stats[0]);
@@ -130,13 +153,19 @@ __global__ void ncc_norm_kernel(const double* a, int64_t na, const double* b, in
 // samples of each other (s1 = max(0, -lag), s2 = max(0, lag)), so each k-tile of both inputs is
 // staged once in LDS (coalesced) and every thread walks its own offsets there.
 constexpr int kNccTile = 1024;
+template <bool BJ = false>
 __global__ __launch_bounds__(256) void ncc_lag_kernel(const double* x, int64_t na, const double* y, int64_t nb,
-                                                      int64_t L, double* corr) {
+                                                      int64_t L, double* corr, const NccJob* jobs) {
   SONAR_FEAT_PRIO();
   __shared__ double xs[kNccTile + 256], ys[kNccTile + 256];
   __shared__ int64_t ovmax_s;
+  if constexpr (BJ) {
+    const NccJob j = load_job(jobs + blockIdx.y);
+    x = j.xa; na = j.na; y = j.xb; nb = j.nb; L = j.L; corr = j.corr;
+  }
   const int64_t nl = 2 * L + 1;
   const int64_t idx0 = (int64_t)blockIdx.x * 256;
+  if (idx0 >= nl) return;
   const int64_t idx = idx0 + threadIdx.x;
   const bool active = idx < nl;
   const int64_t lag = idx - L;
@@ -196,12 +225,33 @@ __global__ __launch_bounds__(256) void ncc_lag_kernel(const double* x, int64_t n
 
 int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t L, double* xa, double* xb,
                double* stats, double* corr, hipStream_t s) {
-  hipLaunchKernelGGL(ncc_stats_kernel, dim3(2), dim3(64), 0, s, a, na, b, nb, stats);
+  const NccJob* none = nullptr;
+  hipLaunchKernelGGL((ncc_stats_kernel<false>), dim3(2), dim3(64), 0, s, a, na, b, nb, stats, none);
   const int64_t nmax = na > nb ? na : nb;
-  hipLaunchKernelGGL(ncc_norm_kernel, dim3((unsigned)((nmax + 255) / 256)), dim3(256), 0, s, a, na, b, nb, stats, xa,
-                     xb);
+  hipLaunchKernelGGL((ncc_norm_kernel<false>), dim3((unsigned)((nmax + 255) / 256)), dim3(256), 0, s, a, na, b, nb, stats, xa,
+                     xb, none);
   const int64_t nl = 2 * L + 1;
-  hipLaunchKernelGGL(ncc_lag_kernel, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, s, xa, na, xb, nb, L, corr);
+  hipLaunchKernelGGL((ncc_lag_kernel<false>), dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, s, xa, na, xb, nb, L, corr,
+                     none);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// launch_ncc over many pairs in three launches (blockIdx.y = pair); the same kernels, arithmetic
+// and order per pair, so the same bits
+int launch_ncc_batch(const NccJob* hjobs, const NccJob* djobs, int nj, hipStream_t s) {
+  if (nj <= 0) return 0;
+  if (nj > 65535) return -1;
+  int64_t nmax = 1, nlmax = 1;
+  for (int k = 0; k < nj; ++k) {
+    nmax = std::max(nmax, std::max(hjobs[k].na, hjobs[k].nb));
+    nlmax = std::max(nlmax, 2 * hjobs[k].L + 1);
+  }
+  hipLaunchKernelGGL((ncc_stats_kernel<true>), dim3(2, (unsigned)nj), dim3(64), 0, s, nullptr, 0, nullptr, 0, nullptr,
+                     djobs);
+  hipLaunchKernelGGL((ncc_norm_kernel<true>), dim3((unsigned)((nmax + 255) / 256), (unsigned)nj), dim3(256), 0, s,
+                     nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, djobs);
+  hipLaunchKernelGGL((ncc_lag_kernel<true>), dim3((unsigned)((nlmax + 255) / 256), (unsigned)nj), dim3(256), 0, s,
+                     nullptr, 0, nullptr, 0, 0, nullptr, djobs);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -92,6 +92,9 @@ void* dbuf(sonar_ctx* c, const std::string& name, size_t bytes);
 // frees every cached device / pinned host buffer of c (sonar_trim; the batch path's NOMEM retry)
 void trim_buffers(sonar_ctx* c);
 void* hbuf(sonar_ctx* c, const std::string& name, size_t bytes);
+// chroma tables of frame size fs at sample rate sr, built once per context (sonar_api.cpp); null on
+// allocation failure
+const sonar_ctx::ChromaT* chroma_tables_for(sonar_ctx* c, int fs, int sr);
 // DTW with the local distances precomputed (dtw_dist_kernel + the 4-wave band kernel) for this
 // feature dimension; opt-in with SONAR_DTW_PRE=1 (the distance waves inside the band kernel are
 // the default: faster at C3 and C5 sizes)

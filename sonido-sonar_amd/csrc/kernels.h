@@ -133,6 +133,37 @@ int launch_tilt(const double* y, int64_t n, int64_t frames, double* tilt, hipStr
 // PCM ingest: f64 -> f32 (RNE); both pointers 16-B aligned (misc_kernels.hip)
 int launch_f64_to_f32(const double* in, float* out, int64_t n, hipStream_t s);
 // NCC (align_kernels.hip)
+// One signal of a batched music-feature launch (launch_music_features_batch): its PCM, the
+// pre-emphasised output, the DC chunk scratch (T chunks), energy (Fe frames) and chroma (F frames)
+struct MfJob {
+  const double* x;
+  int64_t n;
+  double* y;
+  double* ends;
+  double* ystart;
+  int64_t T;
+  double* energy;
+  int64_t Fe;
+  double* chroma;
+  int64_t F;
+};
+int launch_music_features_batch(const MfJob* hjobs, const MfJob* djobs, int nj, int W, int H, int fs,
+                                const double* window, const double* trig, const int* cls, hipStream_t s);
+// DC chunk length of launch_dc_preemph (MfJob::T = ceil(n / chunk))
+int64_t dc_chunks(int64_t n);
+// One pair of a batched NCC launch (launch_ncc_batch): as launch_ncc's arguments
+struct NccJob {
+  const double* a;
+  int64_t na;
+  const double* b;
+  int64_t nb;
+  int64_t L;
+  double* xa;
+  double* xb;
+  double* stats;
+  double* corr;
+};
+int launch_ncc_batch(const NccJob* hjobs, const NccJob* djobs, int nj, hipStream_t s);
 int launch_ncc(const double* a, int64_t na, const double* b, int64_t nb, int64_t L, double* norm_a,
                double* norm_b, double* stats, double* corr, hipStream_t s);
 // AlignmentAnalyzer.addNoise and flatten2DFeatures (align_kernels.hip)

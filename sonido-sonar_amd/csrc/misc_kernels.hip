@@ -95,6 +95,18 @@ __global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f6
   store_out(out, out_f64, t, sqrt(__ddiv_rn(ss, (double)W)));
 }
 
+// a batched launch's job (blockIdx.y, or blockIdx.x for one-wave kernels) into SGPRs
+template <class J>
+__device__ __forceinline__ J load_job(const J* p) {
+  static_assert(sizeof(J) % 4 == 0, "read as dwords");
+  J r;
+  const int* src = reinterpret_cast<const int*>(p);
+  int* dst = reinterpret_cast<int*>(&r);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(J) / 4); ++k) dst[k] = __builtin_amdgcn_readfirstlane(src[k]);
+  return r;
+}
+
 // The same per-frame chains with the block's samples staged in LDS first: a block owns kEnFpb
 // consecutive frames, its 256 threads copy the span [t0*H - 1, (t0+kEnFpb-1)*H + W) with coalesced
 // loads (one padding slot per 256 samples keeps the lanes' hop-strided LDS reads off one bank),
@@ -103,11 +115,18 @@ __global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f6
 constexpr int kEnFpb = 16;
 __device__ __forceinline__ int en_slot(int i) { return i + (i >> 8); }
 
+// BJ: one music-feature job per blockIdx.y (its pre-emphasised signal, length, frames, output)
+template <bool BJ>
 __global__ __launch_bounds__(256) void energy_lds_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W,
-                                                         int H, double alpha, void* out, int out_f64) {
+                                                         int H, double alpha, void* out, int out_f64, const MfJob* jobs) {
   SONAR_FEAT_PRIO();
   extern __shared__ double xs[];
+  if constexpr (BJ) {
+    const MfJob j = load_job(jobs + blockIdx.y);
+    pcm = j.y; n = j.n; Fe = j.Fe; out = j.energy;
+  }
   const int64_t t0 = (int64_t)blockIdx.x * kEnFpb;
+  if (t0 >= Fe) return;
   const int nf = (int)min((int64_t)kEnFpb, Fe - t0);
   const int64_t base = t0 * H - 1;
   const int span = (nf - 1) * H + W + 1;
@@ -293,11 +312,16 @@ __global__ __launch_bounds__(256) void chroma_kernel(const double* y, int64_t n,
 // makes one LDS round trip per two stages with no block barrier after the twiddle table; |X|^2
 // folds into the 12 classes through per-class bin lists (ascending bins: chroma_kernel's order).
 // cls = [13 offsets][bins]: class b owns cls[13 + cls[b] .. 13 + cls[b+1]).
-template <int PPL>
+template <int PPL, bool BJ = false>
 __global__ __launch_bounds__(256) void chroma_wave_kernel(const double* y, int64_t n, int64_t frames, int hop,
                                                           const double* win, const double* trig_g, const int* cls,
-                                                          double* out) {
+                                                          double* out, const MfJob* jobs) {
   SONAR_FEAT_PRIO();
+  if constexpr (BJ) {
+    const MfJob j = load_job(jobs + blockIdx.y);
+    y = j.y; n = j.n; frames = j.F; out = j.chroma;
+    if ((int64_t)blockIdx.x * 4 >= frames) return;
+  }
   constexpr int FS = 64 * PPL, K = FS / 2 + 1;
   constexpr int LG = PPL == 4 ? 8 : (PPL == 8 ? 9 : (PPL == 16 ? 10 : 11));
   static_assert((1 << LG) == FS, "power-of-two frame");
@@ -491,8 +515,8 @@ int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, in
   const int64_t span = (int64_t)(kEnFpb - 1) * H + W + 1;
   const size_t lds = (size_t)(span + (span >> 8) + 1) * sizeof(double);
   if (lds <= 48 * 1024) {
-    hipLaunchKernelGGL(energy_lds_kernel, dim3((unsigned)((Fe + kEnFpb - 1) / kEnFpb)), dim3(256), lds, s, pcm,
-                       pcm_f64, n, Fe, W, H, alpha, out, out_f64);
+    hipLaunchKernelGGL(energy_lds_kernel<false>, dim3((unsigned)((Fe + kEnFpb - 1) / kEnFpb)), dim3(256), lds, s, pcm,
+                       pcm_f64, n, Fe, W, H, alpha, out, out_f64, (const MfJob*)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -5;
   }
   hipLaunchKernelGGL(energy_kernel, dim3((unsigned)((Fe + 255) / 256)), dim3(256), 0, s, pcm, pcm_f64, n, Fe, W, H,
@@ -556,8 +580,9 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
   if (frames <= 0) return 0;
   if (cls && (fs == 256 || fs == 512)) {
     const dim3 grid((unsigned)((frames + 3) / 4));
-    if (fs == 256) hipLaunchKernelGGL(chroma_wave_kernel<4>, grid, dim3(256), 0, s, y, n, frames, hop, window, trig, cls, out);
-    else hipLaunchKernelGGL(chroma_wave_kernel<8>, grid, dim3(256), 0, s, y, n, frames, hop, window, trig, cls, out);
+    const MfJob* none = nullptr;
+    if (fs == 256) hipLaunchKernelGGL((chroma_wave_kernel<4>), grid, dim3(256), 0, s, y, n, frames, hop, window, trig, cls, out, none);
+    else hipLaunchKernelGGL((chroma_wave_kernel<8>), grid, dim3(256), 0, s, y, n, frames, hop, window, trig, cls, out, none);
     return hipGetLastError() == hipSuccess ? 0 : -5;
   }
   const int K = fs / 2 + 1;
@@ -637,12 +662,17 @@ static_assert((kDcSpan + (kDcSpan >> 8) + 1) * sizeof(double) <= 64 * 1024,
               "dc_pass_kernel stages kDcCpb chunks in static LDS: lower kDcCpb for longer chunks");
 __device__ __forceinline__ int dc_slot(int i) { return i + (i >> 8); }
 
-template <bool WRITE>
+template <bool WRITE, bool BJ = false>
 __global__ __launch_bounds__(256) void dc_pass_kernel(const double* x, int64_t n, double R, double alpha,
-                                                      const double* ystart, double* ends, double* z) {
+                                                      const double* ystart, double* ends, double* z, const MfJob* jobs) {
   SONAR_FEAT_PRIO();
   __shared__ double xs[kDcSpan + (kDcSpan >> 8) + 1];
+  if constexpr (BJ) {
+    const MfJob j = load_job(jobs + blockIdx.y);
+    x = j.x; n = j.n; ystart = j.ystart; ends = j.ends; z = j.y;
+  }
   const int64_t c0 = (int64_t)blockIdx.x * kDcCpb;
+  if (c0 * kDcChunk >= n) return;
   const int64_t base = c0 * kDcChunk - 1;
   const int span = (int)(min(n, (c0 + kDcCpb) * kDcChunk) - base);
   for (int i = threadIdx.x; i < span; i += 256) {
@@ -663,8 +693,14 @@ __global__ __launch_bounds__(256) void dc_pass_kernel(const double* x, int64_t n
 // [i, c]), then one carry from the previous block: 162 blocks x 6 shuffle steps for a 60 s stream
 // instead of 10,336 dependent steps.  Rounding differs from the serial chain by a few ulp of the
 // carry, which the DC filter then decays by R per sample.
-__global__ __launch_bounds__(64) void dc_carry_kernel(const double* ends, int64_t T, double RC, double* ystart) {
+template <bool BJ = false>
+__global__ __launch_bounds__(64) void dc_carry_kernel(const double* ends, int64_t T, double RC, double* ystart,
+                                                      const MfJob* jobs) {
   SONAR_FEAT_PRIO();
+  if constexpr (BJ) {   // one wave per job
+    const MfJob j = load_job(jobs + blockIdx.x);
+    ends = j.ends; T = j.T; ystart = j.ystart;
+  }
   const int lane = threadIdx.x;
   double Yin = 0.0;
   for (int64_t i = 0; i < T; i += 64) {
@@ -683,6 +719,7 @@ __global__ __launch_bounds__(64) void dc_carry_kernel(const double* ends, int64_
 }
 
 
+int64_t dc_chunks(int64_t n) { return (n + kDcChunk - 1) / kDcChunk; }
 size_t dc_preemph_scratch_bytes(int64_t n) { return (size_t)(2 * ((n + kDcChunk - 1) / kDcChunk) + 2) * 8; }
 
 int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, double* scratch, hipStream_t s) {
@@ -693,9 +730,47 @@ int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double
   double RC = 1.0;
   for (int k = 0; k < kDcChunk; k++) RC *= R;                 // R^chunk (carry weight of a full chunk)
   const unsigned g = (unsigned)((T + kDcCpb - 1) / kDcCpb);
-  hipLaunchKernelGGL(dc_pass_kernel<false>, dim3(g), dim3(256), 0, s, x, n, R, 0.0, nullptr, ends, nullptr);
-  hipLaunchKernelGGL(dc_carry_kernel, dim3(1), dim3(64), 0, s, ends, T, RC, ystart);
-  hipLaunchKernelGGL(dc_pass_kernel<true>, dim3(g), dim3(256), 0, s, x, n, R, alpha, ystart, nullptr, y);
+  const MfJob* none = nullptr;
+  hipLaunchKernelGGL((dc_pass_kernel<false>), dim3(g), dim3(256), 0, s, x, n, R, 0.0, nullptr, ends, nullptr, none);
+  hipLaunchKernelGGL((dc_carry_kernel<false>), dim3(1), dim3(64), 0, s, ends, T, RC, ystart, none);
+  hipLaunchKernelGGL((dc_pass_kernel<true>), dim3(g), dim3(256), 0, s, x, n, R, alpha, ystart, nullptr, y, none);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// MusicFeatureExtractor energy + chroma of many signals in five launches (jobs on the device in
+// djobs, the same on the host in hjobs for the grid sizes): DC removal + pre-emphasis (the same
+// three passes as launch_dc_preemph), ShortTimeEnergy of the pre-emphasised signal (alpha 0, as
+// music_features_impl), chroma (chroma_wave_kernel, fs 256 or 512; tables shared by every job).
+// Returns -1 without launching when a job does not fit those kernels (the caller then runs the
+// per-signal path).
+int launch_music_features_batch(const MfJob* hjobs, const MfJob* djobs, int nj, int W, int H, int fs,
+                                const double* window, const double* trig, const int* cls, hipStream_t s) {
+  if (nj <= 0) return 0;
+  if (nj > 65535 || !cls || (fs != 256 && fs != 512)) return -1;
+  const int64_t span = (int64_t)(kEnFpb - 1) * H + W + 1;
+  const size_t lds = (size_t)(span + (span >> 8) + 1) * sizeof(double);
+  if (lds > 48 * 1024) return -1;
+  int64_t maxT = 1, maxFe = 1, maxF = 1;
+  for (int k = 0; k < nj; ++k) {
+    if (hjobs[k].n <= 0 || hjobs[k].F <= 0) return -1;
+    maxT = std::max(maxT, hjobs[k].T);
+    maxFe = std::max(maxFe, hjobs[k].Fe);
+    maxF = std::max(maxF, hjobs[k].F);
+  }
+  const double R = 0.995, alpha = 0.95;        // music.go:245-259 (dc_removal / pre_emphasis defaults)
+  double RC = 1.0;
+  for (int k = 0; k < kDcChunk; k++) RC *= R;
+  const dim3 gdc((unsigned)((maxT + kDcCpb - 1) / kDcCpb), (unsigned)nj);
+  hipLaunchKernelGGL((dc_pass_kernel<false, true>), gdc, dim3(256), 0, s, nullptr, 0, R, 0.0, nullptr, nullptr, nullptr, djobs);
+  hipLaunchKernelGGL((dc_carry_kernel<true>), dim3((unsigned)nj), dim3(64), 0, s, nullptr, 0, RC, nullptr, djobs);
+  hipLaunchKernelGGL((dc_pass_kernel<true, true>), gdc, dim3(256), 0, s, nullptr, 0, R, alpha, nullptr, nullptr, nullptr, djobs);
+  hipLaunchKernelGGL((energy_lds_kernel<true>), dim3((unsigned)((maxFe + kEnFpb - 1) / kEnFpb), (unsigned)nj), dim3(256),
+                     lds, s, nullptr, 1, 0, 0, W, H, 0.0, nullptr, 1, djobs);
+  const dim3 gch((unsigned)((maxF + 3) / 4), (unsigned)nj);
+  if (fs == 256)
+    hipLaunchKernelGGL((chroma_wave_kernel<4, true>), gch, dim3(256), 0, s, nullptr, 0, 0, H, window, trig, cls, nullptr, djobs);
+  else
+    hipLaunchKernelGGL((chroma_wave_kernel<8, true>), gch, dim3(256), 0, s, nullptr, 0, 0, H, window, trig, cls, nullptr, djobs);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

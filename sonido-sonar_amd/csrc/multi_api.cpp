@@ -120,7 +120,101 @@ size_t pair_bytes(const PairGeo& p) {
   return al256((size_t)(p.Fq + p.Fr) * 96) + (sonar::detail::dtw_pre_enabled(12) ? al256(sonar::dtw_cn_bytes(p.g)) : 0) +
          al256(sonar::dtw_ck_bytes(p.g)) + al256((size_t)sonar::dtw_run_words(p.g) * 4) + al256(sonar::dtw_dn_bytes(p.g)) +
          al256(sonar::dtw_edge_bytes(p.g)) + al256((size_t)((p.cap + 1023) / 1024) * 256) +
-         al256((size_t)((p.cap + 15) / 16 + 1) * 8) + al256((size_t)p.cap * 16) + al256((size_t)(2 * p.L + 1) * 8);
+         al256((size_t)((p.cap + 15) / 16 + 1) * 8) + al256((size_t)p.cap * 16) + al256((size_t)(2 * p.L + 1) * 8) +
+         // batched features (feat_batch): pre-emphasised signals, DC scratch, energies, NCC inputs
+         al256((size_t)p.nq * 8) + al256((size_t)p.nr * 8) + al256(sonar::dc_preemph_scratch_bytes(p.nq)) +
+         al256(sonar::dc_preemph_scratch_bytes(p.nr)) + 2 * al256((size_t)(p.Eq + p.Er + 2) * 8) + 256;
+}
+
+// SONAR_FEAT_BATCH=0: the pair-by-pair feature launches inside a batch (A/B)
+bool feat_batch_enabled() {
+  const char* e = std::getenv("SONAR_FEAT_BATCH");
+  return !(e && e[0] == '0');
+}
+
+// The batch's music features (music.go:245-376 per signal: DC removal + pre-emphasis, energy,
+// chroma) and energy NCCs (correlation.go:131-409 per pair) in eight launches instead of
+// 13 per pair: per-signal and per-pair regions of the worker's scratch, job tables staged through
+// pinned memory.  Each signal / pair runs the same kernels' arithmetic in the same order as the
+// per-pair path, so the outputs are bit-identical.  Under C5 the per-pair launches were the
+// stream's serial phase: each small latency-bound kernel also waited for room beside the other
+// streams' DTW waves (r03 kernel trace: ~65 % of every worker stream's time in feature kernels).
+// Returns false (nothing launched) when the batch does not fit: signals of different chroma frame
+// sizes or outside the batched kernels' shapes; on an allocation failure it also sets w->err to
+// "batch features: ..." (the caller's NOMEM retry path).
+bool feat_batch(sonar_ctx* w, const std::vector<PairGeo>& pg, int32_t sr, int32_t sw, int32_t hop, int32_t fw,
+                const double* const* q_pcm, const double* const* r_pcm, char* chroma, char* corr, hipStream_t s) {
+  w->err.clear();
+  if (!feat_batch_enabled() || pg.empty() || fw <= 0 || hop <= 0) return false;
+  if (const char* cw = std::getenv("SONAR_CHROMA_WAVE"); cw && std::atoi(cw) == 0) return false;   // chroma_kernel A/B
+  const int n = (int)pg.size();
+  int fs = -1;
+  size_t ysz = 0, dsz = 0, esz = 0, xsz = 0;
+  int ncorr = 0;
+  for (const auto& p : pg) {
+    for (int side = 0; side < 2; ++side) {
+      const int64_t ns = side ? p.nr : p.nq, F = side ? p.Fr : p.Fq;
+      const int f = (int)(ns / F);                                    // music.go:331
+      if (fs < 0) fs = f;
+      if (f != fs) return false;
+      ysz += al256((size_t)ns * 8);
+      dsz += al256((size_t)sonar::dc_preemph_scratch_bytes(ns));
+      esz += al256((size_t)std::max<int64_t>(side ? p.Er : p.Eq, 1) * 8);
+    }
+    if (p.corr) { xsz += al256((size_t)(p.Eq + p.Er) * 8) + 256; ++ncorr; }
+  }
+  if (fs != 256 && fs != 512) return false;
+  const sonar_ctx::ChromaT* ct = sonar::detail::chroma_tables_for(w, fs, sr);
+  char* y = (char*)dbuf(w, "fb.y", ysz);
+  char* dcs = (char*)dbuf(w, "fb.dc", dsz);
+  char* en = (char*)dbuf(w, "fb.energy", esz);
+  char* nx = (char*)dbuf(w, "fb.ncc", std::max<size_t>(xsz, 256));
+  const size_t jb = al256((size_t)2 * n * sizeof(sonar::MfJob)), nb = al256((size_t)std::max(ncorr, 1) * sizeof(sonar::NccJob));
+  char* dj = (char*)dbuf(w, "fb.jobs", jb + nb);
+  char* hj = (char*)sonar::detail::hbuf(w, "fb.hjobs", jb + nb);
+  if (!ct || !y || !dcs || !en || !nx || !dj || !hj) {
+    fail(w, SONAR_ERR_NOMEM, "batch features: allocation failed");
+    return false;
+  }
+  auto* mj = (sonar::MfJob*)hj;
+  auto* nj = (sonar::NccJob*)(hj + jb);
+  size_t yo = 0, doff = 0, eo = 0, xo = 0;
+  int k = 0, m = 0;
+  for (const auto& p : pg) {
+    double* e2[2];
+    for (int side = 0; side < 2; ++side) {
+      const int64_t ns = side ? p.nr : p.nq;
+      sonar::MfJob& j = mj[k++];
+      j.x = side ? r_pcm[p.k] : q_pcm[p.k];
+      j.n = ns;
+      j.y = (double*)(y + yo); yo += al256((size_t)ns * 8);
+      j.T = sonar::dc_chunks(ns);
+      j.ends = (double*)(dcs + doff);
+      j.ystart = j.ends + j.T;
+      doff += al256((size_t)sonar::dc_preemph_scratch_bytes(ns));
+      j.Fe = side ? p.Er : p.Eq;
+      j.energy = (double*)(en + eo); eo += al256((size_t)std::max<int64_t>(j.Fe, 1) * 8);
+      j.F = side ? p.Fr : p.Fq;
+      j.chroma = (double*)(chroma + p.chroma) + (side ? p.Fq * 12 : 0);
+      e2[side] = j.energy;
+    }
+    if (p.corr) {
+      sonar::NccJob& j = nj[m++];
+      j.a = e2[0]; j.na = p.Eq; j.b = e2[1]; j.nb = p.Er; j.L = p.L;
+      j.xa = (double*)(nx + xo);
+      j.xb = j.xa + p.Eq;
+      j.stats = (double*)(nx + xo + al256((size_t)(p.Eq + p.Er) * 8));
+      xo += al256((size_t)(p.Eq + p.Er) * 8) + 256;
+      j.corr = (double*)(corr + p.corr_off);
+    }
+  }
+  (void)sw;
+  if (hipMemcpyAsync(dj, hj, jb + nb, hipMemcpyHostToDevice, s) != hipSuccess) return false;
+  if (sonar::launch_music_features_batch(mj, (const sonar::MfJob*)dj, 2 * n, fw, hop, fs, (const double*)ct->win,
+                                         (const double*)ct->trig, (const int*)ct->cls, s) != 0)
+    return false;
+  if (ncorr && sonar::launch_ncc_batch(nj, (const sonar::NccJob*)(dj + jb), ncorr, s) != 0) return false;
+  return true;
 }
 
 // A batch of pairs on worker w's stream with one host synchronisation: every pair's music
@@ -225,22 +319,29 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   }
   HIP_TRY(w, hipMemsetAsync(runs, 0, runs_b, s));
   if (e_b) HIP_TRY(w, hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, e_b / 4, s));
+  // every pair's music features and energy NCC: batched launches over the whole batch when the
+  // inputs are on the device and every signal fits the batched kernels (feat_batch), else pair by
+  // pair on the worker's scratch
+  const bool fb = device_ptrs && feat_batch(w, pg, sr, sw, hop, fw, q_pcm, r_pcm, chroma, corr, s);
+  if (!fb && !w->err.empty() && w->err.rfind("batch features:", 0) == 0) return SONAR_ERR_NOMEM;
   int64_t acc = 0;
   for (int i = 0; i < n; ++i) {
     const PairGeo& p = pg[i];
     const double *dq = q_pcm[p.k], *dr = r_pcm[p.k];
     double* cq = (double*)(chroma + p.chroma);
     double* cr = cq + p.Fq * 12;
-    if (!device_ptrs) {
-      HIP_TRY(w, hipMemcpyAsync(up_q, dq, (size_t)p.nq * 8, hipMemcpyHostToDevice, s));
-      HIP_TRY(w, hipMemcpyAsync(up_r, dr, (size_t)p.nr * 8, hipMemcpyHostToDevice, s));
-      dq = up_q; dr = up_r;
+    if (!fb) {
+      if (!device_ptrs) {
+        HIP_TRY(w, hipMemcpyAsync(up_q, dq, (size_t)p.nq * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(w, hipMemcpyAsync(up_r, dr, (size_t)p.nr * 8, hipMemcpyHostToDevice, s));
+        dq = up_q; dr = up_r;
+      }
+      int rc = sonar_music_alignment_features(w, dq, p.nq, sr, sw, hop, fw, hop, eq, cq, 1);
+      if (rc == SONAR_OK) rc = sonar_music_alignment_features(w, dr, p.nr, sr, sw, hop, fw, hop, er, cr, 1);
+      if (rc != SONAR_OK) return rc;
+      if (p.corr && sonar::launch_ncc(eq, p.Eq, er, p.Er, p.L, xa, xb, st, (double*)(corr + p.corr_off), s) != 0)
+        return fail(w, SONAR_ERR_DEVICE, "ncc launch failed");
     }
-    int rc = sonar_music_alignment_features(w, dq, p.nq, sr, sw, hop, fw, hop, eq, cq, 1);
-    if (rc == SONAR_OK) rc = sonar_music_alignment_features(w, dr, p.nr, sr, sw, hop, fw, hop, er, cr, 1);
-    if (rc != SONAR_OK) return rc;
-    if (p.corr && sonar::launch_ncc(eq, p.Eq, er, p.Er, p.L, xa, xb, st, (double*)(corr + p.corr_off), s) != 0)
-      return fail(w, SONAR_ERR_DEVICE, "ncc launch failed");
     int32_t* sync = dstat + 8 * i + 4;
     sonar::DtwArgs& a = hargs[i];
     a = sonar::DtwArgs{};

@@ -718,6 +718,27 @@ int sonar_chroma_stft(sonar_ctx* c, const double* pcm, int64_t n, int64_t F, int
     if (sonar::launch_dc_preemph(dp, n, 0.995, 0.95, yb, dcs, s) != 0) return fail(c, SONAR_ERR_DEVICE, "dc launch failed");
     y = yb;
   }
+  const sonar_ctx::ChromaT* ct = sonar::detail::chroma_tables_for(c, fs, sr);
+  if (!ct) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+  const char* cw = std::getenv("SONAR_CHROMA_WAVE");              // 0: the block-per-frame kernel (A/B)
+  const int* cls = (cw && std::atoi(cw) == 0) ? nullptr : (const int*)ct->cls;
+  if (sonar::launch_chroma(y, n, F, hop, fs, (const double*)ct->win, (const double*)ct->trig,
+                           (const int*)ct->map, cls, dout, s) != 0)
+    return fail(c, SONAR_ERR_UNSUPPORTED, "chroma launch failed (frame size too large for LDS?)");
+  if (!device_ptrs) {
+    HIP_TRY(c, hipMemcpyAsync(chroma, dout, F * 12 * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SONAR_OK;
+}
+
+}  // extern "C"
+
+namespace sonar {
+namespace detail {
+// the chroma tables of frame size fs at sample rate sr (ChromaSTFT, chroma_stft.go:45-138), built
+// once per context: Hann window, the bin -> class map, the FFT twiddles, per-class bin lists
+const sonar_ctx::ChromaT* chroma_tables_for(sonar_ctx* c, int fs, int sr) {
   const std::string key = std::to_string(fs) + "|" + std::to_string(sr);
   auto it = c->chroma_tables.find(key);
   if (it == c->chroma_tables.end()) {
@@ -738,19 +759,16 @@ int sonar_chroma_stft(sonar_ctx* c, const double* pcm, int64_t n, int64_t F, int
         if (map[k] == b) cls[13 + e++] = (int)k;
     }
     cls[12] = e;
-    it = c->chroma_tables.emplace(key, sonar_ctx::ChromaT{upload(win), upload(trig), upload(map), upload(cls)}).first;
+    const sonar_ctx::ChromaT t{upload(win), upload(trig), upload(map), upload(cls)};
+    if (!t.win || !t.trig || !t.map || !t.cls) return nullptr;
+    it = c->chroma_tables.emplace(key, t).first;
   }
-  const char* cw = std::getenv("SONAR_CHROMA_WAVE");              // 0: the block-per-frame kernel (A/B)
-  const int* cls = (cw && std::atoi(cw) == 0) ? nullptr : (const int*)it->second.cls;
-  if (sonar::launch_chroma(y, n, F, hop, fs, (const double*)it->second.win, (const double*)it->second.trig,
-                           (const int*)it->second.map, cls, dout, s) != 0)
-    return fail(c, SONAR_ERR_UNSUPPORTED, "chroma launch failed (frame size too large for LDS?)");
-  if (!device_ptrs) {
-    HIP_TRY(c, hipMemcpyAsync(chroma, dout, F * 12 * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-  }
-  return SONAR_OK;
+  return &it->second;
 }
+}  // namespace detail
+}  // namespace sonar
+
+extern "C" {
 
 // ================================================================ NCC ====
 int sonar_ncc(sonar_ctx* c, const double* a, int64_t na, const double* b, int64_t nb, int32_t max_lag, double* corr,

@@ -134,3 +134,50 @@ def test_trim_releases_and_reallocates(ctx, monkeypatch, mixed_pairs):
     got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2)
     for f in sonar.PAIR_FIELDS:
         assert _same(got[f], ref[f]), f
+
+
+@pytest.fixture(scope="module")
+def device_pairs():
+    """Device-resident pairs of 5-12 s (chroma frames of 256 samples: the batched feature launches
+    take the whole batch), plus the same with one 3.3 s pair (257-sample frames: per-pair path)."""
+    import torch
+    rng = np.random.default_rng(12)
+    qs, rs = [], []
+    for k, (sq, sr_) in enumerate([(6.0, 7.5), (9.0, 5.0), (12.0, 10.7), (5.5, 8.9), (7.0, 7.0), (3.3, 3.3)]):
+        q, r = synth.c3_pair(max(sq, sr_), 0.4 + 0.3 * k)[:2]
+        qs.append(torch.from_numpy(np.ascontiguousarray(q[: int(sq * 44100)])).cuda())
+        rs.append(torch.from_numpy(np.ascontiguousarray(r[: int(sr_ * 44100)] +
+                                                        1e-3 * rng.standard_normal(int(sr_ * 44100)))).cuda())
+    torch.cuda.synchronize()
+    return qs, rs
+
+
+def _run_dev(ctx, monkeypatch, qs, rs, **env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    try:
+        return ctx.align_pairs([q.data_ptr() for q in qs], [r.data_ptr() for r in rs],
+                               nq=[q.numel() for q in qs], nr=[r.numel() for r in rs], max_lag_seconds=4.0,
+                               workers=8, device_ptrs=True)
+    finally:
+        for k in env:
+            monkeypatch.delenv(k)
+
+
+@pytest.mark.parametrize("with_short", [False, True])
+@pytest.mark.parametrize("streams", [1, 2])
+def test_batched_features_equal_per_pair(ctx, monkeypatch, device_pairs, streams, with_short):
+    """Device-resident pairs: the batch's music features and NCCs in batched launches (default)
+    against the per-pair launches inside a batch (SONAR_FEAT_BATCH=0) and the unbatched path
+    (SONAR_PAIR_BATCH=0): identical records.  with_short adds a pair whose chroma frames are 257
+    samples, so its batch falls back to the per-pair launches."""
+    qs, rs = device_pairs
+    if not with_short:
+        qs, rs = qs[:-1], rs[:-1]
+    ref = _run_dev(ctx, monkeypatch, qs, rs, SONAR_PAIR_BATCH=0)
+    per = _run_dev(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=streams, SONAR_FEAT_BATCH=0)
+    got = _run_dev(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=streams)
+    assert np.all(ref["status"] == 0) and np.all(got["status"] == 0) and np.all(per["status"] == 0)
+    for f in sonar.PAIR_FIELDS:
+        assert _same(got[f], ref[f]), f
+        assert _same(per[f], ref[f]), f
