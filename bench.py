@@ -397,8 +397,12 @@ def bench_c5(args, world, rank, dev, ctx):
         return ctx.align_pairs([qp[i] for i in idx], [rp[i] for i in idx], nq=[nq[i] for i in idx],
                                nr=[nr[i] for i in idx], max_lag_seconds=args.c5_max_lag,
                                workers=args.c5_workers, device_ptrs=True)
-    run([0])                                   # warm-up: worker contexts, tables, buffers
-    run(list(range(min(len(data), args.c5_workers))))
+    warm_errs = []
+    for idx in ([0], list(range(len(data)))):   # warm-up: worker contexts, tables, buffers
+        try:                                   # recorded, not raised: the timed repetitions decide
+            run(idx)
+        except sonar.SonarError as e:
+            warm_errs.append(str(e))
     torch.cuda.synchronize()
     ctx.dtw_counters(reset=True)
     dts, errs, recd = [], [], None
@@ -429,7 +433,8 @@ def bench_c5(args, world, rank, dev, ctx):
             "c5_max_lag_s": args.c5_max_lag, "c5_workers_per_rank": args.c5_workers, "c5_entry": "sonar_align_pairs",
             "c5_lag_recovered": float(ok.mean()), "c5_dtw_cells_per_pair": F * F,
             "c5_dtw_counters_rank0": counters, "c5_failed_reps": len(errs),
-            **({"c5_error": errs[0]} if errs else {})}
+            "c5_warmup_failed_calls": len(warm_errs),
+            **({"c5_error": errs[0]} if errs else {}), **({"c5_warmup_error": warm_errs[0]} if warm_errs else {})}
 
 
 def bench_c3(args, ctx, dev):

@@ -1947,6 +1947,9 @@ __device__ __forceinline__ int dtww_slot(int64_t row) {
 }
 constexpr int DTWW_DS = 14;                // doubles per ring row: 112 B, b128 reads conflict-free
 constexpr int DTWW_CH = 8;                 // steps per chunk
+#ifndef DTWW_REFRESH
+#define DTWW_REFRESH 1                     // the edge wait's agent-scope acquire per ms (A/B knob)
+#endif
 #ifndef DTWW_EAHEAD
 #define DTWW_EAHEAD 1                      // chunks between an edge poll and its use (A/B 1-3: 1 best)
 #endif
@@ -2006,6 +2009,12 @@ void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
   // another (grid = the batch's wave budget, launch_dtw_batch): a band starts only when a wave
   // is free, so its predecessor (a smaller ticket, taken by a running wave) is usually well ahead
   // and no wave holds a slot waiting down a chain.  Single DTW: one band per block.
+  // DTWW_ACQ: an agent-scope acquire before the first ticket, and the ticket map read with sc1
+  // loads (A/B knob for the first-call deadlocks)
+#ifndef DTWW_ACQ
+#define DTWW_ACQ 1
+#endif
+  if constexpr (BATCH && DTWW_ACQ) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   for (;;) {
   int64_t tb = 0;
   int tk = 0, tt = 0;
@@ -2014,8 +2023,11 @@ void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
       const int t = atomicAdd(bt.ticket, 1);
       tt = t;
       if (bt.map) {
-        if (t < bt.start[bt.n]) {
-          const int2 pb = bt.map[t];
+        const int64_t tot = DTWW_ACQ ? (int64_t)g_load_agent(reinterpret_cast<const uint64_t*>(bt.start + bt.n))
+                                     : bt.start[bt.n];
+        if (t < tot) {
+          const int2 pb = DTWW_ACQ ? __builtin_bit_cast(int2, g_load_agent(reinterpret_cast<const uint64_t*>(bt.map + t)))
+                                   : bt.map[t];
           tk = pb.x;
           tb = pb.y;
         } else {
@@ -2055,7 +2067,10 @@ void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
   // the ring starts zeroed (rows before column 1 are read for cells nobody keeps)
   for (int k = lane; k < (DTWW_RROWS + DTWW_CH) * DTWW_DS / 2; k += 64)
     *reinterpret_cast<double2*>(&ring[2 * k]) = make_double2(0.0, 0.0);
-  if (lane < 16) ctr[lane] = lane == DTW_CTR_TICKET ? __builtin_amdgcn_readfirstlane(tt) : 0;
+  {
+    const int tkt = __builtin_amdgcn_readfirstlane(tt);   // outside the lane < 16 branch: lane 0's ticket
+    if (lane < 16) ctr[lane] = lane == DTW_CTR_TICKET ? tkt : 0;
+  }
   dtw_wave_sync();
   // reference rows in blocks of 16 (192 doubles: 3 per lane), rows past nr as zeros
   auto fetch = [&](int64_t k, double (&v)[3]) {
@@ -2194,6 +2209,8 @@ void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
     uint64_t miss = missing(c, ew);
     if (miss) {
       const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t t_fence = w0;
+      bool fenced = false;
       uint32_t polls = 0;
       do {
         __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);
@@ -2202,6 +2219,14 @@ void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
         if (miss && (++polls & 63) == 0) {
           if (__builtin_amdgcn_readfirstlane(g_load_agent(&a.sync[1]))) return;   // another band gave up
           const uint64_t now = __builtin_amdgcn_s_memrealtime();
+          // the band kernel's edge refresh (DTW_REFRESH_TICKS): one agent-scope acquire per ms
+          // without the edge, counted in diag[13] (diag[14] when the wait then ends)
+          if (DTWW_REFRESH && now - t_fence > DTW_REFRESH_TICKS) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            t_fence = now;
+            fenced = true;
+            if (lane == 0 && a.diag) g_add_agent(&a.diag[13], 1ull);
+          }
           if (polls >= DTW_STALL_POLLS && now - w0 > DTW_STALL_TICKS) {
             // give up: the record is written after the chunk loop (a call inside the loop
             // would cost the loop its register allocation)
@@ -2211,6 +2236,7 @@ void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
         }
       } while (miss);
       if (st_s0 >= 0) break;
+      if (fenced && lane == 0 && a.diag) g_add_agent(&a.diag[14], 1ull);
       if (c > 0) spins += __builtin_amdgcn_s_memrealtime() - w0;   // chunk 0's wait: t_first
     }
     if (a.trace && c == 0) t_first = __builtin_amdgcn_s_memrealtime();

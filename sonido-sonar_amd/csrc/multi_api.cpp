@@ -28,6 +28,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <mutex>
+#include <functional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -143,7 +146,8 @@ bool feat_batch_enabled() {
 // sizes or outside the batched kernels' shapes; on an allocation failure it also sets w->err to
 // "batch features: ..." (the caller's NOMEM retry path).
 bool feat_batch(sonar_ctx* w, const std::vector<PairGeo>& pg, int32_t sr, int32_t sw, int32_t hop, int32_t fw,
-                const double* const* q_pcm, const double* const* r_pcm, char* chroma, char* corr, hipStream_t s) {
+                const double* const* q_pcm, const double* const* r_pcm, char* chroma, char* corr, hipStream_t s,
+                int slot, bool dry = false) {
   w->err.clear();
   if (!feat_batch_enabled() || pg.empty() || fw <= 0 || hop <= 0) return false;
   if (const char* cw = std::getenv("SONAR_CHROMA_WAVE"); cw && std::atoi(cw) == 0) return false;   // chroma_kernel A/B
@@ -171,11 +175,12 @@ bool feat_batch(sonar_ctx* w, const std::vector<PairGeo>& pg, int32_t sr, int32_
   char* nx = (char*)dbuf(w, "fb.ncc", std::max<size_t>(xsz, 256));
   const size_t jb = al256((size_t)2 * n * sizeof(sonar::MfJob)), nb = al256((size_t)std::max(ncorr, 1) * sizeof(sonar::NccJob));
   char* dj = (char*)dbuf(w, "fb.jobs", jb + nb);
-  char* hj = (char*)sonar::detail::hbuf(w, "fb.hjobs", jb + nb);
+  char* hj = (char*)sonar::detail::hbuf(w, "fb.hjobs" + std::to_string(slot), jb + nb);
   if (!ct || !y || !dcs || !en || !nx || !dj || !hj) {
     fail(w, SONAR_ERR_NOMEM, "batch features: allocation failed");
     return false;
   }
+  if (dry) return true;                          // buffers reserved, nothing launched
   auto* mj = (sonar::MfJob*)hj;
   auto* nj = (sonar::NccJob*)(hj + jb);
   size_t yo = 0, doff = 0, eo = 0, xo = 0;
@@ -222,9 +227,21 @@ bool feat_batch(sonar_ctx* w, const std::vector<PairGeo>& pg, int32_t sr, int32_
 // chroma DTWs, then the correlations, path arrays and status words in three copies.  Pairs whose
 // chroma is not finite (the DTW ran the finite-input kernel) are redone one by one through
 // align_one (exact math.Min rules); their indices are appended to `redo`.
+// A batch whose launches and result copies are enqueued: `ev` follows its last copy, `finish`
+// reads the pinned copies and fills the records (run it after ev completes, on the same thread)
+struct PendingBatch {
+  hipEvent_t ev = nullptr;
+  std::function<void()> finish;
+};
+
+// With pend (and no diagnostics switched on) align_batch returns once everything is enqueued and
+// leaves the synchronisation and the scorers to pend->finish, so the worker can enqueue its next
+// batch first: the host scorers and the next batch's setup then overlap this batch's tail on the
+// GPU.  `slot` (0/1) selects the pinned staging set, so the two batches in flight never share one.
 int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* const* q_pcm, const double* const* r_pcm,
                 int32_t sr, int32_t sw, int32_t hop, int32_t fw, int32_t device_ptrs, sonar_pair_record* out,
-                std::vector<int64_t>* redo, std::vector<std::pair<int64_t, std::string>>* errs, int nstreams) {
+                std::vector<int64_t>* redo, std::vector<std::pair<int64_t, std::string>>* errs, int nstreams,
+                int slot = 0, PendingBatch* pend = nullptr, bool dry = false) {
   const int n = (int)in.size();
   if (n == 0) return SONAR_OK;
   HIP_TRY(w, hipSetDevice(w->device));
@@ -274,10 +291,17 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   double* st = (double*)dbuf(w, "ncc.stats", 64);
   double* up_q = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.q", (size_t)maxn * 8);
   double* up_r = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.r", (size_t)maxn * 8);
-  char* h = (char*)sonar::detail::hbuf(w, "pb.host", stat_b + diag_b + args_b + start_b + map_b + corr_b + path_b);
+  char* h = (char*)sonar::detail::hbuf(w, "pb.host" + std::to_string(slot),
+                                       stat_b + diag_b + args_b + start_b + map_b + corr_b + path_b);
   if (!chroma || !CK || !runs || (pre && !Dd) || !Dn || !E || !codes || !wst || !path || !corr || !small || !eq || !er || !xa || !xb || !st ||
       (!device_ptrs && (!up_q || !up_r)) || !h)
     return fail(w, SONAR_ERR_NOMEM, "allocation failed (pair batch)");
+  if (dry) {   // reserve only (sonar_align_pairs' sizing pass): the batched-feature buffers too
+    if (device_ptrs && !feat_batch(w, pg, sr, sw, hop, fw, q_pcm, r_pcm, chroma, corr, s, slot, true) &&
+        w->err.rfind("batch features:", 0) == 0)
+      return SONAR_ERR_NOMEM;
+    return SONAR_OK;
+  }
   int32_t* dstat = (int32_t*)small;                 // per pair: [0..1] plen, [2..3] C[nq][nr], [4..7] sync
   int32_t* ticket = (int32_t*)(small + (size_t)n * 32);
   uint64_t* ddiag = (uint64_t*)(small + stat_b);
@@ -322,7 +346,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   // every pair's music features and energy NCC: batched launches over the whole batch when the
   // inputs are on the device and every signal fits the batched kernels (feat_batch), else pair by
   // pair on the worker's scratch
-  const bool fb = device_ptrs && feat_batch(w, pg, sr, sw, hop, fw, q_pcm, r_pcm, chroma, corr, s);
+  const bool fb = device_ptrs && feat_batch(w, pg, sr, sw, hop, fw, q_pcm, r_pcm, chroma, corr, s, slot);
   if (!fb && !w->err.empty() && w->err.rfind("batch features:", 0) == 0) return SONAR_ERR_NOMEM;
   int64_t acc = 0;
   for (int i = 0; i < n; ++i) {
@@ -395,7 +419,8 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   HIP_TRY(w, hipMemcpyAsync(hstat, small, stat_b + diag_b, hipMemcpyDeviceToHost, s));
   if (corr_b) HIP_TRY(w, hipMemcpyAsync(hcorr, corr, corr_b, hipMemcpyDeviceToHost, s));
   HIP_TRY(w, hipMemcpyAsync(hpath, path, path_b, hipMemcpyDeviceToHost, s));
-  HIP_TRY(w, hipStreamSynchronize(s));
+  const char* dump_dir = std::getenv("SONAR_PAIR_DUMP");
+  auto fin = [=, pg = std::move(pg), state_off = std::move(state_off), trace_off = std::move(trace_off)]() {
   if (dtrace) {
     // ticks of s_memrealtime (100 MHz): band-time = end - start, of which first-edge wait =
     // first - start and later edge waits = the sweep's spin ticks; steps = S per band
@@ -445,7 +470,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
       errs->emplace_back(p.k, why);
       continue;
     }
-    if (const char* dump = std::getenv("SONAR_PAIR_DUMP")) {
+    if (const char* dump = dump_dir) {
       // tests only: the batched DTW's raw outputs of pair k (path length, C[nq][nr], path costs,
       // query and reference indices) into <dump>/pair_<k>.bin, to be checked against the oracle
       const double* pc = (const double*)(hpath + p.path);
@@ -468,6 +493,15 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     sonar::detail::align_finish(ai, nullptr, rec);
     rec->status = SONAR_OK;
   }
+  };
+  // diagnostics read device buffers after the sync, which the next batch would reuse: no deferral
+  if (pend && pend->ev && !dtrace && !dstate && !dump_dir) {
+    HIP_TRY(w, hipEventRecord(pend->ev, s));
+    pend->finish = std::move(fin);
+    return SONAR_OK;
+  }
+  HIP_TRY(w, hipStreamSynchronize(s));
+  fin();
   return SONAR_OK;
 }
 
@@ -562,17 +596,58 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
     batches.push_back(std::move(b));
   }
   std::atomic<size_t> next{0};
+  const char* rev = std::getenv("SONAR_PAIR_RESERVE");
+  const bool reserve = !(rev && rev[0] == '0');
+  std::mutex rmu;
+  std::condition_variable rcv;
+  int rdone = 0;
   std::vector<std::vector<int64_t>> redo(nstreams);
   std::vector<std::vector<std::pair<int64_t, std::string>>> errs(nstreams);
   for (int t = 0; t < nstreams; ++t) {
     th.emplace_back([&, t] {
       sonar_ctx* w = ws[t];
+      // sizing pass: every worker reserves its buffers for the largest of all batches before any
+      // worker launches.  Allocating or freeing device / pinned memory while other workers' DTW
+      // pipelines run stalled them: every fresh-process C5 run lost 9-52 DTWs to band-pipeline
+      // timeouts in the first call (buffers growing batch by batch), none once sizes had settled
+      // (DESIGN §6).  SONAR_PAIR_RESERVE=0 skips it (A/B).
+      if (reserve) {
+        for (const auto& b : batches)
+          if (align_batch(w, b, q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window, device_ptrs, out,
+                          &redo[t], &errs[t], nstreams, 0, nullptr, true) != SONAR_OK)
+            break;                                 // NOMEM: the batch loop's retry path handles it
+        if (hipSetDevice(w->device) == hipSuccess) (void)hipStreamSynchronize(w->stream);
+        std::unique_lock<std::mutex> lk(rmu);
+        if (++rdone == nstreams) rcv.notify_all();
+        else rcv.wait(lk, [&] { return rdone == nstreams; });
+      }
+      // SONAR_PAIR_PIPELINE=1 (opt-in): two batches in flight per worker -- batch b is enqueued,
+      // then batch b-1's results are waited for and scored while b runs.  Measured 1,877 pairs/s
+      // at 8 streams against 1,790 for the default 16 x 1, but one of its first C5 runs ended in a
+      // DTW band-pipeline timeout whose record is not yet explained, so it is not the
+      // default
+      PendingBatch pend[2];
+      const char* pev = std::getenv("SONAR_PAIR_PIPELINE");
+      if (pev && pev[0] == '1')
+        for (auto& x : pend)
+          if (hipSetDevice(w->device) != hipSuccess || hipEventCreateWithFlags(&x.ev, hipEventDisableTiming) != hipSuccess)
+            x.ev = nullptr;
+      int cur = 0;
+      auto drain = [&](PendingBatch& x) {
+        if (!x.finish) return;
+        if (hipEventSynchronize(x.ev) != hipSuccess) (void)hipStreamSynchronize(w->stream);
+        x.finish();
+        x.finish = nullptr;
+      };
       for (size_t bi = next.fetch_add(1); bi < batches.size(); bi = next.fetch_add(1)) {
         int r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window,
-                            device_ptrs, out, &redo[t], &errs[t], nstreams);
+                            device_ptrs, out, &redo[t], &errs[t], nstreams, cur, pend[cur].ev ? &pend[cur] : nullptr);
+        drain(pend[cur ^ 1]);
+        cur ^= 1;
         if (r == SONAR_ERR_NOMEM) {
           // the worker's cached buffers are sized by earlier batches, name by name: release them
           // and retry the batch once; then pair by pair on the unbatched path
+          drain(pend[cur ^ 1]);
           sonar::detail::trim_buffers(w);
           r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window, device_ptrs,
                           out, &redo[t], &errs[t], nstreams);
@@ -587,6 +662,10 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
         if (r != SONAR_OK)
           for (const auto& p : batches[bi]) { out[p.k].status = r; note(r, p.k, w); }
       }
+      drain(pend[cur ^ 1]);
+      drain(pend[cur]);
+      for (auto& x : pend)
+        if (x.ev) (void)hipEventDestroy(x.ev);
       for (int64_t k : redo[t])                    // non-finite chroma: exact single-pair path
         note(align_one(w, q_pcm[k], nq[k], r_pcm[k], nr[k], sample_rate, stft_window, hop, feature_window,
                        max_lag_seconds, device_ptrs, &out[k]), k, w);

@@ -46,11 +46,14 @@ def main():
         except AttributeError:               # an A/B build of an earlier round
             return {}
 
+    t0 = time.perf_counter()
+    werr = None
     try:
         run()
     except sonar.SonarError as e:
-        print(json.dumps({"warmup_error": str(e)}), flush=True)
-    counters()
+        werr = str(e)
+        print(json.dumps({"warmup_error": werr}), flush=True)
+    print(json.dumps({"warmup": True, "s": round(time.perf_counter() - t0, 4), **counters(), "error": werr}), flush=True)
     fails, tot = 0, {}
     for i in range(a.reps):
         t0 = time.perf_counter()

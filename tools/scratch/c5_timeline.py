@@ -25,6 +25,12 @@ def cat(name):
     return "other"
 
 
+# the C5 window: dispatches of queues that ran DTW kernels (the worker streams)
+wq = {r[qkey] for r in rows if cat(r["Kernel_Name"]) == "dtw"}
+rows = [r for r in rows if r[qkey] in wq]
+byname = defaultdict(list)
+for r in rows:
+    byname[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 byq = defaultdict(list)
 for r in rows:
     byq[r[qkey]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), cat(r["Kernel_Name"]), r["Kernel_Name"]))
@@ -57,3 +63,6 @@ for t, d in ev:
     last = t
 hist[cur] += t1 - last
 print("DTW kernels in flight (share of span): " + "  ".join(f"{k}:{v / (t1 - t0):.3f}" for k, v in sorted(hist.items())))
+print("kernels by total time (worker queues):")
+for nm, d in sorted(byname.items(), key=lambda kv: -sum(kv[1]))[:16]:
+    print(f"  {sum(d) / 1e6:9.1f} ms  n={len(d):6d}  mean {sum(d) / len(d) / 1e3:8.1f} us  {cat(nm):5s} {nm[:90]}")
