@@ -52,6 +52,7 @@ def test_injected_stall_in_pair_batch_names_the_pair(ctx, monkeypatch, band2):
         rs.append(r)
     monkeypatch.setenv("SONAR_DTW_DBG_STALL", "4")
     monkeypatch.setenv("SONAR_PAIR_STREAMS", "1")
+    monkeypatch.setenv("SONAR_PAIR_RETRY", "0")   # the batch's own diagnosed error, not the single-pair redo
     t0 = time.perf_counter()
     with pytest.raises(sonar.SonarError) as ei:
         ctx.align_pairs(qs, rs, max_lag_seconds=3.0, workers=8)
