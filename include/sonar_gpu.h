@@ -395,8 +395,10 @@ typedef struct {
  * walk) overlap on the GPU.  HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues
  * (4 by default, at most 32): set GPU_MAX_HW_QUEUES >= SONAR_PAIR_STREAMS in the environment
  * before the first HIP call of the process, or the streams share queues and serialise.  out[k] is
- * filled for every pair; the return is SONAR_OK or the first error (a band pipeline that timed
- * out names the pair and carries its diagnostic record in sonar_last_error). */
+ * filled for every pair; the return is SONAR_OK or the first error.  A pair whose batched band
+ * pipeline timed out is redone once on the single-pair path (exact; counted in
+ * sonar_dtw_counters); with SONAR_PAIR_RETRY=0 it is an error instead, naming the pair and
+ * carrying its diagnostic record in sonar_last_error. */
 int sonar_align_pairs(sonar_ctx* ctx, int64_t npairs, const double* const* q_pcm, const int64_t* nq,
                       const double* const* r_pcm, const int64_t* nr, int32_t sample_rate, int32_t stft_window,
                       int32_t hop, int32_t feature_window, double max_lag_seconds, int32_t workers,
