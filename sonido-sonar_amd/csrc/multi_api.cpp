@@ -626,7 +626,12 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
           if (align_batch(w, b, q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window, device_ptrs, out,
                           &redo[t], &errs[t], nstreams, 0, nullptr, true) != SONAR_OK)
             break;                                 // NOMEM: the batch loop's retry path handles it
-        if (hipSetDevice(w->device) == hipSuccess) (void)hipStreamSynchronize(w->stream);
+        // one small fill on the worker's stream: HIP gives a stream its hardware queue at its first
+        // command, so every worker's queue exists before any worker's DTW pipeline runs
+        if (hipSetDevice(w->device) == hipSuccess) {
+          if (void* z = dbuf(w, "pb.touch", 256)) (void)hipMemsetAsync(z, 0, 256, w->stream);
+          (void)hipStreamSynchronize(w->stream);
+        }
         std::unique_lock<std::mutex> lk(rmu);
         if (++rdone == nstreams) rcv.notify_all();
         else rcv.wait(lk, [&] { return rdone == nstreams; });
