@@ -3065,14 +3065,15 @@ bool dtw_band2_enabled(int dim) {
   return e && e[0] == '1' && dim == 12;
 }
 
-// SONAR_DTW_WAVE=0: the 8-wave dtw_band_kernel instead of the one-wave dtw_wave_kernel for 12-dim
-// FAST checkpoint-mode DTWs (A/B)
+// SONAR_DTW_WAVE=1: the one-wave dtw_wave_kernel instead of the 8-wave dtw_band_kernel for 12-dim
+// FAST checkpoint-mode DTWs, batched and single (opt-in).  Batches ran on it by default until its
+// band pipeline was found to deadlock in a process's first sonar_align_pairs call (DESIGN §6:
+// 20 of 24 fresh processes lost DTWs to it, the band kernel 0 of 4 at the same C5 throughput once
+// the features were batched)
 static bool dtw_wave_enabled() {
   const char* e = std::getenv("SONAR_DTW_WAVE");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
-// the single DTW (one chain of bands, latency-bound) keeps the 8-wave band kernel unless
-// SONAR_DTW_WAVE=1 asks for the one-wave kernel there too
 bool dtw_wave_batch_enabled() { return dtw_wave_enabled(); }
 // the batched one-wave kernel's schedule (A/B; both measured slower on C5, DESIGN Kernel 6):
 // SONAR_DTW_LEAN=1 no cross-chunk pipelining (several waves per SIMD), SONAR_DTW_IL=1 the next

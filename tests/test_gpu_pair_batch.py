@@ -95,12 +95,13 @@ def test_precomputed_distance_pairs(ctx, monkeypatch, mixed_pairs):
         assert _same(got[f], ref[f]), f
 
 
-@pytest.mark.parametrize("env", [dict(SONAR_DTW_WAVE=0), dict(SONAR_DTW_BAND2=1), dict(SONAR_DTW_LEAN=1), dict(SONAR_DTW_IL=1)])
+@pytest.mark.parametrize("env", [dict(SONAR_DTW_WAVE=1), dict(SONAR_DTW_BAND2=1), dict(SONAR_DTW_WAVE=1, SONAR_DTW_LEAN=1),
+                                 dict(SONAR_DTW_WAVE=1, SONAR_DTW_IL=1)])
 def test_batch_dtw_kernels_agree(ctx, monkeypatch, mixed_pairs, env):
-    """The batch's default one-wave DTW kernel (dtw_wave_kernel) against the 8-wave band kernel
-    (SONAR_DTW_WAVE=0), the 128-row kernel (SONAR_DTW_BAND2=1), the one-wave kernel without
-    cross-chunk pipelining (SONAR_DTW_LEAN=1) and with the next chunk's sums fenced between the
-    steps (SONAR_DTW_IL=1): identical records."""
+    """The batch's default 8-wave band kernel (dtw_band_kernel) against the one-wave kernel
+    (SONAR_DTW_WAVE=1) in its three schedules (pipelined; SONAR_DTW_LEAN=1 without cross-chunk
+    pipelining; SONAR_DTW_IL=1 with the next chunk's sums fenced between the steps) and the
+    128-row kernel (SONAR_DTW_BAND2=1): identical records."""
     qs, rs = mixed_pairs
     ref = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2)
     got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2, **env)
