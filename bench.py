@@ -397,14 +397,19 @@ def bench_c5(args, world, rank, dev, ctx):
         return ctx.align_pairs([qp[i] for i in idx], [rp[i] for i in idx], nq=[nq[i] for i in idx],
                                nr=[nr[i] for i in idx], max_lag_seconds=args.c5_max_lag,
                                workers=args.c5_workers, device_ptrs=True)
-    warm_errs = []
+    # a timed-out band pipeline is a failed call here, never a silent single-pair redo (the
+    # library's default retry is off for the whole leg); the warm-up calls' liveness counters are
+    # reported before they are reset, so a first-call failure shows in the line
+    os.environ["SONAR_PAIR_RETRY"] = "0"
+    ctx.dtw_counters(reset=True)
+    warm_errs, warm_redone = [], 0
     for idx in ([0], list(range(len(data)))):   # warm-up: worker contexts, tables, buffers
         try:                                   # recorded, not raised: the timed repetitions decide
-            run(idx)
+            warm_redone += int(np.count_nonzero(run(idx)["flags"]))
         except sonar.SonarError as e:
             warm_errs.append(str(e))
     torch.cuda.synchronize()
-    ctx.dtw_counters(reset=True)
+    warm_counters = ctx.dtw_counters(reset=True)
     dts, errs, recd = [], [], None
     for _ in range(args.reps):
         barrier(world)
@@ -433,7 +438,9 @@ def bench_c5(args, world, rank, dev, ctx):
             "c5_max_lag_s": args.c5_max_lag, "c5_workers_per_rank": args.c5_workers, "c5_entry": "sonar_align_pairs",
             "c5_lag_recovered": float(ok.mean()), "c5_dtw_cells_per_pair": F * F,
             "c5_dtw_counters_rank0": counters, "c5_failed_reps": len(errs),
-            "c5_warmup_failed_calls": len(warm_errs),
+            "c5_warmup_dtw_counters": warm_counters, "c5_warmup_failed_calls": len(warm_errs),
+            "c5_retry": "off (SONAR_PAIR_RETRY=0)", "c5_redone_pairs_last_rep": int(np.count_nonzero(recd["flags"])),
+            "c5_warmup_redone_pairs": warm_redone,
             **({"c5_error": errs[0]} if errs else {}), **({"c5_warmup_error": warm_errs[0]} if warm_errs else {})}
 
 

@@ -383,8 +383,12 @@ typedef struct {
   double dtw_distance;           /* the chroma-DTW candidate (NaN if none)         */
   double peak_lag;               /* NCC peak lag in feature frames (NaN if none)   */
   int32_t status;                /* SONAR_OK or this pair's error code             */
-  int32_t reserved;
+  int32_t flags;                 /* SONAR_PAIR_REDONE_* bits (0: the batched path) */
 } sonar_pair_record;
+
+/* sonar_pair_record.flags: the pair's record came from the single-pair path instead of its batch */
+#define SONAR_PAIR_REDONE_TIMEOUT 1    /* its batched band pipeline timed out (retry on)  */
+#define SONAR_PAIR_REDONE_NONFINITE 2  /* its chroma is not finite (exact math.Min path)  */
 
 /* sonar_align_pair_device over npairs pairs: q_pcm[k] / r_pcm[k] float64 streams of nq[k] / nr[k]
  * samples (device pointers on ctx's device if device_ptrs, else host arrays).  `workers` is the
@@ -397,8 +401,9 @@ typedef struct {
  * before the first HIP call of the process, or the streams share queues and serialise.  out[k] is
  * filled for every pair; the return is SONAR_OK or the first error.  A pair whose batched band
  * pipeline timed out is redone once on the single-pair path (exact; counted in
- * sonar_dtw_counters); with SONAR_PAIR_RETRY=0 it is an error instead, naming the pair and
- * carrying its diagnostic record in sonar_last_error. */
+ * sonar_dtw_counters and flagged SONAR_PAIR_REDONE_TIMEOUT in its record); with
+ * SONAR_PAIR_RETRY=0 it is an error instead, naming the pair and carrying its diagnostic record in
+ * sonar_last_error. */
 int sonar_align_pairs(sonar_ctx* ctx, int64_t npairs, const double* const* q_pcm, const int64_t* nq,
                       const double* const* r_pcm, const int64_t* nr, int32_t sample_rate, int32_t stft_window,
                       int32_t hop, int32_t feature_window, double max_lag_seconds, int32_t workers,

@@ -515,11 +515,7 @@ __device__ __forceinline__ int64_t dtw_cn_off(int64_t b, int64_t S2, int64_t s, 
 // system-scope load, atomic fetch_or(0) at agent and system scope -- so a value that never left the
 // producer can be told apart from one the consumer's caches did not show, and scans that edge row
 // for the first column still holding the sentinel (how far the producer got).
-#ifdef DTW_STALL_INLINE   // A/B knob
-__device__ __forceinline__ void dtw_stall(
-#else
 __device__ __attribute__((noinline)) void dtw_stall(
-#endif
     int32_t* sync, uint64_t* diag, int role, int64_t b, int* ctr,
                                                      const uint64_t* Ein, int64_t nr, uint32_t polls, uint64_t t0) {
   const int lane = threadIdx.x & 63;
@@ -545,9 +541,6 @@ __device__ __attribute__((noinline)) void dtw_stall(
     }
   }
   claimed = __builtin_amdgcn_readfirstlane(claimed);
-#ifdef DTW_STALL_LITE   // A/B knob: no diagnostic record beyond the header
-  claimed = 0;
-#endif
   if (!claimed) return;
   const int64_t lo = prog < cprog ? prog : cprog;
   const int64_t want = lo + DTW_EAHEAD < nr ? lo + DTW_EAHEAD : nr;
@@ -612,23 +605,15 @@ __device__ __forceinline__ void dtw_local_stall(int role, int32_t* sync, int* ct
   }
 }
 
-// PRE: the local distances come precomputed from dtw_dist_kernel (a.Dd), so the block is only
-// the sweep, a distance LOADER wave (global -> the LDS distance ring, several chunks of loads in
-// flight), the code wave and the edge poller: 4 waves and no reference-row ring, which lets 4
-// blocks share a CU (every band of a 51,676-row problem resident at once)
-constexpr int dtw_block_waves(bool pre) { return pre ? 4 : DTW_WAVES; }
-#ifndef DTW_PF
-#define DTW_PF 4                  // loader: distance chunks of global loads in flight
-#endif
-template <int D, bool FAST, bool BANDED, bool BATCH = false, bool PRE = false>
-// (2 blocks of 7 waves per CU: at least 4 waves per SIMD, <= 128 VGPRs)
-__global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
+template <int D, bool FAST, bool BANDED, bool BATCH = false>
+// (2 blocks of 8 waves per CU: at least 4 waves per SIMD, <= 128 VGPRs)
+__global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
   constexpr int DR = D > 0 ? D : 1;
   constexpr int DS = dtw_ring_stride<D>();
-  constexpr int FEEDER_WAVE = PRE ? -1 : DTW_FEEDER_WAVE;
-  constexpr int CODE_WAVE = PRE ? 2 : DTW_CODE_WAVE;
-  constexpr int EDGE_WAVE = PRE ? 3 : DTW_EDGE_WAVE;
-  __shared__ __attribute__((aligned(16))) double ring[PRE ? 2 : (DTW_RROWS + DTW_RMIR) * DS];
+  constexpr int FEEDER_WAVE = DTW_FEEDER_WAVE;
+  constexpr int CODE_WAVE = DTW_CODE_WAVE;
+  constexpr int EDGE_WAVE = DTW_EDGE_WAVE;
+  __shared__ __attribute__((aligned(16))) double ring[(DTW_RROWS + DTW_RMIR) * DS];
   __shared__ __attribute__((aligned(16))) double dring[64][DTW_DROW];   // distance of step t at [l][t % DQ]
   __shared__ __attribute__((aligned(16))) double oring[64][DTW_OROW];   // C of step t at [l][t % OQ]
   __shared__ __attribute__((aligned(16))) double eqa[DTW_EQ];           // C[64b][c] at slot c - 1
@@ -688,11 +673,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   const int64_t nq = a.nq, nr = a.nr, S = a.S, S2 = (a.S + 1) >> 1;
   const int dim = D > 0 ? D : a.dim;
   constexpr uint64_t INF_BITS = 0x7FF0000000000000ull;
-#ifdef DTW_DBG_NOEDGE   // A/B diagnostics: every band independent (wrong results; throughput ceiling)
-  const uint64_t* Ein = nullptr;
-#else
   const uint64_t* Ein = b > 0 ? a.E + (b - 1) * (nr + 1) : nullptr;       // C[64b][j] at index j
-#endif
   const int64_t nblk = (nr + DTW_RBLK - 1) / DTW_RBLK;
   const int64_t i = 64 * b + 1 + lane;
   const bool row_ok = i <= nq;
@@ -701,21 +682,6 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   uint32_t dead_ = 0;
   // spin (LDS only) until `cond` holds; bounded, see DTW_SPIN_CHECK.  A wave that gives up, or sees
   // the block's abort word, sets dead_ and runs out its loop without waiting again.
-#ifdef DTW_OLD_SPIN   // A/B knob: round 2's wait (poll-count bound, no abort word)
-#define SONAR_SPIN_UNTIL(role, cond)                                                  \
-  do {                                                                                \
-    uint64_t sp_ = 0;                                                                 \
-    if (!(cond)) {                                                                    \
-      const uint64_t w0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;            \
-      while (!(cond)) {                                                               \
-        __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);                                     \
-        if (++sp_ > (uint64_t)(1 << 24)) { if (lane == 0) atomicOr(&a.sync[1], 2); break; } \
-      }                                                                               \
-      if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - w0_;             \
-    }                                                                                 \
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
-  } while (0)
-#else
 #define SONAR_SPIN_UNTIL(role, cond)                                                  \
   do {                                                                                \
     if (!dead_ && !(cond)) {                                                          \
@@ -739,12 +705,11 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     }                                                                                 \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
   } while (0)
-#endif
 
   if (wave == FEEDER_WAVE || wave == EDGE_WAVE) {
     // ------------------------------------------------ ring feeder / edge poller
     // two waves, so the edge poll's global-load latency never delays a ring refill
-    const bool do_ring = !PRE && wave == FEEDER_WAVE;
+    const bool do_ring = wave == FEEDER_WAVE;
     int64_t nextblk = 0, have = 0;
     // polls without work since the last one that found work, the realtime of the 64th of them,
     // and the edge poller's refresh state
@@ -760,11 +725,11 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
 #pragma unroll
       for (int k = 0; k < DR; ++k) pv[k] = (lane < DTW_RBLK && row < nr) ? DTW_GLOBAL(a.r)[row * D + k] : 0.0;
     };
-    if constexpr (D > 0 && !PRE) prefetch(0);
+    if constexpr (D > 0) prefetch(0);
     while (true) {
       const int64_t p = SONAR_LDS_LD(prog), cp = SONAR_LDS_LD(cprog);
       bool work = false, wait_edge = false;
-      if (D > 0 && !PRE && do_ring) {
+      if (D > 0 && do_ring) {
         // block m overwrites rows up to r = RBLK*m - RROWS + RBLK - 1, which distance chunks up to
         // index (r + 63) / ECH read (chunk t0 reads rows t0-63 .. t0+7): all of them are done once
         // every distance wave's counter is above that index (wave w has finished every chunk
@@ -806,11 +771,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
           wait_edge = true;
           const int64_t jj = have + 1 + lane;
           uint64_t v = INF_BITS;
-#ifdef DTW_FLAT_EDGE     // A/B knob: the generic-pointer poll (flat_load ... sc1 in the batched kernel)
-          if (jj <= want) v = __hip_atomic_load(Ein + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
           if (jj <= want) v = g_load_agent(Ein + jj);
-#endif
           const uint64_t bad = __builtin_amdgcn_ballot_w64(jj <= want && v == DTW_SENT);
           const int64_t lim = want - have < 64 ? want - have : 64;
           const int64_t got = bad ? (int64_t)__builtin_ctzll(bad) : lim;   // contiguous ready prefix
@@ -826,18 +787,6 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
           }
         }
       }
-#ifdef DTW_OLD_EDGE   // A/B knob: round 2's idle handling (cumulative poll bound)
-      if (do_ring ? (D == 0 || nextblk >= nblk) : have >= ecols) break;
-      (void)wait_edge; (void)fenced; (void)t_fence; (void)t_idle;
-      if (!work) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++idle > (1u << 24)) {
-          if (lane == 0) { atomicOr(&a.sync[1], 1); SONAR_LDS_ST(efill, (int)ecols); SONAR_LDS_ST(rdy, (int)nblk); }
-          break;
-        }
-      }
-    }
-#else
       if (do_ring ? (D == 0 || nextblk >= nblk) : have >= ecols) break;
       if (work) {
         // diag[14]: the first poll after a refresh found new values
@@ -876,7 +825,6 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         }
       }
     }
-#endif
     return;
   }
 
@@ -940,10 +888,8 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         // (one LDS read of the C ring, still holding the chunk, instead of a select over cv[])
         const double cap = u < DTW_ECH ? oring[lane][(s0 + u) & (DTW_OQ - 1)] : ckv;
         const int64_t J = s0 - 56;
-#ifndef DTW_DBG_NOCK   // A/B diagnostics: no checkpoint stores (wrong path costs; timing only)
         if ((s0 & 63) == 56 && J >= 64 && J <= nr)
           DTW_GLOBAL(a.CK)[((b * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = (u < DTW_ECH && lane != 0) ? cap : ckv;
-#endif
         ckv = cap;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -958,7 +904,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   }
 
   double qv[DR];
-  if constexpr (D > 0 && !PRE) {
+  if constexpr (D > 0) {
 #pragma unroll
     for (int k = 0; k < D; ++k) qv[k] = DTW_GLOBAL(a.q)[qrow * D + k];
   }
@@ -978,53 +924,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     return sqrt(sum);
   };
 
-  if (PRE && wave == 1) {
-    // ---------------------------------------------------------- distance loader (PRE)
-    // chunk c = steps 8c .. 8c+7: four 16-B loads per lane (its pairs of steps in Dd), DTW_PF
-    // chunks ahead in registers; written to the distance ring once the sweep has freed the slots
-    // (the same rule as the distance waves), then every dchunk counter is set to c + 1
-    const __attribute__((address_space(1))) double* Db = DTW_GLOBAL(a.Dd) + dtw_cn_off(b, S2, 0, lane);
-    const int64_t nch = (S + DTW_ECH - 1) / DTW_ECH;
-    double buf[DTW_PF][DTW_ECH];
-    auto fetch = [&](int64_t c, double (&v)[DTW_ECH]) {
-      const int64_t p0 = (DTW_ECH * c) >> 1;
-#pragma unroll
-      for (int u = 0; u < DTW_ECH / 2; ++u) {
-        double2 x = make_double2(0.0, 0.0);
-        if (p0 + u < S2) {
-          const dtw_d2 y = *(const __attribute__((address_space(1))) dtw_d2*)(Db + ((p0 + u) << 7));
-          x = make_double2(y.x, y.y);
-        }
-        v[2 * u] = x.x;
-        v[2 * u + 1] = x.y;
-      }
-    };
-#pragma unroll
-    for (int k = 0; k < DTW_PF; ++k)
-      if (k < nch) fetch(k, buf[k]);
-    for (int64_t c0 = 0; c0 < nch; c0 += DTW_PF) {
-#pragma unroll
-      for (int k = 0; k < DTW_PF; ++k) {
-        const int64_t c = c0 + k;
-        if (c < nch) {
-          const int64_t t0 = DTW_ECH * c;
-          SONAR_SPIN_UNTIL(DTW_ROLE_LOADER, SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW_DQ);
-          double* drow = &dring[lane][t0 & (DTW_DQ - 1)];
-#pragma unroll
-          for (int u = 0; u < DTW_ECH; u += 2)
-            *reinterpret_cast<double2*>(drow + u) = make_double2(buf[k][u], buf[k][u + 1]);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          if (lane == 0) {
-#pragma unroll
-            for (int k = 0; k < DTW_NDW; ++k) SONAR_LDS_ST(ctr[k], (int)(c + 1));
-          }
-          if (c + DTW_PF < nch) fetch(c + DTW_PF, buf[k]);
-        }
-      }
-    }
-    return;
-  }
-  if (!PRE && wave >= 1) {   // (every other role returned above)
+  if (wave >= 1) {   // (every other role returned above)
     // ---------------------------------------------------------- distance waves
     const int w = dtw_dist_index(wave);
     for (int64_t c = w; DTW_ECH * c < S; c += DTW_NDW) {
@@ -1036,10 +936,6 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
         const int64_t need = (t0 + DTW_ECH - 1) / DTW_RBLK;             // rows up to t0+7
         const int64_t needc = need < nblk - 1 ? need : nblk - 1;
         SONAR_SPIN_UNTIL(DTW_ROLE_DIST, SONAR_LDS_LD(rdy) >= needc);
-#ifdef DTW_DBG_NODIST   // A/B diagnostics: the distance waves only signal
-#pragma unroll
-        for (int u = 0; u < DTW_ECH; ++u) dv[u] = 0.0;
-#else
         // rows t0-l .. t0-l+7 sit at consecutive slots (mirror), so one base + immediate offsets;
         // steps past S and rows outside [0, nr) give values the sweep never stores.  The chunk's
         // cells advance together, one dimension at a time: each sum is Go's sequential chain,
@@ -1090,7 +986,6 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
             for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt(sum[u]);
           }
         }
-#endif
       } else {
 #pragma unroll
         for (int u = 0; u < DTW_ECH; ++u) dv[u] = dist_rt(t0 + u);
@@ -1109,9 +1004,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   // ---------------------------------------------------------------- sweep wave
   // the min-chain is the pipeline's critical path: it wins VALU arbitration over the distance
   // waves sharing its SIMD (MI355X_MICROARCH.md, "VALU issue is arbitrated ... by priority")
-#ifndef DTW_NOPRIO
   __builtin_amdgcn_s_setprio(3);
-#endif
   const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
   const uint64_t c_start = a.trace ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t t_first = 0;
@@ -1162,11 +1055,7 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
   // behind the counter read that covers them (LDS returns one wave's requests in order), with no
   // wait between the two
   typedef double d2v __attribute__((ext_vector_type(2)));
-#ifdef DTW_NOVOL   // A/B knob: plain loads
-  typedef __attribute__((address_space(3))) d2v lds_d2;
-#else
   typedef __attribute__((address_space(3))) volatile d2v lds_d2;
-#endif
   auto load_chunk = [&](int64_t s0, double (&dc)[DTW_ECH], double (&ech)[DTW_ECH]) {
     const double* dr = &dring[lane][s0 & (DTW_DQ - 1)];
     const double* er = &eqa[s0 & (DTW_EQ - 1)];        // columns s0+1 .. s0+8
@@ -1247,20 +1136,12 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     // the chunk's 8 edge values (lane 63's C) are read back before the release, so the one
     // LDS drain covers both the ring writes and this read
     const double ev = oring[63][(s0 + (lane & (DTW_ECH - 1))) & (DTW_OQ - 1)];
-#ifdef DTW_NOFENCE
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#endif
     if (lane == 0) SONAR_LDS_ST(prog, (int)(s1 < S ? s1 : S));   // steps < s1 are done
     if (Eout) {                                        // one sc1 store of the chunk's 8 edge values
       const int64_t je = s0 + lane - 62;               // lane 63's column at step s0 + lane
       if (lane < DTW_ECH && je >= 1 && je <= nr)
-#ifdef DTW_FLAT_EDGE
-        __hip_atomic_store(Eout + je, __builtin_bit_cast(uint64_t, ev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
         g_store_agent(Eout + je, __builtin_bit_cast(uint64_t, ev));
-#endif
     }
     if (s1 >= S) break;
     if (!ready((int)s1, kc)) {
@@ -1269,11 +1150,9 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
       // the chunk, so the fresh counters and the chunk's data are read back to back (LDS
       // completes a wave's requests in order: data read after a count that covers it is valid),
       // one LDS round trip instead of two; only a still-missing producer spins.
-#ifndef DTW_NOREREAD
       kc = load_ctr();
       load_chunk(s1, dcn, echn);
       if (!ready((int)s1, kc))
-#endif
       {
         SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready((int)s1, kc)));
         load_chunk(s1, dcn, echn);
@@ -1298,1105 +1177,6 @@ __global__ __launch_bounds__(64 * dtw_block_waves(PRE), DTW_MINWAVES) void dtw_b
     tr[8 * b + 3] = (spins_total & 0xFFFFFFull) | ((xcc & 0xFF) << 24) | (hw << 32);
     tr[8 * b + 4] = c_start;
     tr[8 * b + 5] = __builtin_amdgcn_s_memtime();
-  }
-}
-
-// ------------------------------------------------------- DTW: two 64-row sub-bands per block ----
-// dtw_band2_kernel: the band kernel over 128-row bands.  Lane l owns TWO rows, 128B+1+l (the top
-// sub-band = 64-band 2B) and 128B+65+l (the bottom sub-band = 64-band 2B+1).  At step s the top
-// row relaxes column s-l+1 and the bottom row column s-l-63, i.e. the bottom sub-band runs the
-// top's sweep 64 steps later, and its lane 0 takes its upper neighbour C[128B+64][j] from the top
-// sub-band's lane 63 one step earlier: a DPP wave_ror:1 of the top values used as the `old` operand
-// of the bottom's wave_shr:1, so the 64-row hand-off inside the 128-row band is one extra DPP off
-// the dependency chain instead of a global edge (dtw.go:106-135).  The two
-// cells of a step read only the previous step, so the sweep issues two independent min-add chains
-// per step in the latency of one: twice the cells per sweep step, half the global hand-offs and
-// half the bands (a 51,676-row problem is 404 bands: all resident at two blocks per CU).
-// Everything written keeps dtw_band_kernel's 64-row-band layouts (Dn, CK, E per 64-band; the
-// bottom sub-band at its own step s-64), so the walk, exit map, path decode and path-tile kernels
-// are shared.  Block = 8 waves as in dtw_band_kernel: sweep, 4 distance waves (waves 1-2 the top
-// sub-band's chunks, even / odd; 3-4 the bottom's), ring feeder, code wave, edge poller.
-// LDS 77.7 KB (2 blocks per CU): a 192-row reference ring (rows t0-127 .. t0+7 of every chunk in
-// flight), and 24-step distance and C rings per sub-band (slot = step mod 24: three 8-step chunks,
-// so a chunk or a step pair never wraps).
-constexpr int DTW2_RROWS = 192;
-constexpr int DTW2_Q = 24;                 // steps per ring (distance and C rings), 3 chunks
-constexpr int DTW2_ROW = DTW2_Q + 2;       // doubles per lane row: 52 dwords = 52 mod 64 (b128 conflict-free)
-__device__ __forceinline__ double ror1(double v) {      // lane l <- lane l-1, lane 0 <- lane 63
-  const int2 a = __builtin_bit_cast(int2, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, a.x, 0x13C, 0xf, 0xf, false);   // wave_ror:1
-  const int hi = __builtin_amdgcn_update_dpp(0, a.y, 0x13C, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, make_int2(lo, hi));
-}
-
-template <int D, bool FAST, bool BANDED, bool BATCH>
-__global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band2_kernel(DtwArgs a_in, DtwBatch bt) {
-  static_assert(DTW_NDW == 4, "two distance waves per sub-band");
-  constexpr int DR = D > 0 ? D : 1;
-  constexpr int DS = dtw_ring_stride<D>();
-  __shared__ __attribute__((aligned(16))) double ring[(DTW2_RROWS + DTW_RMIR) * DS];
-  __shared__ __attribute__((aligned(16))) double dring[2][64][DTW2_ROW];   // distance of step t at [h][l][t % Q]
-  __shared__ __attribute__((aligned(16))) double oring[2][64][DTW2_ROW];   // C of step t at [h][l][t % Q]
-  __shared__ __attribute__((aligned(16))) double eqa[DTW_EQ];              // C[128B][c] at slot c - 1
-  __shared__ __attribute__((aligned(16))) double eqb[DTW_EQ];              // C[128B][c] at slot c
-  __shared__ __attribute__((aligned(16))) int ctr[16];
-  __shared__ int64_t shb;
-  __shared__ int shk;
-#define SONAR_LDS_LD(x) __hip_atomic_load(&(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-#define SONAR_LDS_ST(x, v) __hip_atomic_store(&(x), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-  int& efill = ctr[DTW_CTR_EFILL];
-  int& cprog = ctr[DTW_CTR_CPROG];
-  int& prog = ctr[DTW_CTR_PROG];
-  int& rdy = ctr[DTW_CTR_RDY];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const double inf = __builtin_inf();
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < 16; ++k) ctr[k] = 0;
-    if constexpr (BATCH) {
-      const int64_t t = atomicAdd(bt.ticket, 1);
-      ctr[DTW_CTR_TICKET] = (int)t;
-      if (t >= bt.start[bt.n]) {
-        shk = 0;
-        shb = INT64_MAX;                               // past the last ticket: the block exits
-      } else if (bt.map) {                             // ticket -> (DTW, 128-row band)
-        const int2 pb = bt.map[t];
-        shk = pb.x;
-        shb = pb.y;
-      } else {                                         // DTW-major: start[k] <= t < start[k + 1]
-        int lo = 0, hi = bt.n;
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (bt.start[mid] <= t) lo = mid; else hi = mid;
-        }
-        shk = lo;
-        shb = t - bt.start[lo];
-      }
-    } else {
-      shb = atomicAdd(&a_in.sync[0], 1);
-      ctr[DTW_CTR_TICKET] = (int)shb;
-    }
-    rdy = -1;
-  }
-  if (threadIdx.x < 64) {        // steps -1 and -2 of both sub-bands: C[i][j <= 0] = +Inf
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      oring[h][lane][DTW2_Q - 1] = inf;
-      oring[h][lane][DTW2_Q - 2] = inf;
-    }
-  }
-  if (threadIdx.x < DTW_EQ) {    // the top edge rings start at +Inf (what a band without one reads)
-    eqa[threadIdx.x] = inf;
-    eqb[threadIdx.x] = inf;
-  }
-  __syncthreads();
-  const int64_t B = shb;
-  const DtwArgs a = BATCH ? load_args_uniform(bt.args + __builtin_amdgcn_readfirstlane(shk)) : a_in;
-  const int64_t nq = a.nq, nr = a.nr, nb = a.nb;
-  if (2 * B >= nb) return;
-  const int64_t b0 = 2 * B, b1 = 2 * B + 1;            // the two 64-row bands (b1 may be absent)
-  const bool has_b1 = b1 < nb;
-  const int64_t S64 = a.S, S2 = (a.S + 1) >> 1;        // steps of one 64-row band: nr + 63
-  const int64_t S = has_b1 ? S64 + 64 : S64;           // steps of this block's sweep
-  const int64_t b = b0;                                // (diagnostics: the top sub-band)
-  constexpr uint64_t INF_BITS = 0x7FF0000000000000ull;
-  const uint64_t* Ein = B > 0 ? a.E + (b0 - 1) * (nr + 1) : nullptr;      // C[128B][j] at index j
-  const int64_t nblk = (nr + DTW_RBLK - 1) / DTW_RBLK;
-  const int64_t i_t = 64 * b0 + 1 + lane, i_b = i_t + 64;
-  const bool ok_t = i_t <= nq, ok_b = i_b <= nq;
-  uint64_t spins_total = 0;
-  uint32_t dead_ = 0;   // a bounded wait gave up: the wave runs out its loop without waiting
-  // DtwArgs::state (diagnostics, nullable): each wave's exit as one word at [8B + wave]: bits
-  // 60-63 how (1 finished, 2 saw the block's abort word, 3 timed out, 4 saw the DTW's error word),
-  // bits 32-59 its position (sweep / code: chunk step, distance: chunk, feeder: ring block, edge:
-  // columns in the rings), bits 0-31 prog, then efill at the moment of exit (16 bits each)
-  int64_t dpos = 0;
-  auto dtw_exit = [&](uint64_t how) {
-    if (a.state && lane == 0) {
-      const uint64_t p = (uint64_t)(uint16_t)SONAR_LDS_LD(prog), e = (uint64_t)(uint16_t)SONAR_LDS_LD(efill);
-      DTW_GLOBAL(a.state)[8 * B + wave] = (how << 60) | ((uint64_t)(dpos & 0xFFFFFFF) << 32) | (p << 16) | e;
-    }
-  };
-#define SONAR_SPIN_UNTIL(role, cond)                                                  \
-  do {                                                                                \
-    if (!dead_ && !(cond)) {                                                          \
-      const uint64_t tr0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;           \
-      uint64_t w0_ = 0;                                                               \
-      uint32_t sp_ = 0, rounds_ = 0;                                                  \
-      while (!(cond)) {                                                               \
-        __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);                                     \
-        if (++sp_ > DTW_SPIN_CHECK) {                                                 \
-          sp_ = 0;                                                                    \
-          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) { dead_ = 1; break; }                 \
-          const uint64_t now_ = __builtin_amdgcn_s_memrealtime();                     \
-          if (!w0_) w0_ = now_;                                                       \
-          else if (++rounds_ >= 16 && now_ - w0_ > DTW_STALL_TICKS) {                 \
-            dtw_local_stall((role), a.sync, ctr, lane);                               \
-            dead_ = 1; break;                                                         \
-          }                                                                           \
-        }                                                                             \
-      }                                                                               \
-      if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - tr0_;            \
-    }                                                                                 \
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
-  } while (0)
-
-  if (wave == DTW_FEEDER_WAVE || wave == DTW_EDGE_WAVE) {
-    // ------------------------------------------------ ring feeder / edge poller (as dtw_band_kernel)
-    const bool do_ring = wave == DTW_FEEDER_WAVE;
-    int64_t nextblk = 0, have = 0;
-    uint32_t idle = 0;
-    uint64_t t_idle = 0, t_fence = 0;
-    bool fenced = false;
-    const int64_t ecols = Ein ? nr : 0;
-    double pv[DR];
-    auto prefetch = [&](int64_t blk) {
-      const int64_t row = DTW_RBLK * blk + lane;
-#pragma unroll
-      for (int k = 0; k < DR; ++k) pv[k] = (lane < DTW_RBLK && row < nr) ? DTW_GLOBAL(a.r)[row * D + k] : 0.0;
-    };
-    if (do_ring) prefetch(0);
-    while (true) {
-      const int64_t p = SONAR_LDS_LD(prog), cp = SONAR_LDS_LD(cprog);
-      bool work = false, wait_edge = false;
-      if (do_ring) {
-        // block m overwrites rows 16m - RROWS .., read by distance chunks t0 <= 16m - RROWS + 15 + 127
-        int mind = SONAR_LDS_LD(ctr[0]);
-#pragma unroll
-        for (int w = 1; w < DTW_NDW; ++w) {
-          const int x = SONAR_LDS_LD(ctr[w]);
-          mind = x < mind ? x : mind;
-        }
-        if (nextblk < nblk &&
-            (nextblk < DTW2_RROWS / DTW_RBLK ||
-             (int64_t)mind > (DTW_RBLK * nextblk - DTW2_RROWS + DTW_RBLK - 1 + 127) / DTW_ECH)) {
-          if (lane < DTW_RBLK) {
-            const int64_t row = DTW_RBLK * nextblk + lane;
-            const int slot = (int)(row % DTW2_RROWS);
-            double* dst = ring + slot * DS;
-            double* mir = ring + (DTW2_RROWS + slot) * DS;
-#pragma unroll
-            for (int k = 0; k < DR; ++k) dst[k] = pv[k];
-            if (slot < DTW_RMIR) {
-#pragma unroll
-              for (int k = 0; k < DR; ++k) mir[k] = pv[k];
-            }
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          if (lane == 0) SONAR_LDS_ST(rdy, (int)nextblk);
-          ++nextblk;
-          if (nextblk < nblk) prefetch(nextblk);
-          work = true;
-        }
-      }
-      if (!do_ring && have < ecols) {
-        const int64_t lo = p < cp ? p : cp;
-        const int64_t want = lo + DTW_EAHEAD < ecols ? lo + DTW_EAHEAD : ecols;
-        if (have < want) {
-          wait_edge = true;
-          const int64_t jj = have + 1 + lane;
-          uint64_t v = INF_BITS;
-          if (jj <= want) v = g_load_agent(Ein + jj);
-          const uint64_t bad = __builtin_amdgcn_ballot_w64(jj <= want && v == DTW_SENT);
-          const int64_t lim = want - have < 64 ? want - have : 64;
-          const int64_t got = bad ? (int64_t)__builtin_ctzll(bad) : lim;
-          if (lane < got) {
-            eqa[(jj - 1) & (DTW_EQ - 1)] = __builtin_bit_cast(double, v);
-            eqb[jj & (DTW_EQ - 1)] = __builtin_bit_cast(double, v);
-          }
-          if (got > 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            have += got;
-            if (lane == 0) SONAR_LDS_ST(efill, (int)have);
-            work = true;
-          }
-        }
-      }
-      if (do_ring ? nextblk >= nblk : have >= ecols) break;
-      if (work) {
-        // diag[14]: the first poll after a refresh found new values
-        if (fenced && lane == 0 && a.diag) g_add_agent(&a.diag[14], 1ull);
-        fenced = false;
-        idle = 0;
-      } else {
-        fenced = false;
-        __builtin_amdgcn_s_sleep(1);
-        if ((++idle & 63) == 0) {
-          if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) {
-            const int st = SONAR_LDS_LD(ctr[DTW_CTR_STALLED]);
-            if (st) dtw_stall(a.sync, a.diag, st, b, ctr, Ein, nr, 0, 0);
-            dpos = do_ring ? nextblk : have;
-            dtw_exit(2);
-            return;
-          }
-          const uint64_t now = __builtin_amdgcn_s_memrealtime();
-          if (idle == 64) t_idle = now;
-          if (wait_edge) {
-            if (g_load_agent(&a.sync[1])) {
-              if (lane == 0) SONAR_LDS_ST(ctr[DTW_CTR_ABORT], 1);
-              dpos = have;
-              dtw_exit(4);
-              return;
-            }
-            if (now - t_idle > DTW_REFRESH_TICKS && now - t_fence > DTW_REFRESH_TICKS) {
-              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-              t_fence = now;
-              fenced = true;
-              if (lane == 0 && a.diag) g_add_agent(&a.diag[13], 1ull);
-            }
-          }
-          if (idle >= DTW_STALL_POLLS && now - t_idle > DTW_STALL_TICKS) {
-            dtw_stall(a.sync, a.diag, do_ring ? DTW_ROLE_FEEDER : DTW_ROLE_EDGE, b, ctr, Ein, nr, idle, t_idle);
-            dpos = do_ring ? nextblk : have;
-            dtw_exit(3);
-            return;
-          }
-        }
-      }
-    }
-    dpos = do_ring ? nextblk : have;
-    dtw_exit(dead_ ? 2 : 1);
-    return;
-  }
-
-  if (wave == DTW_CODE_WAVE) {
-    // --------------------------------------------------------------- code wave
-    // findPreviousStep's code (dtw.go:191-217) of both sub-bands' cells, the 64th-column
-    // checkpoints, in each 64-band's own layout (the bottom sub-band at step s - 64).  Lane 0's
-    // neighbours: the top edge C[128B][*] (eqb) for the top sub-band, the top sub-band's lane 63
-    // C values for the bottom one.
-    uint32_t dacc[2] = {0u, 0u};
-    double ckv[2] = {0.0, 0.0};
-    const int S32 = (int)S, S64i = (int)S64, nr32 = (int)nr;
-    int sb = 0;                                        // ring slot of the chunk's first step
-    for (int s0 = 0; s0 < S32; s0 += DTW_ECH, sb = sb == 2 * DTW_ECH ? 0 : sb + DTW_ECH) {
-      const int need = s0 + DTW_ECH < S32 ? s0 + DTW_ECH : S32;
-      dpos = s0;
-      SONAR_SPIN_UNTIL(DTW_ROLE_CODE, SONAR_LDS_LD(prog) >= need);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int sh = s0 - 64 * h;                    // this sub-band's own step of the chunk
-        if (sh < 0 || (h == 1 && !has_b1) || sh >= S64i) continue;
-        const int64_t bb = b0 + h;
-        double cv[DTW_ECH + 2], nv[DTW_ECH + 2];
-#pragma unroll
-        for (int k = 0; k < DTW_ECH / 2 + 1; ++k) {
-          const int t = s0 - 2 + 2 * k;
-          const int sl = k == 0 ? (sb == 0 ? DTW2_Q - 2 : sb - 2) : sb - 2 + 2 * k;
-          const double2 o = *reinterpret_cast<const double2*>(&oring[h][lane][sl]);
-          double2 n;
-          if (lane > 0) n = *reinterpret_cast<const double2*>(&oring[h][lane - 1][sl]);
-          else if (h == 1) n = *reinterpret_cast<const double2*>(&oring[0][63][sl]);
-          else n = *reinterpret_cast<const double2*>(&eqb[(t + 2) & (DTW_EQ - 1)]);
-          cv[2 * k] = o.x; cv[2 * k + 1] = o.y;
-          nv[2 * k] = n.x; nv[2 * k + 1] = n.y;
-        }
-        if (lane == 0 && h == 0) {
-#pragma unroll
-          for (int u = 0; u < DTW_ECH + 1; ++u) {
-            const int c = s0 + u;                        // nv[u] = C[128B][c]
-            nv[u] = (c == 0 || !Ein || c > nr32) ? ((c == 0 && B == 0) ? 0.0 : inf) : nv[u];
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < DTW_ECH; ++u) {
-          const double up = nv[u + 1], left = cv[u + 1], dg = nv[u];
-          uint32_t code;
-          if constexpr (FAST) {
-            const double best = vmin_f64(up, vmin_f64(left, dg));
-            code = best == up ? 0u : (best == left ? 1u : 2u);
-          } else {
-            double best = up;
-            code = 0;
-            if (left < best) { code = 1; best = left; }
-            if (dg < best) code = 2;
-          }
-          dacc[h] |= code << (2 * ((sh & 8) + u));
-        }
-        // checkpoint columns (as dtw_band_kernel's code wave, in the sub-band's own steps)
-        const int u = (lane - 1 - sh) & 63;
-        const double cap = u < DTW_ECH ? oring[h][lane][sb + u] : ckv[h];
-        const int J = sh - 56;
-        if ((sh & 63) == 56 && J >= 64 && J <= nr32)
-          DTW_GLOBAL(a.CK)[((bb * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = (u < DTW_ECH && lane != 0) ? cap : ckv[h];
-        ckv[h] = cap;
-        if ((sh & 8) || sh + DTW_ECH >= S64i) {           // steps 16w .. 16w+15 of this sub-band complete
-          DTW_GLOBAL(a.Dn)[((bb * a.SW + (sh >> 4)) << 6) + lane] = dacc[h];
-          dacc[h] = 0;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) SONAR_LDS_ST(cprog, need);
-    }
-    if (a.trace && lane == 0) DTW_GLOBAL(a.trace)[8 * B + 6] = spins_total;
-    dpos = S;
-    dtw_exit(dead_ ? 2 : 1);
-    return;
-  }
-
-  if (wave >= 1) {   // (feeder, edge and code returned above)
-    // ---------------------------------------------------------- distance waves
-    // wave 1 + 2h + e: sub-band h, chunks c = e mod 2
-    const int w = wave - 1, h = w >> 1;
-    if (h == 1 && !has_b1) {                           // no bottom sub-band: its chunks are never read
-      if (lane == 0) SONAR_LDS_ST(ctr[w], 1 << 30);
-      dtw_exit(dead_ ? 2 : 1);
-      return;
-    }
-    double qv[DR];
-    {
-      const int64_t qrow = (h ? ok_b : ok_t) ? (h ? i_b : i_t) - 1 : 0;
-#pragma unroll
-      for (int k = 0; k < D; ++k) qv[k] = DTW_GLOBAL(a.q)[qrow * D + k];
-    }
-    const int roff = 64 * h;                           // the sub-band's reference rows lag by 64
-    const int S32 = (int)S, nblk32 = (int)nblk;
-    // the wave's chunks c = e, e+2, ...: ring slot (8c mod 24) and the lane's first reference row
-    // (8c - l - roff mod RROWS), both advanced per chunk
-    int sl = 8 * (w & 1);
-    int rrow = ((8 * (w & 1) - lane - roff) % DTW2_RROWS + DTW2_RROWS) % DTW2_RROWS;
-    for (int c = w & 1; DTW_ECH * c < S32; c += 2) {
-      const int t0 = DTW_ECH * c;
-      dpos = c;
-      SONAR_SPIN_UNTIL(DTW_ROLE_DIST, SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW2_Q);
-      const int need = (t0 + DTW_ECH - 1) / DTW_RBLK;
-      const int needc = need < nblk32 - 1 ? need : nblk32 - 1;
-      SONAR_SPIN_UNTIL(DTW_ROLE_DIST, SONAR_LDS_LD(rdy) >= needc);
-      double dv[DTW_ECH];
-      // rows t0-l-roff .. +7 (mirror: never wraps); rows outside [0, nr) give values never stored
-      const double* rw0 = ring + rrow * DS;
-#pragma unroll
-      for (int g0 = 0; g0 < DTW_ECH; g0 += DTW_DG) {
-        double sum[DTW_DG];
-#pragma unroll
-        for (int k = 0; k < D; k += 2) {
-          double2 rv[DTW_DG];
-#pragma unroll
-          for (int u = 0; u < DTW_DG; ++u) rv[u] = *reinterpret_cast<const double2*>(rw0 + (g0 + u) * DS + k);
-#pragma unroll
-          for (int u = 0; u < DTW_DG; ++u) {
-            const double d0 = qv[k] - rv[u].x;
-            sum[u] = k == 0 ? d0 * d0 : sum[u] + d0 * d0;
-            const double d1 = qv[k + 1] - rv[u].y;
-            sum[u] = sum[u] + d1 * d1;
-          }
-        }
-        if constexpr (FAST) {
-          double mn = sum[0];
-#pragma unroll
-          for (int u = 1; u < DTW_DG; ++u) mn = vmin_f64(mn, sum[u]);
-          if (__builtin_amdgcn_ballot_w64(!(mn >= DTW_SQRT_MIN)) == 0) {
-#pragma unroll
-            for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt_normal(sum[u]);
-          } else {
-#pragma unroll
-            for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt(sum[u]);
-          }
-        } else {
-#pragma unroll
-          for (int u = 0; u < DTW_DG; ++u) dv[g0 + u] = sqrt(sum[u]);
-        }
-      }
-      double* drow = &dring[h][lane][sl];
-#pragma unroll
-      for (int u = 0; u < DTW_ECH; u += 2)
-        *reinterpret_cast<double2*>(drow + u) = make_double2(dv[u], dv[u + 1]);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) SONAR_LDS_ST(ctr[w], c + 1);
-      sl = sl == 0 ? 2 * DTW_ECH : sl - DTW_ECH;       // + 16 mod 24
-      rrow += 2 * DTW_ECH;
-      if (rrow >= DTW2_RROWS) rrow -= DTW2_RROWS;
-    }
-    if (a.trace && lane == 0 && w == 0) DTW_GLOBAL(a.trace)[8 * B + 7] = spins_total;
-    dpos = 1 << 27;
-    dtw_exit(dead_ ? 2 : 1);
-    return;
-  }
-
-  // ---------------------------------------------------------------- sweep wave
-#ifndef DTW_NOPRIO
-  __builtin_amdgcn_s_setprio(3);
-#endif
-  uint64_t* Eout_t = has_b1 ? a.E + b0 * (nr + 1) : nullptr;              // C[128B+64][j]
-  uint64_t* Eout_b = (b1 + 1 < nb) ? a.E + b1 * (nr + 1) : nullptr;       // C[128B+128][j]
-  double out_t = inf, out_b = inf;                     // C[i][j-1]
-  double upp_t = (lane == 0 && B == 0) ? 0.0 : inf;    // C[i-1][j-1]
-  double upp_b = inf;
-  const int64_t band = a.band;
-  // 32-bit steps (nq + nr < 2^31 is checked on the host); sb = the ring slot of the chunk's first
-  // step (s0 mod 24), advanced per chunk instead of divided
-  const int nr32 = (int)nr, S32 = (int)S;
-  struct Ctrs { int d0, d1, d2, d3, ef, cp; };
-  auto ready = [&](int s0, Ctrs k) -> bool {
-    const int c = s0 >> 3;
-    const int dt = (c & 1) ? k.d1 : k.d0, db = (c & 1) ? k.d3 : k.d2;
-    const int neede = s0 + DTW_ECH < nr32 ? s0 + DTW_ECH : nr32;
-    return dt > c && db > c && (!Ein || k.ef >= neede) && k.cp >= s0 + DTW_ECH - DTW2_Q + 2;
-  };
-  typedef int ctr4 __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) volatile ctr4 lds_ctr4;
-  typedef __attribute__((address_space(3))) volatile int lds_int;
-  auto load_ctr = [&]() -> Ctrs {
-    Ctrs k;
-    const ctr4 x = *(lds_ctr4*)(&ctr[0]);
-    k.d0 = x.x; k.d1 = x.y; k.d2 = x.z; k.d3 = x.w;
-    const int ef = *(lds_int*)(&ctr[DTW_CTR_EFILL]);
-    const int cp = *(lds_int*)(&ctr[DTW_CTR_CPROG]);
-    k.ef = ef;
-    k.cp = cp;
-    return k;
-  };
-  typedef double d2v __attribute__((ext_vector_type(2)));
-  typedef __attribute__((address_space(3))) volatile d2v lds_d2;
-  // steps [s0 + u0, s0 + u0 + n) of the chunk at slot sl: both sub-bands' distances and the top
-  // edge (eqa is pre-filled with +Inf, so a band without an edge reads +Inf)
-  auto load_part = [&](int s0, int sl, int u0, int n, double (&dt)[DTW_ECH], double (&db)[DTW_ECH],
-                       double (&ech)[DTW_ECH]) {
-    const double* drt = &dring[0][lane][sl];
-    const double* drb = &dring[1][lane][sl];
-    const double* er = &eqa[s0 & (DTW_EQ - 1)];          // columns s0+1 .. s0+8
-#pragma unroll
-    for (int u = u0; u < u0 + n; u += 2) {
-      const d2v x = *(lds_d2*)(drt + u);
-      const d2v y = *(lds_d2*)(drb + u);
-      const d2v e2 = *(lds_d2*)(er + u);
-      dt[u] = x.x; dt[u + 1] = x.y;
-      db[u] = y.x; db[u + 1] = y.y;
-      ech[u] = e2.x; ech[u + 1] = e2.y;
-    }
-  };
-  // columns past nr (their slots hold older columns) are +Inf; the values are uniform (broadcast
-  // reads), so they move to SGPRs
-  auto fix_edges = [&](int s0, double (&ech)[DTW_ECH]) {
-#pragma unroll
-    for (int u = 0; u < DTW_ECH; ++u) {
-      const double e = s0 + 1 + u > nr32 ? inf : ech[u];
-      const int2 e2 = __builtin_bit_cast(int2, e);
-      ech[u] = __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readfirstlane(e2.x),
-                                                    __builtin_amdgcn_readfirstlane(e2.y)));
-    }
-  };
-  // one step of both sub-bands: the top lane l at column s-l+1 (lane 0's up = the top edge l0up),
-  // the bottom lane l at column s-l-63 (lane 0's up = the top sub-band's lane 63, previous step).
-  // FULL: every lane's columns are in [1, nr] in both sub-bands (rows past nq compute values nobody
-  // reads).
-  auto step = [&](auto full_tag, int s, double l0up, double dt, double db) {
-    constexpr bool FULL = decltype(full_tag)::value;
-    const double up_t = shr1(out_t, l0up);
-    const double up_b = shr1(out_b, ror1(out_t));
-    double bt_, bb_;
-    if constexpr (FAST) {
-      bt_ = vmin_f64(up_t, vmin_f64(out_t, upp_t));
-      bb_ = vmin_f64(up_b, vmin_f64(out_b, upp_b));
-    } else {
-      bt_ = go_min(go_min(up_t, out_t), upp_t);
-      bb_ = go_min(go_min(up_b, out_b), upp_b);
-    }
-    double vt = dt + bt_, vb = db + bb_;
-    const int jt = s - lane + 1, jb = jt - 64;
-    if constexpr (BANDED) {
-      if (i_t - jt > band || jt - i_t > band) vt = inf;
-      if (i_b - jb > band || jb - i_b > band) vb = inf;
-    }
-    if constexpr (FULL) {
-      out_t = vt;
-      out_b = vb;
-    } else {
-      if (ok_t && jt >= 1 && jt <= nr32) out_t = vt;
-      if (ok_b && jb >= 1 && jb <= nr32) out_b = vb;
-    }
-    upp_t = up_t;
-    upp_b = up_b;
-  };
-  auto pair = [&](auto full_tag, int s, int sl, double e0, double e1, double dt0, double dt1, double db0,
-                  double db1) {
-    step(full_tag, s, e0, dt0, db0);
-    const double ot = out_t, ob = out_b;
-    step(full_tag, s + 1, e1, dt1, db1);
-    *reinterpret_cast<double2*>(&oring[0][lane][sl]) = make_double2(ot, out_t);
-    *reinterpret_cast<double2*>(&oring[1][lane][sl]) = make_double2(ob, out_b);
-  };
-
-  // SONAR_DTW_TRACE (a.trace, diagnostics): per 128-row band [8B + 0..7]: start, first chunk ready,
-  // end (s_memrealtime, 10 ns), then the sweep's wait ticks by the first missing input: distances,
-  // top edge, code wave; [6] the code wave's and [7] distance wave 0's wait ticks
-  uint64_t tw_[3] = {0, 0, 0};
-  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-  auto why = [&](int s0, Ctrs k) -> int {
-    const int c = s0 >> 3;
-    const int dt_ = (c & 1) ? k.d1 : k.d0, db_ = (c & 1) ? k.d3 : k.d2;
-    if (!(dt_ > c && db_ > c)) return 0;
-    const int neede = s0 + DTW_ECH < nr32 ? s0 + DTW_ECH : nr32;
-    return (Ein && k.ef < neede) ? 1 : 2;
-  };
-  double dt[DTW_ECH], db[DTW_ECH], ech[DTW_ECH];
-  Ctrs kc = load_ctr();
-  if (!ready(0, kc)) {
-    const int w_ = why(0, kc);
-    const uint64_t t0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-    SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready(0, kc)));
-    if (a.trace) tw_[w_] += __builtin_amdgcn_s_memrealtime() - t0_;
-  }
-  const uint64_t t_first = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-  load_part(0, 0, 0, DTW_ECH, dt, db, ech);
-  fix_edges(0, ech);
-  int sb = 0;
-  for (int s0 = 0; s0 < S32; s0 += DTW_ECH) {
-    const int s1 = s0 + DTW_ECH;
-    const int sbn = sb == 2 * DTW_ECH ? 0 : sb + DTW_ECH;
-    dpos = s1;
-    if ((b0 == a.dbg_stall || b1 == a.dbg_stall) && s0 >= 1024) return;   // fault injection (tests only)
-    // the next chunk's counters and its first half at the chunk's start, its second half once the
-    // first half of this chunk is done (its registers are free then): one chunk of data in flight
-    // (past the last chunk the loads read slots nobody uses)
-    double dtn[DTW_ECH], dbn[DTW_ECH], echn[DTW_ECH];
-    kc = load_ctr();
-    load_part(s1, sbn, 0, DTW_ECH / 2, dtn, dbn, echn);
-    if (s0 >= 127 && s1 <= nr32) {
-#pragma unroll
-      for (int u = 0; u < DTW_ECH; u += 2) {
-        if (u == DTW_ECH / 2) load_part(s1, sbn, DTW_ECH / 2, DTW_ECH / 2, dtn, dbn, echn);
-        pair(std::true_type{}, s0 + u, sb + u, ech[u], ech[u + 1], dt[u], dt[u + 1], db[u], db[u + 1]);
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < DTW_ECH; u += 2) {
-        if (u == DTW_ECH / 2) load_part(s1, sbn, DTW_ECH / 2, DTW_ECH / 2, dtn, dbn, echn);
-        if (s0 + u < S32)
-          pair(std::false_type{}, s0 + u, sb + u, ech[u], ech[u + 1], dt[u], dt[u + 1], db[u], db[u + 1]);
-      }
-    }
-    // the chunk's 8 edge values of each sub-band's last row (lane 63): lanes 0-7 the top's
-    // (-> E[b0], column s0+u-62), lanes 8-15 the bottom's (-> E[b1], column s0+u-126)
-    const int ue = lane & (DTW_ECH - 1);
-    const double ev = oring[lane < DTW_ECH ? 0 : 1][63][sb + ue];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) SONAR_LDS_ST(prog, s1 < S32 ? s1 : S32);
-    {
-      const bool top = lane < DTW_ECH;
-      uint64_t* Eo = top ? Eout_t : Eout_b;
-      const int je = s0 + ue - (top ? 62 : 126);
-      if (lane < 2 * DTW_ECH && Eo && je >= 1 && je <= nr32)
-        g_store_agent(Eo + je, __builtin_bit_cast(uint64_t, ev));
-    }
-    if (s1 >= S32) break;
-    if (!ready(s1, kc)) {
-      kc = load_ctr();
-      load_part(s1, sbn, 0, DTW_ECH, dtn, dbn, echn);
-      if (!ready(s1, kc)) {
-        const int w_ = why(s1, kc);
-        const uint64_t t0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-        SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready(s1, kc)));
-        if (a.trace) tw_[w_] += __builtin_amdgcn_s_memrealtime() - t0_;
-        load_part(s1, sbn, 0, DTW_ECH, dtn, dbn, echn);
-      }
-    }
-    fix_edges(s1, echn);
-#pragma unroll
-    for (int u = 0; u < DTW_ECH; ++u) { dt[u] = dtn[u]; db[u] = dbn[u]; ech[u] = echn[u]; }
-    sb = sbn;
-  }
-  if (a.trace && lane == 0) {
-    auto* tr = DTW_GLOBAL(a.trace);
-    tr[8 * B + 0] = t_start;
-    tr[8 * B + 1] = t_first;
-    tr[8 * B + 2] = __builtin_amdgcn_s_memrealtime();
-    tr[8 * B + 3] = tw_[0];
-    tr[8 * B + 4] = tw_[1];
-    tr[8 * B + 5] = tw_[2];
-  }
-  dpos = S;
-  dtw_exit(dead_ ? 2 : 1);
-  (void)spins_total;
-  (void)S2;
-#undef SONAR_SPIN_UNTIL
-#undef SONAR_LDS_LD
-#undef SONAR_LDS_ST
-}
-
-// ------------------------------------------------------------------ one wave per band ----
-// dtw_wave_kernel: the same cells, the same arithmetic in the same order and the same outputs as
-// dtw_band_kernel<12, FAST, !BANDED> in checkpoint mode (Dn direction words, CK checkpoint
-// columns, E bottom edges), with every role of that kernel's 8-wave block folded into ONE wave per
-// 64-row band: lane l = row 64b+1+l computes its own local distances (reference rows from a
-// 128-row LDS ring the wave refills itself, 16 rows two chunks ahead), the min-chain (DPP
-// wave_shr:1), findPreviousStep's 2-bit code (dtw.go:191-217) from the same up / left / diagonal
-// values, its checkpoint value, and polls the band above's edge row from E itself (sc1 global
-// loads two chunks ahead).  No LDS counters, no hand-offs inside a band.
-//  * Why: in the 8-wave block the CU's issue slots go to waves that mostly wait (C5: ~196 ns per
-//    band step with two blocks per CU, ~40 % VALU busy), and 52 KB of LDS per band leaves 512 of a
-//    51,676-row DTW's 808 bands resident.  Here a band costs 15 KB and 1 wave: every band of C3 is
-//    resident, and under C5 the distances of one wave fill the latency of another's chain.
-//  * Pipelining inside the wave: iteration c sweeps chunk c (8 steps) with distances computed in
-//    iteration c-1 and computes chunk c+1's sums in the same basic block, so the independent sums
-//    fill the min-chain's latency.
-#ifndef DTWW_RROWS_CFG
-#define DTWW_RROWS_CFG 128
-#endif
-// reference rows in the LDS ring (+ DTWW_CH mirrored).  A chunk reads rows 8c-63 .. 8c+7 and the
-// refill writes the block 16-31 rows past the chunk's rows, so 96 rows suffice (13.6 KB per wave:
-// 11 waves per CU instead of 10); 128 makes the slot a mask
-constexpr int DTWW_RROWS = DTWW_RROWS_CFG;
-static_assert(DTWW_RROWS == 128 || DTWW_RROWS == 96, "ring rows");
-__device__ __forceinline__ int dtww_slot(int64_t row) {
-  if constexpr (DTWW_RROWS == 128) {
-    return (int)(row & 127);
-  } else {
-    const int r = (int)(row % DTWW_RROWS);   // row > -DTWW_RROWS
-    return r < 0 ? r + DTWW_RROWS : r;
-  }
-}
-constexpr int DTWW_DS = 14;                // doubles per ring row: 112 B, b128 reads conflict-free
-constexpr int DTWW_CH = 8;                 // steps per chunk
-#ifndef DTWW_REFRESH
-#define DTWW_REFRESH 1                     // the edge wait's agent-scope acquire per ms (A/B knob)
-#endif
-#ifndef DTWW_EAHEAD
-#define DTWW_EAHEAD 1                      // chunks between an edge poll and its use (A/B 1-3: 1 best)
-#endif
-
-// lane 0 <- lane u of v (DPP row_shl:u; lanes 1..63 get values nobody reads)
-template <int U>
-__device__ __forceinline__ double from_lane(double v) {
-  if constexpr (U == 0) {
-    return v;
-  } else {
-    const int2 a = __builtin_bit_cast(int2, v);
-    const int lo = __builtin_amdgcn_update_dpp(0, a.x, 0x100 + U, 0xf, 0xf, true);    // row_shl:U
-    const int hi = __builtin_amdgcn_update_dpp(0, a.y, 0x100 + U, 0xf, 0xf, true);
-    return __builtin_bit_cast(double, make_int2(lo, hi));
-  }
-}
-
-// LDS written by one lane and read by another of the same wave: the hardware keeps a wave's LDS
-// requests in order, so only the compiler has to be kept from moving accesses across this point
-__device__ __forceinline__ void dtw_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// waves per SIMD the register allocation aims at: the single DTW (C3: about one band per SIMD)
-// takes the latency-optimal schedule, a batch of many DTWs several waves per SIMD
-#ifndef DTWW_MINW_BATCH
-#define DTWW_MINW_BATCH 1
-#endif
-#ifndef DTWW_MINW_ONE
-#define DTWW_MINW_ONE 1
-#endif
-// LEAN (batches only, SONAR_DTW_LEAN): no cross-chunk pipelining inside the wave -- a chunk's
-// distances are computed at its start, fenced off from its steps -- so the register file holds
-// one chunk's state and DTWW_MINW_LEAN waves share a SIMD: the latency one wave cannot fill with its
-// own independent sums is filled by the other waves' work
-#ifndef DTWW_MINW_LEAN
-#define DTWW_MINW_LEAN 2
-#endif
-// MODE 2 (DTWW_IL, opt-in SONAR_DTW_IL=1; measured slower): the next chunk's sums are cut into the six dimension
-// pairs and the two halves of the square roots, and each piece is fenced (sched_barrier) together
-// with ONE step of this chunk, its LDS reads issued one piece ahead.  Without the fences the
-// scheduler hoists all 48 reads and sums above the steps (256 VGPRs + 58 AGPRs) and the steps' DPP /
-// min / add chain then runs alone, its latency exposed; fenced, each step's chain hides behind
-// ~48 independent f64 operations.
-constexpr int DTWW_PIPE_MODE = 0, DTWW_LEAN_MODE = 1, DTWW_IL_MODE = 2;
-template <bool BATCH, int MODE = DTWW_PIPE_MODE>
-__global__ __launch_bounds__(64, MODE == DTWW_LEAN_MODE ? DTWW_MINW_LEAN : (BATCH ? DTWW_MINW_BATCH : DTWW_MINW_ONE))
-void dtw_wave_kernel(DtwArgs a_in, DtwBatch bt) {
-  constexpr bool LEAN = MODE == DTWW_LEAN_MODE, IL = MODE == DTWW_IL_MODE;
-  __shared__ __attribute__((aligned(16))) double ring[(DTWW_RROWS + DTWW_CH) * DTWW_DS];
-  __shared__ __attribute__((aligned(16))) double ebuf[2][DTWW_CH];   // lane 63's C of a chunk (parity)
-  __shared__ __attribute__((aligned(16))) int ctr[16];               // dtw_stall's counter layout
-  const int lane = threadIdx.x;
-  const double inf = __builtin_inf();
-  // ---- tickets -> (DTW, band).  BATCH: the wave is persistent and takes one ticket after
-  // another (grid = the batch's wave budget, launch_dtw_batch): a band starts only when a wave
-  // is free, so its predecessor (a smaller ticket, taken by a running wave) is usually well ahead
-  // and no wave holds a slot waiting down a chain.  Single DTW: one band per block.
-  // DTWW_ACQ: an agent-scope acquire before the first ticket, and the ticket map read with sc1
-  // loads (A/B knob for the first-call deadlocks)
-#ifndef DTWW_ACQ
-#define DTWW_ACQ 1
-#endif
-  if constexpr (BATCH && DTWW_ACQ) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  for (;;) {
-  int64_t tb = 0;
-  int tk = 0, tt = 0;
-  if (lane == 0) {
-    if constexpr (BATCH) {
-      const int t = atomicAdd(bt.ticket, 1);
-      tt = t;
-      if (bt.map) {
-        const int64_t tot = DTWW_ACQ ? (int64_t)g_load_agent(reinterpret_cast<const uint64_t*>(bt.start + bt.n))
-                                     : bt.start[bt.n];
-        if (t < tot) {
-          const int2 pb = DTWW_ACQ ? __builtin_bit_cast(int2, g_load_agent(reinterpret_cast<const uint64_t*>(bt.map + t)))
-                                   : bt.map[t];
-          tk = pb.x;
-          tb = pb.y;
-        } else {
-          tb = INT64_MAX;
-        }
-      } else {
-        int lo = 0, hi = bt.n;
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (bt.start[mid] <= t) lo = mid; else hi = mid;
-        }
-        tk = lo;
-        tb = t - bt.start[lo];
-      }
-    } else {
-      tb = atomicAdd(&a_in.sync[0], 1);
-      tt = (int)tb;
-    }
-  }
-  const int64_t b = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(tb >> 32)) << 32) |
-                              (uint32_t)__builtin_amdgcn_readfirstlane((int)tb));
-  const DtwArgs a = BATCH ? load_args_uniform(bt.args + __builtin_amdgcn_readfirstlane(tk)) : a_in;
-  if (b >= a.nb) return;
-  [&]() {   // one band; a `return` in it ends the band, not the wave
-  dtw_wave_sync();   // the previous band's LDS reads are behind the ring reset below
-  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-  const int64_t nq = a.nq, nr = a.nr, S = a.S;
-  const int nr32 = (int)nr;
-  const uint64_t* Ein = b > 0 ? a.E + (b - 1) * (nr + 1) : nullptr;        // C[64b][j] at index j
-  uint64_t* Eout = (b + 1 < a.nb) ? a.E + b * (nr + 1) : nullptr;         // C[64b+64][j]
-  const int64_t i = 64 * b + 1 + lane;
-  const bool row_ok = i <= nq;
-  const int64_t qrow = row_ok ? i - 1 : 0;
-  double qv[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) qv[k] = DTW_GLOBAL(a.q)[qrow * 12 + k];
-  // the ring starts zeroed (rows before column 1 are read for cells nobody keeps)
-  for (int k = lane; k < (DTWW_RROWS + DTWW_CH) * DTWW_DS / 2; k += 64)
-    *reinterpret_cast<double2*>(&ring[2 * k]) = make_double2(0.0, 0.0);
-  {
-    const int tkt = __builtin_amdgcn_readfirstlane(tt);   // outside the lane < 16 branch: lane 0's ticket
-    if (lane < 16) ctr[lane] = lane == DTW_CTR_TICKET ? tkt : 0;
-  }
-  dtw_wave_sync();
-  // reference rows in blocks of 16 (192 doubles: 3 per lane), rows past nr as zeros
-  auto fetch = [&](int64_t k, double (&v)[3]) {
-    const int64_t row = 16 * k + (lane >> 2);
-    if (row < nr) {
-      const auto* p = DTW_GLOBAL(a.r) + row * 12 + 3 * (lane & 3);
-      v[0] = p[0]; v[1] = p[1]; v[2] = p[2];
-    } else {
-      v[0] = v[1] = v[2] = 0.0;
-    }
-  };
-  auto put = [&](int64_t k, const double (&v)[3]) {
-    const int slot = dtww_slot(16 * k + (lane >> 2));
-    double* d = ring + slot * DTWW_DS + 3 * (lane & 3);
-    d[0] = v[0]; d[1] = v[1]; d[2] = v[2];
-    if (slot < DTWW_CH) {
-      d += DTWW_RROWS * DTWW_DS;
-      d[0] = v[0]; d[1] = v[1]; d[2] = v[2];
-    }
-  };
-  // the 8 cells of one chunk: sums in Go's order (distance.go:29-36, unfused), interleaved
-#ifndef DTWW_DG
-#define DTWW_DG 8                          // cells interleaved per pass of the sums
-#endif
-// DTWW_SCHED: keep each dimension pair's LDS reads behind the previous pair's arithmetic (VALU and
-// SALU may still move across, so the min-chain interleaves): fewer reads hoisted, fewer registers
-#ifdef DTWW_SCHED
-#define DTWW_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0x0006)
-#else
-#define DTWW_SCHED_FENCE() ((void)0)
-#endif
-  auto sums = [&](int64_t t0, double (&sm)[DTWW_CH], int glo = 0, int ghi = DTWW_CH) {
-    const double* rw0 = ring + dtww_slot(t0 - lane) * DTWW_DS;
-#ifdef DTWW_PIPE
-    // one dimension pair's reads in flight ahead of the arithmetic: the empty asm "rewrites" the
-    // sums and clobbers memory, so the reads of pair k+2 cannot be hoisted above pair k's
-    // arithmetic (without it the scheduler issues all 48 reads first: 192 VGPRs)
-    (void)glo; (void)ghi;
-    double2 rv[2][DTWW_CH];
-#pragma unroll
-    for (int u = 0; u < DTWW_CH; ++u) rv[0][u] = *reinterpret_cast<const double2*>(rw0 + u * DTWW_DS);
-#pragma unroll
-    for (int k = 0; k < 12; k += 2) {
-      const int cur = (k >> 1) & 1;
-      if (k + 2 < 12) {
-#pragma unroll
-        for (int u = 0; u < DTWW_CH; ++u) rv[cur ^ 1][u] = *reinterpret_cast<const double2*>(rw0 + u * DTWW_DS + k + 2);
-      }
-#pragma unroll
-      for (int u = 0; u < DTWW_CH; ++u) {
-        const double d0 = qv[k] - rv[cur][u].x;
-        sm[u] = k == 0 ? d0 * d0 : sm[u] + d0 * d0;
-        const double d1 = qv[k + 1] - rv[cur][u].y;
-        sm[u] = sm[u] + d1 * d1;
-      }
-      asm volatile("" : "+v"(sm[0]), "+v"(sm[1]), "+v"(sm[2]), "+v"(sm[3]), "+v"(sm[4]), "+v"(sm[5]), "+v"(sm[6]),
-                   "+v"(sm[7]) :: "memory");
-    }
-    return;
-#endif
-#pragma unroll
-    for (int g = glo; g < ghi; g += DTWW_DG) {
-#pragma unroll
-      for (int k = 0; k < 12; k += 2) {
-        double2 rv[DTWW_DG];
-#pragma unroll
-        for (int u = 0; u < DTWW_DG; ++u) rv[u] = *reinterpret_cast<const double2*>(rw0 + (g + u) * DTWW_DS + k);
-#pragma unroll
-        for (int u = 0; u < DTWW_DG; ++u) {
-          const double d0 = qv[k] - rv[u].x;
-          sm[g + u] = k == 0 ? d0 * d0 : sm[g + u] + d0 * d0;   // 0.0 + x == x for x >= +0 or NaN
-          const double d1 = qv[k + 1] - rv[u].y;
-          sm[g + u] = sm[g + u] + d1 * d1;
-        }
-        DTWW_SCHED_FENCE();
-      }
-    }
-  };
-  auto roots = [&](const double (&sm)[DTWW_CH], double (&dv)[DTWW_CH]) {
-    double mn = sm[0];
-#pragma unroll
-    for (int u = 1; u < DTWW_CH; ++u) mn = vmin_f64(mn, sm[u]);
-    if (__builtin_amdgcn_ballot_w64(!(mn >= DTW_SQRT_MIN)) == 0) {
-#pragma unroll
-      for (int u = 0; u < DTWW_CH; ++u) dv[u] = sqrt_normal(sm[u]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < DTWW_CH; ++u) dv[u] = sqrt(sm[u]);
-    }
-  };
-  // top edge of chunk c (columns 8c+1 .. 8c+8) in lanes 0..7, raw words (sentinel = not yet)
-  auto poll = [&](int64_t c) -> uint64_t {
-    const int64_t col = DTWW_CH * c + 1 + lane;
-    return (Ein && lane < DTWW_CH && col <= nr) ? g_load_agent(Ein + col) : 0ull;
-  };
-  auto missing = [&](int64_t c, uint64_t raw) -> uint64_t {
-    const int64_t col = DTWW_CH * c + 1 + lane;
-    return __builtin_amdgcn_ballot_w64(Ein && lane < DTWW_CH && col <= nr && raw == DTW_SENT);
-  };
-
-  double blk[3];
-  fetch(0, blk);
-  put(0, blk);
-  dtw_wave_sync();
-  fetch(1, blk);
-  const int64_t nch = (S + DTWW_CH - 1) / DTWW_CH;
-  uint64_t ewq[DTWW_EAHEAD];                          // polls of chunks c .. c+EAHEAD-1
-#pragma unroll
-  for (int k = 0; k < DTWW_EAHEAD; ++k) ewq[k] = k < nch ? poll(k) : 0ull;
-  double sm[DTWW_CH], dv[DTWW_CH];
-  if constexpr (!LEAN) {
-    sums(0, sm);
-    roots(sm, dv);
-  }
-  double out = inf;                                   // C[i][j-1]; C[i][0] = +Inf
-  double up_prev = (lane == 0 && b == 0) ? 0.0 : inf; // C[i-1][j-1]; C[0][0] = 0
-  double ckv = 0.0;                                   // the lane's C at its latest multiple-of-64 column
-  uint32_t dacc = 0;
-  uint64_t spins = 0, t_first = 0;
-  __attribute__((address_space(1))) uint32_t* Db = DTW_GLOBAL(a.Dn) + ((b * a.SW) << 6) + lane;
-  int64_t st_s0 = -1;                                  // a wait gave up at this chunk (-1: none)
-  uint32_t st_polls = 0;
-  uint64_t st_w0 = 0, st_miss = 0;
-  for (int64_t c = 0; c < nch; ++c) {
-    const int64_t s0 = DTWW_CH * c, s1 = s0 + DTWW_CH;
-    if (b == a.dbg_stall && s0 >= 1024) return;        // fault injection (tests only)
-    // reference rows: block m+1 into the ring and block m+2 requested at chunk 2m (block m+1's
-    // slots were last read by chunk 2m-5; it is first read by chunk 2m+1's distances)
-    if ((c & 1) == 0) {
-      put((c >> 1) + 1, blk);
-      dtw_wave_sync();
-      fetch((c >> 1) + 2, blk);
-    }
-    // this chunk's top edge (polled two chunks ago), then the poll of chunk c+2
-    uint64_t ew = ewq[0];
-    uint64_t miss = missing(c, ew);
-    if (miss) {
-      const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-      uint64_t t_fence = w0;
-      bool fenced = false;
-      uint32_t polls = 0;
-      do {
-        __builtin_amdgcn_s_sleep(DTW_SPIN_SLEEP);
-        if (ew == DTW_SENT) ew = poll(c);
-        miss = missing(c, ew);
-        if (miss && (++polls & 63) == 0) {
-          if (__builtin_amdgcn_readfirstlane(g_load_agent(&a.sync[1]))) return;   // another band gave up
-          const uint64_t now = __builtin_amdgcn_s_memrealtime();
-          // the band kernel's edge refresh (DTW_REFRESH_TICKS): one agent-scope acquire per ms
-          // without the edge, counted in diag[13] (diag[14] when the wait then ends)
-          if (DTWW_REFRESH && now - t_fence > DTW_REFRESH_TICKS) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            t_fence = now;
-            fenced = true;
-            if (lane == 0 && a.diag) g_add_agent(&a.diag[13], 1ull);
-          }
-          if (polls >= DTW_STALL_POLLS && now - w0 > DTW_STALL_TICKS) {
-            // give up: the record is written after the chunk loop (a call inside the loop
-            // would cost the loop its register allocation)
-            st_s0 = s0; st_polls = polls; st_w0 = w0; st_miss = miss;
-            break;
-          }
-        }
-      } while (miss);
-      if (st_s0 >= 0) break;
-      if (fenced && lane == 0 && a.diag) g_add_agent(&a.diag[14], 1ull);
-      if (c > 0) spins += __builtin_amdgcn_s_memrealtime() - w0;   // chunk 0's wait: t_first
-    }
-    if (a.trace && c == 0) t_first = __builtin_amdgcn_s_memrealtime();
-#pragma unroll
-    for (int k = 0; k + 1 < DTWW_EAHEAD; ++k) ewq[k] = ewq[k + 1];
-    ewq[DTWW_EAHEAD - 1] = c + DTWW_EAHEAD < nch ? poll(c + DTWW_EAHEAD) : 0ull;
-    const int64_t colc = s0 + 1 + lane;                // lanes 0..7: C[64b][colc]
-    const double e = (Ein && colc <= nr) ? __builtin_bit_cast(double, ew) : inf;
-    // next chunk's sums, in the same basic block as this chunk's steps (no branch between them):
-    // the independent sums fill the min-chain's latency.  Past the last chunk they read rows nobody
-    // keeps.
-    double smn[DTWW_CH];
-    if constexpr (LEAN) {
-      (void)s1;
-      sums(s0, sm);
-      roots(sm, dv);
-      __builtin_amdgcn_sched_barrier(0);
-    } else if constexpr (IL) {
-      // the pieces are interleaved with the steps below
-    } else {
-#ifndef DTWW_SPLIT
-      sums(s1, smn);
-#else
-      sums(s1, smn, 0, DTWW_CH / 2);
-#endif
-    }
-    // ---- the chunk's steps.  A lane keeps C[i][j] only for its row <= nq and j in [1, nr] (rows
-    // past nq stay +Inf: nothing reads them; dtw_band_kernel also fills them in full chunks)
-    const int jm1 = row_ok ? (int)s0 - lane : INT32_MIN;   // j - 1 at the chunk's first step
-    double o[DTWW_CH];
-    auto step = [&](auto u_tag, double d) {
-      constexpr int u = decltype(u_tag)::value;
-      const int64_t s = s0 + u;
-      const double up = shr1(out, from_lane<u>(e));      // C[i-1][j]; lane 0: C[64b][s+1]
-      const double left = out, dg = up_prev;
-      const double best = vmin_f64(up, vmin_f64(left, dg));
-      const uint32_t code = best == up ? 0u : (best == left ? 1u : 2u);
-      dacc |= code << (2 * ((s0 & 8) + u));
-      const double v = d + best;
-      if ((uint32_t)(jm1 + u) < (uint32_t)nr32) out = v;
-      up_prev = up;
-      if ((((int)s + 1 - lane) & 63) == 0) ckv = out;  // column j = s - l + 1 is a multiple of 64
-      o[u] = out;
-      if constexpr (u == 6) {
-        // every lane holds C[i][J] for J = s0 - 56 (lanes 57-63 met it in this chunk, lane 0
-        // meets J + 64 at step 7): one coalesced 512-B checkpoint store per 64 steps
-        const int64_t J = s0 - 56;
-        if ((s0 & 63) == 56 && J >= 64 && J <= nr)
-          DTW_GLOBAL(a.CK)[((b * (nr >> 6) + (J >> 6) - 1) << 6) + lane] = ckv;
-      }
-    };
-    if constexpr (IL) {
-      // piece k (k = 0, 2, .., 10): dimensions k, k+1 of the next chunk's 8 cells, in Go's order
-      // (distance.go:29-36, unfused; 0.0 + x == x for the first square)
-      const double* rw0 = ring + dtww_slot(s1 - lane) * DTWW_DS;
-      double2 rva[DTWW_CH], rvb[DTWW_CH];
-      auto rd = [&](double2 (&rv)[DTWW_CH], int k) {
-#pragma unroll
-        for (int u = 0; u < DTWW_CH; ++u) rv[u] = *reinterpret_cast<const double2*>(rw0 + u * DTWW_DS + k);
-      };
-      auto ar = [&](const double2 (&rv)[DTWW_CH], int k) {
-#pragma unroll
-        for (int u = 0; u < DTWW_CH; ++u) {
-          const double d0 = qv[k] - rv[u].x;
-          smn[u] = k == 0 ? d0 * d0 : smn[u] + d0 * d0;
-          const double d1 = qv[k + 1] - rv[u].y;
-          smn[u] = smn[u] + d1 * d1;
-        }
-      };
-      double dvn[DTWW_CH];
-      // the fence keeps the machine scheduler from moving work across; the empty asm "redefines" the
-      // values a piece produced, so earlier passes cannot sink its arithmetic into a later piece
-#define DTWW_PIN(v) asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), \
-                                         "+v"(v[6]), "+v"(v[7]))
-#define DTWW_FENCE() __builtin_amdgcn_sched_barrier(0)
-      rd(rva, 0);
-      DTWW_FENCE();
-      rd(rvb, 2);  step(std::integral_constant<int, 0>{}, dv[0]);  ar(rva, 0);  DTWW_PIN(smn);  DTWW_FENCE();
-      rd(rva, 4);  step(std::integral_constant<int, 1>{}, dv[1]);  ar(rvb, 2);  DTWW_PIN(smn);  DTWW_FENCE();
-      rd(rvb, 6);  step(std::integral_constant<int, 2>{}, dv[2]);  ar(rva, 4);  DTWW_PIN(smn);  DTWW_FENCE();
-      rd(rva, 8);  step(std::integral_constant<int, 3>{}, dv[3]);  ar(rvb, 6);  DTWW_PIN(smn);  DTWW_FENCE();
-      rd(rvb, 10); step(std::integral_constant<int, 4>{}, dv[4]);  ar(rva, 8);  DTWW_PIN(smn);  DTWW_FENCE();
-      step(std::integral_constant<int, 5>{}, dv[5]);  ar(rvb, 10);  DTWW_PIN(smn);  DTWW_FENCE();
-      step(std::integral_constant<int, 6>{}, dv[6]);
-#pragma unroll
-      for (int u = 0; u < DTWW_CH / 2; ++u) dvn[u] = sqrt_normal(smn[u]);
-      asm volatile("" : "+v"(dvn[0]), "+v"(dvn[1]), "+v"(dvn[2]), "+v"(dvn[3]));
-      DTWW_FENCE();
-      step(std::integral_constant<int, 7>{}, dv[7]);
-#pragma unroll
-      for (int u = DTWW_CH / 2; u < DTWW_CH; ++u) dvn[u] = sqrt_normal(smn[u]);
-      asm volatile("" : "+v"(dvn[4]), "+v"(dvn[5]), "+v"(dvn[6]), "+v"(dvn[7]));
-      DTWW_FENCE();
-#undef DTWW_FENCE
-#undef DTWW_PIN
-      // sqrt_normal holds for sums in [2^-767, Inf) only; otherwise the full sqrt (same bits)
-      double mn = smn[0];
-#pragma unroll
-      for (int u = 1; u < DTWW_CH; ++u) mn = vmin_f64(mn, smn[u]);
-      if (__builtin_amdgcn_ballot_w64(!(mn >= DTW_SQRT_MIN)) != 0) {
-#pragma unroll
-        for (int u = 0; u < DTWW_CH; ++u) dvn[u] = sqrt(smn[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < DTWW_CH; ++u) dv[u] = dvn[u];
-    } else {
-    step(std::integral_constant<int, 0>{}, dv[0]);
-    step(std::integral_constant<int, 1>{}, dv[1]);
-    step(std::integral_constant<int, 2>{}, dv[2]);
-    step(std::integral_constant<int, 3>{}, dv[3]);
-#ifdef DTWW_SPLIT   // the second half of the next chunk's sums beside the second half of the steps
-    if constexpr (!LEAN) {
-      __builtin_amdgcn_sched_barrier(0);
-      sums(s1, smn, DTWW_CH / 2, DTWW_CH);
-    }
-#endif
-    step(std::integral_constant<int, 4>{}, dv[4]);
-    step(std::integral_constant<int, 5>{}, dv[5]);
-    step(std::integral_constant<int, 6>{}, dv[6]);
-    step(std::integral_constant<int, 7>{}, dv[7]);
-    }
-    // direction words: steps 16w .. 16w+15 (or the last ones)
-    if ((s0 & 8) || s1 >= S) {
-      Db[(s0 >> 4) << 6] = dacc;
-      dacc = 0;
-    }
-    // bottom edge: lane 63's C of the chunk's steps -> lanes 0..7 -> one sc1 store each
-    if (Eout) {
-      double* eb = ebuf[c & 1];
-      if (lane == 63) {
-#pragma unroll
-        for (int u = 0; u < DTWW_CH; u += 2) *reinterpret_cast<double2*>(eb + u) = make_double2(o[u], o[u + 1]);
-      }
-      dtw_wave_sync();
-      const int64_t je = s0 + lane - 62;               // lane 63's column at step s0 + lane
-      if (lane < DTWW_CH && je >= 1 && je <= nr) g_store_agent(Eout + je, __builtin_bit_cast(uint64_t, eb[lane]));
-    }
-    if constexpr (!LEAN && !IL) roots(smn, dv);
-  }
-  if (st_s0 >= 0) {
-    if (lane == 0) {
-      ctr[DTW_CTR_PROG] = (int)st_s0;
-      ctr[DTW_CTR_CPROG] = (int)st_s0;
-      ctr[DTW_CTR_EFILL] = (int)st_s0 + __builtin_ctzll(st_miss);
-      ctr[DTW_CTR_RDY] = (int)((st_s0 + 15) >> 4);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    dtw_stall(a.sync, a.diag, DTW_ROLE_EDGE, b, ctr, Ein, nr, st_polls, st_w0);
-    return;
-  }
-  if (a.trace && lane == 0) {
-    auto* tr = DTW_GLOBAL(a.trace);
-    tr[8 * b + 0] = t_start;
-    tr[8 * b + 1] = t_first;
-    tr[8 * b + 2] = __builtin_amdgcn_s_memrealtime();
-    tr[8 * b + 3] = spins;
-  }
-  (void)nr32;
-  }();
-  if constexpr (!BATCH) return;
   }
 }
 
@@ -2978,66 +1758,6 @@ __global__ __launch_bounds__(256) void dtw_cost_rowmajor_kernel(const double* Cn
   }
 }
 
-// Local distances (EuclideanDistanceFunc, distance.go:29-36: Go's sequential sum, unfused, then
-// sqrt) of every band-step cell into Dd, in Cn's paired band-skewed layout, for the PRE band
-// kernel.  Block = band b x 64 steps; the 127 reference rows those steps touch are staged in LDS
-// (rows padded to 14 doubles: conflict-free 16-B reads), lane l keeps query row 64b+l in
-// registers, and wave w computes steps 16w .. 16w+15 as 8 interleaved chains at a time.  Cells
-// outside the matrix get 0 (the sweep never stores them).
-constexpr int DTW_DIST_TS = 64;
-template <int D>
-__global__ __launch_bounds__(256) void dtw_dist_kernel(const double* q, const double* r, int64_t nq, int64_t nr,
-                                                       int64_t S, double* Dd) {
-  static_assert(D == 12, "the precomputed path is built for chroma (12 dimensions)");
-  constexpr int DS = dtw_ring_stride<D>();
-  constexpr int NR = DTW_DIST_TS + 63;
-  __shared__ __attribute__((aligned(16))) double rr[NR * DS];
-  const int64_t b = blockIdx.y, s0 = (int64_t)blockIdx.x * DTW_DIST_TS, S2 = (S + 1) >> 1;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t rbase = s0 - 63;                    // reference row (j - 1) of local row 0
-  for (int e = threadIdx.x; e < NR * D; e += 256) {
-    const int row = e / D, k = e - row * D;
-    const int64_t jr = rbase + row;
-    rr[row * DS + k] = (jr >= 0 && jr < nr) ? r[jr * D + k] : 0.0;
-  }
-  const int64_t i0 = 64 * b + lane;                 // query row (i - 1)
-  double qv[D];
-#pragma unroll
-  for (int k = 0; k < D; ++k) qv[k] = i0 < nq ? q[i0 * D + k] : 0.0;
-  __syncthreads();
-#pragma unroll
-  for (int g = 0; g < 16; g += 8) {
-    const int sl = 16 * w + g;                        // local step of chain 0
-    const double* rw0 = rr + (sl - lane + 63) * DS;   // local row of (step sl, lane)
-    double sum[8];
-#pragma unroll
-    for (int k = 0; k < D; k += 2) {
-      double2 rv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) rv[u] = *reinterpret_cast<const double2*>(rw0 + u * DS + k);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const double d0 = qv[k] - rv[u].x;
-        sum[u] = k == 0 ? d0 * d0 : sum[u] + d0 * d0;   // 0.0 + x == x for x >= +0 or NaN
-        const double d1 = qv[k + 1] - rv[u].y;
-        sum[u] = sum[u] + d1 * d1;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 8; u += 2) {
-      const int64_t s = s0 + sl + u;
-      if ((s >> 1) >= S2) break;
-      double v[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int64_t jr = s + h - lane;
-        v[h] = (i0 < nq && jr >= 0 && jr < nr) ? sqrt(sum[u + h]) : 0.0;
-      }
-      *reinterpret_cast<double2*>(Dd + dtw_cn_off(b, S2, s, lane)) = make_double2(v[0], v[1]);
-    }
-  }
-}
-
 __global__ void nonfinite_kernel(const double* x, int64_t n, int32_t* flag) {
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
     if (!__builtin_isfinite(x[k])) *flag = 1;
@@ -3052,50 +1772,18 @@ __global__ void nonfinite_batch_kernel(const DtwArgs* args) {
     if (!__builtin_isfinite(k < nqe ? a.q[k] : a.r[k - nqe])) a.sync[2] = 1;
 }
 
-// SONAR_DTW_DBG_STALL=<band> (tests only): fault injection, see DtwArgs::dbg_stall
-int32_t dtw_dbg_stall_band() {
+// SONAR_DTW_DBG_STALL=<band> (tests only): fault injection, see DtwArgs::dbg_stall; "b<band>"
+// injects it into batched launches only (launch_dtw_batch), so the single-pair redo runs clean
+int32_t dtw_dbg_stall_band(bool batch) {
   const char* e = std::getenv("SONAR_DTW_DBG_STALL");
-  return e ? (int32_t)std::atoi(e) : -1;
+  if (!e) return -1;
+  if (e[0] == 'b') return batch ? (int32_t)std::atoi(e + 1) : -1;
+  return (int32_t)std::atoi(e);
 }
 
-// SONAR_DTW_BAND2=1: dtw_band2_kernel (128-row bands) for 12-dim DTWs (opt-in while it is measured;
-// default: the 64-row dtw_band_kernel)
-bool dtw_band2_enabled(int dim) {
-  const char* e = std::getenv("SONAR_DTW_BAND2");
-  return e && e[0] == '1' && dim == 12;
-}
-
-// SONAR_DTW_WAVE=1: the one-wave dtw_wave_kernel instead of the 8-wave dtw_band_kernel for 12-dim
-// FAST checkpoint-mode DTWs, batched and single (opt-in).  Batches ran on it by default until its
-// band pipeline was found to deadlock in a process's first sonar_align_pairs call (DESIGN §6:
-// 20 of 24 fresh processes lost DTWs to it, the band kernel 0 of 4 at the same C5 throughput once
-// the features were batched)
-static bool dtw_wave_enabled() {
-  const char* e = std::getenv("SONAR_DTW_WAVE");
-  return e && e[0] == '1';
-}
-bool dtw_wave_batch_enabled() { return dtw_wave_enabled(); }
-// the batched one-wave kernel's schedule (A/B; both measured slower on C5, DESIGN Kernel 6):
-// SONAR_DTW_LEAN=1 no cross-chunk pipelining (several waves per SIMD), SONAR_DTW_IL=1 the next
-// chunk's sums fenced piece by piece between the steps; default the unfenced pipelined schedule
-static int dtw_wave_mode() {
-  const char* l = std::getenv("SONAR_DTW_LEAN");
-  if (l && l[0] == '1') return DTWW_LEAN_MODE;
-  const char* i = std::getenv("SONAR_DTW_IL");
-  return (i && i[0] == '1') ? DTWW_IL_MODE : DTWW_PIPE_MODE;
-}
-static bool dtw_wave_one_enabled() {
-  const char* e = std::getenv("SONAR_DTW_WAVE");
-  return e && e[0] == '1';
-}
-
-// threads of the batched walk / path scans (one block per DTW): 256 by default so the block fits
-// beside the DTW waves of other batches; SONAR_SCAN_THREADS=1024 (A/B) the single-DTW shape
-static unsigned dtw_batch_scan_threads() {
-  const char* e = std::getenv("SONAR_SCAN_THREADS");
-  const int v = e ? std::atoi(e) : 256;
-  return (v >= 64 && v <= 1024 && v % 64 == 0) ? (unsigned)v : 256u;
-}
+// threads of the batched walk / path scans (one block per DTW): 256, so the block fits beside the
+// DTW waves of other batches (1,024 threads waited for a whole CU to drain under C5)
+constexpr unsigned kBatchScanThreads = 256;
 
 // SONAR_DTW_SERIAL_WALK=1: the one-wave serial backtrack instead of the backtrack by bands (A/B)
 static bool dtw_serial_walk() {
@@ -3124,14 +1812,9 @@ int64_t dtw_cn_index(const DtwGeom& g, int64_t i, int64_t j) {
   return ((b * ((g.S + 1) / 2) + (s >> 1)) << 7) + 2 * l + (s & 1);
 }
 
-void launch_dtw_dist(const double* q, const double* r, const DtwGeom& g, double* Dd, hipStream_t s) {
-  const dim3 grid((unsigned)((g.S + DTW_DIST_TS - 1) / DTW_DIST_TS), (unsigned)g.nb);
-  hipLaunchKernelGGL(dtw_dist_kernel<12>, grid, dim3(256), 0, s, q, r, g.nq, g.nr, g.S, Dd);
-}
-
 int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, const DtwGeom& g, double* Cn,
                uint32_t* Dn, uint64_t* E, int32_t* sync_words, uint32_t* codes, int64_t* plen, uint64_t* trace,
-               hipStream_t s, hipEvent_t mid, double* Dd, double* CK) {
+               hipStream_t s, hipEvent_t mid, double* CK) {
   // sync_words: [0] ticket, [1] error bits, [2] non-finite flag (set by the caller's probe), [3]
   // unused, then the DTW_DIAG_WORDS-word diagnostic record at byte 16 (DTW_SYNC_BYTES in all)
   if (hipMemsetAsync(sync_words, 0, 2 * sizeof(int32_t), s) != hipSuccess) return -5;
@@ -3141,33 +1824,10 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
             trace};
   a.CK = CK;
   a.diag = reinterpret_cast<uint64_t*>(sync_words + 4);
-  a.dbg_stall = dtw_dbg_stall_band();
+  a.dbg_stall = dtw_dbg_stall_band(false);
   if (!Cn && !CK) return -1;
   const DtwBatch nob{};
-  const bool pre = Dd && dim == 12;
-  // SONAR_DTW_DBG_CONC=1 (timing experiment only, WRONG results): the distance kernel on a side
-  // stream concurrently with the band kernel, which does not wait for it
-  static hipStream_t side = nullptr;
-  static hipEvent_t ev_a = nullptr, ev_b = nullptr;
-  const char* conc_env = std::getenv("SONAR_DTW_DBG_CONC");
-  const bool conc = pre && conc_env && conc_env[0] == '1';
-  if (pre) {
-    a.Dd = Dd;
-    if (conc) {
-      if (!side) {
-        hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
-        hipEventCreateWithFlags(&ev_a, hipEventDisableTiming);
-        hipEventCreateWithFlags(&ev_b, hipEventDisableTiming);
-      }
-      hipEventRecord(ev_a, s);
-      hipStreamWaitEvent(side, ev_a, 0);
-      launch_dtw_dist(q, r, g, Dd, side);
-      hipEventRecord(ev_b, side);
-    } else {
-      launch_dtw_dist(q, r, g, Dd, s);
-    }
-  }
-  const dim3 grid((unsigned)g.nb), block(64 * DTW_WAVES), pblock(64 * dtw_block_waves(true));
+  const dim3 grid((unsigned)g.nb), block(64 * DTW_WAVES);
 #define SONAR_DTW_LAUNCH(DD)                                                                          \
   do {                                                                                                \
     if (band > 0) {                                                                                   \
@@ -3178,34 +1838,11 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
       else hipLaunchKernelGGL((dtw_band_kernel<DD, false, false>), grid, block, 0, s, a, nob);        \
     }                                                                                                 \
   } while (0)
-  if (pre) {
-    if (band > 0) {
-      if (fast) hipLaunchKernelGGL((dtw_band_kernel<12, true, true, false, true>), grid, pblock, 0, s, a, nob);
-      else hipLaunchKernelGGL((dtw_band_kernel<12, false, true, false, true>), grid, pblock, 0, s, a, nob);
-    } else {
-      if (fast) hipLaunchKernelGGL((dtw_band_kernel<12, true, false, false, true>), grid, pblock, 0, s, a, nob);
-      else hipLaunchKernelGGL((dtw_band_kernel<12, false, false, false, true>), grid, pblock, 0, s, a, nob);
-    }
-  }
-  else if (dim == 12 && !Cn && dtw_band2_enabled(dim)) {
-    // 128-row bands (dtw_band2_kernel): ceil(nb / 2) blocks
-    const dim3 grid2((unsigned)((g.nb + 1) / 2));
-    if (band > 0) {
-      if (fast) hipLaunchKernelGGL((dtw_band2_kernel<12, true, true, false>), grid2, block, 0, s, a, nob);
-      else hipLaunchKernelGGL((dtw_band2_kernel<12, false, true, false>), grid2, block, 0, s, a, nob);
-    } else {
-      if (fast) hipLaunchKernelGGL((dtw_band2_kernel<12, true, false, false>), grid2, block, 0, s, a, nob);
-      else hipLaunchKernelGGL((dtw_band2_kernel<12, false, false, false>), grid2, block, 0, s, a, nob);
-    }
-  }
-  else if (dim == 12 && !Cn && fast && band <= 0 && dtw_wave_one_enabled())
-    hipLaunchKernelGGL(dtw_wave_kernel<false>, grid, dim3(64), 0, s, a, nob);
-  else if (dim == 12) SONAR_DTW_LAUNCH(12);
+  if (dim == 12) SONAR_DTW_LAUNCH(12);
   else if (dim == 1) SONAR_DTW_LAUNCH(1);
   else SONAR_DTW_LAUNCH(0);
 #undef SONAR_DTW_LAUNCH
   if (mid) hipEventRecord(mid, s);
-  if (conc) hipStreamWaitEvent(s, ev_b, 0);
   if (dtw_serial_walk()) {
     hipLaunchKernelGGL(dtw_walk_kernel, dim3(1), dim3(64), 0, s, Dn, g.nq, g.nr, g.SW, codes, plen);
   } else {
@@ -3249,35 +1886,13 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s) {
 }
 
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
-                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap, int waves) {
+                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap) {
   if (n <= 0 || total_bands <= 0) return 0;
   if (total_bands > INT32_MAX) return -1;
   const DtwArgs none{};
   const DtwBatch bt{dargs, dstart, n, ticket, dmap};
-  const bool pre = hargs[0].Dd != nullptr;
-  if (pre) {
-    for (int k = 0; k < n; ++k) {
-      const DtwGeom g = dtw_geom(hargs[k].nq, hargs[k].nr);
-      launch_dtw_dist(hargs[k].q, hargs[k].r, g, hargs[k].Dd, s);
-    }
-    hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true, true>), dim3((unsigned)total_bands),
-                       dim3(64 * dtw_block_waves(true)), 0, s, none, bt);
-  } else if (dtw_band2_enabled(12)) {   // tickets are 128-row bands (the caller's map and starts)
-    hipLaunchKernelGGL((dtw_band2_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
-                       0, s, none, bt);
-  } else if (!hargs[0].Cn && dtw_wave_batch_enabled()) {
-    const int64_t grid = waves > 0 && waves < total_bands ? waves : total_bands;   // persistent waves
-    const int mode = dtw_wave_mode();
-    if (mode == DTWW_LEAN_MODE)
-      hipLaunchKernelGGL((dtw_wave_kernel<true, DTWW_LEAN_MODE>), dim3((unsigned)grid), dim3(64), 0, s, none, bt);
-    else if (mode == DTWW_IL_MODE)
-      hipLaunchKernelGGL((dtw_wave_kernel<true, DTWW_IL_MODE>), dim3((unsigned)grid), dim3(64), 0, s, none, bt);
-    else
-      hipLaunchKernelGGL((dtw_wave_kernel<true, DTWW_PIPE_MODE>), dim3((unsigned)grid), dim3(64), 0, s, none, bt);
-  } else {
-    hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
-                       0, s, none, bt);
-  }
+  hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES), 0, s,
+                     none, bt);
   if (dtw_serial_walk()) {
     hipLaunchKernelGGL(dtw_walk_batch_kernel, dim3((unsigned)n), dim3(64), 0, s, dargs);
   } else {
@@ -3290,11 +1905,11 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
     hipLaunchKernelGGL(dtw_walk_chain_kernel<true>, dim3((unsigned)n), dim3(64), 0, s, none, dargs);
     hipLaunchKernelGGL((dtw_walk_band_kernel<false, true>), dim3((unsigned)max_nb, (unsigned)n), dim3(64), 0, s, none,
                        dargs);
-    hipLaunchKernelGGL(dtw_walk_scan_kernel<true>, dim3((unsigned)n), dim3(dtw_batch_scan_threads()), 0, s, none, dargs);
+    hipLaunchKernelGGL(dtw_walk_scan_kernel<true>, dim3((unsigned)n), dim3(kBatchScanThreads), 0, s, none, dargs);
     hipLaunchKernelGGL((dtw_walk_band_kernel<true, true>), dim3((unsigned)max_nb, (unsigned)n), dim3(64), 0, s, none,
                        dargs);
   }
-  hipLaunchKernelGGL(dtw_path_scan_kernel<true>, dim3((unsigned)n), dim3(dtw_batch_scan_threads()), 0, s, (const uint32_t*)nullptr,
+  hipLaunchKernelGGL(dtw_path_scan_kernel<true>, dim3((unsigned)n), dim3(kBatchScanThreads), 0, s, (const uint32_t*)nullptr,
                      (int64_t)0, (int64_t)0, (int64_t)0, (int2*)nullptr, dargs);
   const int64_t nw = (max_cap + 15) >> 4;
   hipLaunchKernelGGL(dtw_path_points_kernel<true>, dim3((unsigned)((nw + 255) / 256), (unsigned)n), dim3(256), 0, s,

@@ -95,10 +95,6 @@ void* hbuf(sonar_ctx* c, const std::string& name, size_t bytes);
 // chroma tables of frame size fs at sample rate sr, built once per context (sonar_api.cpp); null on
 // allocation failure
 const sonar_ctx::ChromaT* chroma_tables_for(sonar_ctx* c, int fs, int sr);
-// DTW with the local distances precomputed (dtw_dist_kernel + the 4-wave band kernel) for this
-// feature dimension; opt-in with SONAR_DTW_PRE=1 (the distance waves inside the band kernel are
-// the default: faster at C3 and C5 sizes)
-bool dtw_pre_enabled(int dim);
 // NCC + chroma DTW of one stream pair with two stream synchronisations (align_impl's device
 // path, sonar_api.cpp): ncc_enqueue and dtw_enqueue only launch and queue their small results
 // into pinned host memory; after one hipStreamSynchronize, ncc_metrics_host reads the

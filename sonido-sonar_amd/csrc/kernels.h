@@ -89,7 +89,7 @@ struct MfccPairParams {
   int pow2;             // F5: MFCC.Compute fed |X|^2 -> filterbank of |X|^4
   float* out;           // [F][n_mfcc]
   int lds_src, lds_dct, lds_wave0, lds_bytes;
-  int waves_per_block;  // 4: mfcc_pair_kernel; 8: mfcc_pair2_kernel (two pairs per wave at a time)
+  int waves_per_block;  // 4 (mfcc_pair_kernel)
 };
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s);
 int mfcc_pair_wave_bytes();
@@ -189,7 +189,6 @@ int launch_dtw(const double* q, const double* r, int dim, int band, bool fast, c
                uint32_t* codes /* walk moves, 2 bits each */, int64_t* plen,
                uint64_t* trace /* nullable, [nb][8] diagnostics */, hipStream_t s,
                hipEvent_t mid = nullptr /* recorded between the sweep and the walk */,
-               double* Dd = nullptr /* dim 12: dtw_cn_bytes of scratch -> precomputed distances */,
                double* CK = nullptr /* Cn null: dtw_ck_bytes of checkpoint columns instead */);
 // wstart: scratch of (P + 15) / 16 int2 (each code word's starting cell).  Cn null: only the
 // points (and the zero cost of border points) are written; launch_dtw_path_tiles adds the costs
@@ -216,8 +215,6 @@ struct DtwArgs {
   int32_t *pq, *pr;
   double* pc;
   double* cnm;     // C[nq][nr]
-  // precomputed local distances in Cn's layout (dtw_dist_kernel); null: computed inside the band kernel
-  double* Dd;
   // Cn null: the band kernel keeps only every 64th column of C (CK, dtw_ck_bytes), and the path
   // costs are recomputed per 64 x 64 tile the path visits (launch_dtw_path_tiles); runs holds
   // [0] the tile count, then each tile's first path index (dtw_run_words ints)
@@ -238,11 +235,8 @@ struct DtwArgs {
   //       without a new edge value), [14] those after which the next poll found new values,
   //  [15] waves of this DTW that timed out
   uint64_t* diag;
-  // nullable (diagnostics, SONAR_DTW_STATE): how and where every wave of every band-kernel block
-  // ended, 8 words per block (dtw_band2_kernel)
-  uint64_t* state;
-  // tests only (SONAR_DTW_DBG_STALL=<band>): the sweep of that 64-row band (band kernel) or of the
-  // 128-row band holding it (band2) stops after 1,024 steps without publishing more, so the
+  // tests only (SONAR_DTW_DBG_STALL=<band>): the sweep of that 64-row band stops after 1,024 steps
+  // without publishing more, so the
   // pipeline's bounded waits and its diagnostic record can be exercised; -1: off
   int32_t dbg_stall = -1;
   int32_t pad_;
@@ -267,20 +261,12 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s);
 // path scans (which also save C[nq][nr]) and the path points, in four launches and no host
 // round trip.  The caller zeroes each DTW's sync words and *ticket and fills each E with the
 // sentinel words 0x7FF00001 first; max_cap >= every nq + nr + 1.
-// (hargs: the same array on the host; every Dd set -> distances precomputed per DTW first)
+// (hargs: the same array on the host)
 // dmap (nullable): ticket -> (DTW, band) order, e.g. band-major across the batch so a band waits
 // about one hand-off for its predecessor instead of b of them
-// the 128-row band kernel (dtw_band2_kernel: two 64-row sub-bands per block) runs every 12-dim
-// DTW in checkpoint mode when SONAR_DTW_BAND2=1; launch_dtw_batch's tickets are then 128-row
-// bands: per DTW ceil(nb / 2) of them, and dmap / dstart count those
-bool dtw_band2_enabled(int dim);
-// otherwise (default; SONAR_DTW_WAVE=0: the 8-wave band kernel) the one-wave kernel
-// (dtw_wave_kernel) runs the batch as `waves` persistent waves taking tickets in order (<= 0: one
-// block per ticket)
-bool dtw_wave_batch_enabled();
-int32_t dtw_dbg_stall_band();   // SONAR_DTW_DBG_STALL (tests only), -1 when unset
+int32_t dtw_dbg_stall_band(bool batch);   // SONAR_DTW_DBG_STALL (tests only), -1 when unset
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
-                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr, int waves = 0);
+                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr);
 // sets *flag = 1 if any of the n values is not finite
 int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 // the same probe over q and r of every DTW of a batch (sets args[k].sync[2]); max_elems >= every

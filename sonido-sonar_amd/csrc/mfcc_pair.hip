@@ -417,283 +417,8 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// Two pairs per wave (mfcc_pair2_kernel, the default at the headline shape): the same data flow
-// and arithmetic per pair as mfcc_pair_kernel, with every phase run for TWO independent pairs
-// before the phase's LDS boundary, so one wave_lds_sync retires both pairs' exchanges (5 boundaries
-// per 4 frames instead of per 2) and each phase carries two independent instruction streams.
-// 8-wave blocks (2 waves/SIMD at <= 256 VGPRs): 16 pairs in flight per CU instead of 12; LDS =
-// the shared tables + 8 waves x 2 T2/power regions (~150 KB, one block per CU).
-template <bool POW2, int JT, int MS, int NH>
-__global__ __launch_bounds__(512, 1) void mfcc_pair2_kernel(MfccPairParams p) {
-  constexpr int NPW = 2;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float2* s_cw = reinterpret_cast<float2*>(smem);
-  uint16_t* s_src = reinterpret_cast<uint16_t*>(smem + p.lds_src);
-  float* s_dct = reinterpret_cast<float*>(smem + p.lds_dct);
-  for (int i = threadIdx.x; i < 64 * p.JS; i += blockDim.x) s_cw[i] = p.chunk_w[i];
-  for (int i = threadIdx.x; i < 64 * 16; i += blockDim.x) s_src[i] = p.mel_src[i];
-  for (int i = threadIdx.x; i < 16 * (p.NMP + 4); i += blockDim.x) s_dct[i] = p.dct[i];
-  unsigned char* wbase = smem + p.lds_wave0 + wave * NPW * kWaveBytes;
-  for (int i = lane; i < NPW * kWaveBytes / 16; i += 64)
-    *reinterpret_cast<float4*>(wbase + 16 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
-
-  float win[16];
-#pragma unroll
-  for (int a = 0; a < 16; a++) win[a] = p.window[64 * a + lane];
-  cf tw1[16];
-#pragma unroll
-  for (int k = 1; k < 16; k++) { const float2 v = p.tw1[lane * 16 + k]; tw1[k] = {v.x, v.y}; }
-  const int b0 = lane & 7, kl = lane >> 3;
-  cf tw2[8];
-#pragma unroll
-  for (int c = 1; c < 8; c++) { const float2 v = p.tw2[b0 * 8 + c]; tw2[c] = {v.x, v.y}; }
-  const uint64_t m_hi3 = 0xff00ff00ff00ff00ull, m_lo3 = ~m_hi3;
-  const int t2b0 = (kl - 1) * 8 * kT2Stride + 8 * b0;
-  const int t2b1 = (7 - kl) * 8 * kT2Stride + 64 + 8 * b0;
-  int rA;
-  if (lane < 56) rA = (lane >> 3) + 1 + 16 * (lane & 7);
-  else if (lane < 60) rA = 8 + 16 * (lane - 56);
-  else if (lane < 63) rA = 16 * (lane - 59);
-  else rA = 0;
-  const int rB = (lane == 63) ? 64 : 128 - rA;
-  const bool self = (lane == 63);
-  const int pA = prow(rA) * 8, pB = prow(rB) * 8;
-  const int p8 = 8 * (self ? prow(512) : 18 * (lane & 31) + 16 + (lane >> 5));
-  const int ks = p.chunk_ks[lane];
-  const int nmp = p.NMP;
-
-  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-  const int64_t pb = gw * p.pairs_per_wave;
-  const int64_t NP = (p.F + 1) >> 1;
-  if (pb >= NP) return;
-  const int64_t pe = min(NP, pb + p.pairs_per_wave);
-  const float* pcm = p.pcm;
-  const int H = p.H;
-
-  auto frame_ok = [&](int64_t t) { return t < p.F && t * (int64_t)H + 1024 <= p.n; };
-  auto load_pair = [&](int64_t pi, float (&xr)[16], float (&xi)[16]) {
-    const int64_t t = 2 * pi;
-    const float* b0p = pcm + t * (int64_t)H + lane;
-    const bool ok0 = pi < pe && frame_ok(t), ok1 = pi < pe && frame_ok(t + 1);
-    if (ok0) {
-#pragma unroll
-      for (int a = 0; a < 16; a++) xr[a] = b0p[64 * a];
-    } else {
-#pragma unroll
-      for (int a = 0; a < 16; a++) xr[a] = 0.f;
-    }
-    if (ok1) {
-#pragma unroll
-      for (int a = 0; a < 16; a++) xi[a] = b0p[H + 64 * a];
-    } else {
-#pragma unroll
-      for (int a = 0; a < 16; a++) xi[a] = 0.f;
-    }
-  };
-
-  // the NPW pairs pi0, pi0 + 1 (a pair at or past pe computes on zeros and stores nothing)
-  auto process = [&](int64_t pi0, const float (&xr)[NPW][16], const float (&xi)[NPW][16]) {
-    cf v[NPW][16];
-#pragma unroll
-    for (int q = 0; q < NPW; q++) {
-#pragma unroll
-      for (int a = 0; a < 16; a++) v[q][a] = {xr[q][a] * win[a], xi[q][a] * win[a]};
-      dft16(v[q]);
-#pragma unroll
-      for (int k = 1; k < 16; k++) v[q][k] = cmul(v[q][k], tw1[k]);
-#pragma unroll
-      for (int j = 0; j < 16; j++)
-        if ((j & 4) == 0) { swap32(v[q][j].x, v[q][j + 4].x); swap32(v[q][j].y, v[q][j + 4].y); }
-#pragma unroll
-      for (int j = 0; j < 16; j++)
-        if ((j & 2) == 0) { swap16(v[q][j].x, v[q][j + 2].x); swap16(v[q][j].y, v[q][j + 2].y); }
-      {
-        float ea[4], eb[4];
-#pragma unroll
-        for (int pl = 0; pl < 4; pl++) {
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const int j = 2 * i + 8 * (pl >> 1);
-            ea[i] = (pl & 1) ? v[q][j].y : v[q][j].x;
-            eb[i] = (pl & 1) ? v[q][j + 1].y : v[q][j + 1].x;
-          }
-          swap8x4(ea, eb, m_lo3, m_hi3);
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const int j = 2 * i + 8 * (pl >> 1);
-            if (pl & 1) { v[q][j].y = ea[i]; v[q][j + 1].y = eb[i]; } else { v[q][j].x = ea[i]; v[q][j + 1].x = eb[i]; }
-          }
-        }
-      }
-      dft8<0, 1>(v[q]);
-      dft8<8, 1>(v[q]);
-#pragma unroll
-      for (int c = 1; c < 8; c++) { v[q][c] = cmul(v[q][c], tw2[c]); v[q][8 + c] = cmul(v[q][8 + c], tw2[c]); }
-      unsigned char* wb = wbase + q * kWaveBytes;
-      if (kl != 0) {
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-          *reinterpret_cast<float2*>(wb + t2b0 + kT2Stride * c) = make_float2(v[q][c].x, v[q][c].y);
-          *reinterpret_cast<float2*>(wb + t2b1 + kT2Stride * (7 - c)) = make_float2(v[q][8 + c].x, v[q][8 + c].y);
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-          *reinterpret_cast<float2*>(wb + 8 * b0 + kT2Irreg[0][c]) = make_float2(v[q][c].x, v[q][c].y);
-          *reinterpret_cast<float2*>(wb + 8 * b0 + kT2Irreg[1][c]) = make_float2(v[q][8 + c].x, v[q][8 + c].y);
-        }
-      }
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int q = 0; q < NPW; q++) {
-      const unsigned char* wb = wbase + q * kWaveBytes;
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const float2 u = *reinterpret_cast<const float2*>(wb + lane * kT2Stride + 8 * j);
-        v[q][j] = {u.x, u.y};
-      }
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int q = 0; q < NPW; q++) {
-      unsigned char* wb = wbase + q * kWaveBytes;
-      dft8<0, 1>(v[q]);
-      dft8<8, 1>(v[q]);
-      auto pw = [&](cf a, cf b, int off) {
-        const float sr = a.x + b.x, si = a.y - b.y, dr = a.x - b.x, di = a.y + b.y;
-        float p0 = sr * sr + si * si, p1 = dr * dr + di * di;
-        if (POW2) { p0 *= p0; p1 *= p1; }
-        *reinterpret_cast<float2*>(wb + off) = make_float2(p0, p1);
-      };
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const cf sec = self ? v[q][(8 - c) & 7] : v[q][15 - c];
-        pw(v[q][c], sec, pA + 1152 * c);
-      }
-      pw(self ? v[q][12] : v[q][4], v[q][11], pB + 3456);
-#pragma unroll
-      for (int c = 5; c < 8; c++) {
-        const cf fst = self ? v[q][8 + c] : v[q][c];
-        pw(fst, v[q][15 - c], pB + 1152 * (7 - c));
-      }
-      {
-        const float p0 = v[q][4].x * v[q][4].x * 4.f, p1 = v[q][4].y * v[q][4].y * 4.f;
-        *reinterpret_cast<float2*>(wb + p8) = POW2 ? make_float2(p0 * p0, p1 * p1) : make_float2(p0, p1);
-      }
-    }
-    wave_lds_sync();
-    {
-      const int ib = 16 - (ks & 15);
-      const float2* cw = s_cw + lane * p.JS;
-      const int J = JT ? JT : p.J;
-      float a0[NPW], a1[NPW], c0[NPW], c1[NPW];
-#pragma unroll
-      for (int q = 0; q < NPW; q++) { a0[q] = 0.f; a1[q] = 0.f; c0[q] = 0.f; c1[q] = 0.f; }
-#pragma unroll
-      for (int i = 0; i < J; i++) {
-        const float2 w = cw[i];
-#pragma unroll
-        for (int q = 0; q < NPW; q++) {
-          const unsigned char* pr = wbase + q * kWaveBytes + prow(ks) * 8;
-          const float2 pp = *reinterpret_cast<const float2*>(pr + 8 * i + (i >= ib ? 16 : 0));
-          a0[q] += w.x * pp.x; a1[q] += w.x * pp.y;
-          c0[q] += w.y * pp.x; c1[q] += w.y * pp.y;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < NPW; q++)
-        *reinterpret_cast<float4*>(wbase + q * kWaveBytes + kPartOff + 16 * lane) = make_float4(a0[q], a1[q], c0[q], c1[q]);
-    }
-    wave_lds_sync();
-    if (lane < nmp) {
-      float m0[NPW], m1[NPW];
-#pragma unroll
-      for (int q = 0; q < NPW; q++) { m0[q] = 0.f; m1[q] = 0.f; }
-      const int ms = MS ? MS : p.max_src;
-#pragma unroll
-      for (int i = 0; i < ms; i++) {
-        const uint32_t idx = s_src[64 * i + lane];
-        const int off = (idx & 0x8000u) ? 64 * kT2Stride : kPartOff + 8 * (int)idx;
-#pragma unroll
-        for (int q = 0; q < NPW; q++) {
-          const float2 x = *reinterpret_cast<const float2*>(wbase + q * kWaveBytes + off);
-          m0[q] += x.x;
-          m1[q] += x.y;
-        }
-      }
-      const float lf = -23.025850929940457f;
-#pragma unroll
-      for (int q = 0; q < NPW; q++) {
-        float l0 = m0[q] > 0.f ? __logf(m0[q]) : lf, l1 = m1[q] > 0.f ? __logf(m1[q]) : lf;
-        if (lane >= p.n_mels) { l0 = 0.f; l1 = 0.f; }
-        float* lm = reinterpret_cast<float*>(wbase + q * kWaveBytes + kLogOff);
-        lm[lane] = l0; lm[nmp + lane] = l1;
-      }
-    }
-    wave_lds_sync();
-    {
-      const int qq = lane & 15, f = (lane >> 4) & 1, hh = lane >> 5;
-      const int half = NH ? NH : (nmp >> 1);
-      const float* d = s_dct + qq * (nmp + 4) + hh * half;
-      float s[NPW];
-#pragma unroll
-      for (int q = 0; q < NPW; q++) s[q] = 0.f;
-#pragma unroll
-      for (int m = 0; m < half; m += 4) {
-        const float4 y = *reinterpret_cast<const float4*>(d + m);
-#pragma unroll
-        for (int q = 0; q < NPW; q++) {
-          const float* lm = reinterpret_cast<const float*>(wbase + q * kWaveBytes + kLogOff) + f * nmp + hh * half;
-          const float4 x = *reinterpret_cast<const float4*>(lm + m);
-          s[q] += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < NPW; q++) {
-        const auto r = __builtin_amdgcn_permlane32_swap(u_of(s[q]), u_of(s[q]), false, false);
-        const float sq = s[q] + f_of(r[1]);
-        const int64_t t = 2 * (pi0 + q) + f;
-        if (hh == 0 && qq < p.n_mfcc && t < p.F && pi0 + q < pe) p.out[t * p.n_mfcc + qq] = sq;
-      }
-    }
-    wave_lds_sync();
-  };
-
-  float ar[NPW][16], ai[NPW][16];
-#pragma unroll
-  for (int q = 0; q < NPW; q++) load_pair(pb + q, ar[q], ai[q]);
-  for (int64_t pi = pb; pi < pe; pi += NPW) {
-    float nr[NPW][16], ni[NPW][16];
-    if (pi + NPW < pe) {
-#pragma unroll
-      for (int q = 0; q < NPW; q++) load_pair(pi + NPW + q, nr[q], ni[q]);
-    }
-    process(pi, ar, ai);
-#pragma unroll
-    for (int q = 0; q < NPW; q++) {
-#pragma unroll
-      for (int a = 0; a < 16; a++) { ar[q][a] = nr[q][a]; ai[q][a] = ni[q][a]; }
-    }
-  }
-}
-
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   const int64_t NP = (p.F + 1) >> 1;
-  if (p.waves_per_block == 8) {   // mfcc_pair2_kernel: 8-wave blocks, two pairs per wave at a time
-    const int64_t waves = (NP + p.pairs_per_wave - 1) / p.pairs_per_wave;
-    const int64_t grid = (waves + 7) / 8;
-    const bool head = p.J == 12 && p.max_src <= 8 && p.NMP == 40;
-    auto kern = p.pow2 ? (head ? mfcc_pair2_kernel<true, 12, 8, 20> : mfcc_pair2_kernel<true, 0, 0, 0>)
-                       : (head ? mfcc_pair2_kernel<false, 12, 8, 20> : mfcc_pair2_kernel<false, 0, 0, 0>);
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), p.lds_bytes, s, p);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
-  }
   const int64_t waves = (NP + p.pairs_per_wave - 1) / p.pairs_per_wave;
   const int64_t grid = (waves + 3) / 4;
   const bool head = p.J == 12 && p.max_src <= 8 && p.NMP == 40;

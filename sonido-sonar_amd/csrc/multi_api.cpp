@@ -115,12 +115,12 @@ struct PairGeo {
   int64_t k = 0, nq = 0, nr = 0, Fq = 0, Fr = 0, Eq = 0, Er = 0, L = 0, mlf = 0, cap = 0;
   bool corr = false;
   sonar::DtwGeom g{};
-  size_t chroma = 0, cn = 0, ck = 0, runs = 0, dn = 0, e = 0, codes = 0, wst = 0, path = 0, corr_off = 0;   // region offsets
+  size_t chroma = 0, ck = 0, runs = 0, dn = 0, e = 0, codes = 0, wst = 0, path = 0, corr_off = 0;   // region offsets
 };
 
-// device bytes one pair of a batch holds (chroma, the DTW stores, the path; PRE: the distances)
+// device bytes one pair of a batch holds (chroma, the DTW stores, the path)
 size_t pair_bytes(const PairGeo& p) {
-  return al256((size_t)(p.Fq + p.Fr) * 96) + (sonar::detail::dtw_pre_enabled(12) ? al256(sonar::dtw_cn_bytes(p.g)) : 0) +
+  return al256((size_t)(p.Fq + p.Fr) * 96) +
          al256(sonar::dtw_ck_bytes(p.g)) + al256((size_t)sonar::dtw_run_words(p.g) * 4) + al256(sonar::dtw_dn_bytes(p.g)) +
          al256(sonar::dtw_edge_bytes(p.g)) + al256((size_t)((p.cap + 1023) / 1024) * 256) +
          al256((size_t)((p.cap + 15) / 16 + 1) * 8) + al256((size_t)p.cap * 16) + al256((size_t)(2 * p.L + 1) * 8) +
@@ -147,10 +147,9 @@ bool feat_batch_enabled() {
 // "batch features: ..." (the caller's NOMEM retry path).
 bool feat_batch(sonar_ctx* w, const std::vector<PairGeo>& pg, int32_t sr, int32_t sw, int32_t hop, int32_t fw,
                 const double* const* q_pcm, const double* const* r_pcm, char* chroma, char* corr, hipStream_t s,
-                int slot, bool dry = false) {
+                bool dry = false) {
   w->err.clear();
   if (!feat_batch_enabled() || pg.empty() || fw <= 0 || hop <= 0) return false;
-  if (const char* cw = std::getenv("SONAR_CHROMA_WAVE"); cw && std::atoi(cw) == 0) return false;   // chroma_kernel A/B
   const int n = (int)pg.size();
   int fs = -1;
   size_t ysz = 0, dsz = 0, esz = 0, xsz = 0;
@@ -175,7 +174,7 @@ bool feat_batch(sonar_ctx* w, const std::vector<PairGeo>& pg, int32_t sr, int32_
   char* nx = (char*)dbuf(w, "fb.ncc", std::max<size_t>(xsz, 256));
   const size_t jb = al256((size_t)2 * n * sizeof(sonar::MfJob)), nb = al256((size_t)std::max(ncorr, 1) * sizeof(sonar::NccJob));
   char* dj = (char*)dbuf(w, "fb.jobs", jb + nb);
-  char* hj = (char*)sonar::detail::hbuf(w, "fb.hjobs" + std::to_string(slot), jb + nb);
+  char* hj = (char*)sonar::detail::hbuf(w, "fb.hjobs", jb + nb);
   if (!ct || !y || !dcs || !en || !nx || !dj || !hj) {
     fail(w, SONAR_ERR_NOMEM, "batch features: allocation failed");
     return false;
@@ -223,37 +222,25 @@ bool feat_batch(sonar_ctx* w, const std::vector<PairGeo>& pg, int32_t sr, int32_
 }
 
 // A batch of pairs on worker w's stream with one host synchronisation: every pair's music
-// features and energy NCC (stream-ordered launches), then ONE launch_dtw_batch over all their
-// chroma DTWs, then the correlations, path arrays and status words in three copies.  Pairs whose
-// chroma is not finite (the DTW ran the finite-input kernel) are redone one by one through
-// align_one (exact math.Min rules); their indices are appended to `redo`.
-// A batch whose launches and result copies are enqueued: `ev` follows its last copy, `finish`
-// reads the pinned copies and fills the records (run it after ev completes, on the same thread)
-struct PendingBatch {
-  hipEvent_t ev = nullptr;
-  std::function<void()> finish;
-};
-
-// With pend (and no diagnostics switched on) align_batch returns once everything is enqueued and
-// leaves the synchronisation and the scorers to pend->finish, so the worker can enqueue its next
-// batch first: the host scorers and the next batch's setup then overlap this batch's tail on the
-// GPU.  `slot` (0/1) selects the pinned staging set, so the two batches in flight never share one.
+// features and energy NCC (batched launches, feat_batch), then ONE launch_dtw_batch over all their
+// chroma DTWs, then the correlations, path arrays and status words in three copies.  Pairs to be
+// redone on the single-pair path (align_one) are appended to `redo` with the record flag that says
+// why: SONAR_PAIR_REDONE_NONFINITE (the chroma is not finite: the batch ran the finite-input
+// kernel, the exact math.Min rules are on the single-pair path) or SONAR_PAIR_REDONE_TIMEOUT (the
+// band pipeline timed out and the retry is on).  dry: reserve the buffers only.
 int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* const* q_pcm, const double* const* r_pcm,
-                int32_t sr, int32_t sw, int32_t hop, int32_t fw, int32_t device_ptrs, sonar_pair_record* out,
-                std::vector<int64_t>* redo, std::vector<std::pair<int64_t, std::string>>* errs, int nstreams,
-                int slot = 0, PendingBatch* pend = nullptr, bool dry = false) {
+                int32_t sr, int32_t sw, int32_t hop, int32_t fw, int32_t device_ptrs, bool retry_timeouts,
+                sonar_pair_record* out, std::vector<std::pair<int64_t, int32_t>>* redo,
+                std::vector<std::pair<int64_t, std::string>>* errs, bool dry = false) {
   const int n = (int)in.size();
   if (n == 0) return SONAR_OK;
   HIP_TRY(w, hipSetDevice(w->device));
   hipStream_t s = w->stream;
   std::vector<PairGeo> pg = in;
-  const bool pre = sonar::detail::dtw_pre_enabled(12);
-  const bool band2 = !pre && sonar::dtw_band2_enabled(12);   // tickets over 128-row bands
-  size_t chroma_b = 0, cn_b = 0, ck_b = 0, runs_b = 0, dn_b = 0, e_b = 0, codes_b = 0, wst_b = 0, path_b = 0, corr_b = 0;
-  int64_t maxE = 1, maxn = 1, max_cap = 1, total_bands = 0;
+  size_t chroma_b = 0, ck_b = 0, runs_b = 0, dn_b = 0, e_b = 0, codes_b = 0, wst_b = 0, path_b = 0, corr_b = 0;
+  int64_t maxE = 1, maxn = 1, max_cap = 1, total_bands = 0, maxnb = 0;
   for (auto& p : pg) {
     p.chroma = chroma_b; chroma_b += al256((size_t)(p.Fq + p.Fr) * 96);
-    if (pre) { p.cn = cn_b; cn_b += al256(sonar::dtw_cn_bytes(p.g)); }
     p.ck = ck_b; ck_b += al256(sonar::dtw_ck_bytes(p.g));
     p.runs = runs_b; runs_b += al256((size_t)sonar::dtw_run_words(p.g) * 4);
     p.dn = dn_b; dn_b += al256(sonar::dtw_dn_bytes(p.g));
@@ -265,7 +252,8 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     maxE = std::max({maxE, p.Eq, p.Er});
     maxn = std::max({maxn, p.nq, p.nr});
     max_cap = std::max(max_cap, p.cap);
-    total_bands += band2 ? (p.g.nb + 1) / 2 : p.g.nb;   // band-kernel tickets
+    maxnb = std::max(maxnb, p.g.nb);
+    total_bands += p.g.nb;   // band-kernel tickets
   }
   // small (device) and the head of h (pinned host) share one layout: per-pair status words + the
   // batch ticket, the per-pair band-kernel diagnostic records, then the DTW arguments, ticket
@@ -276,7 +264,6 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* chroma = (char*)dbuf(w, "pb.chroma", chroma_b);
   char* CK = (char*)dbuf(w, "pb.CK", ck_b);
   char* runs = (char*)dbuf(w, "pb.runs", runs_b);
-  char* Dd = pre ? (char*)dbuf(w, "pb.Dd", cn_b) : nullptr;
   char* Dn = (char*)dbuf(w, "pb.Dn", dn_b);
   char* E = (char*)dbuf(w, "pb.E", e_b);
   char* codes = (char*)dbuf(w, "pb.codes", codes_b);
@@ -291,13 +278,12 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   double* st = (double*)dbuf(w, "ncc.stats", 64);
   double* up_q = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.q", (size_t)maxn * 8);
   double* up_r = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.r", (size_t)maxn * 8);
-  char* h = (char*)sonar::detail::hbuf(w, "pb.host" + std::to_string(slot),
-                                       stat_b + diag_b + args_b + start_b + map_b + corr_b + path_b);
-  if (!chroma || !CK || !runs || (pre && !Dd) || !Dn || !E || !codes || !wst || !path || !corr || !small || !eq || !er || !xa || !xb || !st ||
-      (!device_ptrs && (!up_q || !up_r)) || !h)
+  char* h = (char*)sonar::detail::hbuf(w, "pb.host", stat_b + diag_b + args_b + start_b + map_b + corr_b + path_b);
+  if (!chroma || !CK || !runs || !Dn || !E || !codes || !wst || !path || !corr || !small || !eq || !er || !xa || !xb ||
+      !st || (!device_ptrs && (!up_q || !up_r)) || !h)
     return fail(w, SONAR_ERR_NOMEM, "allocation failed (pair batch)");
   if (dry) {   // reserve only (sonar_align_pairs' sizing pass): the batched-feature buffers too
-    if (device_ptrs && !feat_batch(w, pg, sr, sw, hop, fw, q_pcm, r_pcm, chroma, corr, s, slot, true) &&
+    if (device_ptrs && !feat_batch(w, pg, sr, sw, hop, fw, q_pcm, r_pcm, chroma, corr, s, true) &&
         w->err.rfind("batch features:", 0) == 0)
       return SONAR_ERR_NOMEM;
     return SONAR_OK;
@@ -317,36 +303,12 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* hcorr = h + ab + args_b + start_b + map_b;
   char* hpath = hcorr + corr_b;
   HIP_TRY(w, hipMemsetAsync(small, 0, stat_b + diag_b, s));
-  // SONAR_DTW_STATE=<dir> (diagnostics): every band-kernel block's per-wave exit words
-  // (DtwArgs::state), written to <dir>/state_pair<k>.bin for each pair whose pipeline timed out
-  const char* state_dir = std::getenv("SONAR_DTW_STATE");
-  std::vector<size_t> state_off(n, 0);
-  char* dstate = nullptr;
-  if (state_dir) {
-    size_t sb = 0;
-    for (int i = 0; i < n; ++i) { state_off[i] = sb; sb += al256((size_t)(pg[i].g.nb + 1) * 64); }
-    dstate = (char*)dbuf(w, "pb.state", sb);
-    if (!dstate) return fail(w, SONAR_ERR_NOMEM, "allocation failed (state)");
-    HIP_TRY(w, hipMemsetAsync(dstate, 0, sb, s));
-  }
-  // SONAR_DTW_BATCH_TRACE=1 (diagnostics): every band's start / first-edge / end / edge-wait ticks
-  // (dtw_wave_kernel's trace words), summed per batch into a line on stderr
-  const bool btrace = [] { const char* e = std::getenv("SONAR_DTW_BATCH_TRACE"); return e && e[0] == '1'; }();
-  std::vector<size_t> trace_off(n, 0);
-  uint64_t* dtrace = nullptr;
-  size_t trace_b = 0;
-  if (btrace) {
-    for (int i = 0; i < n; ++i) { trace_off[i] = trace_b; trace_b += (size_t)pg[i].g.nb * 8; }
-    dtrace = (uint64_t*)dbuf(w, "pb.trace", trace_b * 8);
-    if (!dtrace) return fail(w, SONAR_ERR_NOMEM, "allocation failed (trace)");
-    HIP_TRY(w, hipMemsetAsync(dtrace, 0, trace_b * 8, s));
-  }
   HIP_TRY(w, hipMemsetAsync(runs, 0, runs_b, s));
   if (e_b) HIP_TRY(w, hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, e_b / 4, s));
   // every pair's music features and energy NCC: batched launches over the whole batch when the
   // inputs are on the device and every signal fits the batched kernels (feat_batch), else pair by
   // pair on the worker's scratch
-  const bool fb = device_ptrs && feat_batch(w, pg, sr, sw, hop, fw, q_pcm, r_pcm, chroma, corr, s, slot);
+  const bool fb = device_ptrs && feat_batch(w, pg, sr, sw, hop, fw, q_pcm, r_pcm, chroma, corr, s);
   if (!fb && !w->err.empty() && w->err.rfind("batch features:", 0) == 0) return SONAR_ERR_NOMEM;
   int64_t acc = 0;
   for (int i = 0; i < n; ++i) {
@@ -375,75 +337,32 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     a.codes = (uint32_t*)(codes + p.codes); a.plen = (int64_t*)(dstat + 8 * i); a.wstart = (int2*)(wst + p.wst);
     a.pc = (double*)(path + p.path); a.pq = (int32_t*)(a.pc + p.cap); a.pr = a.pq + p.cap;
     a.cnm = (double*)(dstat + 8 * i + 2);
-    a.Dd = pre ? (double*)(Dd + p.cn) : nullptr;
     a.diag = ddiag + (size_t)i * sonar::DTW_DIAG_WORDS;
-    a.state = dstate ? (uint64_t*)(dstate + state_off[i]) : nullptr;
-    a.trace = dtrace ? dtrace + trace_off[i] : nullptr;
-    a.dbg_stall = sonar::dtw_dbg_stall_band();
+    a.dbg_stall = sonar::dtw_dbg_stall_band(true);
     hstart[i] = acc;
-    acc += band2 ? (p.g.nb + 1) / 2 : p.g.nb;
+    acc += p.g.nb;
   }
   hstart[n] = acc;
-  // band-major tickets across the batch (SONAR_DTW_BAND_MAJOR=0: DTW-major): band b of every DTW
-  // before band b+1 of any, so a block waits about one hand-off for its predecessor band rather
-  // than b of them while holding its slot
-  const char* bm = std::getenv("SONAR_DTW_BAND_MAJOR");
-  const bool band_major = !(bm && std::atoi(bm) == 0);
-  if (band_major) {
-    int64_t t = 0, maxnb = 0;
-    auto blocks = [&](const PairGeo& p) { return band2 ? (p.g.nb + 1) / 2 : p.g.nb; };
-    for (const auto& p : pg) maxnb = std::max(maxnb, blocks(p));
+  // band-major tickets across the batch: band b of every DTW before band b+1 of any, so a block
+  // waits about one hand-off for its predecessor band rather than b of them while holding its slot
+  {
+    int64_t t = 0;
     for (int64_t b = 0; b < maxnb; ++b)
       for (int i = 0; i < n; ++i)
-        if (b < blocks(pg[i])) hmap[t++] = make_int2(i, (int)b);
+        if (b < pg[i].g.nb) hmap[t++] = make_int2(i, (int)b);
   }
-  HIP_TRY(w, hipMemcpyAsync(dargs, hargs, args_b + start_b + (band_major ? map_b : 0), hipMemcpyHostToDevice, s));
+  HIP_TRY(w, hipMemcpyAsync(dargs, hargs, args_b + start_b + map_b, hipMemcpyHostToDevice, s));
   // the non-finite probe of every pair's chroma in one launch (flags in each pair's sync[2])
   int64_t max_el = 0;
   for (const auto& p : pg) max_el = std::max(max_el, (p.Fq + p.Fr) * 12);
   if (sonar::launch_nonfinite_batch(dargs, n, max_el, s) != 0) return fail(w, SONAR_ERR_DEVICE, "dtw launch failed");
-  // the one-wave DTW kernel: one block per ticket (its waves keep taking tickets while any are
-  // left, so a block launched after the last ticket exits at once).  SONAR_DTW_WAVES=<n> caps the
-  // grid at n persistent waves instead -- measured slower for every n tried (32-160 per stream,
-  // profiles/r03s5_c5_persistent_ab.log): a batch's DTW then cannot take the slots that the other
-  // streams' feature phases leave free
-  int waves = 0;
-  if (!pre && !band2 && sonar::dtw_wave_batch_enabled()) {
-    const char* wev = std::getenv("SONAR_DTW_WAVES");
-    waves = wev ? std::atoi(wev) : 0;
-  }
-  (void)nstreams;
-  if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s,
-                              band_major ? dmap : nullptr, waves) != 0)
+  if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s, dmap) != 0)
     return fail(w, SONAR_ERR_DEVICE, "dtw batch launch failed");
   HIP_TRY(w, hipMemcpyAsync(hstat, small, stat_b + diag_b, hipMemcpyDeviceToHost, s));
   if (corr_b) HIP_TRY(w, hipMemcpyAsync(hcorr, corr, corr_b, hipMemcpyDeviceToHost, s));
   HIP_TRY(w, hipMemcpyAsync(hpath, path, path_b, hipMemcpyDeviceToHost, s));
+  HIP_TRY(w, hipStreamSynchronize(s));
   const char* dump_dir = std::getenv("SONAR_PAIR_DUMP");
-  const char* rtv = std::getenv("SONAR_PAIR_RETRY");         // 0: a timed-out pair stays failed (A/B)
-  const bool retry_timeouts = !(rtv && rtv[0] == '0');
-  auto fin = [=, pg = std::move(pg), state_off = std::move(state_off), trace_off = std::move(trace_off)]() {
-  if (dtrace) {
-    // ticks of s_memrealtime (100 MHz): band-time = end - start, of which first-edge wait =
-    // first - start and later edge waits = the sweep's spin ticks; steps = S per band
-    std::vector<uint64_t> tr(trace_b);
-    if (hipMemcpy(tr.data(), dtrace, trace_b * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-      double busy = 0, first = 0, spin = 0, steps = 0;
-      uint64_t t0 = UINT64_MAX, t1 = 0;
-      for (int i = 0; i < n; ++i)
-        for (int64_t b = 0; b < pg[i].g.nb; ++b) {
-          const uint64_t* r = tr.data() + trace_off[i] + 8 * b;
-          if (!r[2]) continue;
-          busy += (double)(r[2] - r[0]); first += (double)(r[1] - r[0]); spin += (double)r[3];
-          steps += (double)pg[i].g.S;
-          t0 = std::min(t0, r[0]); t1 = std::max(t1, r[2]);
-        }
-      std::fprintf(stderr, "{\"dtw_batch_trace\": {\"pairs\": %d, \"band_us\": %.1f, \"first_wait_us\": %.1f, "
-                   "\"spin_us\": %.1f, \"steps\": %.0f, \"ns_per_step_busy\": %.2f, \"ns_per_step_compute\": %.2f, \"span_us\": %.1f}}\n",
-                   n, busy / 100.0, first / 100.0, spin / 100.0, steps, busy * 10.0 / steps,
-                   (busy - first - spin) * 10.0 / steps, (double)(t1 - t0) / 100.0);
-    }
-  }
   for (int i = 0; i < n; ++i) {
     const PairGeo& p = pg[i];
     const char* ps = hstat + (size_t)i * 32;
@@ -454,37 +373,29 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     std::memcpy(&cnm, ps + 8, 8);
     std::memcpy(sync, ps + 16, 16);
     sonar_pair_record* rec = &out[p.k];
-    if (sync[2]) { redo->push_back(p.k); continue; }
+    if (sync[2]) { redo->emplace_back(p.k, SONAR_PAIR_REDONE_NONFINITE); continue; }
     alignas(8) char sblk[sonar::DTW_SYNC_BYTES];
     std::memcpy(sblk, sync, 16);
     std::memcpy(sblk + 16, hdiag + (size_t)i * sonar::DTW_DIAG_WORDS, 8 * sonar::DTW_DIAG_WORDS);
     const std::string why = sonar::detail::dtw_status(w, sblk);
-    if (!why.empty() && retry_timeouts && !dstate) {
-      // the band pipeline of this pair timed out (an open issue: mostly in a process's first
-      // call): the pair is redone once on the single-pair path (exact, separately
-      // synchronised); the timeout stays counted in sonar_dtw_counters
-      // (SONAR_PAIR_RETRY=0 reports it as the pair's error instead)
-      redo->push_back(p.k);
-      continue;
-    }
     if (!why.empty()) {
-      if (dstate) {
-        std::vector<uint64_t> st((size_t)(p.g.nb + 1) * 8);
-        if (hipMemcpy(st.data(), dstate + state_off[i], st.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-          const std::string fn = std::string(state_dir) + "/state_pair" + std::to_string(p.k) + ".bin";
-          if (FILE* f = std::fopen(fn.c_str(), "wb")) { std::fwrite(st.data(), 8, st.size(), f); std::fclose(f); }
-        }
+      if (retry_timeouts) {
+        // the band pipeline of this pair timed out: redone once on the single-pair path (exact,
+        // separately synchronised); the record carries SONAR_PAIR_REDONE_TIMEOUT and the timeout
+        // stays counted in sonar_dtw_counters
+        redo->emplace_back(p.k, SONAR_PAIR_REDONE_TIMEOUT);
+        continue;
       }
       std::memset(rec, 0, sizeof(*rec));
       rec->status = fail(w, SONAR_ERR_DEVICE, why);
       errs->emplace_back(p.k, why);
       continue;
     }
-    if (const char* dump = dump_dir) {
+    if (dump_dir) {
       // tests only: the batched DTW's raw outputs of pair k (path length, C[nq][nr], path costs,
       // query and reference indices) into <dump>/pair_<k>.bin, to be checked against the oracle
       const double* pc = (const double*)(hpath + p.path);
-      const std::string fn = std::string(dump) + "/pair_" + std::to_string(p.k) + ".bin";
+      const std::string fn = std::string(dump_dir) + "/pair_" + std::to_string(p.k) + ".bin";
       if (FILE* f = std::fopen(fn.c_str(), "wb")) {
         std::fwrite(&P, 8, 1, f);
         std::fwrite(&cnm, 8, 1, f);
@@ -502,16 +413,8 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     ai.P = P; ai.nqc = p.Fq; ai.nrc = p.Fr; ai.dist = cnm / (double)P;   // dtw.go:88-91
     sonar::detail::align_finish(ai, nullptr, rec);
     rec->status = SONAR_OK;
+    rec->flags = 0;
   }
-  };
-  // diagnostics read device buffers after the sync, which the next batch would reuse: no deferral
-  if (pend && pend->ev && !dtrace && !dstate && !dump_dir) {
-    HIP_TRY(w, hipEventRecord(pend->ev, s));
-    pend->finish = std::move(fin);
-    return SONAR_OK;
-  }
-  HIP_TRY(w, hipStreamSynchronize(s));
-  fin();
   return SONAR_OK;
 }
 
@@ -606,66 +509,45 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
     batches.push_back(std::move(b));
   }
   std::atomic<size_t> next{0};
-  const char* rev = std::getenv("SONAR_PAIR_RESERVE");
-  const bool reserve = !(rev && rev[0] == '0');
+  // SONAR_PAIR_RETRY=0: a pair whose band pipeline timed out is an error (the bench's setting);
+  // default: it is redone once on the single-pair path and flagged SONAR_PAIR_REDONE_TIMEOUT
+  const char* rtv = std::getenv("SONAR_PAIR_RETRY");
+  const bool retry_timeouts = !(rtv && rtv[0] == '0');
   std::mutex rmu;
   std::condition_variable rcv;
   int rdone = 0;
-  std::vector<std::vector<int64_t>> redo(nstreams);
+  std::vector<std::vector<std::pair<int64_t, int32_t>>> redo(nstreams);
   std::vector<std::vector<std::pair<int64_t, std::string>>> errs(nstreams);
   for (int t = 0; t < nstreams; ++t) {
     th.emplace_back([&, t] {
       sonar_ctx* w = ws[t];
       // sizing pass: every worker reserves its buffers for the largest of all batches before any
-      // worker launches.  Allocating or freeing device / pinned memory while other workers' DTW
-      // pipelines run stalled them: every fresh-process C5 run lost 9-52 DTWs to band-pipeline
-      // timeouts in the first call (buffers growing batch by batch), none once sizes had settled
-      // (DESIGN §6).  SONAR_PAIR_RESERVE=0 skips it (A/B).
-      if (reserve) {
-        for (const auto& b : batches)
-          if (align_batch(w, b, q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window, device_ptrs, out,
-                          &redo[t], &errs[t], nstreams, 0, nullptr, true) != SONAR_OK)
-            break;                                 // NOMEM: the batch loop's retry path handles it
-        // one small fill on the worker's stream: HIP gives a stream its hardware queue at its first
-        // command, so every worker's queue exists before any worker's DTW pipeline runs
-        if (hipSetDevice(w->device) == hipSuccess) {
-          if (void* z = dbuf(w, "pb.touch", 256)) (void)hipMemsetAsync(z, 0, 256, w->stream);
-          (void)hipStreamSynchronize(w->stream);
-        }
+      // worker launches, so no device or pinned allocation (which synchronises the device) happens
+      // while other workers' band pipelines run
+      for (const auto& b : batches)
+        if (align_batch(w, b, q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window, device_ptrs,
+                        retry_timeouts, out, &redo[t], &errs[t], true) != SONAR_OK)
+          break;                                   // NOMEM: the batch loop's retry path handles it
+      // one small fill on the worker's stream: HIP gives a stream its hardware queue at its first
+      // command, so every worker's queue exists before any worker's DTW pipeline runs
+      if (hipSetDevice(w->device) == hipSuccess) {
+        if (void* z = dbuf(w, "pb.touch", 256)) (void)hipMemsetAsync(z, 0, 256, w->stream);
+        (void)hipStreamSynchronize(w->stream);
+      }
+      {
         std::unique_lock<std::mutex> lk(rmu);
         if (++rdone == nstreams) rcv.notify_all();
         else rcv.wait(lk, [&] { return rdone == nstreams; });
       }
-      // SONAR_PAIR_PIPELINE=1 (opt-in): two batches in flight per worker -- batch b is enqueued,
-      // then batch b-1's results are waited for and scored while b runs.  Measured 1,877 pairs/s
-      // at 8 streams against 1,790 for the default 16 x 1, but one of its first C5 runs ended in a
-      // DTW band-pipeline timeout whose record is not yet explained, so it is not the
-      // default
-      PendingBatch pend[2];
-      const char* pev = std::getenv("SONAR_PAIR_PIPELINE");
-      if (pev && pev[0] == '1')
-        for (auto& x : pend)
-          if (hipSetDevice(w->device) != hipSuccess || hipEventCreateWithFlags(&x.ev, hipEventDisableTiming) != hipSuccess)
-            x.ev = nullptr;
-      int cur = 0;
-      auto drain = [&](PendingBatch& x) {
-        if (!x.finish) return;
-        if (hipEventSynchronize(x.ev) != hipSuccess) (void)hipStreamSynchronize(w->stream);
-        x.finish();
-        x.finish = nullptr;
-      };
       for (size_t bi = next.fetch_add(1); bi < batches.size(); bi = next.fetch_add(1)) {
         int r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window,
-                            device_ptrs, out, &redo[t], &errs[t], nstreams, cur, pend[cur].ev ? &pend[cur] : nullptr);
-        drain(pend[cur ^ 1]);
-        cur ^= 1;
+                            device_ptrs, retry_timeouts, out, &redo[t], &errs[t]);
         if (r == SONAR_ERR_NOMEM) {
           // the worker's cached buffers are sized by earlier batches, name by name: release them
           // and retry the batch once; then pair by pair on the unbatched path
-          drain(pend[cur ^ 1]);
           sonar::detail::trim_buffers(w);
           r = align_batch(w, batches[bi], q_pcm, r_pcm, sample_rate, stft_window, hop, feature_window, device_ptrs,
-                          out, &redo[t], &errs[t], nstreams);
+                          retry_timeouts, out, &redo[t], &errs[t]);
           if (r == SONAR_ERR_NOMEM) {
             sonar::detail::trim_buffers(w);
             r = SONAR_OK;
@@ -677,13 +559,11 @@ int sonar_align_pairs(sonar_ctx* c, int64_t npairs, const double* const* q_pcm, 
         if (r != SONAR_OK)
           for (const auto& p : batches[bi]) { out[p.k].status = r; note(r, p.k, w); }
       }
-      drain(pend[cur ^ 1]);
-      drain(pend[cur]);
-      for (auto& x : pend)
-        if (x.ev) (void)hipEventDestroy(x.ev);
-      for (int64_t k : redo[t])                    // non-finite chroma: exact single-pair path
+      for (const auto& [k, why] : redo[t]) {       // exact single-pair path, flagged in the record
         note(align_one(w, q_pcm[k], nq[k], r_pcm[k], nr[k], sample_rate, stft_window, hop, feature_window,
                        max_lag_seconds, device_ptrs, &out[k]), k, w);
+        out[k].flags |= why;
+      }
     });
   }
   for (auto& x : th) x.join();

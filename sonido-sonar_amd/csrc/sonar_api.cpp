@@ -57,12 +57,6 @@ void* hbuf(sonar_ctx* c, const std::string& name, size_t bytes) {
   return b.ptr;
 }
 
-bool dtw_pre_enabled(int dim) {
-  if (dim != 12) return false;
-  const char* e = std::getenv("SONAR_DTW_PRE");                   // opt-in: measured slower
-  return e && std::atoi(e) != 0;
-}
-
 // brackets the dominant kernel of a call with a HIP event pair on its stream
 hipEvent_t timed_begin(sonar_ctx* c, hipStream_t s) {
   if (!c->timing) return nullptr;
@@ -531,25 +525,19 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
       q.lds_src = al(64 * t.JS * 8);
       q.lds_dct = q.lds_src + 64 * 16 * 2;
       q.lds_wave0 = q.lds_dct + al(16 * (t.NMP + 4) * 4);
-      // mfcc_pair_kernel (4 waves, 3 blocks per CU); SONAR_MFCC_PAIR2=1: mfcc_pair2_kernel (8 waves x
-      // two pairs each, one block per CU; measured 3-6 % slower, DESIGN.md Kernel 1a) when its 16
-      // wave regions fit next to the tables
-      const char* p2env = std::getenv("SONAR_MFCC_PAIR2");
-      const bool two = p2env && p2env[0] == '1' && q.lds_wave0 + 16 * sonar::mfcc_pair_wave_bytes() <= 160 * 1024;
-      q.waves_per_block = two ? 8 : 4;
-      q.lds_bytes = q.lds_wave0 + (two ? 16 : 4) * sonar::mfcc_pair_wave_bytes();
+      // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU
+      q.waves_per_block = 4;
+      q.lds_bytes = q.lds_wave0 + 4 * sonar::mfcc_pair_wave_bytes();
       int dev_cus = 256;
       hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
-      const int64_t NP = (F + 1) / 2, target_waves = (int64_t)dev_cus * (two ? 8 : 12);
+      const int64_t NP = (F + 1) / 2, target_waves = (int64_t)dev_cus * 12;
       q.pairs_per_wave = std::max<int64_t>(1, (NP + target_waves - 1) / target_waves);
-      if (two) q.pairs_per_wave += q.pairs_per_wave & 1;   // whole iterations of two pairs
-      if (std::getenv("SONAR_DEBUG_SYNC")) hipDeviceSynchronize();
       hipEvent_t tend = timed_begin(c, s);
       if (sonar::launch_mfcc_pair(q, s) != 0)
         return fail(c, SONAR_ERR_DEVICE, std::string("mfcc kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
       timed_end(c, s, tend);
       pair_done = true;
-      c->last_fp_kernel = two ? "mfcc_pair2_kernel" : "mfcc_pair_kernel";
+      c->last_fp_kernel = "mfcc_pair_kernel";
     }
   }
   if (need_fft && !generic && !pair_done) {
@@ -645,7 +633,6 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     }
   }
   if (!dev) {
-    if (std::getenv("SONAR_DEBUG_SYNC")) hipDeviceSynchronize();
     for (auto& m : copies) HIP_TRY(c, hipMemcpyAsync(m.host, m.devp, m.bytes, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
   }
@@ -720,8 +707,7 @@ int sonar_chroma_stft(sonar_ctx* c, const double* pcm, int64_t n, int64_t F, int
   }
   const sonar_ctx::ChromaT* ct = sonar::detail::chroma_tables_for(c, fs, sr);
   if (!ct) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
-  const char* cw = std::getenv("SONAR_CHROMA_WAVE");              // 0: the block-per-frame kernel (A/B)
-  const int* cls = (cw && std::atoi(cw) == 0) ? nullptr : (const int*)ct->cls;
+  const int* cls = (const int*)ct->cls;
   if (sonar::launch_chroma(y, n, F, hop, fs, (const double*)ct->win, (const double*)ct->trig,
                            (const int*)ct->map, cls, dout, s) != 0)
     return fail(c, SONAR_ERR_UNSUPPORTED, "chroma launch failed (frame size too large for LDS?)");
@@ -868,9 +854,7 @@ int sonar_dtw(sonar_ctx* c, const double* q, int64_t nq, const double* r, int64_
     if (!e) HIP_TRY(c, hipEventCreate(&e));
   hipEvent_t tend = timed_begin(c, s);
   HIP_TRY(c, hipEventRecord(c->dtw_ev[0], s));
-  double* Dd = sonar::detail::dtw_pre_enabled(dim) ? (double*)dbuf(c, "dtw.Dd", sonar::dtw_cn_bytes(g)) : nullptr;
-  if (sonar::detail::dtw_pre_enabled(dim) && !Dd) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (distances)");
-  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, codes, pl, trace, s, c->dtw_ev[1], Dd, CK) != 0)
+  if (sonar::launch_dtw(dq, dr, dim, band, fast, g, Cn, Dn, E, sync, codes, pl, trace, s, c->dtw_ev[1], CK) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
   HIP_TRY(c, hipEventRecord(c->dtw_ev[2], s));
   timed_end(c, s, tend);
@@ -1032,9 +1016,7 @@ int dtw_enqueue(sonar_ctx* c, const double* dq, int64_t nq, const double* dr, in
   HIP_TRY(c, hipMemsetAsync(sync + 2, 0, 4, s));
   if (sonar::launch_nonfinite(dq, nq * dim, sync + 2, s) || sonar::launch_nonfinite(dr, nr * dim, sync + 2, s))
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
-  double* Dd = sonar::detail::dtw_pre_enabled(dim) ? (double*)dbuf(c, "dtw.Dd", sonar::dtw_cn_bytes(g)) : nullptr;
-  if (sonar::detail::dtw_pre_enabled(dim) && !Dd) return fail(c, SONAR_ERR_NOMEM, "allocation failed (dtw)");
-  if (sonar::launch_dtw(dq, dr, dim, band, true, g, nullptr, Dn, E, sync, codes, pl, nullptr, s, nullptr, Dd, CK) != 0)
+  if (sonar::launch_dtw(dq, dr, dim, band, true, g, nullptr, Dn, E, sync, codes, pl, nullptr, s, nullptr, CK) != 0)
     return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
   HIP_TRY(c, hipMemcpyAsync(st, pl, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipMemcpyAsync(st + 1, sync, sonar::DTW_SYNC_BYTES, hipMemcpyDeviceToHost, s));
@@ -1060,9 +1042,8 @@ int dtw_finish(sonar_ctx* c, DtwPending* p, const int32_t** hq, const int32_t** 
   int32_t nfw[3];
   std::memcpy(nfw, p->st + 1, 12);
   if (nfw[2] != 0) {                                              // non-finite input: exact math.Min rules
-    double* Dd = sonar::detail::dtw_pre_enabled(p->dim) ? (double*)dbuf(c, "dtw.Dd", sonar::dtw_cn_bytes(g)) : nullptr;
     if (sonar::launch_dtw(p->dq, p->dr, p->dim, p->band, false, g, nullptr, Dn, E, sync, codes, pl, nullptr, s, nullptr,
-                          Dd, CK))
+                          CK))
       return fail(c, SONAR_ERR_DEVICE, "dtw launch failed");
     HIP_TRY(c, hipMemcpyAsync(p->st, pl, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipMemcpyAsync(p->st + 1, sync, sonar::DTW_SYNC_BYTES, hipMemcpyDeviceToHost, s));

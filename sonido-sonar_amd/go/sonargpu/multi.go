@@ -33,7 +33,10 @@ type PairRecord struct {
 	TemporalOffset, OffsetConfidence, AlignmentSimilarity, AlignmentQuality float64
 	Method                                                                   int
 	CorrOffsetSeconds, DTWDistance, PeakLag                                  float64
-	Err                                                                      error
+	// Redone: the record came from the single-pair path (SONAR_PAIR_REDONE_TIMEOUT /
+	// SONAR_PAIR_REDONE_NONFINITE bits), not from the pair's batch
+	Redone int
+	Err    error
 }
 
 // pairArgs builds the C pointer/length arrays of the pairs' streams, pinning every slice.
@@ -69,7 +72,7 @@ func records(recs []C.sonar_pair_record) []PairRecord {
 			TemporalOffset: float64(r.temporal_offset), OffsetConfidence: float64(r.offset_confidence),
 			AlignmentSimilarity: float64(r.alignment_similarity), AlignmentQuality: float64(r.alignment_quality),
 			Method: int(r.method), CorrOffsetSeconds: float64(r.corr_offset_seconds),
-			DTWDistance: float64(r.dtw_distance), PeakLag: float64(r.peak_lag),
+			DTWDistance: float64(r.dtw_distance), PeakLag: float64(r.peak_lag), Redone: int(r.flags),
 		}
 		if r.status != C.SONAR_OK {
 			out[k].Err = fmt.Errorf("sonargpu: pair %d failed (%d)", k, int(r.status))

@@ -19,6 +19,8 @@ from ._abi import (  # noqa: F401
     FpConfig,
     PairRecord,
     PAIR_FIELDS,
+    PAIR_REDONE_NONFINITE,
+    PAIR_REDONE_TIMEOUT,
     multi_shard,
     WINDOWS,
     abi_version,

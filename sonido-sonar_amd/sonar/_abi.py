@@ -150,10 +150,12 @@ class PairRecord(C.Structure):
     """sonar_pair_record: what ExtractAlignmentFeatures leaves per pair (extractors/alignment.go:139-219)."""
     _fields_ = [(n, C.c_double) for n in ("temporal_offset", "offset_confidence", "alignment_similarity",
                                           "alignment_quality", "method", "corr_offset_seconds", "dtw_distance",
-                                          "peak_lag")] + [("status", C.c_int32), ("reserved", C.c_int32)]
+                                          "peak_lag")] + [("status", C.c_int32), ("flags", C.c_int32)]
 
 
 PAIR_FIELDS = [f for f, _ in PairRecord._fields_[:8]]
+PAIR_REDONE_TIMEOUT = 1     # sonar_pair_record.flags (include/sonar_gpu.h)
+PAIR_REDONE_NONFINITE = 2
 
 _lib = None
 _vp, _d, _i32p, _i64p = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
@@ -317,6 +319,7 @@ def records_dict(recs):
     """sonar_pair_record array -> dict of numpy arrays (PAIR_FIELDS + status)."""
     out = {f: np.array([getattr(r, f) for r in recs]) for f in PAIR_FIELDS}
     out["status"] = np.array([r.status for r in recs], dtype=np.int32)
+    out["flags"] = np.array([r.flags for r in recs], dtype=np.int32)
     return out
 
 

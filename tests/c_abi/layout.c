@@ -120,6 +120,6 @@ int main(void) {
   F(sonar_pair_record, temporal_offset); F(sonar_pair_record, offset_confidence);
   F(sonar_pair_record, alignment_similarity); F(sonar_pair_record, alignment_quality);
   F(sonar_pair_record, method); F(sonar_pair_record, corr_offset_seconds); F(sonar_pair_record, dtw_distance);
-  F(sonar_pair_record, peak_lag); F(sonar_pair_record, status); F(sonar_pair_record, reserved);
+  F(sonar_pair_record, peak_lag); F(sonar_pair_record, status); F(sonar_pair_record, flags);
   return 0;
 }

@@ -4,8 +4,9 @@ record, and the rest of the block and every band below it give up within millise
 pipeline is an error that names its cause, not a hang -- and the context stays usable.
 
 The stall is injected (SONAR_DTW_DBG_STALL=<band>: that band's sweep stops after 1,024 steps
-without publishing more), in the single-DTW path (sonar_dtw), in the batched pair path
-(sonar_align_pairs) and with the 128-row band kernel (SONAR_DTW_BAND2=1)."""
+without publishing more), in the single-DTW path (sonar_dtw) and in the batched pair path
+(sonar_align_pairs), with the retry off (the batch's own diagnosed error) and on (the pair is redone
+on the single-pair path, its record flagged SONAR_PAIR_REDONE_TIMEOUT, the timeout counted)."""
 import time
 
 import numpy as np
@@ -22,9 +23,7 @@ def _seq(n, seed):
     return np.random.default_rng(seed).random((n, 12))
 
 
-@pytest.mark.parametrize("band2", ["0", "1"])
-def test_injected_stall_is_a_diagnosed_error(ctx, monkeypatch, band2):
-    monkeypatch.setenv("SONAR_DTW_BAND2", band2)
+def test_injected_stall_is_a_diagnosed_error(ctx, monkeypatch):
     q, r = _seq(2000, 1), _seq(3000, 2)           # 32 bands of 64 rows
     monkeypatch.setenv("SONAR_DTW_DBG_STALL", "5")
     t0 = time.perf_counter()
@@ -42,9 +41,7 @@ def test_injected_stall_is_a_diagnosed_error(ctx, monkeypatch, band2):
     assert got["distance"] == ref["distance"]
 
 
-@pytest.mark.parametrize("band2", ["0", "1"])
-def test_injected_stall_in_pair_batch_names_the_pair(ctx, monkeypatch, band2):
-    monkeypatch.setenv("SONAR_DTW_BAND2", band2)
+def test_injected_stall_in_pair_batch_names_the_pair(ctx, monkeypatch):
     qs, rs = [], []
     for k in range(3):
         q, r, _ = synth.c5_pair(k, seconds=8.0)    # 1,374 chroma frames: 22 bands
@@ -64,3 +61,28 @@ def test_injected_stall_in_pair_batch_names_the_pair(ctx, monkeypatch, band2):
     monkeypatch.delenv("SONAR_DTW_DBG_STALL")
     got = ctx.align_pairs(qs, rs, max_lag_seconds=3.0, workers=8)
     assert np.all(got["status"] == 0)
+
+
+def test_injected_batch_stall_is_redone_and_flagged(ctx, monkeypatch):
+    """Retry on (the default): a pair whose batched band pipeline stalls (injected into the batch
+    launch only, "b<band>") is redone on the single-pair path -- status 0, the record equal to the
+    unbatched path's, flagged SONAR_PAIR_REDONE_TIMEOUT -- and the timeout is counted."""
+    qs, rs = [], []
+    for k in range(3):
+        q, r, _ = synth.c5_pair(k, seconds=8.0)
+        qs.append(q)
+        rs.append(r)
+    monkeypatch.setenv("SONAR_PAIR_BATCH", "0")
+    ref = ctx.align_pairs(qs, rs, max_lag_seconds=3.0, workers=8)
+    monkeypatch.delenv("SONAR_PAIR_BATCH")
+    ctx.dtw_counters(reset=True)
+    monkeypatch.setenv("SONAR_DTW_DBG_STALL", "b4")
+    monkeypatch.setenv("SONAR_PAIR_STREAMS", "1")
+    got = ctx.align_pairs(qs, rs, max_lag_seconds=3.0, workers=8)
+    monkeypatch.delenv("SONAR_DTW_DBG_STALL")
+    assert np.all(got["status"] == 0)
+    assert np.all(got["flags"] == sonar.PAIR_REDONE_TIMEOUT), got["flags"]
+    assert ctx.dtw_counters(reset=True)["dtw_timeouts"] >= 1
+    for f in sonar.PAIR_FIELDS:
+        a, b = np.asarray(got[f], float), np.asarray(ref[f], float)
+        assert np.array_equal(a, b, equal_nan=True), f

@@ -4,9 +4,6 @@ of analyzers/spectral.go:385-545 + spectral/mfcc.go:113-245) on the configuratio
 route to it (f32 PCM, f32 output, MFCC only, W = 1024), and against the general fused
 kernel (SONAR_FP_GENERIC) on the same input.
 
-Both headline kernels are covered: mfcc_pair_kernel (the default) and mfcc_pair2_kernel (two
-pairs per wave, SONAR_MFCC_PAIR2=1).
-
 Tolerance (north_star: float features within 1e-4 relative): 1e-4 of the frame's MFCC
 L2 norm -- the near-zero coefficients c1..c12 carry rounding of the large c0, so a
 per-coefficient relative bound is not meaningful in f32."""
@@ -33,15 +30,6 @@ def _ref(x, H=256, sr=44100, nm=40, nc=13, power=False, win="hann"):
 
 
 _EXPECT = {"kernel": "mfcc_pair_kernel"}
-
-
-@pytest.fixture(params=["mfcc_pair_kernel", "mfcc_pair2_kernel"], autouse=True)
-def pair_kernel(request, monkeypatch):
-    """every test runs on both headline kernels: the one-pair default and the two-pairs-per-wave
-    variant (SONAR_MFCC_PAIR2=1)"""
-    monkeypatch.setenv("SONAR_MFCC_PAIR2", "1" if request.param == "mfcc_pair2_kernel" else "0")
-    _EXPECT["kernel"] = request.param
-    return request.param
 
 
 def _fp(ctx, x, cfg, kernel=None):

@@ -1,11 +1,10 @@
 """The batched pair path of sonar_align_pairs (one band-kernel launch over a batch's chroma DTWs,
 batched walk / path decode, one host sync per batch) against the unbatched path
-(SONAR_PAIR_BATCH=0: one sonar_align_pair_device per pair), and the opt-in precomputed-distance
-DTW (SONAR_DTW_PRE=1: dtw_dist_kernel + the 4-wave band kernel) against the default band kernel,
-and the DTW kernel variants (one-wave batch default, 8-wave band, 128-row) against each other.
-Pairs are independent and both paths run the same arithmetic, so records must be identical
-(NaN-aware), for pairs of different lengths, any batch cut, and a pair whose chroma is not finite
-(the batch redoes it through the exact math.Min path)."""
+(SONAR_PAIR_BATCH=0: one sonar_align_pair_device per pair).  Pairs are independent and both paths
+run the same arithmetic, so records must be identical (NaN-aware), for pairs of different lengths,
+any batch cut, and a pair whose chroma is not finite (the batch redoes it through the exact
+math.Min path and flags the record SONAR_PAIR_REDONE_NONFINITE).  Every batched run here also
+checks that no band pipeline timed out (the retry would hide it)."""
 import numpy as np
 import pytest
 
@@ -33,10 +32,14 @@ def mixed_pairs():
 
 
 def _run(ctx, monkeypatch, qs, rs, **env):
+    env.setdefault("SONAR_PAIR_RETRY", 0)     # a timed-out pipeline is an error here, never a silent redo
     for k, v in env.items():
         monkeypatch.setenv(k, str(v))
     try:
-        return ctx.align_pairs(qs, rs, max_lag_seconds=4.0, workers=4)
+        ctx.dtw_counters(reset=True)
+        out = ctx.align_pairs(qs, rs, max_lag_seconds=4.0, workers=4)
+        assert ctx.dtw_counters(reset=True)["dtw_timeouts"] == 0
+        return out
     finally:
         for k in env:
             monkeypatch.delenv(k)
@@ -70,60 +73,9 @@ def test_batched_nonfinite_pair_redone_exactly(ctx, monkeypatch, mixed_pairs):
     assert np.array_equal(got["status"], ref["status"])
     for f in sonar.PAIR_FIELDS:
         assert _same(got[f], ref[f]), f
-
-
-@pytest.mark.parametrize("nq,nr,band", [(1000, 1000, -1), (700, 1333, -1), (1500, 960, 200), (63, 65, -1),
-                                        (4100, 3900, -1)])
-def test_precomputed_distance_dtw_bit_exact(ctx, monkeypatch, nq, nr, band):
-    rng = np.random.default_rng(nq + nr)
-    q = rng.random((nq, 12))
-    r = np.roll(rng.random((nr, 12)), 3, axis=0)
-    ref = ctx.dtw(q, r, band=band)
-    monkeypatch.setenv("SONAR_DTW_PRE", "1")
-    got = ctx.dtw(q, r, band=band)
-    monkeypatch.delenv("SONAR_DTW_PRE")
-    assert _same(got["distance"], ref["distance"])
-    for k in ("path_q", "path_r", "path_cost"):   # (banded: Inf - Inf costs are NaN in both)
-        assert _same(got[k], ref[k]), k
-
-
-def test_precomputed_distance_pairs(ctx, monkeypatch, mixed_pairs):
-    qs, rs = mixed_pairs
-    ref = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2)
-    got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2, SONAR_DTW_PRE=1)
-    for f in sonar.PAIR_FIELDS:
-        assert _same(got[f], ref[f]), f
-
-
-@pytest.mark.parametrize("env", [dict(SONAR_DTW_WAVE=1), dict(SONAR_DTW_BAND2=1), dict(SONAR_DTW_WAVE=1, SONAR_DTW_LEAN=1),
-                                 dict(SONAR_DTW_WAVE=1, SONAR_DTW_IL=1)])
-def test_batch_dtw_kernels_agree(ctx, monkeypatch, mixed_pairs, env):
-    """The batch's default 8-wave band kernel (dtw_band_kernel) against the one-wave kernel
-    (SONAR_DTW_WAVE=1) in its three schedules (pipelined; SONAR_DTW_LEAN=1 without cross-chunk
-    pipelining; SONAR_DTW_IL=1 with the next chunk's sums fenced between the steps) and the
-    128-row kernel (SONAR_DTW_BAND2=1): identical records."""
-    qs, rs = mixed_pairs
-    ref = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2)
-    got = _run(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=2, **env)
-    assert np.all(ref["status"] == 0) and np.all(got["status"] == 0)
-    for f in sonar.PAIR_FIELDS:
-        assert _same(got[f], ref[f]), f
-
-
-@pytest.mark.parametrize("nq,nr", [(1000, 1000), (700, 1333), (63, 65), (4100, 3900), (64, 5000), (3000, 64)])
-def test_wave_kernel_single_dtw_bit_exact(ctx, monkeypatch, nq, nr):
-    """dtw_wave_kernel on a single DTW (SONAR_DTW_WAVE=1) against the band kernel: path, path
-    costs and distance bit-exact, ragged last bands and one-band / one-chunk shapes included."""
-    rng = np.random.default_rng(3 * nq + nr)
-    q = rng.random((nq, 12))
-    r = np.roll(rng.random((nr, 12)), 5, axis=0)
-    ref = ctx.dtw(q, r)
-    monkeypatch.setenv("SONAR_DTW_WAVE", "1")
-    got = ctx.dtw(q, r)
-    monkeypatch.delenv("SONAR_DTW_WAVE")
-    assert got["distance"] == ref["distance"]
-    for k in ("path_q", "path_r", "path_cost"):
-        assert np.array_equal(got[k], ref[k]), k
+    flagged = np.nonzero(got["flags"])[0].tolist()
+    assert flagged == [1, 3], flagged
+    assert np.all(got["flags"][[1, 3]] == sonar.PAIR_REDONE_NONFINITE)
 
 
 def test_trim_releases_and_reallocates(ctx, monkeypatch, mixed_pairs):
@@ -154,12 +106,17 @@ def device_pairs():
 
 
 def _run_dev(ctx, monkeypatch, qs, rs, **env):
+    env.setdefault("SONAR_PAIR_RETRY", 0)
     for k, v in env.items():
         monkeypatch.setenv(k, str(v))
     try:
-        return ctx.align_pairs([q.data_ptr() for q in qs], [r.data_ptr() for r in rs],
-                               nq=[q.numel() for q in qs], nr=[r.numel() for r in rs], max_lag_seconds=4.0,
-                               workers=8, device_ptrs=True)
+        ctx.dtw_counters(reset=True)
+        out = ctx.align_pairs([q.data_ptr() for q in qs], [r.data_ptr() for r in rs],
+                              nq=[q.numel() for q in qs], nr=[r.numel() for r in rs], max_lag_seconds=4.0,
+                              workers=8, device_ptrs=True)
+        assert ctx.dtw_counters(reset=True)["dtw_timeouts"] == 0
+        assert np.all(out["flags"] == 0)
+        return out
     finally:
         for k in env:
             monkeypatch.delenv(k)
