@@ -418,9 +418,11 @@ const char* sonar_multi_last_error(const sonar_multi* m);
 int32_t sonar_multi_size(const sonar_multi* m);
 sonar_ctx* sonar_multi_ctx(sonar_multi* m, int32_t rank);   /* the rank's context (do not destroy) */
 
-/* Frame shard g of G over n samples at W/H: frames [f0, f1) = [g F / G, (g+1) F / G) with
- * F = sonar_stft_frames(n, W, H), and the samples they read [s0, s1) = [f0 H, (f1-1) H + W)
- * (empty shard: f0 == f1, s0 == s1).  Pure arithmetic, the same on every host. */
+/* Frame shard g of G over n samples at W/H: frames [f0, f1) = [e(g), e(g+1)) with
+ * e(k) = floor(k F / G) rounded down to even (e(G) = F), F = sonar_stft_frames(n, W, H), and the
+ * samples they read [s0, s1) = [f0 H, (f1-1) H + W) (empty shard: f0 == f1, s0 == s1).  Even
+ * boundaries keep the headline kernel's frame pairs, so the shards reassemble bit-identically to
+ * the unsharded call.  Pure arithmetic, the same on every host. */
 int sonar_multi_shard(int64_t n, int32_t window_size, int32_t hop_size, int32_t n_shards, int32_t shard,
                       int64_t* f0, int64_t* f1, int64_t* s0, int64_t* s1);
 

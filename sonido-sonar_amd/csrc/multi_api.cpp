@@ -586,8 +586,11 @@ int sonar_multi_shard(int64_t n, int32_t W, int32_t H, int32_t G, int32_t g, int
   if (W <= 0 || H <= 0 || G <= 0 || g < 0 || g >= G || !f0 || !f1 || !s0 || !s1) return SONAR_ERR_INVALID;
   const int64_t F = sonar_stft_frames(n, W, H);
   if (F <= 0) return SONAR_ERR_TOO_SHORT;
-  *f0 = F * g / G;
-  *f1 = F * (g + 1) / G;
+  // every inner boundary even: a shard's frame pairs (mfcc_pair_kernel transforms frames 2p, 2p+1
+  // as one complex FFT) are the unsharded call's pairs, so shards reassemble bit-identically
+  auto edge = [&](int64_t k) { return k >= G ? F : ((F * k / G) & ~(int64_t)1); };
+  *f0 = edge(g);
+  *f1 = edge(g + 1);
   if (*f1 <= *f0) { *s0 = *s1 = (*f0) * H; return SONAR_OK; }
   *s0 = (*f0) * H;
   *s1 = std::min<int64_t>((*f1 - 1) * H + W, n);   // a lone frame of a signal shorter than W reads n samples

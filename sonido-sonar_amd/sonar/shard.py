@@ -30,7 +30,12 @@ def stft_frames(n: int, W: int, H: int) -> int:
 
 
 def frame_range(F: int, world: int, rank: int) -> tuple[int, int]:
-    return F * rank // world, F * (rank + 1) // world
+    """Frames [f0, f1) of `rank`: contiguous, covering [0, F), every boundary inside even, so a
+    shard's frame pairs (the headline kernel transforms frames 2p, 2p+1 as one complex FFT) are
+    the unsharded run's pairs and the gathered timeline is bit-identical to it (sonar_multi_shard)."""
+    def edge(g):
+        return F if g >= world else (F * g // world) & ~1
+    return edge(rank), edge(rank + 1)
 
 
 def sample_span(f0: int, f1: int, W: int, H: int) -> tuple[int, int]:

@@ -2,9 +2,10 @@
 
 * ``assert_rel``: per-element relative error with an explicit floor, so small-valued elements
   are checked too (|got - ref| <= rtol * max(|ref|, floor)).
-* ``assert_mfcc``: MFCC rows; every coefficient with |ref| > 1e-3 * ||row|| within ``rtol`` of
-  itself, and every coefficient within ``rtol`` of the row norm (near-zero coefficients are
-  rounding noise relative to themselves, SURVEY.md §7 "fp32 vs 1e-4 relative").
+* ``assert_mfcc``: MFCC rows; every coefficient within ``rtol`` of the row norm, and per
+  coefficient relative to itself in tiers (f32: 1e-4 for |c| > 0.1 ||row||, 1e-3 for
+  |c| > 0.01 ||row||, 1e-2 for |c| > 1e-3 ||row||; f64: at most 1e-6).  Smaller coefficients are
+  rounding noise relative to themselves (SURVEY.md §7 "fp32 vs 1e-4 relative").
 * ``rolloff_borderline`` / ``assert_rolloff``: the rolloff bin is an index and must be exact.
   The kernel reproduces Go's sequential chains (spectral_rolloff.go:29-49) on ITS magnitudes;
   those differ from the oracle's by FFT rounding, so a mismatch is allowed only on a frame whose
@@ -43,21 +44,39 @@ def mfcc_errors(got, ref):
     return float(e_row.max()), float(e_coef.max()), bad
 
 
+# per-coefficient tiers of assert_mfcc: (coefficient floor as a fraction of the row norm, bound
+# as a multiple of rtol).  f32 (rtol 1e-4, the north star's "float features within 1e-4
+# relative"): |c| > 0.1 ||row|| within 1e-4 of itself, |c| > 0.01 ||row|| within 1e-3, |c| > 1e-3
+# ||row|| within 1e-2 (measured worst cases over the whole hour: 1.6e-5, ~1.1e-4, 6.7e-4).
+MFCC_TIERS_F32 = ((1e-1, 1.0), (1e-2, 10.0), (1e-3, 100.0))
+
+
+def mfcc_tier_errors(got, ref):
+    """{floor: max relative error of the coefficients with |ref| > floor * ||row||}"""
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    norms = np.linalg.norm(ref, axis=1)[:, None]
+    norms = np.where(norms == 0, 1.0, norms)
+    out = {}
+    for fl, _ in MFCC_TIERS_F32:
+        big = np.abs(ref) > fl * norms
+        out[fl] = float(np.max(np.abs(got - ref)[big] / np.abs(ref)[big])) if big.any() else 0.0
+    return out
+
+
 def assert_mfcc(got, ref, rtol):
+    """MFCC rows against the oracle: every coefficient within rtol of the row's L2 norm, and per
+    coefficient relative to itself by tiers.  rtol >= 1e-5 (f32 kernels): MFCC_TIERS_F32.
+    rtol < 1e-5 (f64 kernels): 10 / 100 / 1000 x rtol, capped at 1e-6 for every tier."""
     got, ref = np.asarray(got), np.asarray(ref)
     assert got.shape == ref.shape, (got.shape, ref.shape)
     norms = np.linalg.norm(ref, axis=1)[:, None]
     norms = np.where(norms == 0, 1.0, norms)
     e_row = np.max(np.abs(got - ref) / norms)
     assert e_row < rtol, ("row-norm", e_row)
-    big = np.abs(ref) > 1e-3 * norms
-    if big.any():
-        e_coef = np.max(np.abs(got - ref)[big] / np.abs(ref)[big])
-        # a coefficient at 1e-3 of its row carries the row's absolute rounding: 1e3 * rtol worst case
-        assert e_coef < rtol * 1e3, ("per-coefficient", e_coef)
-        strong = np.abs(ref) > 1e-1 * norms
-        e_strong = np.max(np.abs(got - ref)[strong] / np.abs(ref)[strong])
-        assert e_strong < rtol * 10, ("per-coefficient (|c| > 0.1 ||row||)", e_strong)
+    errs = mfcc_tier_errors(got, ref)
+    for (fl, mult), f64mult in zip(MFCC_TIERS_F32, (10.0, 100.0, 1000.0)):
+        bound = rtol * mult if rtol >= 1e-5 else min(rtol * f64mult, 1e-6)
+        assert errs[fl] <= bound, (f"per-coefficient (|c| > {fl:g} ||row||)", errs[fl], bound)
     return e_row
 
 

@@ -12,7 +12,7 @@ import pytest
 
 import oracle as O
 import sonar
-from parity import assert_rolloff
+from parity import assert_mfcc, assert_rolloff
 from sonar import synth
 
 pytestmark = pytest.mark.gpu
@@ -88,6 +88,7 @@ def test_mfcc_f32_headline_config(ctx):
     assert got.shape == ref.shape == (3442, 13)
     e = np.max(np.abs(got - ref), axis=1) / np.linalg.norm(ref, axis=1)
     assert e.max() < 1e-4, (np.nonzero(~(e < 1e-4))[0][:16].tolist(), int((~(e < 1e-4)).sum()))
+    assert_mfcc(got, ref, 1e-4)                  # + per-coefficient tiers (parity.MFCC_TIERS_F32)
 
 
 def test_mfcc_sample_rate_zero_constant(ctx):
