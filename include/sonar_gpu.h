@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define SONAR_ABI_VERSION 3
+#define SONAR_ABI_VERSION 4
 
 enum {
   SONAR_OK = 0,
@@ -73,7 +73,9 @@ enum {
   SONAR_ERR_EMPTY = -3,        /* "empty signal" / "empty sequences provided"   */
   SONAR_ERR_UNSUPPORTED = -4,  /* configuration not implemented on the GPU path */
   SONAR_ERR_DEVICE = -5,       /* HIP runtime error                             */
-  SONAR_ERR_NOMEM = -6         /* device allocation failed                      */
+  SONAR_ERR_NOMEM = -6,        /* device allocation failed                      */
+  SONAR_ERR_PANIC = -7         /* the Go reference panics on this input (message: Go's runtime
+                                  error text); see the entry for what *out then holds */
 };
 
 /* window types: analyzers.WindowType (fingerprint/analyzers/windowing.go:13-23) */
@@ -342,6 +344,29 @@ void sonar_feature_config_default(sonar_feature_config* cfg);
  * ("is_speech", "voicing_probability", "spectral_tilt", "pause_duration") groups when enabled. */
 int sonar_extract_speech_features(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate,
                                   const sonar_feature_config* cfg, sonar_result** out);
+
+/* NewMusicFeatureExtractor(cfg) + ExtractFeatures(STFT(pcm, W, H), pcm, sample_rate)
+ * (fingerprint/extractors/music.go:70-583).  cfg: sample_rate = FeatureConfig.SampleRate (the
+ * analyzers' and MFCC's rate), window_size / hop_size = FeatureConfig (ShortTimeEnergy frames,
+ * chroma hop), stft_window_size / stft_hop_size / window_type = the spectrogram; sample_rate
+ * (the argument) = SpectrogramResult.SampleRate.  Result arrays: "spectral_centroid" ..
+ * "spectral_slope", "spectral_flux" (F, [0] = 0), "zero_crossing_rate" (F zeros, never filled in
+ * Go), "spectral_contrast" (F x 6), "mfcc" (F x 13 of |X|^4 over 26 mels, F5), "chroma" (F x 12),
+ * "rms_energy", "envelope_shape", "peak_amplitude", "average_amplitude", then "dynamic_range",
+ * "onset_density", "attack_time", "crest_factor", "silence_ratio", "activity_level",
+ * "short_time_energy", "energy_variance", "energy_entropy", "loudness_range",
+ * "low_energy_ratio", "high_energy_ratio" and the harmonic block "pitch_estimate",
+ * "pitch_confidence", "voicing_strength", "harmonic_ratio", "inharmonicity_ratio",
+ * "tonal_centroid" (zero by F7 unless the chroma frame is exactly 1024 samples).
+ * The reference panics in extractTemporalFeatures for every signal of >= 1536 samples
+ * (music.go:403 passes percentiles 10 and 90 where fractions are expected:
+ * "index out of range [10 (L-1)] with length L") and for a signal with no energy frame
+ * (music.go:383: "integer divide by zero").  Then the call returns SONAR_ERR_PANIC with that
+ * text and *out holds the arrays computed before the panic (the spectral group, "mfcc",
+ * "chroma", "rms_energy", and after the division also "envelope_shape" and the amplitudes);
+ * the caller frees it.  float64. */
+int sonar_extract_music_features(sonar_ctx* ctx, const double* pcm, int64_t n, int32_t sample_rate,
+                                 const sonar_feature_config* cfg, sonar_result** out);
 
 /* AudioData{PCM, SampleRate, Metadata.ContentType}.  content_type is the raw
  * metadata string ("music", "news", "talk", ... ; unknown strings -> content

@@ -47,6 +47,7 @@ def lib():
         L.or_mfcc_frames.argtypes = [_d, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
                                      C.c_double, C.c_int, C.c_double, C.c_int, C.c_int, _d]
         L.or_spectral_descriptors.argtypes = [_d, C.c_int64, C.c_int, C.c_int] + [_d] * 9
+        L.or_spectral_contrast.argtypes = [_d, C.c_int64, C.c_int, C.c_int, C.c_int, _d]
         L.or_preemphasis.argtypes = [_d, C.c_int64, C.c_double, _d]
         L.or_dc_removal.argtypes = [_d, C.c_int64, C.c_double, _d]
         L.or_zcr_frames.argtypes = [_d, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, _d]
@@ -462,6 +463,89 @@ def speech_features_reference(pcm, sample_rate, fc):
     lo[:m], hi[:m] = d["low_ratio"][:m], d["high_ratio"][:m]
     out["energy_entropy"], out["low_energy_ratio"], out["high_energy_ratio"] = ent, lo, hi
     return out
+
+
+def spectral_contrast(mag, sample_rate, num_bands=6):
+    """SpectralContrast(sample_rate, num_bands).Compute per magnitude row (spectral_contrast.go:26-185)."""
+    mag = _f64(mag)
+    F, K = mag.shape
+    out = np.zeros((F, num_bands))
+    lib().or_spectral_contrast(_p(mag), F, K, sample_rate, num_bands, _p(out))
+    return out
+
+
+def music_features_reference(pcm, sample_rate, fc):
+    """MusicFeatureExtractor.ExtractFeatures (fingerprint/extractors/music.go:178-583), fp64, composed
+    from the oracle's pieces.  fc: dict(sample_rate, window_size, hop_size, stft_window_size,
+    stft_hop_size).  Returns (features, panic): panic is Go's runtime error text where the reference
+    panics (music.go:383 integer divide by zero with no energy frame; music.go:403 index out of range
+    for >= 2 RMS frames of 1024 / 512, i.e. >= 1536 samples), features then holding what was computed
+    before the panic."""
+    pcm = _f64(pcm)
+    n = len(pcm)
+    csr = fc["sample_rate"]
+    W, H = fc["stft_window_size"], fc["stft_hop_size"]
+    mag = stft_mag(pcm, W, H, nthreads=8)
+    F, K = mag.shape
+    y = preemphasis(dc_removal(pcm, 0.995), 0.95)                       # preprocessAudio (:245-259)
+    out = {}
+    d = spectral_descriptors(mag, csr)                                  # extractSpectralFeatures (:261-302)
+    for k in ["centroid", "rolloff", "bandwidth", "flatness", "crest", "slope"]:
+        out["spectral_" + k] = d[k]
+    flux = np.zeros(F)
+    flux[1:] = d["flux"]
+    out["spectral_flux"] = flux
+    out["zero_crossing_rate"] = np.zeros(F)
+    out["spectral_contrast"] = spectral_contrast(mag, csr, 6)
+    out["mfcc"] = mfcc_frames(mag * mag, csr, n_coef=13, n_mels=26)     # Compute(|X|^2) -> |X|^4 (F5)
+    out["chroma"] = chroma_music(pcm, F, fc["hop_size"], csr)           # (:327-376)
+    rms = short_time_energy(y, fc["window_size"], fc["hop_size"])       # extractTemporalFeatures (:378-458)
+    out["rms_energy"] = rms
+    Fe = len(rms)
+    if Fe == 0:
+        return out, "runtime error: integer divide by zero"
+    fse = n // Fe
+    out["envelope_shape"] = short_time_energy(y, fse, fc["hop_size"])
+    a = np.abs(y)
+    out["peak_amplitude"] = float(a.max())
+    out["average_amplitude"] = float(np.cumsum(a)[-1] / n)             # Go's sequential sum
+    L = (n - 1024) // 512 + 1 if n >= 1024 else 0
+    if L >= 2:
+        return out, f"runtime error: index out of range [{int(10.0 * (L - 1))}] with length {L}"
+    out["dynamic_range"] = 0.0
+    if n <= 512:
+        raise ValueError("temporal feature extraction failed: signal too short for given window size and hop size")
+    out["onset_density"] = 0.0
+    out["attack_time"] = np.zeros(0)
+    crest = np.zeros(Fe)
+    for i in range(Fe):
+        pk = a[i * fse: min(i * fse + fse, n)].max()
+        if rms[i] > 0:
+            crest[i] = pk / rms[i]
+    out["crest_factor"] = crest
+    out["silence_ratio"] = 0.0                                          # RMS < -40 never holds
+    out["activity_level"] = np.ones(Fe)
+    out["short_time_energy"] = rms                                      # extractEnergyFeatures (:460-525)
+    out["energy_variance"] = float(np.var(rms, ddof=1)) if Fe >= 2 else 0.0
+    out["energy_entropy"] = np.where(rms > 0, -rms * np.log2(np.where(rms > 0, rms, 1.0)), 0.0)
+    pos = rms[rms > 0]
+    out["loudness_range"] = float(20 * np.log10(rms.max() / pos.min())) if len(pos) else 0.0
+    e = mag * mag
+    lo, hi = np.zeros(F), np.zeros(F)
+    for t in range(F):
+        tot = np.cumsum(e[t])[-1]
+        l_ = np.cumsum(e[t, : K // 4])[-1] if K // 4 else 0.0
+        h_ = np.cumsum(e[t, 3 * K // 4 + 1:])[-1] if K - (3 * K // 4 + 1) > 0 else 0.0
+        if tot > 0:
+            lo[t], hi[t] = l_ / tot, h_ / tot
+    out["low_energy_ratio"], out["high_energy_ratio"] = lo, hi
+    pe, pc, vs = np.zeros(F), np.zeros(F), np.zeros(F)                  # extractHarmonicFeatures (:528-583, F7)
+    if n // F == 1024:
+        pe[0], pc[0], vs[0] = YinTrack().step(*yin_raw(y[:1024], csr)[:2])
+    out["pitch_estimate"], out["pitch_confidence"], out["voicing_strength"] = pe, pc, vs
+    out["harmonic_ratio"], out["inharmonicity_ratio"] = np.zeros(F), np.zeros(F)
+    out["tonal_centroid"] = d["centroid"] * vs
+    return out, None
 
 
 def align_features_reference(qe, re_, qc, rc, q_pcm_len, r_pcm_len, sample_rate, feature_sample_rate, hop,

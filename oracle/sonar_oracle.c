@@ -6,6 +6,7 @@
  */
 #include "sonar_oracle.h"
 #include <math.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
@@ -1211,4 +1212,60 @@ int64_t or_formant_frames(const double* sig, int64_t n, int sr, int frame_size, 
     or_formant_frame(sig + i, frame_size, sr, recs + 24 * f, coeffs ? coeffs + (p + 1) * f : NULL,
                      refl ? refl + p * f : NULL);
   return f;
+}
+
+/* SpectralContrast(sample_rate, num_bands).Compute per row (algorithms/spectral/spectral_contrast.go:
+ * 26-137, initializeBands :140-185): log-spaced band edges from 200 Hz to Nyquist, per band |X|^2,
+ * insertion sort ascending, mean of the bottom and top 20 % (at least one value each) in sorted
+ * order, 10 log10(peak / valley) (valley <= 0 -> 1e-10, peak <= 0 -> 0).  out is F x num_bands. */
+static int64_t or_go_int(double x) {   /* Go int(float64) on amd64: NaN / out of range -> MinInt64 */
+    if (!(x >= -9.2233720368547758e18 && x < 9.2233720368547758e18)) return INT64_MIN;
+    return (int64_t)x;
+}
+void or_spectral_contrast(const double* mag, int64_t F, int K, int sr, int nb, double* out) {
+    int* edges = malloc(sizeof(int) * (nb + 1));
+    const double nyq = (double)sr / 2.0;
+    double maxf = nyq;
+    if (maxf <= 200.0) maxf = 400.0;
+    const double lmin = log10(200.0), lmax = log10(maxf), step = (lmax - lmin) / (double)nb;
+    for (int i = 0; i <= nb; i++) {
+        int64_t b = or_go_int(pow(10.0, lmin + (double)i * step) * (double)(K - 1) / nyq);
+        if (b >= K) b = K - 1;
+        if (b < 0) b = 0;
+        edges[i] = (int)b;
+    }
+    for (int i = 1; i <= nb; i++) if (edges[i] <= edges[i - 1]) edges[i] = edges[i - 1] + 1;
+    double* buf = malloc(sizeof(double) * (K > 0 ? K : 1));
+    for (int64_t t = 0; t < F; t++) {
+        const double* s = mag + t * K;
+        for (int b = 0; b < nb; b++) {
+            const int st = edges[b];
+            int en = edges[b + 1];
+            if (en > K) en = K;
+            double c = 0.0;
+            if (st < en) {
+                const int L = en - st;
+                for (int i = 0; i < L; i++) buf[i] = s[st + i] * s[st + i];
+                for (int i = 1; i < L; i++) {                 /* insertion sort, :83-92 */
+                    const double key = buf[i];
+                    int j = i - 1;
+                    while (j >= 0 && buf[j] > key) { buf[j + 1] = buf[j]; j--; }
+                    buf[j + 1] = key;
+                }
+                int vc = (int)(0.2 * (double)L), pc = (int)(0.2 * (double)L);
+                if (vc == 0) vc = 1;
+                if (pc == 0) pc = 1;
+                double valley = 0.0, peak = 0.0;
+                for (int i = 0; i < vc; i++) valley += buf[i];
+                valley /= (double)vc;
+                for (int i = L - pc; i < L; i++) peak += buf[i];
+                peak /= (double)pc;
+                if (valley <= 0) valley = 1e-10;
+                c = peak <= 0 ? 0.0 : 10.0 * log10(peak / valley);
+            }
+            out[t * nb + b] = c;
+        }
+    }
+    free(buf);
+    free(edges);
 }

@@ -64,6 +64,8 @@ int    or_detect_from_audio(const double* pcm, int64_t n, int sr, double thr, do
 int64_t or_formant_frames(const double* sig, int64_t n, int sample_rate, int frame_size, int hop, double* recs,
                           double* coeffs, double* refl);
 
+/* SpectralContrast.Compute per row (spectral_contrast.go:26-185), F x nb */
+void or_spectral_contrast(const double* mag, int64_t F, int K, int sr, int nb, double* out);
 #ifdef __cplusplus
 }
 #endif

@@ -273,6 +273,16 @@ int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 // (nq + nr) * dim
 int launch_nonfinite_batch(const DtwArgs* dargs, int n, int64_t max_elems, hipStream_t s);
 
+// MusicFeatureExtractor per-frame parts (music_kernels.hip): spectral contrast over the
+// nbands bands [edges[b], edges[b+1]) of each magnitude row (contrast F x nbands) and the music
+// low / high band energy ratios (nullable); maxband = the widest band
+int launch_music_frames(const double* mag, int64_t F, int K, const int* edges, int nbands, int maxband,
+                        double* contrast, double* lo_ratio, double* hi_ratio, hipStream_t s);
+// out[0] = max |y|, out[1] = sum |y| in sample order (one wave)
+int launch_abs_stats(const double* y, int64_t n, double* out, hipStream_t s);
+// out[i] = max |y| over frame i = [i fs, min(i fs + fs, n))
+int launch_frame_peak(const double* y, int64_t n, int64_t frames, int64_t fs, double* out, hipStream_t s);
+
 // LPC formants (lpc_kernels.hip): one block per frame; out is sonar_formant_frame[frames]
 int launch_formants(const double* pcm, int64_t frames, int64_t hop, int W, int p, int sr, int frame_ok_len,
                     const double* ham, sonar_formant_frame* out, double* coeffs, double* refl, hipStream_t s);

@@ -43,6 +43,8 @@ var (
 	ErrUnsupported = errors.New("sonargpu: unsupported configuration")
 	ErrDevice      = errors.New("sonargpu: HIP runtime error")
 	ErrNoMem       = errors.New("sonargpu: device allocation failed")
+	// ErrPanic: the Go reference panics on this input; the message is the runtime error text
+	ErrPanic = errors.New("sonargpu: the reference panics on this input")
 )
 
 // Precision of the device arithmetic.
@@ -98,6 +100,8 @@ func (x *Context) err(rc C.int) error {
 		base = ErrDevice
 	case C.SONAR_ERR_NOMEM:
 		base = ErrNoMem
+	case C.SONAR_ERR_PANIC:
+		base = ErrPanic
 	default:
 		base = ErrInvalid
 	}
@@ -330,6 +334,28 @@ func (x *Context) ExtractSpeech(pcm []float64, sampleRate, stftWindow, stftHop i
 		return nil, x.err(rc)
 	}
 	return x.collect(res), nil
+}
+
+// ExtractMusic = NewMusicFeatureExtractor(&cfg).ExtractFeatures(STFT(pcm, W, H), pcm, sampleRate)
+// (fingerprint/extractors/music.go:70-583).  Where the reference panics (every signal of 1,536
+// samples or more, music.go:403; no energy frame, :383) the error wraps ErrPanic with Go's
+// runtime message, and the returned Result holds the arrays computed before that point.  A
+// drop-in that must keep the reference's behaviour exactly calls panic(err) there.
+func (x *Context) ExtractMusic(pcm []float64, sampleRate, stftWindow, stftHop int, cfg FeatureConfig) (*Result, error) {
+	var fc C.sonar_feature_config
+	C.sonar_feature_config_default(&fc)
+	fc.sample_rate, fc.window_size, fc.hop_size = C.int32_t(cfg.SampleRate), C.int32_t(cfg.WindowSize), C.int32_t(cfg.HopSize)
+	fc.stft_window_size, fc.stft_hop_size, fc.precision = C.int32_t(stftWindow), C.int32_t(stftHop), C.int32_t(cfg.Precision)
+	var res *C.sonar_result
+	rc := C.sonar_extract_music_features(x.c, f64p(pcm), C.int64_t(len(pcm)), C.int32_t(sampleRate), &fc, &res)
+	var partial *Result
+	if res != nil {
+		partial = x.collect(res)
+	}
+	if rc != C.SONAR_OK {
+		return partial, x.err(rc)
+	}
+	return partial, nil
 }
 
 // AlignFeatures = AlignmentExtractor.ExtractAlignmentFeatures on the energy envelopes

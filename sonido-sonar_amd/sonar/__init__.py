@@ -42,5 +42,7 @@ from ._abi import (  # noqa: F401
     INGEST_DEVICE_CONVERT,
     INGEST_HOST_CONVERT,
     ERR_EMPTY,
+    ERR_TOO_SHORT,
+    ERR_PANIC,
     EXPORTED_SYMBOLS,
 )

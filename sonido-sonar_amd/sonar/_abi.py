@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("SONAR_LIB") or os.path.join(_PKG, "lib", "libsonar_gp
 HEADER = os.path.join(_REPO, "include", "sonar_gpu.h")
 
 OK, ERR_INVALID, ERR_TOO_SHORT, ERR_EMPTY, ERR_UNSUPPORTED, ERR_DEVICE, ERR_NOMEM = 0, -1, -2, -3, -4, -5, -6
+ERR_PANIC = -7          # SONAR_ERR_PANIC: the Go reference panics on this input (message: its runtime error)
 FP_MFCC, FP_MAGNITUDE, FP_SPECTRAL, FP_ZCR, FP_ENERGY, FP_COMPLEX, FP_PHASE = 1, 2, 4, 8, 16, 32, 64
 FP_GENERIC = 1 << 30   # force the general fused kernel (A/B checks of the f32 MFCC path)
 F32, F64 = 0, 1
@@ -213,6 +214,9 @@ def lib():
     L.sonar_feature_config_default.restype = None
     L.sonar_extract_speech_features.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(FeatureConfig),
                                                 C.POINTER(_vp)]
+    if hasattr(L, "sonar_extract_music_features"):
+        L.sonar_extract_music_features.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(FeatureConfig),
+                                                   C.POINTER(_vp)]
     L.sonar_align_features.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, _vp, C.c_int64, _vp, C.c_int64,
                                        C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                        C.c_double, C.POINTER(_vp)]
@@ -678,6 +682,22 @@ class Context:
         self._check(self._L.sonar_extract_speech_features(self._h, _ptr(pcm) if len(pcm) else None, len(pcm),
                                                           sample_rate, C.byref(cfg), C.byref(h)))
         return self._result(h)
+
+    def extract_music_features(self, pcm, sample_rate, cfg: FeatureConfig = None):
+        """sonar_extract_music_features: MusicFeatureExtractor.ExtractFeatures as a dict of arrays.
+        Where the Go reference panics (SONAR_ERR_PANIC) this raises SonarError whose .partial holds
+        the arrays computed before the panic."""
+        pcm = _f64(pcm)
+        cfg = cfg or self.feature_config()
+        h = C.c_void_p()
+        rc = self._L.sonar_extract_music_features(self._h, _ptr(pcm) if len(pcm) else None, len(pcm), sample_rate,
+                                                  C.byref(cfg), C.byref(h))
+        partial = self._result(h) if h.value else None
+        if rc != OK:
+            err = SonarError(rc, self._L.sonar_last_error(self._h).decode())
+            err.partial = partial
+            raise err
+        return partial
 
     def align_features(self, q_energy, r_energy, q_chroma=None, r_chroma=None, q_pcm_len=0, r_pcm_len=0,
                        sample_rate=44100, feature_sample_rate=44100, hop_size=256, window_size=1024,

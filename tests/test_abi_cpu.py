@@ -15,7 +15,7 @@ def test_library_exports_header_symbols():
 
 
 def test_abi_version_and_sizes():
-    assert sonar.abi_version() == 3
+    assert sonar.abi_version() == 4
     assert sonar.stft_frames(441000, 1024, 256) == 1719
     assert sonar.stft_frames(1000, 1024, 256) == 1        # Go truncating division
     assert sonar.stft_frames(0, 1024, 256) < 0

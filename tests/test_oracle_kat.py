@@ -168,3 +168,22 @@ def test_bytes_to_float64_kat():
     got = O.bytes_to_float64(data)
     assert got.tolist() == [1.0, -2.0, 3.141592653589793]
     assert O.bytes_to_float64(b"") is None and O.bytes_to_float64(b"\x00" * 7) is None
+
+
+def test_spectral_contrast_known_answers():
+    """SpectralContrast (spectral_contrast.go:26-185): a flat spectrum has 0 dB in every band; a band
+    whose top 20 % of power sits 100x above the rest reads 20 dB; sr = 0 puts the six bands on
+    bins [0,1), [1,2), ... (Go's int(+Inf) -> MinInt64 -> 0, then the monotonic fix-up)."""
+    K = 513
+    flat = np.ones((2, K))
+    assert np.allclose(O.spectral_contrast(flat, 44100), 0.0, atol=0)
+    mag = np.ones((1, K))
+    c0 = O.spectral_contrast(mag, 44100)
+    # band 5 = bins [234, 512): 278 values, top int(0.2 * 278) = 55 of them at power 100
+    mag[0, 512 - 55:512] = 10.0
+    c = O.spectral_contrast(mag, 44100)
+    assert c[0, 5] == pytest.approx(20.0, abs=1e-12) and np.array_equal(c[0, :5], c0[0, :5])
+    z = np.abs(np.random.default_rng(0).standard_normal((3, K))) + 0.1
+    cz = O.spectral_contrast(z, 0)
+    # bands of one bin each: bottom and top 20 % are that bin -> 0 dB
+    assert np.allclose(cz, 0.0, atol=1e-12)
