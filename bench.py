@@ -384,6 +384,33 @@ def bench_dtw(ctx, n, steps, parity=False):
     return out
 
 
+def load_c5_families():
+    """The newest committed profiles/*_c5_families.json (tools/c5_families.py over a rocprofv3
+    kernel trace of a C5 run): each kernel family's share of the summed GPU kernel time."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c5_families.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        return {"source": os.path.relpath(path, ROOT), "note": d.get("note", ""),
+                "shares": {k: round(v["share"], 4) for k, v in d["families"].items()},
+                "total_kernel_ms": d["total_kernel_ms"]}
+    return None
+
+
+def c5_roofline(P, dt, samples_per_pair, F):
+    """C5's HBM roof (the path is far below it: the bound is the DTW wavefront chains and the
+    latency-bound feature kernels).  Algorithmic bytes per pair: both
+    streams' f64 PCM read once + the chroma DTW's F x F cells at the checkpoint mode's 0.625 B/cell
+    (bench_dtw); achieved = pairs/s x that; the kernel families' GPU-time shares come from the
+    newest committed profile."""
+    per_pair = samples_per_pair * 8 + DTW_BYTES_PER_CELL * F * F
+    achieved = P * per_pair / dt / 1e9
+    return {"bound": "wavefront", "unit": "GB/s", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "frac": achieved / HBM_PEAK_GBS, "alg_bytes_per_pair": per_pair,
+            "alg_bytes_breakdown": {"pcm_f64": samples_per_pair * 8, "dtw_cells": F * F,
+                                    "dtw_bytes_per_cell": DTW_BYTES_PER_CELL},
+            "kernel_families": load_c5_families()}
+
+
 def bench_c5(args, world, rank, dev, ctx):
     """BASELINE config C5 (path B): P stream pairs sharded over the ranks by contiguous pair ranges
     (sonar/pairs.py), each pair through the music-extractor energy + chroma and
@@ -440,6 +467,7 @@ def bench_c5(args, world, rank, dev, ctx):
     ok = np.minimum(np.abs(allrec[:, ipl] - lag_frames), np.abs(allrec[:, ipl] + lag_frames)) <= 1.5
     F = int((args.c5_seconds * SR - W) // H + 1)
     return {"c5_pairs_per_s": P / dt, "c5_ms": dt * 1e3, "c5_reps": len(dts),
+            "c5_roofline": c5_roofline(P, dt, float(np.mean(nq) + np.mean(nr)), F),
             "c5_pairs_per_s_spread": [P / max(dts), P / min(dts)],
             "c5_frames_per_s": 2 * P * F / dt, "c5_frames_note": "both streams' STFT frames of every pair (BASELINE configs[4])",
             "c5_pairs": P, "c5_seconds_per_stream": args.c5_seconds,

@@ -498,6 +498,9 @@ def music_features_reference(pcm, sample_rate, fc):
     out["zero_crossing_rate"] = np.zeros(F)
     out["spectral_contrast"] = spectral_contrast(mag, csr, 6)
     out["mfcc"] = mfcc_frames(mag * mag, csr, n_coef=13, n_mels=26)     # Compute(|X|^2) -> |X|^4 (F5)
+    if fc["hop_size"] <= 0:                                             # stft.go:54-56 via :358-361
+        raise ValueError("chroma feature extraction failed: chroma computation failed at frame 0: "
+                         "hop size must be positive")
     out["chroma"] = chroma_music(pcm, F, fc["hop_size"], csr)           # (:327-376)
     rms = short_time_energy(y, fc["window_size"], fc["hop_size"])       # extractTemporalFeatures (:378-458)
     out["rms_energy"] = rms

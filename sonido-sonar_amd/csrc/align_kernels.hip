@@ -1765,11 +1765,20 @@ __global__ void nonfinite_kernel(const double* x, int64_t n, int32_t* flag) {
 
 // the probe over both sequences of every DTW of a batch (blockIdx.y = the DTW): one launch per
 // batch instead of two per pair on the batch's stream
+// Also fills the DTW's band-edge rows E with the sentinel the band kernel polls for (what a
+// hipMemsetD32Async per batch did before: one launch fewer per batch).  Same stream, earlier
+// kernel: the stores are visible to the band kernel's sc1 polls.
 __global__ void nonfinite_batch_kernel(const DtwArgs* args) {
   const DtwArgs a = load_args_uniform(args + blockIdx.y);
   const int64_t nqe = a.nq * a.dim, n = nqe + a.nr * a.dim;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
     if (!__builtin_isfinite(k < nqe ? a.q[k] : a.r[k - nqe])) a.sync[2] = 1;
+  if (a.nb > 1) {   // E[b][j], b < nb - 1, j <= nr (dtw_edge_bytes)
+    const int64_t ne = (a.nb - 1) * (a.nr + 1);
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ne; k += stride)
+      a.E[k] = 0x7FF000017FF00001ull;
+  }
 }
 
 // SONAR_DTW_DBG_STALL=<band> (tests only): fault injection, see DtwArgs::dbg_stall; "b<band>"
@@ -1936,7 +1945,8 @@ int launch_dtw_cost_rowmajor(const double* Cn, const DtwGeom& g, double* out, hi
 }
 
 int launch_nonfinite_batch(const DtwArgs* dargs, int n, int64_t max_elems, hipStream_t s) {
-  if (n <= 0 || max_elems <= 0) return 0;
+  if (n <= 0) return 0;
+  if (max_elems < 1) max_elems = 1;
   int64_t blocks = (max_elems + 255) / 256;
   if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(nonfinite_batch_kernel, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, dargs);

@@ -3,11 +3,11 @@
 //  zcr_kernel      ZeroCrossingRate.Compute on pre-emphasised frames
 //                  (algorithms/spectral/zero_crossing_rate.go:37-52, called at
 //                  fingerprint/extractors/speech.go:351-358)
-//  energy_kernel   Energy.ComputeShortTimeEnergy (algorithms/temporal/energy.go:25-50)
+//  energy_wave_kernel  Energy.ComputeShortTimeEnergy (algorithms/temporal/energy.go:25-50)
 //  yin_kernel      PitchDetector.detectPitchYin core (algorithms/tonal/pitch_detection.go:282-420)
 //  chroma_kernel   ChromaSTFT.ComputeChroma on one music-extractor frame
 //                  (algorithms/chroma/chroma_stft.go:45-138, fingerprint/extractors/music.go:327-376)
-//  dc_local/carry/apply_kernel  DCRemoval.Process + PreEmphasis.Process (music.go:245-259)
+//  dc_block/carry_kernel  DCRemoval.Process + PreEmphasis.Process (music.go:245-259)
 //
 // Decision-bearing arithmetic (sign tests, sums feeding thresholds) is float64
 // with explicit _rn intrinsics: no FMA contraction, Go's evaluation order.
@@ -55,46 +55,6 @@ __global__ __launch_bounds__(256) void zcr_kernel(const void* pcm, int pcm_f64, 
   }
 }
 
-#ifndef SONAR_ENERGY_B
-#define SONAR_ENERGY_B 16
-#endif
-// one thread per energy frame, sequential sum in Go's order.  The frame's samples are read in
-// batches of 16 with the next batch in flight while this one accumulates (the dependent add
-// chain then no longer waits on every load: 0.39 -> see DESIGN Kernel 2).  Fallback for windows whose
-// block span does not fit the LDS budget of energy_lds_kernel below.
-__global__ __launch_bounds__(256) void energy_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H,
-                                                     double alpha, void* out, int out_f64) {
-  SONAR_FEAT_PRIO();
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= Fe) return;
-  const int64_t s = t * H;
-  double ss = 0.0;
-  double prev = s > 0 ? pre_x(pcm, pcm_f64, s - 1) : 0.0;
-  constexpr int B = SONAR_ENERGY_B;
-  double cur[B], nxt[B];
-#pragma unroll
-  for (int j = 0; j < B; j++) cur[j] = j < W ? pre_x(pcm, pcm_f64, s + j) : 0.0;
-  int k = 0;
-  for (; k + B <= W; k += B) {
-#pragma unroll
-    for (int j = 0; j < B; j++) nxt[j] = k + B + j < W ? pre_x(pcm, pcm_f64, s + k + B + j) : 0.0;
-#pragma unroll
-    for (int j = 0; j < B; j++) {
-      const double y = __dsub_rn(cur[j], __dmul_rn(alpha, prev));
-      prev = cur[j];
-      ss = __dadd_rn(ss, __dmul_rn(y, y));
-    }
-#pragma unroll
-    for (int j = 0; j < B; j++) cur[j] = nxt[j];
-  }
-  for (int j = 0; k + j < W; j++) {
-    const double y = __dsub_rn(cur[j], __dmul_rn(alpha, prev));
-    prev = cur[j];
-    ss = __dadd_rn(ss, __dmul_rn(y, y));
-  }
-  store_out(out, out_f64, t, sqrt(__ddiv_rn(ss, (double)W)));
-}
-
 // a batched launch's job (blockIdx.y, or blockIdx.x for one-wave kernels) into SGPRs
 template <class J>
 __device__ __forceinline__ J load_job(const J* p) {
@@ -107,59 +67,81 @@ __device__ __forceinline__ J load_job(const J* p) {
   return r;
 }
 
-// The same per-frame chains with the block's samples staged in LDS first: a block owns kEnFpb
-// consecutive frames, its 256 threads copy the span [t0*H - 1, (t0+kEnFpb-1)*H + W) with coalesced
-// loads (one padding slot per 256 samples keeps the lanes' hop-strided LDS reads off one bank),
-// then lane f runs frame t0+f's Go-order chain out of LDS.  Same operations in the same order as
-// energy_kernel (bit-identical); the chains no longer wait on a global round trip per batch.
-constexpr int kEnFpb = 16;
-__device__ __forceinline__ int en_slot(int i) { return i + (i >> 8); }
+// Phase boundary of a wave-private LDS exchange (see mfcc_pair.hip): DS ops stay on their side,
+// and every DS op of the phase has retired before another lane's words are read or overwritten.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 
-// BJ: one music-feature job per blockIdx.y (its pre-emphasised signal, length, frames, output)
+// Energy.ComputeShortTimeEnergy (energy.go:25-50) of pre-emphasised frames, every lane one frame:
+// Go's order needs each frame's sum as ONE sequential chain, so the lane count is the frame count.
+// A wave owns 64 consecutive frames and walks them in rounds of kEnP samples: each round it loads
+// the 64 frames' next kEnP samples with 4-row x 16-column coalesced loads (the next round's are in
+// flight while this one runs), transposes them through a wave-private LDS tile [frame][kEnP + 2]
+// (row stride 144 B: the lanes' b128 reads hit distinct banks), and every lane adds its frame's
+// kEnP terms.  Same operations in the same order as Go: y = x - alpha x_prev, ss += y * y,
+// sqrt(ss / W).  36 KB of LDS per 4-wave block, no span limit (any W, H).
+constexpr int kEnP = 16;                 // samples per round
+constexpr int kEnRow = kEnP + 2;         // LDS row stride in doubles
+
 template <bool BJ>
-__global__ __launch_bounds__(256) void energy_lds_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W,
-                                                         int H, double alpha, void* out, int out_f64, const MfJob* jobs) {
+__global__ __launch_bounds__(256) void energy_wave_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W,
+                                                          int H, double alpha, void* out, int out_f64,
+                                                          const MfJob* jobs) {
   SONAR_FEAT_PRIO();
-  extern __shared__ double xs[];
+  __shared__ __attribute__((aligned(16))) double tile[4][64 * kEnRow];
   if constexpr (BJ) {
     const MfJob j = load_job(jobs + blockIdx.y);
     pcm = j.y; n = j.n; Fe = j.Fe; out = j.energy;
   }
-  const int64_t t0 = (int64_t)blockIdx.x * kEnFpb;
-  if (t0 >= Fe) return;
-  const int nf = (int)min((int64_t)kEnFpb, Fe - t0);
-  const int64_t base = t0 * H - 1;
-  const int span = (nf - 1) * H + W + 1;
-  for (int i = threadIdx.x; i < span; i += 256) {
-    const int64_t g = base + i;
-    xs[en_slot(i)] = (g >= 0 && g < n) ? pre_x(pcm, pcm_f64, g) : 0.0;
-  }
-  __syncthreads();
-  const int f = threadIdx.x;
-  if (f >= nf) return;
-  const int o = f * H;                         // xs index of x[s-1]; x[s-1] = 0 when s = 0 (g = -1)
-  double prev = xs[en_slot(o)];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t f0 = ((int64_t)blockIdx.x * 4 + w) * 64;        // this wave's first frame
+  if (f0 >= Fe) return;
+  double* tl = tile[w];
+  // loader role: round sample (row r = 4 i + lane / 16, column c = lane % 16)
+  const int lr = lane >> 4, lc = lane & 15;
+  auto load_round = [&](int k0, double (&v)[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t g = (f0 + 4 * i + lr) * (int64_t)H + k0 + lc;
+      v[i] = g < n ? pre_x(pcm, pcm_f64, g) : 0.0;
+    }
+  };
+  const int64_t s = (f0 + lane) * (int64_t)H;                    // this lane's frame start
+  double prev = (s > 0 && s - 1 < n) ? pre_x(pcm, pcm_f64, s - 1) : 0.0;
   double ss = 0.0;
-  constexpr int B = 16;
-  double cur[B];
-  int k = 0;
-  for (; k + B <= W; k += B) {
+  double nx[16];
+  load_round(0, nx);
+  for (int k0 = 0; k0 < W; k0 += kEnP) {
 #pragma unroll
-    for (int j = 0; j < B; j++) cur[j] = xs[en_slot(o + 1 + k + j)];
+    for (int i = 0; i < 16; ++i) tl[(4 * i + lr) * kEnRow + lc] = nx[i];
+    wave_lds_sync();
+    if (k0 + kEnP < W) load_round(k0 + kEnP, nx);
+    double cur[kEnP];
 #pragma unroll
-    for (int j = 0; j < B; j++) {
-      const double y = __dsub_rn(cur[j], __dmul_rn(alpha, prev));
-      prev = cur[j];
-      ss = __dadd_rn(ss, __dmul_rn(y, y));
+    for (int j = 0; j < kEnP; j += 2) {
+      const double2 v2 = *reinterpret_cast<const double2*>(tl + lane * kEnRow + j);
+      cur[j] = v2.x; cur[j + 1] = v2.y;
+    }
+    wave_lds_sync();
+    if (k0 + kEnP <= W) {
+#pragma unroll
+      for (int j = 0; j < kEnP; ++j) {
+        const double y = __dsub_rn(cur[j], __dmul_rn(alpha, prev));
+        prev = cur[j];
+        ss = __dadd_rn(ss, __dmul_rn(y, y));
+      }
+    } else {
+      for (int j = 0; j < W - k0; ++j) {
+        const double y = __dsub_rn(cur[j], __dmul_rn(alpha, prev));
+        prev = cur[j];
+        ss = __dadd_rn(ss, __dmul_rn(y, y));
+      }
     }
   }
-  for (; k < W; k++) {
-    const double c = xs[en_slot(o + 1 + k)];
-    const double y = __dsub_rn(c, __dmul_rn(alpha, prev));
-    prev = c;
-    ss = __dadd_rn(ss, __dmul_rn(y, y));
-  }
-  store_out(out, out_f64, t0 + f, sqrt(__ddiv_rn(ss, (double)W)));
+  if (f0 + lane < Fe) store_out(out, out_f64, f0 + lane, sqrt(__ddiv_rn(ss, (double)W)));
 }
 
 // YIN per 1024-sample frame (hop 512 for extractHarmonicFeatures, 256 for the voice-quality
@@ -512,15 +494,9 @@ int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H,
 int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H, double alpha, void* out,
                   int out_f64, hipStream_t s) {
   if (Fe <= 0) return 0;
-  const int64_t span = (int64_t)(kEnFpb - 1) * H + W + 1;
-  const size_t lds = (size_t)(span + (span >> 8) + 1) * sizeof(double);
-  if (lds <= 48 * 1024) {
-    hipLaunchKernelGGL(energy_lds_kernel<false>, dim3((unsigned)((Fe + kEnFpb - 1) / kEnFpb)), dim3(256), lds, s, pcm,
-                       pcm_f64, n, Fe, W, H, alpha, out, out_f64, (const MfJob*)nullptr);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
-  }
-  hipLaunchKernelGGL(energy_kernel, dim3((unsigned)((Fe + 255) / 256)), dim3(256), 0, s, pcm, pcm_f64, n, Fe, W, H,
-                     alpha, out, out_f64);
+  if (W <= 0 || H <= 0) return -4;
+  hipLaunchKernelGGL(energy_wave_kernel<false>, dim3((unsigned)((Fe + 255) / 256)), dim3(256), 0, s, pcm, pcm_f64, n,
+                     Fe, W, H, alpha, out, out_f64, (const MfJob*)nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -604,95 +580,98 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
 }
 
 // DC removal y[n] = x[n] - x[n-1] + R y[n-1] (dc_removal.go:101-124) followed by pre-emphasis
-// z[n] = y[n] - alpha y[n-1] (pre_emphasis.go:135-155), both with zero state, as three passes
-// over chunks of kDcChunk samples: (1) each chunk's response from a zero state -> its end value;
-// (2) one wave chains the chunk carries Y_c = e_c + R^chunk Y_{c-1} in order; (3) each chunk
-// re-runs the recurrence from its true start state and writes z.  Every sample goes through
-// the same sequential recurrence as Go; only the chunk start states differ: pass (2) combines
-// the carries with a Kogge-Stone scan of affine maps (log2 64 = 6 levels, reassociated), so a
-// start state carries a few ulp of |Y| of rounding that Go's serial chain does not (measured max
-// |dY| 9e-16 on unit-variance input), decaying as 0.995^k inside the chunk: outputs agree with
-// Go to ~1e-15 relative, energies to 1e-12 (tests), the NCC peak exactly (test_gpu_fullsize:
-// 5-min streams against the oracle's serial chain).  (The warm-up version it replaces ran 8,192
-// extra samples per 1,024-sample chunk.)  256-sample chunks:
-// 4x the lanes of 1,024 for the latency-bound passes, C5 726 -> ~760 pairs/s (tools/dc_ab.sh).
-#ifndef SONAR_DC_CHUNK
-#define SONAR_DC_CHUNK 256
-#endif
-constexpr int kDcChunk = SONAR_DC_CHUNK;
-
-template <bool WRITE, typename LD>
-__device__ __forceinline__ double dc_run(LD x, int64_t s, int64_t e, double R, double alpha, double y1,
-                                         double* z) {
-  double x1 = s > 0 ? x(s - 1) : 0.0;
-  constexpr int B = 16;
-  double cur[B], nxt[B];
-#pragma unroll
-  for (int j = 0; j < B; j++) cur[j] = s + j < e ? x(s + j) : 0.0;
-  int64_t i = s;
-  for (; i + B <= e; i += B) {
-#pragma unroll
-    for (int j = 0; j < B; j++) nxt[j] = i + B + j < e ? x(i + B + j) : 0.0;
-#pragma unroll
-    for (int j = 0; j < B; j++) {
-      const double yv = __dadd_rn(__dsub_rn(cur[j], x1), __dmul_rn(R, y1));
-      if (WRITE) z[i + j] = __dsub_rn(yv, __dmul_rn(alpha, y1));
-      x1 = cur[j]; y1 = yv;
-    }
-#pragma unroll
-    for (int j = 0; j < B; j++) cur[j] = nxt[j];
-  }
-  for (int j = 0; i + j < e; j++) {
-    const double yv = __dadd_rn(__dsub_rn(cur[j], x1), __dmul_rn(R, y1));
-    if (WRITE) z[i + j] = __dsub_rn(yv, __dmul_rn(alpha, y1));
-    x1 = cur[j]; y1 = yv;
-  }
-  return y1;
-}
-
-// Passes (1) and (3) on LDS-staged input: a block owns kDcCpb consecutive chunks, its 256 threads
-// copy x[c0*chunk - 1, (c0+kDcCpb)*chunk) with coalesced loads (one padding slot per 256 samples:
-// the lanes' chunk-strided reads land on distinct banks), then lane c runs chunk c0+c's
-// recurrence out of LDS -- the same operations as from global memory, without a global round
-// trip per 16-sample batch.
-// chunks per block: 16, fewer for long chunks so the staged span fits 64 KB of static LDS
-constexpr int kDcCpb = 7936 / kDcChunk < 16 ? 7936 / kDcChunk : 16;
-constexpr int kDcSpan = kDcCpb * kDcChunk + 1;
-static_assert((kDcSpan + (kDcSpan >> 8) + 1) * sizeof(double) <= 64 * 1024,
-              "dc_pass_kernel stages kDcCpb chunks in static LDS: lower kDcCpb for longer chunks");
-__device__ __forceinline__ int dc_slot(int i) { return i + (i >> 8); }
+// z[n] = y[n] - alpha y[n-1] (pre_emphasis.go:135-155), both from zero state, lane-dense:
+//  * a 256-thread block owns kDcBlk = 4,096 samples, lane c the 16-sample chunk c.  The block stages
+//    its samples (and the one before) in LDS with coalesced loads; every lane runs Go's recurrence
+//    over its chunk from a zero state, which gives the chunk's affine map Y -> e_c + R^16 Y.
+//  * an inclusive Kogge-Stone scan of the 256 maps (6 shuffle levels per wave, then the waves'
+//    totals through LDS) gives every chunk's map from the block start.
+//  * pass (1) stores the block's map (its end value from a zero start); pass (2), one wave per
+//    signal, chains the blocks' maps (dc_carry_kernel: Y_b = ends[b] + R^4096 Y_{b-1}); pass (3)
+//    redoes (1)'s scan, takes chunk c's start state from the block's true start, re-runs Go's
+//    recurrence over the chunk and writes z back through LDS with coalesced stores.
+// Every sample goes through Go's sequential recurrence from a start state equal to Go's up to the
+// scan's rounding (a few ulp of |Y|, reassociated affine maps), outputs within ~1e-15 of Go's
+// relative to the signal scale (tests: chroma 1e-9, energies 1e-12, the NCC peak exact).
+// The round-3 form ran 256-sample chunks with 16 of a block's 256 lanes busy.
+constexpr int kDcL = 16;                              // samples per lane
+constexpr int kDcBlk = 256 * kDcL;                    // samples per block
+__device__ __forceinline__ int dc_slot(int i) { return i + (i >> 4); }   // lane stride 17 doubles
+constexpr int kDcSlots = kDcBlk + 1 + ((kDcBlk + 1) >> 4) + 1;
 
 template <bool WRITE, bool BJ = false>
-__global__ __launch_bounds__(256) void dc_pass_kernel(const double* x, int64_t n, double R, double alpha,
-                                                      const double* ystart, double* ends, double* z, const MfJob* jobs) {
+__global__ __launch_bounds__(256) void dc_block_kernel(const double* x, int64_t n, double R, double R16, double alpha,
+                                                       const double* ystart, double* ends, double* z,
+                                                       const MfJob* jobs) {
   SONAR_FEAT_PRIO();
-  __shared__ double xs[kDcSpan + (kDcSpan >> 8) + 1];
+  __shared__ double xs[kDcSlots];
+  __shared__ double wtot[2][4];                       // the waves' inclusive totals (B, A)
   if constexpr (BJ) {
     const MfJob j = load_job(jobs + blockIdx.y);
     x = j.x; n = j.n; ystart = j.ystart; ends = j.ends; z = j.y;
   }
-  const int64_t c0 = (int64_t)blockIdx.x * kDcCpb;
-  if (c0 * kDcChunk >= n) return;
-  const int64_t base = c0 * kDcChunk - 1;
-  const int span = (int)(min(n, (c0 + kDcCpb) * kDcChunk) - base);
-  for (int i = threadIdx.x; i < span; i += 256) {
-    const int64_t g = base + i;
+  const int64_t base = (int64_t)blockIdx.x * kDcBlk;  // first sample of the block
+  if (base >= n) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int span = (int)min((int64_t)kDcBlk, n - base);
+  for (int i = tid; i <= span; i += 256) {            // xs[slot(i)] = x[base - 1 + i]
+    const int64_t g = base - 1 + i;
     xs[dc_slot(i)] = g >= 0 ? x[g] : 0.0;
   }
   __syncthreads();
-  const int64_t c = c0 + threadIdx.x;
-  const int64_t s = c * kDcChunk;
-  if ((int)threadIdx.x >= kDcCpb || s >= n) return;
-  auto ld = [&](int64_t g) { return xs[dc_slot((int)(g - base))]; };
-  if (WRITE) dc_run<true>(ld, s, min(n, s + kDcChunk), R, alpha, ystart[c], z);
-  else ends[c] = dc_run<false>(ld, s, min(n, s + kDcChunk), R, 0.0, 0.0, nullptr);
+  const int c0 = kDcL * tid;                           // chunk start (block-relative)
+  const int m = min(kDcL, max(0, span - c0));         // valid samples of this chunk
+  double v[kDcL + 1];                                  // v[0] = x[s - 1], v[1..16] = the chunk
+#pragma unroll
+  for (int j = 0; j <= kDcL; ++j) v[j] = xs[dc_slot(c0 + j)];
+  // the chunk's response from a zero state
+  double e = 0.0;
+#pragma unroll
+  for (int j = 0; j < kDcL; ++j)
+    if (j < m) e = __dadd_rn(__dsub_rn(v[j + 1], v[j]), __dmul_rn(R, e));
+  // inclusive scan of the maps (B, A): (B2, A2) o (B1, A1) = (B2 + A2 B1, A2 A1)
+  double B = e, A = R16;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const double Bp = __shfl_up(B, d, 64), Ap = __shfl_up(A, d, 64);
+    if (lane >= d) { B = __dadd_rn(B, __dmul_rn(A, Bp)); A = __dmul_rn(A, Ap); }
+  }
+  if (lane == 63) { wtot[0][w] = B; wtot[1][w] = A; }
+  __syncthreads();
+  double Bw = 0.0, Aw = 1.0;                           // the earlier waves' composite
+  for (int u = 0; u < w; ++u) {
+    const double Bu = wtot[0][u], Au = wtot[1][u];
+    Bw = __dadd_rn(Bu, __dmul_rn(Au, Bw));
+    Aw = __dmul_rn(Au, Aw);
+  }
+  if (!WRITE) {
+    if (tid == 255) ends[blockIdx.x] = __dadd_rn(B, __dmul_rn(A, Bw));   // the block's end from zero
+    return;
+  }
+  // chunk c's start: the exclusive composite applied to the block's true start Yb
+  const double Yb = ystart[blockIdx.x];
+  double Be = __shfl_up(B, 1, 64), Ae = __shfl_up(A, 1, 64);
+  if (lane == 0) { Be = 0.0; Ae = 1.0; }
+  Be = __dadd_rn(Be, __dmul_rn(Ae, Bw));
+  Ae = __dmul_rn(Ae, Aw);
+  double y1 = (tid == 0) ? Yb : __dadd_rn(Be, __dmul_rn(Ae, Yb));
+  double out[kDcL];
+#pragma unroll
+  for (int j = 0; j < kDcL; ++j) {
+    const double yv = __dadd_rn(__dsub_rn(v[j + 1], v[j]), __dmul_rn(R, y1));
+    out[j] = __dsub_rn(yv, __dmul_rn(alpha, y1));
+    y1 = yv;
+  }
+  __syncthreads();                                     // every lane has its inputs: reuse xs for z
+#pragma unroll
+  for (int j = 0; j < kDcL; ++j) xs[dc_slot(c0 + j)] = out[j];
+  __syncthreads();
+  for (int i = tid; i < span; i += 256) z[base + i] = xs[dc_slot(i)];
 }
 
-// one wave: ystart[c] = Y_{c-1}, Y_c = ends[c] + RC Y_{c-1}, Y_{-1} = 0.  Each 64-chunk block is
-// a 6-step Kogge-Stone scan of the affine maps Y -> B + A Y (lane c ends with the map of chunks
-// [i, c]), then one carry from the previous block: 162 blocks x 6 shuffle steps for a 60 s stream
-// instead of 10,336 dependent steps.  Rounding differs from the serial chain by a few ulp of the
-// carry, which the DC filter then decays by R per sample.
+// one wave: ystart[c] = Y_{c-1}, Y_c = ends[c] + RC Y_{c-1}, Y_{-1} = 0 over the blocks' maps.
+// Each 64-block group is a 6-step Kogge-Stone scan of the affine maps Y -> B + A Y (lane c ends
+// with the map of blocks [i, c]), then one carry from the previous group.
 template <bool BJ = false>
 __global__ __launch_bounds__(64) void dc_carry_kernel(const double* ends, int64_t T, double RC, double* ystart,
                                                       const MfJob* jobs) {
@@ -718,22 +697,29 @@ __global__ __launch_bounds__(64) void dc_carry_kernel(const double* ends, int64_
   }
 }
 
+namespace {
+double dc_pow(double R, int k) {                       // R^k by repeated products (host)
+  double r = 1.0;
+  for (int i = 0; i < k; ++i) r *= R;
+  return r;
+}
+}  // namespace
 
-int64_t dc_chunks(int64_t n) { return (n + kDcChunk - 1) / kDcChunk; }
-size_t dc_preemph_scratch_bytes(int64_t n) { return (size_t)(2 * ((n + kDcChunk - 1) / kDcChunk) + 2) * 8; }
+int64_t dc_chunks(int64_t n) { return (n + kDcBlk - 1) / kDcBlk; }
+size_t dc_preemph_scratch_bytes(int64_t n) { return (size_t)(2 * dc_chunks(n) + 2) * 8; }
 
 int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, double* scratch, hipStream_t s) {
   if (n <= 0) return 0;
-  const int64_t T = (n + kDcChunk - 1) / kDcChunk;
+  const int64_t T = dc_chunks(n);
   double* ends = scratch;
   double* ystart = scratch + T;
-  double RC = 1.0;
-  for (int k = 0; k < kDcChunk; k++) RC *= R;                 // R^chunk (carry weight of a full chunk)
-  const unsigned g = (unsigned)((T + kDcCpb - 1) / kDcCpb);
+  const double R16 = dc_pow(R, kDcL), RC = dc_pow(R, kDcBlk);
   const MfJob* none = nullptr;
-  hipLaunchKernelGGL((dc_pass_kernel<false>), dim3(g), dim3(256), 0, s, x, n, R, 0.0, nullptr, ends, nullptr, none);
+  hipLaunchKernelGGL((dc_block_kernel<false>), dim3((unsigned)T), dim3(256), 0, s, x, n, R, R16, 0.0, nullptr, ends,
+                     nullptr, none);
   hipLaunchKernelGGL((dc_carry_kernel<false>), dim3(1), dim3(64), 0, s, ends, T, RC, ystart, none);
-  hipLaunchKernelGGL((dc_pass_kernel<true>), dim3(g), dim3(256), 0, s, x, n, R, alpha, ystart, nullptr, y, none);
+  hipLaunchKernelGGL((dc_block_kernel<true>), dim3((unsigned)T), dim3(256), 0, s, x, n, R, R16, alpha, ystart, nullptr,
+                     y, none);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -746,10 +732,7 @@ int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double
 int launch_music_features_batch(const MfJob* hjobs, const MfJob* djobs, int nj, int W, int H, int fs,
                                 const double* window, const double* trig, const int* cls, hipStream_t s) {
   if (nj <= 0) return 0;
-  if (nj > 65535 || !cls || (fs != 256 && fs != 512)) return -1;
-  const int64_t span = (int64_t)(kEnFpb - 1) * H + W + 1;
-  const size_t lds = (size_t)(span + (span >> 8) + 1) * sizeof(double);
-  if (lds > 48 * 1024) return -1;
+  if (nj > 65535 || !cls || (fs != 256 && fs != 512) || W <= 0 || H <= 0) return -1;
   int64_t maxT = 1, maxFe = 1, maxF = 1;
   for (int k = 0; k < nj; ++k) {
     if (hjobs[k].n <= 0 || hjobs[k].F <= 0) return -1;
@@ -758,14 +741,15 @@ int launch_music_features_batch(const MfJob* hjobs, const MfJob* djobs, int nj, 
     maxF = std::max(maxF, hjobs[k].F);
   }
   const double R = 0.995, alpha = 0.95;        // music.go:245-259 (dc_removal / pre_emphasis defaults)
-  double RC = 1.0;
-  for (int k = 0; k < kDcChunk; k++) RC *= R;
-  const dim3 gdc((unsigned)((maxT + kDcCpb - 1) / kDcCpb), (unsigned)nj);
-  hipLaunchKernelGGL((dc_pass_kernel<false, true>), gdc, dim3(256), 0, s, nullptr, 0, R, 0.0, nullptr, nullptr, nullptr, djobs);
+  const double R16 = dc_pow(R, kDcL), RC = dc_pow(R, kDcBlk);
+  const dim3 gdc((unsigned)maxT, (unsigned)nj);
+  hipLaunchKernelGGL((dc_block_kernel<false, true>), gdc, dim3(256), 0, s, nullptr, 0, R, R16, 0.0, nullptr, nullptr,
+                     nullptr, djobs);
   hipLaunchKernelGGL((dc_carry_kernel<true>), dim3((unsigned)nj), dim3(64), 0, s, nullptr, 0, RC, nullptr, djobs);
-  hipLaunchKernelGGL((dc_pass_kernel<true, true>), gdc, dim3(256), 0, s, nullptr, 0, R, alpha, nullptr, nullptr, nullptr, djobs);
-  hipLaunchKernelGGL((energy_lds_kernel<true>), dim3((unsigned)((maxFe + kEnFpb - 1) / kEnFpb), (unsigned)nj), dim3(256),
-                     lds, s, nullptr, 1, 0, 0, W, H, 0.0, nullptr, 1, djobs);
+  hipLaunchKernelGGL((dc_block_kernel<true, true>), gdc, dim3(256), 0, s, nullptr, 0, R, R16, alpha, nullptr, nullptr,
+                     nullptr, djobs);
+  hipLaunchKernelGGL((energy_wave_kernel<true>), dim3((unsigned)((maxFe + 255) / 256), (unsigned)nj), dim3(256), 0, s,
+                     nullptr, 1, 0, 0, W, H, 0.0, nullptr, 1, djobs);
   const dim3 gch((unsigned)((maxF + 3) / 4), (unsigned)nj);
   if (fs == 256)
     hipLaunchKernelGGL((chroma_wave_kernel<4, true>), gch, dim3(256), 0, s, nullptr, 0, 0, H, window, trig, cls, nullptr, djobs);

@@ -310,7 +310,6 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* hpath = hcorr + corr_b;
   HIP_TRY(w, hipMemsetAsync(small, 0, stat_b + diag_b, s));
   HIP_TRY(w, hipMemsetAsync(runs, 0, runs_b, s));
-  if (e_b) HIP_TRY(w, hipMemsetD32Async((hipDeviceptr_t)E, 0x7FF00001u, e_b / 4, s));
   // every pair's music features and energy NCC: batched launches over the whole batch when the
   // inputs are on the device and every signal fits the batched kernels (feat_batch), else pair by
   // pair on the worker's scratch
@@ -358,9 +357,11 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
         if (b < pg[i].g.nb) hmap[t++] = make_int2(i, (int)b);
   }
   HIP_TRY(w, hipMemcpyAsync(dargs, hargs, args_b + start_b + map_b, hipMemcpyHostToDevice, s));
-  // the non-finite probe of every pair's chroma in one launch (flags in each pair's sync[2])
+  // the non-finite probe of every pair's chroma in one launch (flags in each pair's sync[2]); the
+  // same launch fills every pair's band-edge rows E with the band kernel's sentinel
   int64_t max_el = 0;
-  for (const auto& p : pg) max_el = std::max(max_el, (p.Fq + p.Fr) * 12);
+  for (const auto& p : pg)
+    max_el = std::max({max_el, (p.Fq + p.Fr) * 12, (int64_t)(sonar::dtw_edge_bytes(p.g) / 8)});
   if (sonar::launch_nonfinite_batch(dargs, n, max_el, s) != 0) return fail(w, SONAR_ERR_DEVICE, "dtw launch failed");
 #ifndef SONAR_DBG_C5_NODTW   // A/B timing builds only (wrong records): no DTW
   if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s, dmap) != 0)

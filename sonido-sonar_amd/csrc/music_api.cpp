@@ -5,8 +5,8 @@
 // the band energy ratios, the DC / pre-emphasis scan, chroma and energy kernels of the alignment
 // path); the host runs only Go's O(frames) scalar tails.
 //
-// The reference panics inside extractTemporalFeatures for almost every input (SURVEY.md F15,
-// DESIGN.md Kernel 10): music.go:403 passes the percentiles 10 and 90 where
+// The reference panics inside extractTemporalFeatures for almost every input (DESIGN.md F15 and
+// Kernel 10): music.go:403 passes the percentiles 10 and 90 where
 // DynamicRange.calculatePercentileRange (temporal/dynamic_range.go:58-76) expects fractions, so
 // int(10 * (L - 1)) indexes past the L RMS frames (1024 / 512) of any signal with L >= 2
 // (n >= 1536 samples); and a signal with no energy frame divides by zero at music.go:383.  Such a
@@ -149,6 +149,11 @@ int sonar_extract_music_features(sonar_ctx* c, const double* pcm, int64_t n, int
   // ---- chroma (:327-376) on the preprocessed PCM -------------------------------------------
   double* dchroma = (double*)dbuf(c, "mx.chroma", (size_t)Fz * 12 * 8);
   if (!dchroma) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (chroma)");
+  // FeatureConfig.HopSize <= 0: the per-frame ChromaSTFT's STFT rejects it (stft.go:54-56), and
+  // ExtractFeatures returns the wrapped error (music.go:218-221, :358-361)
+  if (fc->hop_size <= 0)
+    return fail(c, SONAR_ERR_INVALID,
+                "chroma feature extraction failed: chroma computation failed at frame 0: hop size must be positive");
   rc = sonar_chroma_stft(c, dy, n, F, fc->hop_size, csr, 0, dchroma, 1);
   if (rc != SONAR_OK) return rc;
 

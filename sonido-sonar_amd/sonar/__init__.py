@@ -41,6 +41,7 @@ from ._abi import (  # noqa: F401
     F64,
     INGEST_DEVICE_CONVERT,
     INGEST_HOST_CONVERT,
+    ERR_INVALID,
     ERR_EMPTY,
     ERR_TOO_SHORT,
     ERR_PANIC,

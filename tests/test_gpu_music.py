@@ -10,8 +10,10 @@ fails with SONAR_ERR_PANIC and Go's runtime message, and the arrays computed bef
 oracle.  Below 1536 samples every group is compared (the harmonic block is zero by F7 except for a
 1024-sample frame, where DetectPitch runs).
 
-Tolerances: 1e-9 relative (floors at 1e-6 of the array's peak) for the float features, exact for
-peak amplitudes and counts."""
+Tolerances: 1e-9 relative (floors at 1e-6 of the array's peak) for the float features, 1e-8 for the
+spectral slope (a log-log regression over every bin above 1e-10, as in test_gpu_stft_mfcc), 1e-9
+relative or 1e-4 dB for the spectral contrast (a dB ratio whose valley can sit far below the frame's
+peak bin), exact for the rolloff bin, peak amplitudes and counts."""
 import numpy as np
 import pytest
 
@@ -41,7 +43,16 @@ def _compare(got, ref):
         if k == "mfcc":
             assert_mfcc(got[k], v, 1e-9)
         elif k == "spectral_rolloff" or k == "peak_amplitude":
-            assert np.array_equal(np.asarray(got[k], float), np.asarray(v, float)), k
+            assert np.array_equal(np.ravel(np.asarray(got[k], float)), np.ravel(np.asarray(v, float))), k
+        elif k == "spectral_slope":
+            _close(got[k], v, k, 1e-8)
+        elif k == "spectral_contrast":
+            # 10 log10(peak / valley) of sorted band powers: a valley far below the frame's peak bin
+            # carries the FFT's rounding relative to that PEAK (~1e-16 of it), so in dB the error
+            # is absolute: 1e-9 relative or 1e-4 dB, whichever is larger
+            g, r = np.asarray(got[k], float), np.asarray(v, float)
+            assert g.shape == r.shape, k
+            assert np.all(np.abs(g - r) <= np.maximum(1e-9 * np.abs(r), 1e-4)), (k, float(np.max(np.abs(g - r))))
         else:
             _close(got[k], v, k)
 
@@ -70,7 +81,7 @@ def test_panic_regime_partial_results(ctx, seconds):
 def test_no_energy_frame_divides_by_zero(ctx):
     """FeatureConfig.WindowSize unset (0, F13): no ShortTimeEnergy frame -> len(pcm) / 0 (:383)."""
     x = synth.sweep(1.0)
-    got, err, ref, panic = _run(ctx, x, window_size=0, hop_size=0)
+    got, err, ref, panic = _run(ctx, x, window_size=0, hop_size=256)
     assert panic == "runtime error: integer divide by zero"
     assert err is not None and err.code == sonar.ERR_PANIC and err.msg == panic
     _compare(got, ref)
@@ -101,6 +112,18 @@ def test_short_signal_temporal_error(ctx):
         ctx.extract_music_features(x, 44100, cfg)
     assert ei.value.code == sonar.ERR_TOO_SHORT
     assert "temporal feature extraction failed" in ei.value.msg
+
+
+def test_zero_hop_chroma_error(ctx):
+    """FeatureConfig.HopSize unset (0): the chroma STFT rejects it (stft.go:54-56) and
+    ExtractFeatures returns the wrapped error (music.go:218-221)."""
+    x = synth.sweep(0.5)
+    cfg, fc = _fc(ctx, window_size=0, hop_size=0)
+    with pytest.raises(ValueError) as oe:
+        O.music_features_reference(x, 44100, fc)
+    with pytest.raises(sonar.SonarError) as ei:
+        ctx.extract_music_features(x, 44100, cfg)
+    assert ei.value.code == sonar.ERR_INVALID and ei.value.msg == str(oe.value)
 
 
 def test_invalid_input(ctx):
