@@ -88,8 +88,8 @@ struct MfccPairParams {
   int n_mels, n_mfcc;   // n_mfcc <= 16
   int pow2;             // F5: MFCC.Compute fed |X|^2 -> filterbank of |X|^4
   float* out;           // [F][n_mfcc]
-  int lds_src, lds_dct, lds_tab, lds_wave0, lds_bytes;   // lds_tab: window + w_64 tables (16-wave blocks)
-  int waves_per_block;  // 4 or 16 (mfcc_pair_kernel's WPB)
+  int lds_src, lds_dct, lds_tab, lds_wave0, lds_bytes;   // lds_tab: window + w_64 tables
+  int waves_per_block;  // 4 (mfcc_pair_kernel)
 };
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s);
 int mfcc_pair_wave_bytes();

@@ -187,14 +187,9 @@ constexpr int kLogOff = kPartOff + 64 * 16;   // logmel [2][NMP]
 
 // JT / MS / NH: compile-time chunk length, sources per filter and DCT half-length for the
 // headline bank (40 mels at 44.1 kHz: 12 / 8 / 20); 0 = read from p (runtime loops).
-// RS: the hop in 64-sample rows when frame t+1's rows are frame t's rows shifted by RS (H = 64 RS,
-// the headline's H = 256: RS = 4): a pair then loads 16 + RS rows instead of 32; 0 = any hop.
-// WPB: waves per block.  4: three 4-wave blocks per CU (12 waves, <= 168 VGPRs), the window and
-// twiddles in VGPRs.  16: one 16-wave block per CU (4 waves per SIMD, <= 128 VGPRs), the window
-// and the w_64 twiddles read from LDS tables the 16 waves share (the per-wave regions then fill
-// 136 of the 160 KB).
-template <bool POW2, int JT, int MS, int NH, int RS, int WPB>
-__global__ __launch_bounds__(64 * WPB, WPB == 16 ? 4 : 3) void mfcc_pair_kernel(MfccPairParams p) {
+// Four waves per block, three blocks per CU (12 waves, <= 168 VGPRs).
+template <bool POW2, int JT, int MS, int NH>
+__global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 #ifdef SONAR_PAIR_REGTAB   // A/B: window and w_64 twiddles held in VGPRs
   constexpr bool TL = false;
 #else
@@ -269,43 +264,30 @@ __global__ __launch_bounds__(64 * WPB, WPB == 16 ? 4 : 3) void mfcc_pair_kernel(
   const float* pcm = p.pcm;
   const int H = p.H;
 
-  // The pair's PCM rows through a buffer descriptor over this wave's samples up to the end of the
-  // last frame, (F-1) H + 1024: the hardware range check returns 0 past it, so the loads need no
-  // branches (a lone last frame's partner frame t+1 = F reads frame t's samples and zeros: a finite
-  // partner whose outputs are not stored, the same for a frame shard ending there as for the whole
-  // stream, so shards stay bit-identical).  n < 1024 (Go's single all-zero frame, spectral.go:409
-  // and :524-534): an empty range, every row 0.
-  // RS > 0: rows 0 .. 15 + RS from frame t's start (frame t+1 = rows RS ..); RS == 0: frame t's 16
-  // rows, then frame t+1's 16
-  constexpr int NX = RS ? 16 + RS : 32;
-  const int64_t base = 2 * pb * (int64_t)H;                   // first sample this wave reads
-  const int64_t avail = p.n < 1024 ? 0 : (p.F - 1) * (int64_t)H + 1024 - base;
-  const uint32_t nbytes = avail * 4 > (int64_t)0xFFFFFFF0 ? 0xFFFFFFF0u : (uint32_t)(avail * 4);
-  // (descriptor inputs made provably wave-uniform, the descriptor built at each use: otherwise it
-  // lives in VGPRs and every load becomes a readfirstlane loop)
-  const uint64_t bp = reinterpret_cast<uint64_t>(pcm + base);
-  const uint32_t bp_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bp);
-  const uint32_t bp_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(bp >> 32));
-  const int nb_u = __builtin_amdgcn_readfirstlane((int)nbytes);
-  auto ld = [&](uint32_t off) {
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((uint64_t)bp_hi << 32) | bp_lo), (short)0, nb_u, 0x00020000);
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
-  };
-  auto load_pair = [&](int64_t pi, float (&x)[NX]) {
-    const uint32_t o = (uint32_t)(2 * (pi - pb) * H + lane) * 4u;
-    if constexpr (RS) {
+  // frame t's 16 rows and frame t+1's; a frame past the last one (the lone last frame of an odd F,
+  // whole stream or shard alike: shard edges are even) or one that does not fit (n < 1024: Go's
+  // single all-zero frame, spectral.go:409 and :524-534) reads zeros
+  auto frame_ok = [&](int64_t t) { return t < p.F && t * (int64_t)H + 1024 <= p.n; };
+  auto load_pair = [&](int64_t pi, float (&xr)[16], float (&xi)[16]) {
+    const int64_t t = 2 * pi;
+    const float* b0p = pcm + t * (int64_t)H + lane;
+    if (frame_ok(t)) {
 #pragma unroll
-      for (int a = 0; a < NX; a++) x[a] = ld(o + 256u * a);
+      for (int a = 0; a < 16; a++) xr[a] = b0p[64 * a];
     } else {
 #pragma unroll
-      for (int a = 0; a < 16; a++) x[a] = ld(o + 256u * a);
+      for (int a = 0; a < 16; a++) xr[a] = 0.f;
+    }
+    if (frame_ok(t + 1)) {
 #pragma unroll
-      for (int a = 0; a < 16; a++) x[16 + a] = ld(o + 4u * H + 256u * a);
+      for (int a = 0; a < 16; a++) xi[a] = b0p[H + 64 * a];
+    } else {
+#pragma unroll
+      for (int a = 0; a < 16; a++) xi[a] = 0.f;
     }
   };
 
-  auto process = [&](int64_t pi, const float (&x)[NX]) {
+  auto process = [&](int64_t pi, const float (&xr)[16], const float (&xi)[16]) {
     cf v[16];
     if constexpr (TL) {
 #pragma unroll
@@ -314,15 +296,8 @@ __global__ __launch_bounds__(64 * WPB, WPB == 16 ? 4 : 3) void mfcc_pair_kernel(
         win[a] = w4.x; win[a + 1] = w4.y; win[a + 2] = w4.z; win[a + 3] = w4.w;
       }
     }
-    if constexpr (RS) {
-      // frame t+1 = rows RS .. RS+15 (when t+1 is past the last frame: frame t's tail and zeros,
-      // a finite partner whose outputs are not stored)
 #pragma unroll
-      for (int a = 0; a < 16; a++) v[a] = {x[a] * win[a], x[a + RS] * win[a]};
-    } else {
-#pragma unroll
-      for (int a = 0; a < 16; a++) v[a] = {x[a] * win[a], x[16 + a] * win[a]};
-    }
+    for (int a = 0; a < 16; a++) v[a] = {xr[a] * win[a], xi[a] * win[a]};
     // ---- pass 1: DFT16 over a, twiddle w_1024^{b k1} -----------------------------
     dft16(v);
 #pragma unroll
@@ -475,21 +450,14 @@ __global__ __launch_bounds__(64 * WPB, WPB == 16 ? 4 : 3) void mfcc_pair_kernel(
     wave_lds_sync();
   };
 
-  float x[NX];
-#ifdef SONAR_PAIR_NOPF    // A/B: no prefetch (20-32 fewer live VGPRs, the load latency exposed)
+  float ar[16], ai[16];
+  load_pair(pb, ar, ai);
   for (int64_t pi = pb; pi < pe; ++pi) {
-    load_pair(pi, x);
-    process(pi, x);
-  }
-  return;
-#endif
-  load_pair(pb, x);
-  for (int64_t pi = pb; pi < pe; ++pi) {
-    float xn[NX];
-    if (pi + 1 < pe) load_pair(pi + 1, xn);       // next pair's PCM in flight during this one
-    process(pi, x);
+    float nr[16], ni[16];
+    if (pi + 1 < pe) load_pair(pi + 1, nr, ni);     // next pair's PCM in flight during this one
+    process(pi, ar, ai);
 #pragma unroll
-    for (int a = 0; a < NX; a++) x[a] = xn[a];
+    for (int a = 0; a < 16; a++) { ar[a] = nr[a]; ai[a] = ni[a]; }
   }
 }
 
@@ -497,21 +465,14 @@ __global__ __launch_bounds__(64 * WPB, WPB == 16 ? 4 : 3) void mfcc_pair_kernel(
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   const int64_t NP = (p.F + 1) >> 1;
   const int64_t waves = (NP + p.pairs_per_wave - 1) / p.pairs_per_wave;
-  const int wpb = p.waves_per_block == 16 ? 16 : 4;
-  const int64_t grid = (waves + wpb - 1) / wpb;
+  const int64_t grid = (waves + 3) / 4;
   const bool head = p.J == 12 && p.max_src <= 8 && p.NMP == 40;
-  const bool rs4 = head && p.H == 256;
-  void (*kern)(MfccPairParams);
-#define SONAR_PAIR_KERN(W_)                                                                                   \
-  kern = p.pow2 ? (head ? (rs4 ? mfcc_pair_kernel<true, 12, 8, 20, 4, W_> : mfcc_pair_kernel<true, 12, 8, 20, 0, W_>) \
-                        : mfcc_pair_kernel<true, 0, 0, 0, 0, W_>)                                              \
-                : (head ? (rs4 ? mfcc_pair_kernel<false, 12, 8, 20, 4, W_> : mfcc_pair_kernel<false, 12, 8, 20, 0, W_>) \
-                        : mfcc_pair_kernel<false, 0, 0, 0, 0, W_>)
-  if (wpb == 16) { SONAR_PAIR_KERN(16); } else { SONAR_PAIR_KERN(4); }
-#undef SONAR_PAIR_KERN
+  void (*kern)(MfccPairParams) =
+      p.pow2 ? (head ? mfcc_pair_kernel<true, 12, 8, 20> : mfcc_pair_kernel<true, 0, 0, 0>)
+             : (head ? mfcc_pair_kernel<false, 12, 8, 20> : mfcc_pair_kernel<false, 0, 0, 0>);
   if (p.lds_bytes > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * wpb), p.lds_bytes, s, p);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), p.lds_bytes, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -525,12 +525,9 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
       q.lds_src = al(64 * t.JS * 8);
       q.lds_dct = q.lds_src + 64 * 16 * 2;
       q.lds_tab = q.lds_dct + al(16 * (t.NMP + 4) * 4);
-#ifndef SONAR_PAIR_WPB
-#define SONAR_PAIR_WPB 4
-#endif
-      // mfcc_pair_kernel: 4 waves per block and 3 blocks per CU, or one 16-wave block per CU
-      // with the window / w_64 tables in LDS (64 x 20 floats + 8 x 10 float2)
-      q.waves_per_block = SONAR_PAIR_WPB;
+      // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU; the window / w_64 tables
+      // (64 x 20 floats + 8 x 10 float2) after the filterbank / DCT tables
+      q.waves_per_block = 4;
       q.lds_wave0 = q.lds_tab + 64 * 20 * 4 + 8 * 10 * 8;
       q.lds_bytes = q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes();
       int dev_cus = 256;

@@ -13,7 +13,8 @@ oracle.  Below 1536 samples every group is compared (the harmonic block is zero 
 Tolerances: 1e-9 relative (floors at 1e-6 of the array's peak) for the float features, 1e-8 for the
 spectral slope (a log-log regression over every bin above 1e-10, as in test_gpu_stft_mfcc), 1e-9
 relative or 1e-4 dB for the spectral contrast (a dB ratio whose valley can sit far below the frame's
-peak bin), exact for the rolloff bin, peak amplitudes and counts."""
+peak bin), exact for the rolloff bin and counts.  The peak amplitude (max |y| of the preprocessed
+signal) is within 1e-9 like the other floats: y carries the DC scan's rounding (DESIGN.md Kernel 4)."""
 import numpy as np
 import pytest
 
@@ -42,7 +43,7 @@ def _compare(got, ref):
         assert k in got, k
         if k == "mfcc":
             assert_mfcc(got[k], v, 1e-9)
-        elif k == "spectral_rolloff" or k == "peak_amplitude":
+        elif k == "spectral_rolloff":
             assert np.array_equal(np.ravel(np.asarray(got[k], float)), np.ravel(np.asarray(v, float))), k
         elif k == "spectral_slope":
             _close(got[k], v, k, 1e-8)
