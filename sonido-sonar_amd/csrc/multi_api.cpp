@@ -277,6 +277,10 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* path = (char*)dbuf(w, "pb.path", path_b);
   char* corr = (char*)dbuf(w, "pb.corr", corr_b);
   char* small = (char*)dbuf(w, "pb.small", stat_b + diag_b + args_b + start_b + map_b);
+  // SONAR_DTW_TRACE=<file> (diagnostics): every band's sweep timestamps (dtw_band_kernel's trace
+  // words) appended to <file> as {pair, band, 8 trace words} records
+  const char* trace_path = std::getenv("SONAR_DTW_TRACE");
+  char* trb = trace_path ? (char*)dbuf(w, "pb.trace", (size_t)total_bands * 64) : nullptr;
   double* eq = (double*)dbuf(w, "pb.eq", (size_t)maxE * 8);
   double* er = (double*)dbuf(w, "pb.er", (size_t)maxE * 8);
   double* xa = (double*)dbuf(w, "ncc.xa", (size_t)maxE * 8);
@@ -343,6 +347,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     a.pc = (double*)(path + p.path); a.pq = (int32_t*)(a.pc + p.cap); a.pr = a.pq + p.cap;
     a.cnm = (double*)(dstat + 8 * i + 2);
     a.diag = ddiag + (size_t)i * sonar::DTW_DIAG_WORDS;
+    a.trace = trb ? (uint64_t*)(trb + (size_t)acc * 64) : nullptr;
     a.dbg_stall = sonar::dtw_dbg_stall_band(true);
     hstart[i] = acc;
     acc += p.g.nb;
@@ -370,7 +375,22 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   HIP_TRY(w, hipMemcpyAsync(hstat, small, stat_b + diag_b, hipMemcpyDeviceToHost, s));
   if (corr_b) HIP_TRY(w, hipMemcpyAsync(hcorr, corr, corr_b, hipMemcpyDeviceToHost, s));
   HIP_TRY(w, hipMemcpyAsync(hpath, path, path_b, hipMemcpyDeviceToHost, s));
+  std::vector<uint64_t> htr(trb ? (size_t)total_bands * 8 : 0);
+  if (trb) HIP_TRY(w, hipMemcpyAsync(htr.data(), trb, htr.size() * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(w, hipStreamSynchronize(s));
+  if (trb) {
+    static std::mutex trace_mu;
+    std::lock_guard<std::mutex> lk(trace_mu);
+    if (FILE* f = std::fopen(trace_path, "ab")) {
+      for (int i = 0; i < n; ++i)
+        for (int64_t b = 0; b < pg[i].g.nb; ++b) {
+          const uint64_t hdr[2] = {(uint64_t)pg[i].k, (uint64_t)b};
+          std::fwrite(hdr, 8, 2, f);
+          std::fwrite(htr.data() + (size_t)(hstart[i] + b) * 8, 8, 8, f);
+        }
+      std::fclose(f);
+    }
+  }
   const char* dump_dir = std::getenv("SONAR_PAIR_DUMP");
   for (int i = 0; i < n; ++i) {
     const PairGeo& p = pg[i];

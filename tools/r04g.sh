@@ -1,7 +1,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -q --maxfail=10 --timeout 200 --timeout-method thread tests/test_gpu_music.py tests/test_gpu_mfcc_pair.py tests/test_gpu_stft_mfcc.py tests/test_gpu_fullsize.py tests/test_gpu_multi.py tests/test_gpu_dist.py tests/test_gpu_golden.py tests/test_gpu_pair_batch.py > gpurun_out/r04g_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest -q --maxfail=10 --timeout 200 --timeout-method thread tests/test_gpu_music.py tests/test_gpu_mfcc_pair.py tests/test_gpu_stft_mfcc.py tests/test_gpu_fullsize.py tests/test_gpu_multi.py tests/test_gpu_dist.py tests/test_gpu_golden.py tests/test_gpu_pair_batch.py tests/test_gpu_features_edges.py tests/test_gpu_pairs.py > gpurun_out/r04g_tests.log 2>&1
 rc=$?
 tail -5 gpurun_out/r04g_tests.log
 [ $rc -le 1 ] || { echo "test run ended with rc=$rc"; exit 1; }
@@ -22,3 +22,7 @@ for t in default noedge default noedge; do
   SONAR_PAIR_RETRY=0 SONAR_LIB=$PWD/$L timeout -k 10 150 python3 tools/c5_stress.py --reps 2 > gpurun_out/r04g_c5_$t.jsonl 2>/dev/null || { echo "c5 fail $t"; exit 1; }
   echo "c5 $t: $(grep -o '"pairs_per_s": [0-9.]*' gpurun_out/r04g_c5_$t.jsonl | tr '\n' ' ')"
 done
+rm -f gpurun_out/r04g_c5_trace.bin
+SONAR_DTW_TRACE=$PWD/gpurun_out/r04g_c5_trace.bin SONAR_PAIR_RETRY=0 timeout -k 10 150 python3 tools/c5_stress.py --reps 1 > gpurun_out/r04g_c5_traced.jsonl 2>/dev/null || { echo "c5 trace fail"; exit 1; }
+python3 tools/dtw_batch_trace.py gpurun_out/r04g_c5_trace.bin 10396 | tee gpurun_out/r04g_c5_trace_summary.txt
+rm -f gpurun_out/r04g_c5_trace.bin
