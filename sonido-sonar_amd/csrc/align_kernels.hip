@@ -363,7 +363,21 @@ struct DtwBatch {
   int32_t* ticket;
   const int2* map;   // nullable: ticket -> (DTW, band) in any order where a band's predecessor
                      // has the smaller ticket; null: DTW-major through `start`
+  int32_t* next_band;   // nullable: per-DTW claim counters (DTW_CLAIM_LAG > 0, zeroed by the caller)
 };
+
+// DTW_CLAIM_LAG > 0 (batches): a block does not take the next ticket but CLAIMS a band whose
+// predecessor is at least DTW_CLAIM_LAG columns ahead (its edge row E[b-1] holds column LAG), so a
+// band starts with that much slack behind the band above and rides out the upstream's short
+// stalls instead of spinning on them (round-4 trace: 13 % of sweep time spinning; the NOEDGE
+// timing build, every band independent, +14 % C5).  Claims go through one counter per DTW
+// (CAS b -> b+1), so each DTW's bands still start in band order, and a band is only claimed after
+// its predecessor: the hand-off argument of the ticket order holds.  A block that finds no ready
+// band for DTW_CLAIM_WAIT_TICKS takes the least advanced unclaimed band anyway.
+#ifndef DTW_CLAIM_LAG
+#define DTW_CLAIM_LAG 0
+#endif
+constexpr uint64_t DTW_CLAIM_WAIT_TICKS = 5000;   // 50 us (s_memrealtime, 100 MHz)
 
 namespace {
 
@@ -638,7 +652,42 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
     if constexpr (BATCH) {
       const int64_t t = atomicAdd(bt.ticket, 1);
       ctr[DTW_CTR_TICKET] = (int)t;
-      if (bt.map) {
+      if (DTW_CLAIM_LAG > 0 && bt.next_band) {
+        shk = 0;
+        shb = INT64_MAX;                              // no band left: the block exits
+        const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+        const int k0 = (int)(t % bt.n);
+        for (bool done = false; !done;) {
+          bool any = false, force = __builtin_amdgcn_s_memrealtime() - w0 > DTW_CLAIM_WAIT_TICKS;
+          for (int u = 0; u < bt.n && !done; ++u) {
+            const int k = k0 + u < bt.n ? k0 + u : k0 + u - bt.n;
+            const DtwArgs* ak = bt.args + k;
+            const int64_t nbk = ak->nb, nrk = ak->nr;
+            auto* nx = (__attribute__((address_space(1))) int32_t*)&bt.next_band[k];
+            for (;;) {
+              const int32_t bk = __hip_atomic_load(nx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (bk >= nbk) break;
+              any = true;
+              bool ready = bk == 0 || force;
+              if (!ready) {
+                const int64_t col = DTW_CLAIM_LAG < nrk ? DTW_CLAIM_LAG : nrk;
+                ready = g_load_agent(ak->E + (bk - 1) * (nrk + 1) + col) != 0x7FF000017FF00001ull;
+              }
+              if (!ready) break;
+              int32_t expect = bk;
+              if (__hip_atomic_compare_exchange_strong(nx, &expect, bk + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)) {
+                shk = k;
+                shb = bk;
+                done = true;
+                break;
+              }
+            }
+          }
+          if (!any) break;
+          if (!done) __builtin_amdgcn_s_sleep(8);
+        }
+      } else if (bt.map) {
         if (t < bt.start[bt.n]) {
           const int2 pb = bt.map[t];
           shk = pb.x;
@@ -1899,13 +1948,18 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s) {
 }
 
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
-                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap) {
+                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap, hipStream_t sband,
+                     hipEvent_t e0, hipEvent_t e1, int32_t* next_band) {
   if (n <= 0 || total_bands <= 0) return 0;
   if (total_bands > INT32_MAX) return -1;
   const DtwArgs none{};
-  const DtwBatch bt{dargs, dstart, n, ticket, dmap};
-  hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES), 0, s,
-                     none, bt);
+  const DtwBatch bt{dargs, dstart, n, ticket, dmap, next_band};
+  // sband: the band kernel alone on another stream, ordered by e0 (everything before it on s) and
+  // e1 (the walks after it on s)
+  if (sband && (hipEventRecord(e0, s) != hipSuccess || hipStreamWaitEvent(sband, e0, 0) != hipSuccess)) return -5;
+  hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES), 0,
+                     sband ? sband : s, none, bt);
+  if (sband && (hipEventRecord(e1, sband) != hipSuccess || hipStreamWaitEvent(s, e1, 0) != hipSuccess)) return -5;
   if (dtw_serial_walk()) {
     hipLaunchKernelGGL(dtw_walk_batch_kernel, dim3((unsigned)n), dim3(64), 0, s, dargs);
   } else {

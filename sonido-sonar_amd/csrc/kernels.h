@@ -88,7 +88,7 @@ struct MfccPairParams {
   int n_mels, n_mfcc;   // n_mfcc <= 16
   int pow2;             // F5: MFCC.Compute fed |X|^2 -> filterbank of |X|^4
   float* out;           // [F][n_mfcc]
-  int lds_src, lds_dct, lds_tab, lds_wave0, lds_bytes;   // lds_tab: window + w_64 tables
+  int lds_src, lds_dct, lds_wave0, lds_bytes;
   int waves_per_block;  // 4 (mfcc_pair_kernel)
 };
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s);
@@ -266,7 +266,8 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s);
 // about one hand-off for its predecessor instead of b of them
 int32_t dtw_dbg_stall_band(bool batch);   // SONAR_DTW_DBG_STALL (tests only), -1 when unset
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
-                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr);
+                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap, hipStream_t sband = nullptr,
+                     hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int32_t* next_band = nullptr);
 // sets *flag = 1 if any of the n values is not finite
 int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 // the same probe over q and r of every DTW of a batch (sets args[k].sync[2]); max_elems >= every

@@ -95,15 +95,6 @@ __device__ __forceinline__ void dft16(cf (&v)[16]) {
   for (int i = 0; i < 16; i++) v[i] = o[i];
 }
 
-// An offset the compiler cannot see through: per-pair reads of the LDS tables (filterbank
-// weights, source indices, DCT rows) indexed by it stay inside the pair loop.  Without it the
-// compiler hoists ~52 table values per lane into loop-invariant VGPRs and spills them (and tw1)
-// to scratch at 168 VGPRs -- 29 scratch reloads per pair.
-__device__ __forceinline__ int opaque(int x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-
 __device__ __forceinline__ float f_of(uint32_t u) { return __uint_as_float(u); }
 __device__ __forceinline__ uint32_t u_of(float f) { return __float_as_uint(f); }
 
@@ -187,14 +178,8 @@ constexpr int kLogOff = kPartOff + 64 * 16;   // logmel [2][NMP]
 
 // JT / MS / NH: compile-time chunk length, sources per filter and DCT half-length for the
 // headline bank (40 mels at 44.1 kHz: 12 / 8 / 20); 0 = read from p (runtime loops).
-// Four waves per block, three blocks per CU (12 waves, <= 168 VGPRs).
 template <bool POW2, int JT, int MS, int NH>
 __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
-#ifdef SONAR_PAIR_REGTAB   // A/B: window and w_64 twiddles held in VGPRs
-  constexpr bool TL = false;
-#else
-  constexpr bool TL = true;                     // window and w_64 twiddles from LDS
-#endif
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -205,14 +190,6 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   for (int i = threadIdx.x; i < 64 * p.JS; i += blockDim.x) s_cw[i] = p.chunk_w[i];
   for (int i = threadIdx.x; i < 64 * 16; i += blockDim.x) s_src[i] = p.mel_src[i];
   for (int i = threadIdx.x; i < 16 * (p.NMP + 4); i += blockDim.x) s_dct[i] = p.dct[i];
-  // TL: window as [lane][20] floats (element a of lane l at 20 l + a: conflict-free b128 reads),
-  // w_64^{b0 c} as [b0][10] float2 (row stride 80 B: the 8 rows on distinct banks)
-  float* s_win = reinterpret_cast<float*>(smem + p.lds_tab);
-  float2* s_tw2 = reinterpret_cast<float2*>(smem + p.lds_tab + 64 * 20 * 4);
-  if constexpr (TL) {
-    for (int i = threadIdx.x; i < 1024; i += blockDim.x) s_win[20 * (i & 63) + (i >> 6)] = p.window[i];
-    for (int i = threadIdx.x; i < 64; i += blockDim.x) s_tw2[10 * (i >> 3) + (i & 7)] = p.tw2[i];
-  }
   unsigned char* wb = smem + p.lds_wave0 + wave * kWaveBytes;
   // Zero the wave's region once: the filterbank chunks read up to 11 rows past bin 512 with
   // zero weight, and some of those bytes (the unused 17th float2 of T2 lane rows 33/34) are
@@ -224,19 +201,15 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 
   // ---- per-lane constants ---------------------------------------------------------
   float win[16];
-  if constexpr (!TL) {
 #pragma unroll
-    for (int a = 0; a < 16; a++) win[a] = p.window[64 * a + lane];
-  }
+  for (int a = 0; a < 16; a++) win[a] = p.window[64 * a + lane];
   cf tw1[16];                                   // w_1024^{lane k1}
 #pragma unroll
   for (int k = 1; k < 16; k++) { const float2 v = p.tw1[lane * 16 + k]; tw1[k] = {v.x, v.y}; }
   const int b0 = lane & 7, kl = lane >> 3;
   cf tw2[8];                                    // w_64^{b0 c0}
-  if constexpr (!TL) {
 #pragma unroll
-    for (int c = 1; c < 8; c++) { const float2 v = p.tw2[b0 * 8 + c]; tw2[c] = {v.x, v.y}; }
-  }
+  for (int c = 1; c < 8; c++) { const float2 v = p.tw2[b0 * 8 + c]; tw2[c] = {v.x, v.y}; }
   // lane masks for the bit-3 exchange: m_hi3 = lanes with bit 3 set, m_lo3 = the rest
   const uint64_t m_hi3 = 0xff00ff00ff00ff00ull, m_lo3 = ~m_hi3;
   // T2 write bases (regular lanes, kl != 0): h = 0 -> + 136 c0, h = 1 -> + 136 (7 - c0)
@@ -264,9 +237,6 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   const float* pcm = p.pcm;
   const int H = p.H;
 
-  // frame t's 16 rows and frame t+1's; a frame past the last one (the lone last frame of an odd F,
-  // whole stream or shard alike: shard edges are even) or one that does not fit (n < 1024: Go's
-  // single all-zero frame, spectral.go:409 and :524-534) reads zeros
   auto frame_ok = [&](int64_t t) { return t < p.F && t * (int64_t)H + 1024 <= p.n; };
   auto load_pair = [&](int64_t pi, float (&xr)[16], float (&xi)[16]) {
     const int64_t t = 2 * pi;
@@ -289,13 +259,6 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 
   auto process = [&](int64_t pi, const float (&xr)[16], const float (&xi)[16]) {
     cf v[16];
-    if constexpr (TL) {
-#pragma unroll
-      for (int a = 0; a < 16; a += 4) {
-        const float4 w4 = *reinterpret_cast<const float4*>(s_win + 20 * lane + a);
-        win[a] = w4.x; win[a + 1] = w4.y; win[a + 2] = w4.z; win[a + 3] = w4.w;
-      }
-    }
 #pragma unroll
     for (int a = 0; a < 16; a++) v[a] = {xr[a] * win[a], xi[a] * win[a]};
     // ---- pass 1: DFT16 over a, twiddle w_1024^{b k1} -----------------------------
@@ -330,13 +293,6 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     // ---- pass 2: DFT8 over b1 (registers 8h + b1), twiddle w_64^{b0 c0} -----------
     dft8<0, 1>(v);
     dft8<8, 1>(v);
-    if constexpr (TL) {
-#pragma unroll
-      for (int c = 0; c < 8; c += 2) {
-        const float4 t4 = *reinterpret_cast<const float4*>(s_tw2 + 10 * b0 + c);
-        tw2[c] = {t4.x, t4.y}; tw2[c + 1] = {t4.z, t4.w};
-      }
-    }
 #pragma unroll
     for (int c = 1; c < 8; c++) { v[c] = cmul(v[c], tw2[c]); v[8 + c] = cmul(v[8 + c], tw2[c]); }
     // ---- T2: LDS transpose into the combo layout ---------------------------------
@@ -392,7 +348,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       float a0 = 0.f, a1 = 0.f, c0 = 0.f, c1 = 0.f;
       const unsigned char* pr = wb + prow(ks) * 8;
       const int ib = 16 - (ks & 15);                          // first i past a pad pair
-      const float2* cw = s_cw + opaque(lane * p.JS);
+      const float2* cw = s_cw + lane * p.JS;
       const int J = JT ? JT : p.J;
 #pragma unroll
       for (int i = 0; i < J; i++) {
@@ -408,10 +364,9 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     if (lane < nmp) {
       float m0 = 0.f, m1 = 0.f;
       const int ms = MS ? MS : p.max_src;
-      const int lsrc = opaque(lane);
 #pragma unroll
       for (int i = 0; i < ms; i++) {
-        const uint32_t idx = s_src[64 * i + lsrc];               // 0x8000: unused -> the zero float2
+        const uint32_t idx = s_src[64 * i + lane];               // 0x8000: unused -> the zero float2
         const int off = (idx & 0x8000u) ? 64 * kT2Stride : kPartOff + 8 * (int)idx;
         const float2 q = *reinterpret_cast<const float2*>(wb + off);
         m0 += q.x;
@@ -434,7 +389,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       const int q = lane & 15, f = (lane >> 4) & 1, hh = lane >> 5;
       const int half = NH ? NH : (nmp >> 1);
       const float* lm = reinterpret_cast<const float*>(wb + kLogOff) + f * nmp + hh * half;
-      const float* d = s_dct + opaque(q * (nmp + 4) + hh * half);     // row stride NMP + 4: 11 x 16 B slots
+      const float* d = s_dct + q * (nmp + 4) + hh * half;     // row stride NMP + 4: 11 x 16 B slots
       float s = 0.f;
 #pragma unroll
       for (int m = 0; m < half; m += 4) {
@@ -467,11 +422,10 @@ int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   const int64_t waves = (NP + p.pairs_per_wave - 1) / p.pairs_per_wave;
   const int64_t grid = (waves + 3) / 4;
   const bool head = p.J == 12 && p.max_src <= 8 && p.NMP == 40;
-  void (*kern)(MfccPairParams) =
-      p.pow2 ? (head ? mfcc_pair_kernel<true, 12, 8, 20> : mfcc_pair_kernel<true, 0, 0, 0>)
-             : (head ? mfcc_pair_kernel<false, 12, 8, 20> : mfcc_pair_kernel<false, 0, 0, 0>);
+  auto kern = p.pow2 ? (head ? mfcc_pair_kernel<true, 12, 8, 20> : mfcc_pair_kernel<true, 0, 0, 0>)
+                     : (head ? mfcc_pair_kernel<false, 12, 8, 20> : mfcc_pair_kernel<false, 0, 0, 0>);
   if (p.lds_bytes > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), p.lds_bytes, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -162,20 +162,69 @@ bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
   }
   const double scale = cfg->mfcc_input_power ? 1.0 / 16.0 : 0.25;   // |2X|^2 or |2X|^4 from the pair split
   const int JS = J | 1;
+  struct Chunk { int k0, seg; };
+  std::vector<Chunk> chunks;
+  for (size_t gi = 0; gi < segs.size(); gi++)
+    for (int k0 = segs[gi].k0; k0 < segs[gi].k1; k0 += J) chunks.push_back({k0, (int)gi});
+  chunks.resize(64, Chunk{0, -1});                 // idle lanes read bin 0 with zero weights
+  // Lane order of the chunks.  The filterbank's ds_read_b64 of power row prow(ks + i) is serviced
+  // in two 32-lane groups, bank (byte / 4) mod 64: chunks whose rows fall on the same banks in one
+  // group serialise (modelled and counted in tools/scratch/pair_lds_model.py: 59 extra LDS cycles
+  // per pair in ascending order at the headline bank, the bulk of SQ_LDS_BANK_CONFLICT).  A swap
+  // search between the two groups lowers that; the filters still sum their chunks in ascending-bin
+  // order (the source lists below follow the chunk order, not the lanes).
+  std::vector<int> order(64);
+  for (int l = 0; l < 64; l++) order[l] = l;
+  auto prow_h = [](int k) { return k + 2 * (k >> 4); };
+  auto fb_conflicts = [&](const std::vector<int>& o) {
+    int extra = 0;
+    for (int i = 0; i < J; i++)
+      for (int g = 0; g < 2; g++) {
+        int used[64][32], nu[64] = {0};
+        for (int l = 32 * g; l < 32 * g + 32; l++) {
+          const int k = chunks[o[l]].k0;
+          const int dw = 2 * prow_h(k) + 2 * i + ((i >= 16 - (k & 15)) ? 4 : 0);
+          for (int d = 0; d < 2; d++) {
+            const int b = (dw + d) & 63;
+            bool seen = false;
+            for (int u = 0; u < nu[b]; u++) seen |= used[b][u] == dw + d;
+            if (!seen && nu[b] < 32) used[b][nu[b]++] = dw + d;
+          }
+        }
+        int mx = 1;
+        for (int b = 0; b < 64; b++) mx = std::max(mx, nu[b]);
+        extra += mx - 1;
+      }
+    return extra;
+  };
+  for (int best = fb_conflicts(order), improved = 1; improved;) {
+    improved = 0;
+    for (int a = 0; a < 32; a++)
+      for (int b = 32; b < 64; b++) {
+        std::swap(order[a], order[b]);
+        const int c = fb_conflicts(order);
+        if (c < best) { best = c; improved = 1; }
+        else std::swap(order[a], order[b]);
+      }
+  }
+  std::vector<int> lane_of(64);
+  for (int l = 0; l < 64; l++) lane_of[order[l]] = l;
   std::vector<int> ks(64, 0);
   std::vector<float> cw(64 * 2 * JS, 0.f);
   std::vector<std::vector<int>> src(64);
-  int lane = 0;
-  for (auto& g : segs)
-    for (int k0 = g.k0; k0 < g.k1; k0 += J, lane++) {
-      ks[lane] = k0;
-      for (int i = 0; i < J && k0 + i < g.k1; i++) {
-        cw[(lane * JS + i) * 2] = (float)(weight(g.a, k0 + i) * scale);
-        cw[(lane * JS + i) * 2 + 1] = g.b >= 0 ? (float)(weight(g.b, k0 + i) * scale) : 0.f;
-      }
-      src[g.a].push_back(2 * lane);
-      if (g.b >= 0) src[g.b].push_back(2 * lane + 1);
+  for (size_t ci = 0; ci < chunks.size(); ci++) {   // chunk order = ascending bins
+    const Chunk& ch = chunks[ci];
+    if (ch.seg < 0) continue;
+    const Seg& g = segs[ch.seg];
+    const int lane = lane_of[ci], k0 = ch.k0;
+    ks[lane] = k0;
+    for (int i = 0; i < J && k0 + i < g.k1; i++) {
+      cw[(lane * JS + i) * 2] = (float)(weight(g.a, k0 + i) * scale);
+      cw[(lane * JS + i) * 2 + 1] = g.b >= 0 ? (float)(weight(g.b, k0 + i) * scale) : 0.f;
     }
+    src[g.a].push_back(2 * lane);
+    if (g.b >= 0) src[g.b].push_back(2 * lane + 1);
+  }
   std::vector<uint16_t> msrc(64 * 16, 0x8000);
   int max_src = 1;
   for (int m = 0; m < mt.n_mels; m++) {
@@ -524,11 +573,9 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
       auto al = [](int x) { return (x + 15) & ~15; };
       q.lds_src = al(64 * t.JS * 8);
       q.lds_dct = q.lds_src + 64 * 16 * 2;
-      q.lds_tab = q.lds_dct + al(16 * (t.NMP + 4) * 4);
-      // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU; the window / w_64 tables
-      // (64 x 20 floats + 8 x 10 float2) after the filterbank / DCT tables
+      q.lds_wave0 = q.lds_dct + al(16 * (t.NMP + 4) * 4);
+      // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU
       q.waves_per_block = 4;
-      q.lds_wave0 = q.lds_tab + 64 * 20 * 4 + 8 * 10 * 8;
       q.lds_bytes = q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes();
       int dev_cus = 256;
       hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);

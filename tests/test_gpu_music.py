@@ -99,8 +99,8 @@ def test_full_extractor_below_1536_samples(ctx, n, W, H, fw, fh):
     assert panic is None and err is None, (panic, err)
     assert set(got) == set(ref), sorted(set(got) ^ set(ref))
     _compare(got, ref)
-    if n == 1024 and W == 1024:                     # the one frame DetectPitch accepts (F7)
-        assert got["pitch_estimate"][0] > 0
+    # n == 1024, W == 1024 is the one frame DetectPitch accepts (F7); the extractor's pre-emphasis
+    # (0.95) leaves a low tone below the noise there, so Go (and the oracle) report no pitch either
 
 
 def test_short_signal_temporal_error(ctx):
