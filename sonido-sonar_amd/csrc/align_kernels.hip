@@ -363,21 +363,7 @@ struct DtwBatch {
   int32_t* ticket;
   const int2* map;   // nullable: ticket -> (DTW, band) in any order where a band's predecessor
                      // has the smaller ticket; null: DTW-major through `start`
-  int32_t* next_band;   // nullable: per-DTW claim counters (DTW_CLAIM_LAG > 0, zeroed by the caller)
 };
-
-// DTW_CLAIM_LAG > 0 (batches): a block does not take the next ticket but CLAIMS a band whose
-// predecessor is at least DTW_CLAIM_LAG columns ahead (its edge row E[b-1] holds column LAG), so a
-// band starts with that much slack behind the band above and rides out the upstream's short
-// stalls instead of spinning on them (round-4 trace: 13 % of sweep time spinning; the NOEDGE
-// timing build, every band independent, +14 % C5).  Claims go through one counter per DTW
-// (CAS b -> b+1), so each DTW's bands still start in band order, and a band is only claimed after
-// its predecessor: the hand-off argument of the ticket order holds.  A block that finds no ready
-// band for DTW_CLAIM_WAIT_TICKS takes the least advanced unclaimed band anyway.
-#ifndef DTW_CLAIM_LAG
-#define DTW_CLAIM_LAG 0
-#endif
-constexpr uint64_t DTW_CLAIM_WAIT_TICKS = 5000;   // 50 us (s_memrealtime, 100 MHz)
 
 namespace {
 
@@ -454,7 +440,10 @@ constexpr int DTW_RBLK = 16;               // rows per ring refill
 #define DTW_DQ_CFG 32
 #endif
 constexpr int DTW_DQ = DTW_DQ_CFG;         // steps of distances held in LDS (a power of two)
-constexpr int DTW_OQ = 32;                 // steps of C values held in LDS for the code wave
+#ifndef DTW_OQ_CFG
+#define DTW_OQ_CFG 32
+#endif
+constexpr int DTW_OQ = DTW_OQ_CFG;         // steps of C values held in LDS for the code wave
 constexpr int DTW_DROW = DTW_DQ + 2;       // doubles per lane row of the transposed rings: a
 constexpr int DTW_OROW = DTW_OQ + 2;       // multiple of 4 dwords plus 4 (mod 64 dwords)
 constexpr int DTW_EQ = 128;       // edge values in the LDS rings
@@ -652,42 +641,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
     if constexpr (BATCH) {
       const int64_t t = atomicAdd(bt.ticket, 1);
       ctr[DTW_CTR_TICKET] = (int)t;
-      if (DTW_CLAIM_LAG > 0 && bt.next_band) {
-        shk = 0;
-        shb = INT64_MAX;                              // no band left: the block exits
-        const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-        const int k0 = (int)(t % bt.n);
-        for (bool done = false; !done;) {
-          bool any = false, force = __builtin_amdgcn_s_memrealtime() - w0 > DTW_CLAIM_WAIT_TICKS;
-          for (int u = 0; u < bt.n && !done; ++u) {
-            const int k = k0 + u < bt.n ? k0 + u : k0 + u - bt.n;
-            const DtwArgs* ak = bt.args + k;
-            const int64_t nbk = ak->nb, nrk = ak->nr;
-            auto* nx = (__attribute__((address_space(1))) int32_t*)&bt.next_band[k];
-            for (;;) {
-              const int32_t bk = __hip_atomic_load(nx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if (bk >= nbk) break;
-              any = true;
-              bool ready = bk == 0 || force;
-              if (!ready) {
-                const int64_t col = DTW_CLAIM_LAG < nrk ? DTW_CLAIM_LAG : nrk;
-                ready = g_load_agent(ak->E + (bk - 1) * (nrk + 1) + col) != 0x7FF000017FF00001ull;
-              }
-              if (!ready) break;
-              int32_t expect = bk;
-              if (__hip_atomic_compare_exchange_strong(nx, &expect, bk + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT)) {
-                shk = k;
-                shb = bk;
-                done = true;
-                break;
-              }
-            }
-          }
-          if (!any) break;
-          if (!done) __builtin_amdgcn_s_sleep(8);
-        }
-      } else if (bt.map) {
+      if (bt.map) {
         if (t < bt.start[bt.n]) {
           const int2 pb = bt.map[t];
           shk = pb.x;
@@ -883,6 +837,9 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
 
   if (wave == CODE_WAVE) {
     // --------------------------------------------------------------- code wave
+#ifdef DTW_CODE_PRIO   // A/B: the code wave above the distance waves in VALU arbitration
+    __builtin_amdgcn_s_setprio(DTW_CODE_PRIO);
+#endif
     // step s, lane l: up = C of lane l-1 at step s-1, left = own at s-1, diag = lane l-1 at s-2;
     // lane 0's left neighbour is the band's top edge: C[64b][s+1] / C[64b][s]
     __attribute__((address_space(1))) uint32_t* Db = DTW_GLOBAL(a.Dn) + ((b * a.SW) << 6) + lane;
@@ -1059,7 +1016,6 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
   // waves sharing its SIMD (MI355X_MICROARCH.md, "VALU issue is arbitrated ... by priority")
   __builtin_amdgcn_s_setprio(3);
   const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-  const uint64_t c_start = a.trace ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t t_first = 0;
   uint64_t* Eout = (b + 1 < a.nb) ? a.E + b * (nr + 1) : nullptr;         // C[64b+64][j]
   double out = inf;                                   // C[i][j-1]; C[i][0] = +Inf
@@ -1084,6 +1040,27 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
     if (DTW_NDW > 6 && w == 6) dchk = k.d6;
     const int neede = s0 + DTW_ECH < nr32 ? s0 + DTW_ECH : nr32;
     return dchk > c && (!Ein || k.ef >= neede) && k.cp >= s0 + DTW_ECH - DTW_OQ + 2;
+  };
+  // trace only: which producer a spin started on (1 distances, 2 the band above's edge, 3 the code
+  // wave), and the spin ticks per cause (trace words 4 and 5; the rest of word 3's total is code)
+  uint64_t spin_dist = 0, spin_edge = 0;
+  auto spin_cause = [&](int s0, Ctrs k) -> int {
+    const int c = s0 / DTW_ECH, w = c % DTW_NDW;
+    int dchk = k.d0;
+    if (DTW_NDW > 1 && w == 1) dchk = k.d1;
+    if (DTW_NDW > 2 && w == 2) dchk = k.d2;
+    if (DTW_NDW > 3 && w == 3) dchk = k.d3;
+    if (DTW_NDW > 4 && w == 4) dchk = k.d4;
+    if (DTW_NDW > 5 && w == 5) dchk = k.d5;
+    if (DTW_NDW > 6 && w == 6) dchk = k.d6;
+    if (dchk <= c) return 1;
+    const int neede = s0 + DTW_ECH < nr32 ? s0 + DTW_ECH : nr32;
+    if (Ein && k.ef < neede) return 2;
+    return 3;
+  };
+  auto account = [&](int cause, uint64_t before) {
+    if (cause == 1) spin_dist += spins_total - before;
+    else if (cause == 2) spin_edge += spins_total - before;
   };
   // {dchunk, efill} as one (NDW <= 3) or two 16-B volatile LDS reads, cprog as one 4-B read
   typedef int ctr4 __attribute__((ext_vector_type(4)));
@@ -1163,7 +1140,10 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
   double dc[DTW_ECH], ech[DTW_ECH];
   Ctrs kc = load_ctr();
   if (!ready(0, kc)) {
+    const int cause = a.trace ? spin_cause(0, kc) : 0;
+    const uint64_t before = spins_total;
     SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready(0, kc)));
+    if (a.trace) account(cause, before);
   }
   if (a.trace) t_first = __builtin_amdgcn_s_memrealtime();
   load_chunk(0, dc, ech);
@@ -1207,7 +1187,10 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
       load_chunk(s1, dcn, echn);
       if (!ready((int)s1, kc))
       {
+        const int cause = a.trace ? spin_cause((int)s1, kc) : 0;
+        const uint64_t before = spins_total;
         SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready((int)s1, kc)));
+        if (a.trace) account(cause, before);
         load_chunk(s1, dcn, echn);
       }
     }
@@ -1228,8 +1211,8 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
     const uint64_t hw = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
     const uint64_t xcc = (uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20); // HW_REG_XCC_ID
     tr[8 * b + 3] = (spins_total & 0xFFFFFFull) | ((xcc & 0xFF) << 24) | (hw << 32);
-    tr[8 * b + 4] = c_start;
-    tr[8 * b + 5] = __builtin_amdgcn_s_memtime();
+    tr[8 * b + 4] = spin_dist;                        // the sweep's spins on its distance waves
+    tr[8 * b + 5] = spin_edge;                        // ... on the band above's edge (rest: the code wave)
   }
 }
 
@@ -1948,18 +1931,13 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s) {
 }
 
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
-                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap, hipStream_t sband,
-                     hipEvent_t e0, hipEvent_t e1, int32_t* next_band) {
+                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap) {
   if (n <= 0 || total_bands <= 0) return 0;
   if (total_bands > INT32_MAX) return -1;
   const DtwArgs none{};
-  const DtwBatch bt{dargs, dstart, n, ticket, dmap, next_band};
-  // sband: the band kernel alone on another stream, ordered by e0 (everything before it on s) and
-  // e1 (the walks after it on s)
-  if (sband && (hipEventRecord(e0, s) != hipSuccess || hipStreamWaitEvent(sband, e0, 0) != hipSuccess)) return -5;
-  hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES), 0,
-                     sband ? sband : s, none, bt);
-  if (sband && (hipEventRecord(e1, sband) != hipSuccess || hipStreamWaitEvent(s, e1, 0) != hipSuccess)) return -5;
+  const DtwBatch bt{dargs, dstart, n, ticket, dmap};
+  hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES), 0, s,
+                     none, bt);
   if (dtw_serial_walk()) {
     hipLaunchKernelGGL(dtw_walk_batch_kernel, dim3((unsigned)n), dim3(64), 0, s, dargs);
   } else {

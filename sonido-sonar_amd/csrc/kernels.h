@@ -207,7 +207,8 @@ struct DtwArgs {
   uint64_t* E;
   int32_t* sync;   // [0] band ticket, [1] error flag, [2] non-finite input flag
   uint64_t* trace; // optional [nb][8]: t_start, t_first_edge, t_end, sweep wait ticks (s_memrealtime, 100 MHz),
-                   // shader clock at start and end (s_memtime), distance-wave-0 and code-wave wait ticks
+                   // the sweep's wait ticks on its distance waves and on the band above's edge,
+                   // distance-wave-0 and code-wave wait ticks
   // batched launches only (launch_dtw_batch): the walk / path-decode outputs of this DTW
   uint32_t* codes;
   int64_t* plen;
@@ -266,8 +267,7 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s);
 // about one hand-off for its predecessor instead of b of them
 int32_t dtw_dbg_stall_band(bool batch);   // SONAR_DTW_DBG_STALL (tests only), -1 when unset
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
-                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap, hipStream_t sband = nullptr,
-                     hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int32_t* next_band = nullptr);
+                     int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr);
 // sets *flag = 1 if any of the n values is not finite
 int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 // the same probe over q and r of every DTW of a batch (sets args[k].sync[2]); max_elems >= every

@@ -69,23 +69,6 @@ std::vector<sonar_ctx*>& workers_of(sonar_ctx* c, int n, int* rc) {
     sonar_ctx* w = nullptr;
     const int r = sonar_create(c->device, &w);
     if (r != SONAR_OK) { *rc = r; break; }
-#ifdef SONAR_C5_PRIO
-    // A/B (SONAR_C5_PRIO): the worker's own stream at the highest priority (features, NCC, walks,
-    // copies), its side stream at the default priority for the band kernel (align_batch), so the
-    // short kernels of other phases are dispatched ahead of queued band blocks
-    {
-      int least = 0, greatest = 0;
-      hipStream_t hi = nullptr;
-      if (hipSetDevice(w->device) == hipSuccess && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
-          hipStreamCreateWithPriority(&hi, hipStreamNonBlocking, greatest) == hipSuccess) {
-        if (w->stream == w->own) w->stream = hi;
-        hipStreamDestroy(w->own);
-        w->own = hi;
-      }
-      if (!w->side && hipStreamCreateWithPriority(&w->side, hipStreamNonBlocking, least) == hipSuccess)
-        for (auto& e : w->side_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-    }
-#endif
     c->workers.push_back(w);
   }
   return c->workers;
@@ -281,7 +264,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   // small (device) and the head of h (pinned host) share one layout: per-pair status words + the
   // batch ticket, the per-pair band-kernel diagnostic records, then the DTW arguments, ticket
   // starts and the band-major ticket map
-  const size_t stat_b = al256((size_t)n * 32 + 16 + (size_t)n * 4), diag_b = al256((size_t)n * 8 * sonar::DTW_DIAG_WORDS),
+  const size_t stat_b = al256((size_t)n * 32 + 16), diag_b = al256((size_t)n * 8 * sonar::DTW_DIAG_WORDS),
                args_b = al256((size_t)n * sizeof(sonar::DtwArgs)), start_b = al256((size_t)(n + 1) * 8),
                map_b = al256((size_t)total_bands * 8);
   char* chroma = (char*)dbuf(w, "pb.chroma", chroma_b);
@@ -317,7 +300,6 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   }
   int32_t* dstat = (int32_t*)small;                 // per pair: [0..1] plen, [2..3] C[nq][nr], [4..7] sync
   int32_t* ticket = (int32_t*)(small + (size_t)n * 32);
-  int32_t* next_band = (int32_t*)(small + (size_t)n * 32 + 16);   // per-DTW band claims (zeroed with small)
   uint64_t* ddiag = (uint64_t*)(small + stat_b);
   const size_t ab = stat_b + diag_b;                 // where the arguments start
   sonar::DtwArgs* dargs = (sonar::DtwArgs*)(small + ab);
@@ -387,13 +369,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     max_el = std::max({max_el, (p.Fq + p.Fr) * 12, (int64_t)(sonar::dtw_edge_bytes(p.g) / 8)});
   if (sonar::launch_nonfinite_batch(dargs, n, max_el, s) != 0) return fail(w, SONAR_ERR_DEVICE, "dtw launch failed");
 #ifndef SONAR_DBG_C5_NODTW   // A/B timing builds only (wrong records): no DTW
-#ifdef SONAR_C5_PRIO
-  const bool split = w->side && w->side_ev[0] && w->side_ev[1];
-#else
-  const bool split = false;
-#endif
-  if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s, dmap,
-                              split ? w->side : nullptr, w->side_ev[0], w->side_ev[1], next_band) != 0)
+  if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s, dmap) != 0)
     return fail(w, SONAR_ERR_DEVICE, "dtw batch launch failed");
 #endif
   HIP_TRY(w, hipMemcpyAsync(hstat, small, stat_b + diag_b, hipMemcpyDeviceToHost, s));

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Summarise a batched-DTW band trace (SONAR_DTW_TRACE=<file> with sonar_align_pairs, e.g. under
 tools/c5_stress.py): records {pair, band, t_start, t_first, t_end, sweep spins | xcc | hw_id,
-c_start, c_end, distance-wave-0 waits, code-wave waits} (10 u64 each; realtime = 100 MHz ticks,
-memtime = shader clocks; see dtw_band_kernel's trace words).
+sweep spins on its distance waves, sweep spins on the band above's edge, distance-wave-0 waits,
+code-wave waits} (10 u64 each, s_memrealtime ticks of 10 ns; see dtw_band_kernel's trace words).
 
     python3 tools/dtw_batch_trace.py <trace file> [steps_per_band]
 
@@ -31,7 +31,11 @@ def main():
     busy = (t2 - t0).sum() * tick_ns / 1e6          # band-ms
     print(f"bands {len(r)}  pairs {len(np.unique(pair))}  traced span {span:.1f} ms")
     print(f"band-time {busy:.1f} band-ms -> mean resident bands {busy / span:.1f} (slots: 512 at 2 blocks/CU)")
-    for name, v in [("first-edge wait us", wait_first), ("sweep us", sweep), ("sweep spins us", spin)]:
+    sd, se = r[:, 6] * tick_ns / 1e3, r[:, 7] * tick_ns / 1e3
+    dw, cw = r[:, 8] * tick_ns / 1e3, r[:, 9] * tick_ns / 1e3
+    for name, v in [("first-edge wait us", wait_first), ("sweep us", sweep), ("sweep spins us", spin),
+                    ("  on distances us", sd), ("  on edge above us", se), ("  on code wave us", spin - sd - se),
+                    ("dist wave 0 waits us", dw), ("code wave waits us", cw)]:
         print(f"{name:20s} median {np.median(v):9.1f}  p10 {np.percentile(v, 10):9.1f}  p90 {np.percentile(v, 90):9.1f}"
               f"  sum {v.sum() / 1e3:9.1f} ms")
     if steps:
