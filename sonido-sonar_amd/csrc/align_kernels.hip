@@ -440,6 +440,12 @@ constexpr int DTW_RBLK = 16;               // rows per ring refill
 #define DTW_DQ_CFG 32
 #endif
 constexpr int DTW_DQ = DTW_DQ_CFG;         // steps of distances held in LDS (a power of two)
+#ifndef DTW_CODE_PRIO
+#define DTW_CODE_PRIO 2           // s_setprio of the code wave (A/B: 0, 1, 2, 3)
+#endif
+#ifndef DTW_AUX_PRIO
+#define DTW_AUX_PRIO 0            // s_setprio of the ring feeder and the edge poller (A/B)
+#endif
 #ifndef DTW_OQ_CFG
 #define DTW_OQ_CFG 32
 #endif
@@ -715,6 +721,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
 
   if (wave == FEEDER_WAVE || wave == EDGE_WAVE) {
     // ------------------------------------------------ ring feeder / edge poller
+    if (DTW_AUX_PRIO) __builtin_amdgcn_s_setprio(DTW_AUX_PRIO);
     // two waves, so the edge poll's global-load latency never delays a ring refill
     const bool do_ring = wave == FEEDER_WAVE;
     int64_t nextblk = 0, have = 0;
@@ -837,9 +844,12 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
 
   if (wave == CODE_WAVE) {
     // --------------------------------------------------------------- code wave
-#ifdef DTW_CODE_PRIO   // A/B: the code wave above the distance waves in VALU arbitration
+    // above the distance waves in issue arbitration (below the sweep's 3): the sweep spins on
+    // the code wave's progress once the C ring is full, and the four distance waves, which run
+    // ahead of the sweep, otherwise take the code wave's issue slots.  Trace of a C5 call
+    // (profiles/r04j_c5_band_trace.txt): half of the sweep's spins were on the code wave.
+    // Measured (profiles/r04k_ab.log): C5 1,862-1,880 -> 2,087-2,116 pairs/s.
     __builtin_amdgcn_s_setprio(DTW_CODE_PRIO);
-#endif
     // step s, lane l: up = C of lane l-1 at step s-1, left = own at s-1, diag = lane l-1 at s-2;
     // lane 0's left neighbour is the band's top edge: C[64b][s+1] / C[64b][s]
     __attribute__((address_space(1))) uint32_t* Db = DTW_GLOBAL(a.Dn) + ((b * a.SW) << 6) + lane;
