@@ -1641,24 +1641,20 @@ __global__ __launch_bounds__(256) void dtw_path_points_kernel(const uint32_t* co
   const uint32_t x = codes[w];
   const int n = (int)(P - 16 * w < 16 ? P - 16 * w : 16);
   int i = wstart[w].x, j = wstart[w].y;
-  double c[16];
-  int ii[16], jj[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    ii[k] = i; jj[k] = j;
-    c[k] = 0.0;
-    if (Cn && k < n && i > 0 && j > 0) c[k] = __dsub_rn(cn_at(Cn, S, i, j), cn_at(Cn, S, i - 1, j - 1));
-    const uint32_t m = (x >> (2 * k)) & 3u;
-    i -= m != 1u;
-    j -= m != 0u;
-  }
+  // one move at a time, stored at once (no per-word arrays: 108 -> ~30 VGPRs, so these blocks fit
+  // on a CU beside the band kernel's two under C5)
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     if (k < n) {
       const int64_t f = P - 1 - (16 * w + k);
-      pq[f] = ii[k] - 1; pr[f] = jj[k] - 1;
-      if (Cn || ii[k] == 0 || jj[k] == 0) pc[f] = c[k];   // (CK mode: the tile pass writes the rest)
+      pq[f] = i - 1; pr[f] = j - 1;
+      double c = 0.0;
+      if (Cn && i > 0 && j > 0) c = __dsub_rn(cn_at(Cn, S, i, j), cn_at(Cn, S, i - 1, j - 1));
+      if (Cn || i == 0 || j == 0) pc[f] = c;            // (CK mode: the tile pass writes the rest)
     }
+    const uint32_t m = (x >> (2 * k)) & 3u;
+    i -= m != 1u;
+    j -= m != 0u;
   }
 }
 

@@ -257,7 +257,18 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     }
   };
 
+  // Phase-dependent issue priority (HL_PRIO).  1 (default): a wave in the LDS-bound epilogue
+  // (pass 3, power rows, filterbank, ln, DCT: five LDS phases, few VALU) issues ahead of the waves
+  // in the VALU-bound FFT passes, so its short VALU bursts between LDS round trips are not queued
+  // behind 3-6 wave-instructions of FFT arithmetic, and its LDS traffic overlaps their VALU work.
+  // Same-box A/B (profiles/r04n_ab.log): 0.475-0.481 ms against 0.505-0.509 ms at priority 0;
+  // 2 (the reverse) 0.483-0.492 ms.
+#ifndef HL_PRIO
+#define HL_PRIO 1
+#endif
   auto process = [&](int64_t pi, const float (&xr)[16], const float (&xi)[16]) {
+    if (HL_PRIO == 1 || HL_PRIO >= 3) __builtin_amdgcn_s_setprio(0);
+    if (HL_PRIO == 2) __builtin_amdgcn_s_setprio(1);
     cf v[16];
 #pragma unroll
     for (int a = 0; a < 16; a++) v[a] = {xr[a] * win[a], xi[a] * win[a]};
@@ -295,6 +306,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     dft8<8, 1>(v);
 #pragma unroll
     for (int c = 1; c < 8; c++) { v[c] = cmul(v[c], tw2[c]); v[8 + c] = cmul(v[8 + c], tw2[c]); }
+    if (HL_PRIO == 3) __builtin_amdgcn_s_setprio(1);     // A/B: from the T2 transpose on
     // ---- T2: LDS transpose into the combo layout ---------------------------------
     if (kl != 0) {
 #pragma unroll
@@ -316,6 +328,9 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       v[j] = {u.x, u.y};
     }
     wave_lds_sync();
+    if (HL_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    if (HL_PRIO == 4) __builtin_amdgcn_s_setprio(3);     // A/B: the epilogue at the top level
+    if (HL_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     // ---- pass 3: DFT8 over b0 for both combos --------------------------------------
     dft8<0, 1>(v);    // A[c1] = Z[rA + 128 c1]
     dft8<8, 1>(v);    // B[c1] = Z[rB + 128 c1]

@@ -77,13 +77,16 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // Energy.ComputeShortTimeEnergy (energy.go:25-50) of pre-emphasised frames, every lane one frame:
 // Go's order needs each frame's sum as ONE sequential chain, so the lane count is the frame count.
-// A wave owns 64 consecutive frames and walks them in rounds of kEnP samples: each round it loads
-// the 64 frames' next kEnP samples with 4-row x 16-column coalesced loads (the next round's are in
-// flight while this one runs), transposes them through a wave-private LDS tile [frame][kEnP + 2]
-// (row stride 144 B: the lanes' b128 reads hit distinct banks), and every lane adds its frame's
-// kEnP terms.  Same operations in the same order as Go: y = x - alpha x_prev, ss += y * y,
-// sqrt(ss / W).  36 KB of LDS per 4-wave block, no span limit (any W, H).
-constexpr int kEnP = 16;                 // samples per round
+// A wave owns 64 consecutive frames and walks them in rounds of kEnP = 8 samples: each round it
+// loads the 64 frames' next 8 samples (8 rows x 8 columns per load instruction), transposes them
+// through a wave-private LDS tile [frame][10 doubles] (row stride 80 B: the lanes' b128 reads hit
+// distinct banks), and every lane adds its frame's 8 terms.  Same operations in the same order as
+// Go: y = x - alpha x_prev, ss += y * y, sqrt(ss / W).  No span limit (any W, H).
+// Footprint sized for C5, where these blocks run beside the DTW band kernel's two blocks per CU
+// (104 KB of LDS, 4 waves x 104 VGPRs per SIMD): 20 KB of LDS per 4-wave block and 54 VGPRs (no
+// register prefetch of the next round), so one fits next to them.  (The first round-4 form --
+// 16-sample rounds, 37 KB, 148 VGPRs with the prefetch -- fitted beside none.)
+constexpr int kEnP = 8;                  // samples per round
 constexpr int kEnRow = kEnP + 2;         // LDS row stride in doubles
 
 template <bool BJ>
@@ -100,25 +103,26 @@ __global__ __launch_bounds__(256) void energy_wave_kernel(const void* pcm, int p
   const int64_t f0 = ((int64_t)blockIdx.x * 4 + w) * 64;        // this wave's first frame
   if (f0 >= Fe) return;
   double* tl = tile[w];
-  // loader role: round sample (row r = 4 i + lane / 16, column c = lane % 16)
-  const int lr = lane >> 4, lc = lane & 15;
-  auto load_round = [&](int k0, double (&v)[16]) {
+  // loader role: round sample (row r = 8 i + lane / 8, column c = lane % 8)
+  const int lr = lane >> 3, lc = lane & 7;
+  auto load_round = [&](int k0, double (&v)[8]) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int64_t g = (f0 + 4 * i + lr) * (int64_t)H + k0 + lc;
+    for (int i = 0; i < 8; ++i) {
+      const int64_t g = (f0 + 8 * i + lr) * (int64_t)H + k0 + lc;
       v[i] = g < n ? pre_x(pcm, pcm_f64, g) : 0.0;
     }
   };
   const int64_t s = (f0 + lane) * (int64_t)H;                    // this lane's frame start
   double prev = (s > 0 && s - 1 < n) ? pre_x(pcm, pcm_f64, s - 1) : 0.0;
   double ss = 0.0;
-  double nx[16];
-  load_round(0, nx);
   for (int k0 = 0; k0 < W; k0 += kEnP) {
+    {
+      double nx[8];
+      load_round(k0, nx);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) tl[(4 * i + lr) * kEnRow + lc] = nx[i];
+      for (int i = 0; i < 8; ++i) tl[(8 * i + lr) * kEnRow + lc] = nx[i];
+    }
     wave_lds_sync();
-    if (k0 + kEnP < W) load_round(k0 + kEnP, nx);
     double cur[kEnP];
 #pragma unroll
     for (int j = 0; j < kEnP; j += 2) {
@@ -581,26 +585,29 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
 
 // DC removal y[n] = x[n] - x[n-1] + R y[n-1] (dc_removal.go:101-124) followed by pre-emphasis
 // z[n] = y[n] - alpha y[n-1] (pre_emphasis.go:135-155), both from zero state, lane-dense:
-//  * a 256-thread block owns kDcBlk = 4,096 samples, lane c the 16-sample chunk c.  The block stages
+//  * a 256-thread block owns kDcBlk = 2,048 samples, lane c the 8-sample chunk c.  The block stages
 //    its samples (and the one before) in LDS with coalesced loads; every lane runs Go's recurrence
-//    over its chunk from a zero state, which gives the chunk's affine map Y -> e_c + R^16 Y.
+//    over its chunk from a zero state, which gives the chunk's affine map Y -> e_c + R^8 Y.
 //  * an inclusive Kogge-Stone scan of the 256 maps (6 shuffle levels per wave, then the waves'
 //    totals through LDS) gives every chunk's map from the block start.
 //  * pass (1) stores the block's map (its end value from a zero start); pass (2), one wave per
-//    signal, chains the blocks' maps (dc_carry_kernel: Y_b = ends[b] + R^4096 Y_{b-1}); pass (3)
+//    signal, chains the blocks' maps (dc_carry_kernel: Y_b = ends[b] + R^2048 Y_{b-1}); pass (3)
 //    redoes (1)'s scan, takes chunk c's start state from the block's true start, re-runs Go's
 //    recurrence over the chunk and writes z back through LDS with coalesced stores.
 // Every sample goes through Go's sequential recurrence from a start state equal to Go's up to the
 // scan's rounding (a few ulp of |Y|, reassociated affine maps), outputs within ~1e-15 of Go's
 // relative to the signal scale (tests: chroma 1e-9, energies 1e-12, the NCC peak exact).
-// The round-3 form ran 256-sample chunks with 16 of a block's 256 lanes busy.
-constexpr int kDcL = 16;                              // samples per lane
+// The round-3 form ran 256-sample chunks with 16 of a block's 256 lanes busy.  Block size: 18 KB
+// of LDS and <= 96 VGPRs, so one fits on a CU beside the DTW band kernel's two blocks under C5
+// (the first round-4 form, 4,096-sample blocks, needed 35 KB).
+constexpr int kDcL = 8;                               // samples per lane
 constexpr int kDcBlk = 256 * kDcL;                    // samples per block
-__device__ __forceinline__ int dc_slot(int i) { return i + (i >> 4); }   // lane stride 17 doubles
-constexpr int kDcSlots = kDcBlk + 1 + ((kDcBlk + 1) >> 4) + 1;
+static_assert(kDcL == 8, "dc_slot pads one slot per kDcL samples");
+__device__ __forceinline__ int dc_slot(int i) { return i + (i >> 3); }   // lane stride 9 doubles
+constexpr int kDcSlots = kDcBlk + 1 + (kDcBlk + 1) / kDcL + 1;      // > dc_slot(kDcBlk)
 
 template <bool WRITE, bool BJ = false>
-__global__ __launch_bounds__(256) void dc_block_kernel(const double* x, int64_t n, double R, double R16, double alpha,
+__global__ __launch_bounds__(256) void dc_block_kernel(const double* x, int64_t n, double R, double RL, double alpha,
                                                        const double* ystart, double* ends, double* z,
                                                        const MfJob* jobs) {
   SONAR_FEAT_PRIO();
@@ -630,7 +637,7 @@ __global__ __launch_bounds__(256) void dc_block_kernel(const double* x, int64_t 
   for (int j = 0; j < kDcL; ++j)
     if (j < m) e = __dadd_rn(__dsub_rn(v[j + 1], v[j]), __dmul_rn(R, e));
   // inclusive scan of the maps (B, A): (B2, A2) o (B1, A1) = (B2 + A2 B1, A2 A1)
-  double B = e, A = R16;
+  double B = e, A = RL;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const double Bp = __shfl_up(B, d, 64), Ap = __shfl_up(A, d, 64);
@@ -655,16 +662,14 @@ __global__ __launch_bounds__(256) void dc_block_kernel(const double* x, int64_t 
   Be = __dadd_rn(Be, __dmul_rn(Ae, Bw));
   Ae = __dmul_rn(Ae, Aw);
   double y1 = (tid == 0) ? Yb : __dadd_rn(Be, __dmul_rn(Ae, Yb));
-  double out[kDcL];
+  // every lane read its inputs before the scan's barrier above: z goes straight back into xs
+  // (slot c0 + j = sample base + c0 + j), with no register copy of the chunk's outputs
 #pragma unroll
   for (int j = 0; j < kDcL; ++j) {
     const double yv = __dadd_rn(__dsub_rn(v[j + 1], v[j]), __dmul_rn(R, y1));
-    out[j] = __dsub_rn(yv, __dmul_rn(alpha, y1));
+    xs[dc_slot(c0 + j)] = __dsub_rn(yv, __dmul_rn(alpha, y1));
     y1 = yv;
   }
-  __syncthreads();                                     // every lane has its inputs: reuse xs for z
-#pragma unroll
-  for (int j = 0; j < kDcL; ++j) xs[dc_slot(c0 + j)] = out[j];
   __syncthreads();
   for (int i = tid; i < span; i += 256) z[base + i] = xs[dc_slot(i)];
 }
@@ -713,12 +718,12 @@ int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double
   const int64_t T = dc_chunks(n);
   double* ends = scratch;
   double* ystart = scratch + T;
-  const double R16 = dc_pow(R, kDcL), RC = dc_pow(R, kDcBlk);
+  const double RL = dc_pow(R, kDcL), RC = dc_pow(R, kDcBlk);
   const MfJob* none = nullptr;
-  hipLaunchKernelGGL((dc_block_kernel<false>), dim3((unsigned)T), dim3(256), 0, s, x, n, R, R16, 0.0, nullptr, ends,
+  hipLaunchKernelGGL((dc_block_kernel<false>), dim3((unsigned)T), dim3(256), 0, s, x, n, R, RL, 0.0, nullptr, ends,
                      nullptr, none);
   hipLaunchKernelGGL((dc_carry_kernel<false>), dim3(1), dim3(64), 0, s, ends, T, RC, ystart, none);
-  hipLaunchKernelGGL((dc_block_kernel<true>), dim3((unsigned)T), dim3(256), 0, s, x, n, R, R16, alpha, ystart, nullptr,
+  hipLaunchKernelGGL((dc_block_kernel<true>), dim3((unsigned)T), dim3(256), 0, s, x, n, R, RL, alpha, ystart, nullptr,
                      y, none);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
@@ -741,12 +746,12 @@ int launch_music_features_batch(const MfJob* hjobs, const MfJob* djobs, int nj, 
     maxF = std::max(maxF, hjobs[k].F);
   }
   const double R = 0.995, alpha = 0.95;        // music.go:245-259 (dc_removal / pre_emphasis defaults)
-  const double R16 = dc_pow(R, kDcL), RC = dc_pow(R, kDcBlk);
+  const double RL = dc_pow(R, kDcL), RC = dc_pow(R, kDcBlk);
   const dim3 gdc((unsigned)maxT, (unsigned)nj);
-  hipLaunchKernelGGL((dc_block_kernel<false, true>), gdc, dim3(256), 0, s, nullptr, 0, R, R16, 0.0, nullptr, nullptr,
+  hipLaunchKernelGGL((dc_block_kernel<false, true>), gdc, dim3(256), 0, s, nullptr, 0, R, RL, 0.0, nullptr, nullptr,
                      nullptr, djobs);
   hipLaunchKernelGGL((dc_carry_kernel<true>), dim3((unsigned)nj), dim3(64), 0, s, nullptr, 0, RC, nullptr, djobs);
-  hipLaunchKernelGGL((dc_block_kernel<true, true>), gdc, dim3(256), 0, s, nullptr, 0, R, R16, alpha, nullptr, nullptr,
+  hipLaunchKernelGGL((dc_block_kernel<true, true>), gdc, dim3(256), 0, s, nullptr, 0, R, RL, alpha, nullptr, nullptr,
                      nullptr, djobs);
   hipLaunchKernelGGL((energy_wave_kernel<true>), dim3((unsigned)((maxFe + 255) / 256), (unsigned)nj), dim3(256), 0, s,
                      nullptr, 1, 0, 0, W, H, 0.0, nullptr, 1, djobs);

@@ -8,7 +8,7 @@ n=300_000
 x=rng.standard_normal(n)+0.3
 R=0.995; alpha=0.95
 ref=O.preemphasis(O.dc_removal(x,R),alpha)
-L=16; BLK=256*L
+L=8; BLK=256*L
 def pw(r,k):
     v=1.0
     for _ in range(k): v*=r
@@ -20,8 +20,8 @@ def chunk_e(b):
     base=b*BLK
     e=np.zeros(256)
     for c in range(256):
-        s=base+16*c; y=0.0
-        for j in range(16):
+        s=base+L*c; y=0.0
+        for j in range(L):
             if s+j<n: y=(xp[s+j+1]-xp[s+j])+R*y
         e[c]=y
     return e
@@ -59,8 +59,8 @@ for b in range(T):
         else: Be,Ae=B[c-1],A[c-1]
         Be=Be+Ae*Bw; Ae=Ae*Aw
         y1=Yb if c==0 else Be+Ae*Yb
-        s=base+16*c
-        for j in range(16):
+        s=base+L*c
+        for j in range(L):
             if s+j>=n: break
             yv=(xp[s+j+1]-xp[s+j])+R*y1
             z[s+j]=yv-alpha*y1; y1=yv
