@@ -443,6 +443,9 @@ constexpr int DTW_DQ = DTW_DQ_CFG;         // steps of distances held in LDS (a 
 #ifndef DTW_CODE_PRIO
 #define DTW_CODE_PRIO 2           // s_setprio of the code wave (A/B: 0, 1, 2, 3)
 #endif
+#ifndef DTW_DIST_PRIO
+#define DTW_DIST_PRIO 0           // s_setprio of the distance waves (A/B)
+#endif
 #ifndef DTW_AUX_PRIO
 #define DTW_AUX_PRIO 0            // s_setprio of the ring feeder and the edge poller (A/B)
 #endif
@@ -946,6 +949,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
 
   if (wave >= 1) {   // (every other role returned above)
     // ---------------------------------------------------------- distance waves
+    if (DTW_DIST_PRIO) __builtin_amdgcn_s_setprio(DTW_DIST_PRIO);
     const int w = dtw_dist_index(wave);
     for (int64_t c = w; DTW_ECH * c < S; c += DTW_NDW) {
       const int64_t t0 = DTW_ECH * c;
@@ -1807,9 +1811,9 @@ __global__ void nonfinite_kernel(const double* x, int64_t n, int32_t* flag) {
 
 // the probe over both sequences of every DTW of a batch (blockIdx.y = the DTW): one launch per
 // batch instead of two per pair on the batch's stream
-// Also fills the DTW's band-edge rows E with the sentinel the band kernel polls for (what a
-// hipMemsetD32Async per batch did before: one launch fewer per batch).  Same stream, earlier
-// kernel: the stores are visible to the band kernel's sc1 polls.
+// Also fills the DTW's band-edge rows E with the sentinel the band kernel polls for and zeroes its
+// path-tile run counters (what a hipMemsetD32Async and a hipMemsetAsync per batch did before).
+// Same stream, earlier kernel: the stores are visible to the band kernel's sc1 polls.
 __global__ void nonfinite_batch_kernel(const DtwArgs* args) {
   const DtwArgs a = load_args_uniform(args + blockIdx.y);
   const int64_t nqe = a.nq * a.dim, n = nqe + a.nr * a.dim;
@@ -1820,6 +1824,10 @@ __global__ void nonfinite_batch_kernel(const DtwArgs* args) {
     const int64_t ne = (a.nb - 1) * (a.nr + 1);
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ne; k += stride)
       a.E[k] = 0x7FF000017FF00001ull;
+  }
+  if (a.runs) {     // the path-tile run counters (dtw_run_words), read after the band kernel
+    const int64_t nw = a.nb + (a.nr + 63) / 64 + 2;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nw; k += stride) a.runs[k] = 0;
   }
 }
 

@@ -274,9 +274,13 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* E = (char*)dbuf(w, "pb.E", e_b);
   char* codes = (char*)dbuf(w, "pb.codes", codes_b);
   char* wst = (char*)dbuf(w, "pb.wstart", wst_b);
-  char* path = (char*)dbuf(w, "pb.path", path_b);
-  char* corr = (char*)dbuf(w, "pb.corr", corr_b);
-  char* small = (char*)dbuf(w, "pb.small", stat_b + diag_b + args_b + start_b + map_b);
+  // small holds, in the pinned host buffer's layout: status words + ticket, diagnostic records, DTW
+  // arguments, ticket starts, band-major map, correlations, paths -- so the batch's results come
+  // back in ONE copy (each runtime copy is a blit kernel that needs a CU beside the band blocks)
+  const size_t small_b = stat_b + diag_b + args_b + start_b + map_b + corr_b + path_b;
+  char* small = (char*)dbuf(w, "pb.small", small_b);
+  char* corr = small ? small + (stat_b + diag_b + args_b + start_b + map_b) : nullptr;
+  char* path = small ? corr + corr_b : nullptr;
   // SONAR_DTW_TRACE=<file> (diagnostics): every band's sweep timestamps (dtw_band_kernel's trace
   // words) appended to <file> as {pair, band, 8 trace words} records
   const char* trace_path = std::getenv("SONAR_DTW_TRACE");
@@ -313,7 +317,6 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* hcorr = h + ab + args_b + start_b + map_b;
   char* hpath = hcorr + corr_b;
   HIP_TRY(w, hipMemsetAsync(small, 0, stat_b + diag_b, s));
-  HIP_TRY(w, hipMemsetAsync(runs, 0, runs_b, s));
   // every pair's music features and energy NCC: batched launches over the whole batch when the
   // inputs are on the device and every signal fits the batched kernels (feat_batch), else pair by
   // pair on the worker's scratch
@@ -372,9 +375,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s, dmap) != 0)
     return fail(w, SONAR_ERR_DEVICE, "dtw batch launch failed");
 #endif
-  HIP_TRY(w, hipMemcpyAsync(hstat, small, stat_b + diag_b, hipMemcpyDeviceToHost, s));
-  if (corr_b) HIP_TRY(w, hipMemcpyAsync(hcorr, corr, corr_b, hipMemcpyDeviceToHost, s));
-  HIP_TRY(w, hipMemcpyAsync(hpath, path, path_b, hipMemcpyDeviceToHost, s));
+  HIP_TRY(w, hipMemcpyAsync(hstat, small, small_b, hipMemcpyDeviceToHost, s));
   std::vector<uint64_t> htr(trb ? (size_t)total_bands * 8 : 0);
   if (trb) HIP_TRY(w, hipMemcpyAsync(htr.data(), trb, htr.size() * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(w, hipStreamSynchronize(s));

@@ -11,6 +11,15 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     python3 "$R/bench.py" > "$OUT/bench_traced.log" 2>&1 || { echo "trace pass failed"; exit 1; }
 rm -f "$OUT"/trace/*_kernel_trace.csv   # per-dispatch rows: tens of MB, the stats CSV is the summary
 echo "trace done"
+# the headline alone under the tracer, 200 timed steps after 20 warm-up steps: the stats average is
+# then steady-state launches only, and the same traced run's own JSON line (its HIP-event
+# kernel_ms and ms_per_step) is the like-for-like comparison
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/hl_trace" -o run -- \
+    python3 "$R/bench.py" --no-cpu-baseline --no-f64 --dtw-len 0 --c5-pairs 0 --c3-seconds 0 --c4-seconds 0 --c6-gallery 0 --c7-seconds 0 --ingest-reps 0 --steps 200 --warmup 20 > "$OUT/hl_traced.json" 2> "$OUT/hl_traced.err" || { echo "headline trace failed"; exit 1; }
+rm -f "$OUT"/hl_trace/*_kernel_trace.csv
+f=$(find "$OUT/hl_trace" -name '*kernel_stats.csv' | head -1)
+cp "$f" "$R/gpurun_out/${TAG}_headline_kernel_stats.csv"; cp "$OUT/hl_traced.json" "$R/gpurun_out/${TAG}_headline_traced.json"
+echo "headline trace done"
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/$c" -o run -- \
       python3 "$R/bench.py" --no-cpu-baseline --dtw-len 0 --c5-pairs 0 --c6-gallery 0 --c7-seconds 0 --ingest-reps 0 --no-f64 --c3-seconds 0 --c4-seconds 0 --steps 5 --warmup 1 > "$OUT/$c.log" 2>&1 \
