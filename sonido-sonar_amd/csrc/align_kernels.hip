@@ -444,7 +444,8 @@ constexpr int DTW_DQ = DTW_DQ_CFG;         // steps of distances held in LDS (a 
 #define DTW_CODE_PRIO 2           // s_setprio of the code wave (A/B: 0, 1, 2, 3)
 #endif
 #ifndef DTW_DIST_PRIO
-#define DTW_DIST_PRIO 0           // s_setprio of the distance waves (A/B)
+#define DTW_DIST_PRIO 0           // s_setprio of the distance waves (A/B; 1 starved the feeder / edge
+                                  // poller into 1 s band timeouts, profiles/r04pq_ab.log)
 #endif
 #ifndef DTW_AUX_PRIO
 #define DTW_AUX_PRIO 0            // s_setprio of the ring feeder and the edge poller (A/B)
