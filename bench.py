@@ -54,8 +54,11 @@ FP32_PEAK_TFS = 157.3                            # FP32 vector (= f32 MFMA) peak
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # headline steps are ~0.5 ms launches: 20 untimed warm-up steps let the clocks settle after
+    # the process's first GPU work (round 4: 200-step runs timed 0.45 ms per launch, 20-step runs
+    # after 3 warm-ups 0.46-0.49 ms on the same build), 50 timed steps are still ~25 ms
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--seconds", type=float, default=3600.0, help="audio seconds per GPU (1 h config)")
     ap.add_argument("--dtw-len", type=int, default=51676, help="DTW sequence length (0 = skip); C3 = 51,676")
     ap.add_argument("--dtw-steps", type=int, default=3)
