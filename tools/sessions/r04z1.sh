@@ -1,4 +1,4 @@
-# Round-4 final evidence, part 1 (tools/r04z2.sh is part 2): PMC passes on the final HEAD (DTW band
+# Round-4 final evidence, part 1 (tools/sessions/r04z2.sh is part 2): PMC passes on the final HEAD (DTW band
 # kernel at C3 size, headline kernel) and the C5 kernel families; the summaries the bench line
 # reads (profiles/*dtw_pmc*, *_c5_families) are committed before part 2 runs the bench.
 set -o pipefail
