@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--c3-seconds", type=float, default=300.0, help="C3 stream length (0 = skip)")
     ap.add_argument("--c4-seconds", type=float, default=1800.0, help="C4 speech length at 16 kHz (0 = skip)")
     ap.add_argument("--ingest-reps", type=int, default=3, help="row f3 PCM-ingest repetitions (0 = skip)")
+    ap.add_argument("--batch-signals", type=int, default=1000,
+                    help="sonar_fingerprint_batch leg: short streams in one batch (0 = skip)")
+    ap.add_argument("--batch-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES for this process (0 = leave as is)")
     ap.add_argument("--cpu-seconds", type=float, default=0.0, help="force CPU-baseline sample length")
@@ -765,6 +768,50 @@ def c6_cpu_baseline(args):
                       "statistics per call as comparison.go does, float64, 1 thread"}
 
 
+def bench_fp_batch(args, ctx, dev, cfg):
+    """sonar_fingerprint_batch (SpectralAnalyzer.ComputeSTFTBatch, spectral.go:234-285) over many short
+    device-resident streams with the headline configuration: ONE mfcc_pair_kernel launch for the batch,
+    against a loop of per-signal sonar_fingerprint calls (the same kernel, one launch per signal).
+    Wall time per batch on the ctx stream, median of --reps; rows checked equal between the two."""
+    k, secs = args.batch_signals, args.batch_seconds
+    rng = np.random.default_rng(11)
+    lens = [int(secs * SR) + int(rng.integers(0, 4096)) for _ in range(k)]
+    gen = torch.Generator(device=dev).manual_seed(5)
+    sigs = [0.3 * torch.randn(L, device=dev, dtype=torch.float32, generator=gen) for L in lens]
+    Fs = [sonar.stft_frames(L, cfg.window_size, cfg.hop_size) for L in lens]
+    nc = cfg.n_mfcc
+    outs_b = [torch.empty((f, nc), device=dev) for f in Fs]
+    outs_s = [torch.empty((f, nc), device=dev) for f in Fs]
+    ptrs = [x.data_ptr() for x in sigs]
+    pb, ps = [o.data_ptr() for o in outs_b], [o.data_ptr() for o in outs_s]
+
+    def batch():
+        ctx.fingerprint_batch_device(ptrs, lens, pb, cfg)
+
+    def loop():
+        for p_, L, o in zip(ptrs, lens, ps):
+            ctx.fingerprint_device(p_, L, cfg, mfcc=o)
+
+    times = {}
+    for name, fn in (("batch", batch), ("loop", loop)):
+        fn()
+        torch.cuda.synchronize(dev)
+        ts = []
+        for _ in range(max(args.reps, 1)):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        times[name] = float(np.median(ts))
+    same = all(torch.equal(a, b) for a, b in zip(outs_b, outs_s))
+    Ft = int(sum(Fs))
+    return {"fp_batch": {"entry": "sonar_fingerprint_batch", "signals": k, "seconds_per_signal": secs,
+                         "frames": Ft, "batch_ms": times["batch"] * 1e3, "batch_frames_per_s": Ft / times["batch"],
+                         "loop_ms": times["loop"] * 1e3, "loop_frames_per_s": Ft / times["loop"],
+                         "speedup_vs_loop": times["loop"] / times["batch"], "rows_equal_single_calls": bool(same),
+                         "note": "device-resident f32 streams, wall time incl. host launch overhead"}}
+
+
 def bench_ingest(args, ctx, pcm, cfg, F):
     """Row f3: the decoder's f64le byte stream of this rank's hour
     (Decoder.bytesToFloat64, transcode/decoder.go:850-871) from pageable host memory into device
@@ -892,6 +939,8 @@ def main():
                                      parity=rank == 0 and world == 1 and not args.no_cpu_baseline))
     if args.ingest_reps > 0:
         leg("ingest", lambda: bench_ingest(args, ctx, pcm, cfg, F))
+    if args.batch_signals > 0:
+        leg("fp_batch", lambda: bench_fp_batch(args, ctx, dev, cfg))
     if args.c5_pairs > 0:
         leg("c5", lambda: bench_c5(args, world, rank, dev, ctx))
         if rank == 0 and world == 1 and not args.no_cpu_baseline:

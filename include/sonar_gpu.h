@@ -15,6 +15,7 @@
  *                                 SpeechFeatureExtractor.extractSpectralFeatures
  *                                 (fingerprint/extractors/speech.go:320) and
  *                                 Energy.ComputeShortTimeEnergy (algorithms/temporal/energy.go:25)
+ *   sonar_fingerprint_batch    <- SpectralAnalyzer.ComputeSTFTBatch (fingerprint/analyzers/spectral.go:234)
  *   sonar_pitch_yin            <- PitchDetector.DetectPitch per-frame YIN core
  *                                 (algorithms/tonal/pitch_detection.go:225-420)
  *   sonar_chroma_stft          <- MusicFeatureExtractor.extractChromaFeatures
@@ -194,6 +195,16 @@ void sonar_fp_cfg_default(sonar_fp_cfg* cfg);
  * spectral descriptors -> SONAR_ERR_UNSUPPORTED), as go-dsp's FFTReal takes any length. */
 int sonar_fingerprint(sonar_ctx* ctx, const void* pcm, int64_t n, const sonar_fp_cfg* cfg,
                       sonar_fp_out* out);
+/* SpectralAnalyzer.ComputeSTFTBatch (fingerprint/analyzers/spectral.go:234-285): sonar_fingerprint
+ * of `count` signals with one configuration; out[i] receives signal i's outputs (sizes as for
+ * sonar_fingerprint with n[i]).  count <= 0 -> SONAR_ERR_EMPTY "no signals provided"; the first
+ * failing signal by index -> its code with "error processing signal i: <message>" (:276-281), and
+ * nothing is launched when a signal fails ComputeSTFTWithWindow's argument checks.  The f32 MFCC
+ * configuration at W = 1024 (flags == SONAR_FP_MFCC, precision / pcm_dtype / out_dtype F32) runs
+ * every signal's frames in ONE mfcc_pair_kernel launch; other configurations run sonar_fingerprint
+ * per signal on the ctx stream.  cfg->device_ptrs applies to every pcm[i] and out[i] buffer. */
+int sonar_fingerprint_batch(sonar_ctx* ctx, const void* const* pcm, const int64_t* n, int32_t count,
+                            const sonar_fp_cfg* cfg, sonar_fp_out* out);
 
 /* ---- PCM ingest: the decoder's f64le byte stream -> device samples.
  * Replaces Decoder.bytesToFloat64 + processFFmpegOutput's empty check (transcode/decoder.go:850-871,

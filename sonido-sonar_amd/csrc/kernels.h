@@ -90,6 +90,10 @@ struct MfccPairParams {
   float* out;           // [F][n_mfcc]
   int lds_src, lds_dct, lds_wave0, lds_bytes;
   int waves_per_block;  // 4 (mfcc_pair_kernel)
+  // sonar_fingerprint_batch: nseg > 0 signals, F = 2 x the batch's pairs, pcm / n / out unused;
+  // seg (device) = {pcm address[nseg], n[nseg], F[nseg], out address[nseg], first pair[nseg + 1]}
+  const int64_t* seg;
+  int nseg;
 };
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s);
 int mfcc_pair_wave_bytes();

@@ -27,6 +27,8 @@
 //    filterbank as per-lane bin chunks of one filter pair each (rise/fall
 //    partials, weights from an LDS table), partial sums -> ln -> DCT (+lifter)
 //    on 52 lanes, coalesced stores.
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace sonar {
@@ -178,7 +180,9 @@ constexpr int kLogOff = kPartOff + 64 * 16;   // logmel [2][NMP]
 
 // JT / MS / NH: compile-time chunk length, sources per filter and DCT half-length for the
 // headline bank (40 mels at 44.1 kHz: 12 / 8 / 20); 0 = read from p (runtime loops).
-template <bool POW2, int JT, int MS, int NH>
+// SEG: a batch of signals (sonar_fingerprint_batch) -- p.seg is the segment table, the pair index
+// runs over all signals' frame pairs, and each wave follows its range across signal boundaries.
+template <bool POW2, int JT, int MS, int NH, bool SEG>
 __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
@@ -234,21 +238,56 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   const int64_t NP = (p.F + 1) >> 1;
   if (pb >= NP) return;
   const int64_t pe = min(NP, pb + p.pairs_per_wave);
-  const float* pcm = p.pcm;
   const int H = p.H;
 
-  auto frame_ok = [&](int64_t t) { return t < p.F && t * (int64_t)H + 1024 <= p.n; };
+  // The signal a pair belongs to (wave-uniform).  One signal: pairs [0, NP) of p.pcm / p.out.  SEG:
+  // seg = {pcm address[nseg], n[nseg], F[nseg], out address[nseg], first pair[nseg + 1]}; the
+  // loads (one pair ahead) and the processing each keep their own cursor, advanced monotonically.
+  struct Sig { const float* pcm; int64_t n, F; float* out; int64_t p0, p1; int s; };
+  // The table is read with vector loads (the kernel's stores keep it off the scalar cache); the
+  // values are wave-uniform, so readfirstlane parks them in SGPRs.
+  auto ld = [&](int i) {
+    const int64_t v = p.seg[i];
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  };
+  auto sig_at = [&](int s) {
+    const int ns = p.nseg;
+    Sig g;
+    g.pcm = reinterpret_cast<const float*>(ld(s)); g.n = ld(ns + s); g.F = ld(2 * ns + s);
+    g.out = reinterpret_cast<float*>(ld(3 * ns + s)); g.p0 = ld(4 * ns + s); g.p1 = ld(4 * ns + s + 1);
+    g.s = s;
+    return g;
+  };
+  Sig gl, gp;
+  if (SEG) {
+    int lo = 0, hi = p.nseg - 1;                        // last signal whose first pair <= pb
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (ld(4 * p.nseg + mid) <= pb) lo = mid; else hi = mid - 1;
+    }
+    gl = sig_at(lo);
+  } else {
+    gl = Sig{p.pcm, p.n, p.F, p.out, 0, NP, 0};
+  }
+  gp = gl;
+  auto advance = [&](Sig& g, int64_t pi) {
+    if (SEG) while (pi >= g.p1) g = sig_at(g.s + 1);
+  };
+
+  auto frame_ok = [&](const Sig& g, int64_t t) { return t < g.F && t * (int64_t)H + 1024 <= g.n; };
   auto load_pair = [&](int64_t pi, float (&xr)[16], float (&xi)[16]) {
-    const int64_t t = 2 * pi;
-    const float* b0p = pcm + t * (int64_t)H + lane;
-    if (frame_ok(t)) {
+    advance(gl, pi);
+    const int64_t t = 2 * (pi - gl.p0);
+    const float* b0p = gl.pcm + t * (int64_t)H + lane;
+    if (frame_ok(gl, t)) {
 #pragma unroll
       for (int a = 0; a < 16; a++) xr[a] = b0p[64 * a];
     } else {
 #pragma unroll
       for (int a = 0; a < 16; a++) xr[a] = 0.f;
     }
-    if (frame_ok(t + 1)) {
+    if (frame_ok(gl, t + 1)) {
 #pragma unroll
       for (int a = 0; a < 16; a++) xi[a] = b0p[H + 64 * a];
     } else {
@@ -267,6 +306,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 #define HL_PRIO 1
 #endif
   auto process = [&](int64_t pi, const float (&xr)[16], const float (&xi)[16]) {
+    advance(gp, pi);
     if (HL_PRIO == 1 || HL_PRIO >= 3) __builtin_amdgcn_s_setprio(0);
     if (HL_PRIO == 2) __builtin_amdgcn_s_setprio(1);
     cf v[16];
@@ -396,8 +436,8 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     wave_lds_sync();
     // ---- DCT-II (+ lifter): lane = q + 16 f + 32 h, half h of the filters ----------------
 #ifdef MFCC_DBG_NODCT   // A/B diagnostics: the DCT's share of the kernel (the most MFMA could save)
-    if ((lane & 15) < p.n_mfcc && (lane >> 5) == 0 && 2 * pi + ((lane >> 4) & 1) < p.F)
-      p.out[(2 * pi + ((lane >> 4) & 1)) * p.n_mfcc + (lane & 15)] = reinterpret_cast<const float*>(wb + kLogOff)[lane & 15];
+    if ((lane & 15) < p.n_mfcc && (lane >> 5) == 0 && 2 * (pi - gp.p0) + ((lane >> 4) & 1) < gp.F)
+      gp.out[(2 * (pi - gp.p0) + ((lane >> 4) & 1)) * p.n_mfcc + (lane & 15)] = reinterpret_cast<const float*>(wb + kLogOff)[lane & 15];
     if (false)
 #endif
     {
@@ -414,8 +454,8 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       }
       const auto r = __builtin_amdgcn_permlane32_swap(u_of(s), u_of(s), false, false);
       s += f_of(r[1]);                                          // lanes < 32: + lane + 32
-      const int64_t t = 2 * pi + f;
-      if (hh == 0 && q < p.n_mfcc && t < p.F) p.out[t * p.n_mfcc + q] = s;
+      const int64_t t = 2 * (pi - gp.p0) + f;
+      if (hh == 0 && q < p.n_mfcc && t < gp.F) gp.out[t * p.n_mfcc + q] = s;
     }
     wave_lds_sync();
   };
@@ -437,8 +477,12 @@ int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   const int64_t waves = (NP + p.pairs_per_wave - 1) / p.pairs_per_wave;
   const int64_t grid = (waves + 3) / 4;
   const bool head = p.J == 12 && p.max_src <= 8 && p.NMP == 40;
-  auto kern = p.pow2 ? (head ? mfcc_pair_kernel<true, 12, 8, 20> : mfcc_pair_kernel<true, 0, 0, 0>)
-                     : (head ? mfcc_pair_kernel<false, 12, 8, 20> : mfcc_pair_kernel<false, 0, 0, 0>);
+  auto pick = [&](auto seg) {
+    constexpr bool S = decltype(seg)::value;
+    return p.pow2 ? (head ? mfcc_pair_kernel<true, 12, 8, 20, S> : mfcc_pair_kernel<true, 0, 0, 0, S>)
+                  : (head ? mfcc_pair_kernel<false, 12, 8, 20, S> : mfcc_pair_kernel<false, 0, 0, 0, S>);
+  };
+  auto kern = p.nseg > 0 ? pick(std::true_type{}) : pick(std::false_type{});
   if (p.lds_bytes > 64 * 1024)
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), p.lds_bytes, s, p);

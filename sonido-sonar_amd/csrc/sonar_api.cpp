@@ -420,6 +420,43 @@ void sonar_fp_cfg_default(sonar_fp_cfg* c) {
 // ======================================================= sonar_fingerprint ==
 }  // extern "C"
 
+namespace {
+// the headline kernel's tables for a configuration, built once per context
+const PairTables& pair_tables_for(sonar_ctx* c, const sonar_fp_cfg* cfg) {
+  char key[512];
+  std::snprintf(key, sizeof(key), "%d|%d|%d|%d|%.17g|%.17g|%d|%.17g|%d|%d", cfg->window_type, cfg->sample_rate,
+                cfg->n_mfcc, cfg->n_filters, cfg->low_freq, cfg->high_freq, cfg->use_lifter, cfg->lifter,
+                cfg->filterbank, cfg->mfcc_input_power);
+  auto it = c->pair_tables.find(key);
+  if (it == c->pair_tables.end()) {
+    PairTables t;
+    build_pair_tables(cfg, t);
+    it = c->pair_tables.emplace(key, t).first;
+  }
+  return it->second;
+}
+
+// tables, LDS carve and work split of one mfcc_pair_kernel launch over NP frame pairs
+void fill_pair_params(sonar_ctx* c, const PairTables& t, const sonar_fp_cfg* cfg, int64_t NP,
+                      sonar::MfccPairParams& q) {
+  q.window = t.window; q.tw1 = (const float2*)t.tw1; q.tw2 = (const float2*)t.tw2;
+  q.chunk_ks = t.chunk_ks; q.chunk_w = (const float2*)t.chunk_w; q.mel_src = t.mel_src; q.dct = t.dct;
+  q.J = t.J; q.JS = t.JS; q.max_src = t.max_src; q.NMP = t.NMP; q.n_mels = t.n_mels; q.n_mfcc = t.n_mfcc;
+  q.pow2 = cfg->mfcc_input_power != 0;
+  auto al = [](int x) { return (x + 15) & ~15; };
+  q.lds_src = al(64 * t.JS * 8);
+  q.lds_dct = q.lds_src + 64 * 16 * 2;
+  q.lds_wave0 = q.lds_dct + al(16 * (t.NMP + 4) * 4);
+  // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU
+  q.waves_per_block = 4;
+  q.lds_bytes = q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes();
+  int dev_cus = 256;
+  hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  const int64_t target_waves = (int64_t)dev_cus * 12;
+  q.pairs_per_wave = std::max<int64_t>(1, (NP + target_waves - 1) / target_waves);
+}
+}  // namespace
+
 namespace sonar {
 namespace detail {
 // pcm_dev: pcm is already device memory even though the outputs are host buffers
@@ -552,35 +589,12 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
                                   SONAR_FP_GENERIC | 0x80000000u));
   bool pair_done = false;
   if (pair_ok) {
-    char key[512];
-    std::snprintf(key, sizeof(key), "%d|%d|%d|%d|%.17g|%.17g|%d|%.17g|%d|%d", cfg->window_type, cfg->sample_rate,
-                  cfg->n_mfcc, cfg->n_filters, cfg->low_freq, cfg->high_freq, cfg->use_lifter, cfg->lifter,
-                  cfg->filterbank, cfg->mfcc_input_power);
-    auto it = c->pair_tables.find(key);
-    if (it == c->pair_tables.end()) {
-      PairTables t;
-      build_pair_tables(cfg, t);
-      it = c->pair_tables.emplace(key, t).first;
-    }
-    const PairTables& t = it->second;
+    const PairTables& t = pair_tables_for(c, cfg);
     if (t.ok) {
       sonar::MfccPairParams q{};
+      fill_pair_params(c, t, cfg, (F + 1) / 2, q);
       q.pcm = (const float*)dpcm; q.n = n; q.F = F; q.H = H;
-      q.window = t.window; q.tw1 = (const float2*)t.tw1; q.tw2 = (const float2*)t.tw2;
-      q.chunk_ks = t.chunk_ks; q.chunk_w = (const float2*)t.chunk_w; q.mel_src = t.mel_src; q.dct = t.dct;
-      q.J = t.J; q.JS = t.JS; q.max_src = t.max_src; q.NMP = t.NMP; q.n_mels = t.n_mels; q.n_mfcc = t.n_mfcc; q.pow2 = cfg->mfcc_input_power != 0;
       q.out = (float*)d_mfcc;
-      auto al = [](int x) { return (x + 15) & ~15; };
-      q.lds_src = al(64 * t.JS * 8);
-      q.lds_dct = q.lds_src + 64 * 16 * 2;
-      q.lds_wave0 = q.lds_dct + al(16 * (t.NMP + 4) * 4);
-      // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU
-      q.waves_per_block = 4;
-      q.lds_bytes = q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes();
-      int dev_cus = 256;
-      hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
-      const int64_t NP = (F + 1) / 2, target_waves = (int64_t)dev_cus * 12;
-      q.pairs_per_wave = std::max<int64_t>(1, (NP + target_waves - 1) / target_waves);
       hipEvent_t tend = timed_begin(c, s);
       if (sonar::launch_mfcc_pair(q, s) != 0)
         return fail(c, SONAR_ERR_DEVICE, std::string("mfcc kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -694,6 +708,97 @@ extern "C" {
 
 int sonar_fingerprint(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cfg* cfg, sonar_fp_out* out) {
   return sonar::detail::fingerprint_impl(c, pcm, n, cfg, out, cfg && cfg->device_ptrs != 0);
+}
+
+// SpectralAnalyzer.ComputeSTFTBatch (fingerprint/analyzers/spectral.go:234-285): every signal through
+// ComputeSTFTWithWindow with one configuration; the first failing signal (by index) reports
+// "error processing signal i: <its error>" (:276-281).  The f32 MFCC configuration at W = 1024 runs
+// all signals' frame pairs in ONE mfcc_pair_kernel launch (segment table, mfcc_pair.hip SEG); any
+// other configuration runs sonar_fingerprint per signal on the context's stream.
+int sonar_fingerprint_batch(sonar_ctx* c, const void* const* pcm, const int64_t* n, int32_t count,
+                            const sonar_fp_cfg* cfg, sonar_fp_out* out) {
+  if (!c) return SONAR_ERR_INVALID;
+  if (count <= 0) return fail(c, SONAR_ERR_EMPTY, "no signals provided");
+  if (!pcm || !n || !cfg || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
+  const int W = cfg->window_size, H = cfg->hop_size;
+  auto sig_fail = [&](int i, int code, const std::string& msg) {
+    return fail(c, code, "error processing signal " + std::to_string(i) + ": " + msg);
+  };
+  // ComputeSTFTWithWindow's checks per signal, in its order (spectral.go:386-412)
+  for (int i = 0; i < count; i++) {
+    if (n[i] <= 0 || !pcm[i]) return sig_fail(i, SONAR_ERR_EMPTY, "empty signal");
+    if (W <= 0) return sig_fail(i, SONAR_ERR_INVALID, "window size must be positive");
+    if (H <= 0) return sig_fail(i, SONAR_ERR_INVALID, "hop size must be positive");
+    if (go_frames(n[i], W, H) <= 0)
+      return sig_fail(i, SONAR_ERR_TOO_SHORT, "signal too short for given window size and hop size");
+  }
+  const bool dev = cfg->device_ptrs != 0;
+  const bool one_launch = W == 1024 && cfg->flags == SONAR_FP_MFCC && cfg->precision == SONAR_F32 &&
+                          cfg->pcm_dtype == SONAR_F32 && cfg->out_dtype == SONAR_F32;
+  const PairTables* tp = one_launch ? &pair_tables_for(c, cfg) : nullptr;
+  if (!tp || !tp->ok) {
+    for (int i = 0; i < count; i++) {
+      const int rc = sonar::detail::fingerprint_impl(c, pcm[i], n[i], cfg, &out[i], dev);
+      if (rc != SONAR_OK) return sig_fail(i, rc, c->err);
+    }
+    return SONAR_OK;
+  }
+  const PairTables& t = *tp;
+  for (int i = 0; i < count; i++)
+    if (!out[i].mfcc) return fail(c, SONAR_ERR_INVALID, "out[" + std::to_string(i) + "].mfcc is null");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  // segment table {pcm address, n, F, out address, first pair} and the batch's buffers
+  std::vector<int64_t> seg(5 * (size_t)count + 1);
+  int64_t NP = 0, ns = 0, nf = 0;
+  for (int i = 0; i < count; i++) {
+    const int64_t F = go_frames(n[i], W, H);
+    seg[2 * (size_t)count + i] = F; seg[(size_t)count + i] = n[i];
+    seg[4 * (size_t)count + i] = NP;
+    NP += (F + 1) / 2; ns += n[i]; nf += F;
+  }
+  seg[5 * (size_t)count] = NP;
+  float* dpcm = nullptr;
+  float* dout = nullptr;
+  if (!dev) {
+    dpcm = (float*)dbuf(c, "fpb.pcm", (size_t)ns * 4);
+    dout = (float*)dbuf(c, "fpb.mfcc", (size_t)nf * t.n_mfcc * 4);
+    if (!dpcm || !dout) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (batch)");
+  }
+  int64_t po = 0, fo = 0;
+  for (int i = 0; i < count; i++) {
+    if (dev) {
+      seg[i] = (int64_t)(uintptr_t)pcm[i];
+      seg[3 * (size_t)count + i] = (int64_t)(uintptr_t)out[i].mfcc;
+    } else {
+      HIP_TRY(c, hipMemcpyAsync(dpcm + po, pcm[i], (size_t)n[i] * 4, hipMemcpyHostToDevice, s));
+      seg[i] = (int64_t)(uintptr_t)(dpcm + po);
+      seg[3 * (size_t)count + i] = (int64_t)(uintptr_t)(dout + fo * t.n_mfcc);
+    }
+    po += n[i]; fo += seg[2 * (size_t)count + i];
+  }
+  int64_t* dseg = (int64_t*)dbuf(c, "fpb.seg", seg.size() * 8);
+  if (!dseg) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (batch table)");
+  HIP_TRY(c, hipMemcpyAsync(dseg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, s));
+  sonar::MfccPairParams q{};
+  fill_pair_params(c, t, cfg, NP, q);
+  q.F = 2 * NP; q.H = H;
+  q.seg = dseg; q.nseg = count;
+  hipEvent_t tend = timed_begin(c, s);
+  if (sonar::launch_mfcc_pair(q, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, std::string("mfcc kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+  timed_end(c, s, tend);
+  c->last_fp_kernel = "mfcc_pair_kernel";
+  if (!dev) {
+    fo = 0;
+    for (int i = 0; i < count; i++) {
+      const int64_t F = seg[2 * (size_t)count + i];
+      HIP_TRY(c, hipMemcpyAsync(out[i].mfcc, dout + fo * t.n_mfcc, (size_t)F * t.n_mfcc * 4, hipMemcpyDeviceToHost, s));
+      fo += F;
+    }
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  return SONAR_OK;
 }
 
 // ========================================================= YIN, chroma ====

@@ -185,3 +185,64 @@ func (x *Multi) AlignPairs(queries, references [][]float64, sampleRate, stftWind
 		C.double(maxLagSeconds), C.int32_t(workers), &recs[0])
 	return records(recs), x.err(rc)
 }
+
+// FingerprintBatch32 is SpectralAnalyzer.ComputeSTFTBatch (fingerprint/analyzers/spectral.go:234-285)
+// followed by MFCC.ComputeFrames per signal, on float32 samples (sonar_fingerprint_batch): at
+// W = 1024 every signal's frames run in ONE kernel launch.  Returns one F_i x NumCoefficients
+// matrix per signal; errors name the first failing signal as ComputeSTFTBatch does.
+func (x *Context) FingerprintBatch32(signals [][]float32, windowSize, hopSize, sampleRate int,
+	p MFCCParams) ([][][]float32, error) {
+	k := len(signals)
+	if k == 0 {
+		return nil, fmt.Errorf("no signals provided: %w", ErrEmpty)
+	}
+	var cfg C.sonar_fp_cfg
+	C.sonar_fp_cfg_default(&cfg)
+	cfg.window_size, cfg.hop_size, cfg.sample_rate = C.int32_t(windowSize), C.int32_t(hopSize), C.int32_t(sampleRate)
+	cfg.n_mfcc, cfg.n_filters = C.int32_t(p.NumCoefficients), C.int32_t(p.NumFilters)
+	cfg.low_freq, cfg.high_freq, cfg.lifter = C.double(p.LowFreq), C.double(p.HighFreq), C.double(p.LifterCoeff)
+	cfg.use_lifter = b2i(p.UseLiftering)
+	cfg.flags = C.SONAR_FP_MFCC
+	cfg.precision, cfg.pcm_dtype, cfg.out_dtype = C.SONAR_F32, C.SONAR_F32, C.SONAR_F32
+	nc := p.NumCoefficients
+	if nc <= 0 {
+		nc = 13
+	}
+	var pin runtime.Pinner // the C arrays hold pointers to the Go slices during the call
+	defer pin.Unpin()
+	pp := C.malloc(C.size_t(k) * C.size_t(unsafe.Sizeof(uintptr(0))))
+	defer C.free(pp)
+	op := C.calloc(C.size_t(k), C.size_t(unsafe.Sizeof(C.sonar_fp_out{})))
+	defer C.free(op)
+	ptrs := unsafe.Slice((*unsafe.Pointer)(pp), k)
+	outs := unsafe.Slice((*C.sonar_fp_out)(op), k)
+	ns := make([]C.int64_t, k)
+	flats := make([][]float32, k)
+	frames := make([]int, k)
+	for i, s := range signals {
+		ptrs[i] = nil
+		ns[i] = C.int64_t(len(s))
+		if len(s) > 0 {
+			pin.Pin(&s[0])
+			ptrs[i] = unsafe.Pointer(&s[0])
+		}
+		frames[i] = int(C.sonar_stft_frames(C.int64_t(len(s)), C.int32_t(windowSize), C.int32_t(hopSize)))
+		if frames[i] > 0 {
+			flats[i] = make([]float32, frames[i]*nc)
+			pin.Pin(&flats[i][0])
+			outs[i].mfcc = unsafe.Pointer(&flats[i][0])
+		}
+	}
+	if rc := C.sonar_fingerprint_batch(x.c, (*unsafe.Pointer)(pp), &ns[0], C.int32_t(k), &cfg,
+		(*C.sonar_fp_out)(op)); rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	res := make([][][]float32, k)
+	for i := range signals {
+		res[i] = make([][]float32, frames[i])
+		for f := 0; f < frames[i]; f++ {
+			res[i][f] = flats[i][f*nc : (f+1)*nc : (f+1)*nc]
+		}
+	}
+	return res, nil
+}

@@ -199,6 +199,8 @@ def lib():
     L.sonar_fp_cfg_default.argtypes = [C.POINTER(FpConfig)]
     L.sonar_fp_cfg_default.restype = None
     L.sonar_fingerprint.argtypes = [_vp, _vp, C.c_int64, C.POINTER(FpConfig), C.POINTER(FpOut)]
+    L.sonar_fingerprint_batch.argtypes = [_vp, C.POINTER(_vp), C.POINTER(C.c_int64), C.c_int32,
+                                          C.POINTER(FpConfig), C.POINTER(FpOut)]
     L.sonar_pitch_yin.argtypes = [_vp, _vp, C.c_int64, C.c_int32, _vp, _vp, _vp, C.c_int32]
     L.sonar_chroma_stft.argtypes = [_vp, _vp, C.c_int64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _vp, C.c_int32]
     L.sonar_ncc.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, _vp, _vp, C.c_int32]
@@ -419,6 +421,34 @@ class Context:
         res, out = self._fp_outputs(n, cfg)
         self._check(self._L.sonar_fingerprint(self._h, _ptr(pcm) if n else None, n, C.byref(cfg), C.byref(out)))
         return res
+
+    def fingerprint_batch(self, signals, cfg: FpConfig):
+        """sonar_fingerprint_batch (SpectralAnalyzer.ComputeSTFTBatch, spectral.go:234-285), host
+        buffers: one dict of numpy arrays per signal, as fingerprint() returns."""
+        dt = np.float64 if cfg.pcm_dtype == F64 else np.float32
+        sigs = [np.ascontiguousarray(x, dtype=dt) for x in signals]
+        cfg.device_ptrs = 0
+        k = len(sigs)
+        ptrs = (_vp * max(k, 1))(*[x.ctypes.data if x.size else None for x in sigs])
+        ns = (C.c_int64 * max(k, 1))(*[x.size for x in sigs])
+        outs = (FpOut * max(k, 1))()
+        res = []
+        for i, x in enumerate(sigs):
+            r, o = self._fp_outputs(x.size, cfg)
+            res.append(r)
+            outs[i] = o
+        self._check(self._L.sonar_fingerprint_batch(self._h, ptrs, ns, k, C.byref(cfg), outs))
+        return res
+
+    def fingerprint_batch_device(self, pcm_ptrs, ns, mfcc_ptrs, cfg: FpConfig):
+        """Device-pointer form (async on the ctx stream): MFCC outputs only (mfcc_ptrs[i] -> F_i x n_mfcc)."""
+        cfg.device_ptrs = 1
+        k = len(pcm_ptrs)
+        outs = (FpOut * max(k, 1))()
+        for i, m in enumerate(mfcc_ptrs):
+            outs[i].mfcc = m
+        self._check(self._L.sonar_fingerprint_batch(self._h, (_vp * max(k, 1))(*pcm_ptrs),
+                                                    (C.c_int64 * max(k, 1))(*ns), k, C.byref(cfg), outs))
 
     def fingerprint_f64le(self, data, cfg: FpConfig, mode=INGEST_HOST_CONVERT):
         """sonar_fingerprint_f64le: the decoder's f64le bytes (decoder.go:850-871) straight into path A."""
