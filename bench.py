@@ -803,10 +803,18 @@ def bench_fp_batch(args, ctx, dev, cfg):
             torch.cuda.synchronize(dev)
             ts.append(time.perf_counter() - t0)
         times[name] = float(np.median(ts))
+    ctx.last_kernel_ms()                     # the batched launch alone, HIP events on the ctx stream
+    ctx.enable_kernel_timing(True)
+    for _ in range(max(args.reps, 1)):
+        batch()
+    ctx.enable_kernel_timing(False)
+    kms = ctx.last_kernel_ms()
     same = all(torch.equal(a, b) for a, b in zip(outs_b, outs_s))
     Ft = int(sum(Fs))
     return {"fp_batch": {"entry": "sonar_fingerprint_batch", "signals": k, "seconds_per_signal": secs,
                          "frames": Ft, "batch_ms": times["batch"] * 1e3, "batch_frames_per_s": Ft / times["batch"],
+                         "batch_kernel_ms": kms, "batch_kernel_frames_per_s": Ft / (kms * 1e-3),
+                         "batch_kernel_valu_frac": Ft * FLOPS_PER_FRAME / (kms * 1e-3) / 1e12 / FP32_PEAK_TFS,
                          "loop_ms": times["loop"] * 1e3, "loop_frames_per_s": Ft / times["loop"],
                          "speedup_vs_loop": times["loop"] / times["batch"], "rows_equal_single_calls": bool(same),
                          "note": "device-resident f32 streams, wall time incl. host launch overhead"}}

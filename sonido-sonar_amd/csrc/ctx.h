@@ -67,6 +67,9 @@ struct sonar_ctx {
   // band-kernel liveness counters (sonar_dtw_counters): edge refresh fences, those followed by new
   // edge values, DTWs that timed out, waves that timed out
   long long dtw_ctr[4] = {0, 0, 0, 0};
+  // sonar_fingerprint_batch: its segment table's pinned staging is rewritten only after the previous
+  // call's upload of it has completed (this event)
+  hipEvent_t fpb_ev = nullptr;
 };
 
 struct sonar_result {

@@ -303,6 +303,7 @@ void sonar_destroy(sonar_ctx* c) {
   }
   for (auto& e : c->ev_pool) { hipEventDestroy(e.first); hipEventDestroy(e.second); }
   if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->fpb_ev) hipEventDestroy(c->fpb_ev);
   if (c->ev1) hipEventDestroy(c->ev1);
   for (auto& e : c->dtw_ev)
     if (e) hipEventDestroy(e);
@@ -748,8 +749,13 @@ int sonar_fingerprint_batch(sonar_ctx* c, const void* const* pcm, const int64_t*
     if (!out[i].mfcc) return fail(c, SONAR_ERR_INVALID, "out[" + std::to_string(i) + "].mfcc is null");
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
-  // segment table {pcm address, n, F, out address, first pair} and the batch's buffers
-  std::vector<int64_t> seg(5 * (size_t)count + 1);
+  // segment table {pcm address, n, F, out address, first pair} in pinned staging, and the batch's
+  // buffers; the staging is reused once the previous call's table upload has completed
+  const size_t seg_n = 5 * (size_t)count + 1;
+  if (c->fpb_ev) HIP_TRY(c, hipEventSynchronize(c->fpb_ev));
+  else HIP_TRY(c, hipEventCreateWithFlags(&c->fpb_ev, hipEventDisableTiming));
+  int64_t* seg = (int64_t*)hbuf(c, "fpb.seg", seg_n * 8);
+  if (!seg) return fail(c, SONAR_ERR_NOMEM, "pinned allocation failed (batch table)");
   int64_t NP = 0, ns = 0, nf = 0;
   for (int i = 0; i < count; i++) {
     const int64_t F = go_frames(n[i], W, H);
@@ -777,9 +783,10 @@ int sonar_fingerprint_batch(sonar_ctx* c, const void* const* pcm, const int64_t*
     }
     po += n[i]; fo += seg[2 * (size_t)count + i];
   }
-  int64_t* dseg = (int64_t*)dbuf(c, "fpb.seg", seg.size() * 8);
+  int64_t* dseg = (int64_t*)dbuf(c, "fpb.seg", seg_n * 8);
   if (!dseg) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (batch table)");
-  HIP_TRY(c, hipMemcpyAsync(dseg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(dseg, seg, seg_n * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipEventRecord(c->fpb_ev, s));
   sonar::MfccPairParams q{};
   fill_pair_params(c, t, cfg, NP, q);
   q.F = 2 * NP; q.H = H;
