@@ -33,6 +33,7 @@ struct PairTables {
   int* chunk_ks = nullptr;
   uint16_t* mel_src = nullptr;
   float* dct = nullptr;
+  float* zeros = nullptr;   // 1024 zero samples (frames past the signal)
   int J = 0, JS = 0, NMP = 0, n_mels = 0, n_mfcc = 0, max_src = 0;
 };
 

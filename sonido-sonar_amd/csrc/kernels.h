@@ -81,6 +81,7 @@ struct MfccPairParams {
   const float2* chunk_w;   // [64][JS] (weight of slot a, weight of slot b), 1/4 (or 1/16) folded
   const uint16_t* mel_src; // [16][64] partial-sum float2 index (2 lane + slot), bit 15 = unused
   const float* dct;     // [16][NMP + 4] DCT-II rows with the lifter folded in
+  const float* zeros;   // [1024] zeros: the samples of frames past the signal
   int J;                // bins per chunk (<= 16)
   int JS;               // chunk_w row stride = J | 1 (odd: conflict-free b64 reads)
   int max_src;          // most partial sums of one filter (<= 16)

@@ -58,10 +58,10 @@ __device__ __forceinline__ void dft8(cf (&v)[N]) {
   dft4(e0, e1, e2, e3);
   dft4(o0, o1, o2, o3);
   o1 = w8_1(o1); o2 = negi(o2); o3 = w8_3(o3);
-  v[O] = cadd(e0, o0); v[O + 4 * S] = csub(e0, o0);
   v[O + S] = cadd(e1, o1); v[O + 5 * S] = csub(e1, o1);
-  v[O + 2 * S] = cadd(e2, o2); v[O + 6 * S] = csub(e2, o2);
   v[O + 3 * S] = cadd(e3, o3); v[O + 7 * S] = csub(e3, o3);
+  v[O] = cadd(e0, o0); v[O + 4 * S] = csub(e0, o0);
+  v[O + 2 * S] = cadd(e2, o2); v[O + 6 * S] = csub(e2, o2);
 }
 
 // w16^j, j in 1..9
@@ -77,11 +77,15 @@ template <int J> __device__ __forceinline__ cf w16(cf a) {
   }
 }
 
-// forward DFT16 of v[0..15] in place (natural-order output), 4 x 4
+// forward DFT16 of v[0..15] in place (natural-order output), 4 x 4; INNER = false: the inner DFT4s
+// were done by the caller (dft16_windowed)
+template <bool INNER = true>
 __device__ __forceinline__ void dft16(cf (&v)[16]) {
   // inner DFT4 over n1 of v[4 n1 + n2] -> Y[n2][k1] stored at v[4 k1 + n2]
+  if (INNER) {
 #pragma unroll
-  for (int n2 = 0; n2 < 4; n2++) dft4(v[n2], v[4 + n2], v[8 + n2], v[12 + n2]);
+    for (int n2 = 0; n2 < 4; n2++) dft4(v[n2], v[4 + n2], v[8 + n2], v[12 + n2]);
+  }
   v[4 + 1] = w16<1>(v[4 + 1]); v[4 + 2] = w16<2>(v[4 + 2]); v[4 + 3] = w16<3>(v[4 + 3]);
   v[8 + 1] = w16<2>(v[8 + 1]); v[8 + 2] = w16<4>(v[8 + 2]); v[8 + 3] = w16<6>(v[8 + 3]);
   v[12 + 1] = w16<3>(v[12 + 1]); v[12 + 2] = w16<6>(v[12 + 2]); v[12 + 3] = w16<9>(v[12 + 3]);
@@ -95,6 +99,23 @@ __device__ __forceinline__ void dft16(cf (&v)[16]) {
   }
 #pragma unroll
   for (int i = 0; i < 16; i++) v[i] = o[i];
+}
+
+// DFT16 of the windowed pair z[a] = w[a] (xr[a] + i xi[a]): the window multiply is fused into the
+// inner DFT4s' first butterflies (w0 x0 +- w8 x8 as one product and two FMAs, 48 VALU instead of 64)
+__device__ __forceinline__ void dft16_windowed(const float (&xr)[16], const float (&xi)[16], const float (&w)[16],
+                                               cf (&v)[16]) {
+#pragma unroll
+  for (int n2 = 0; n2 < 4; n2++) {
+    const int a0 = n2, a1 = 4 + n2, a2 = 8 + n2, a3 = 12 + n2;
+    const float p0r = xr[a0] * w[a0], p0i = xi[a0] * w[a0], p1r = xr[a1] * w[a1], p1i = xi[a1] * w[a1];
+    const cf t0 = {__builtin_fmaf(xr[a2], w[a2], p0r), __builtin_fmaf(xi[a2], w[a2], p0i)};
+    const cf t1 = {__builtin_fmaf(-xr[a2], w[a2], p0r), __builtin_fmaf(-xi[a2], w[a2], p0i)};
+    const cf t2 = {__builtin_fmaf(xr[a3], w[a3], p1r), __builtin_fmaf(xi[a3], w[a3], p1i)};
+    const cf t3 = negi(cf{__builtin_fmaf(-xr[a3], w[a3], p1r), __builtin_fmaf(-xi[a3], w[a3], p1i)});
+    v[a0] = cadd(t0, t2); v[a2] = csub(t0, t2); v[a1] = cadd(t1, t3); v[a3] = csub(t1, t3);
+  }
+  dft16<false>(v);
 }
 
 __device__ __forceinline__ float f_of(uint32_t u) { return __uint_as_float(u); }
@@ -189,10 +210,15 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // ---- shared tables -> LDS ---------------------------------------------------
   float2* s_cw = reinterpret_cast<float2*>(smem);                                  // [64][J] (wa, wb)
-  uint16_t* s_src = reinterpret_cast<uint16_t*>(smem + p.lds_src);                 // [16][64] partial float2 idx
+  uint16_t* s_src = reinterpret_cast<uint16_t*>(smem + p.lds_src);                 // [16][64] source byte offsets
   float* s_dct = reinterpret_cast<float*>(smem + p.lds_dct);                       // [16][NMP + 4], lifter folded
   for (int i = threadIdx.x; i < 64 * p.JS; i += blockDim.x) s_cw[i] = p.chunk_w[i];
-  for (int i = threadIdx.x; i < 64 * 16; i += blockDim.x) s_src[i] = p.mel_src[i];
+  // as byte offsets into the wave's region: a partial sum's float2 (kPartOff + 8 idx), or for an
+  // unused source (bit 15) the float2 that stays zero past the T2 rows
+  for (int i = threadIdx.x; i < 64 * 16; i += blockDim.x) {
+    const uint32_t idx = p.mel_src[i];
+    s_src[i] = (uint16_t)((idx & 0x8000u) ? 64 * kT2Stride : kPartOff + 8 * (int)idx);
+  }
   for (int i = threadIdx.x; i < 16 * (p.NMP + 4); i += blockDim.x) s_dct[i] = p.dct[i];
   unsigned char* wb = smem + p.lds_wave0 + wave * kWaveBytes;
   // Zero the wave's region once: the filterbank chunks read up to 11 rows past bin 512 with
@@ -275,10 +301,23 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     if (SEG) while (pi >= g.p1) g = sig_at(g.s + 1);
   };
 
+#ifndef HL_PF_LATE
+#define HL_PF_LATE 1
+#endif
   auto frame_ok = [&](const Sig& g, int64_t t) { return t < g.F && t * (int64_t)H + 1024 <= g.n; };
   auto load_pair = [&](int64_t pi, float (&xr)[16], float (&xi)[16]) {
     advance(gl, pi);
     const int64_t t = 2 * (pi - gl.p0);
+    if (HL_PF_LATE) {
+      // unconditional loads: a frame past the signal (the last pair's second frame of an odd F, or
+      // a frame of a signal shorter than W) reads p.zeros instead -- a wave-uniform pointer select,
+      // so the loaded registers have one definition and stay in place across the loop's back edge
+      const float* f0 = frame_ok(gl, t) ? gl.pcm + t * (int64_t)H : p.zeros;
+      const float* f1 = frame_ok(gl, t + 1) ? gl.pcm + (t + 1) * (int64_t)H : p.zeros;
+#pragma unroll
+      for (int a = 0; a < 16; a++) { xr[a] = f0[lane + 64 * a]; xi[a] = f1[lane + 64 * a]; }
+      return;
+    }
     const float* b0p = gl.pcm + t * (int64_t)H + lane;
     if (frame_ok(gl, t)) {
 #pragma unroll
@@ -305,15 +344,27 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 #ifndef HL_PRIO
 #define HL_PRIO 1
 #endif
-  auto process = [&](int64_t pi, const float (&xr)[16], const float (&xi)[16]) {
+  auto process = [&](int64_t pi, float (&xr)[16], float (&xi)[16]) {
     advance(gp, pi);
     if (HL_PRIO == 1 || HL_PRIO >= 3) __builtin_amdgcn_s_setprio(0);
     if (HL_PRIO == 2) __builtin_amdgcn_s_setprio(1);
     cf v[16];
+#ifndef HL_WFMA
+#define HL_WFMA 1
+#endif
+    if (HL_WFMA) {
+      dft16_windowed(xr, xi, win, v);            // window fused into pass 1's first butterflies
+    } else {
 #pragma unroll
-    for (int a = 0; a < 16; a++) v[a] = {xr[a] * win[a], xi[a] * win[a]};
+      for (int a = 0; a < 16; a++) v[a] = {xr[a] * win[a], xi[a] * win[a]};
+    }
+    // the next pair's PCM into the same registers, now that this pair's samples are windowed: in
+    // flight during the whole pair, and no register copies across the loop's back edge
+    // (unconditional, so the registers carry one definition round the loop: the last pair of the
+    // wave's range loads itself again)
+    if (HL_PF_LATE) load_pair(pi + 1 < pe ? pi + 1 : pi, xr, xi);
     // ---- pass 1: DFT16 over a, twiddle w_1024^{b k1} -----------------------------
-    dft16(v);
+    if (!HL_WFMA) dft16(v);
 #pragma unroll
     for (int k = 1; k < 16; k++) v[k] = cmul(v[k], tw1[k]);
     // ---- T1: register bits 0-2 <-> lane bits 3-5 --------------------------------
@@ -417,13 +468,12 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     wave_lds_sync();
     // ---- ln of the filter sums (lane = filter) ----------------------------------------
     if (lane < nmp) {
-      float m0 = 0.f, m1 = 0.f;
       const int ms = MS ? MS : p.max_src;
+      const float2 q0 = *reinterpret_cast<const float2*>(wb + s_src[lane]);   // every filter has a source
+      float m0 = q0.x, m1 = q0.y;
 #pragma unroll
-      for (int i = 0; i < ms; i++) {
-        const uint32_t idx = s_src[64 * i + lane];               // 0x8000: unused -> the zero float2
-        const int off = (idx & 0x8000u) ? 64 * kT2Stride : kPartOff + 8 * (int)idx;
-        const float2 q = *reinterpret_cast<const float2*>(wb + off);
+      for (int i = 1; i < ms; i++) {
+        const float2 q = *reinterpret_cast<const float2*>(wb + s_src[64 * i + lane]);
         m0 += q.x;
         m1 += q.y;
       }
@@ -445,9 +495,14 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       const int half = NH ? NH : (nmp >> 1);
       const float* lm = reinterpret_cast<const float*>(wb + kLogOff) + f * nmp + hh * half;
       const float* d = s_dct + q * (nmp + 4) + hh * half;     // row stride NMP + 4: 11 x 16 B slots
-      float s = 0.f;
+      float s;                                                  // half >= 4 (NMP is a multiple of 8)
+      {
+        const float4 x = *reinterpret_cast<const float4*>(lm);
+        const float4 y = *reinterpret_cast<const float4*>(d);
+        s = x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+      }
 #pragma unroll
-      for (int m = 0; m < half; m += 4) {
+      for (int m = 4; m < half; m += 4) {
         const float4 x = *reinterpret_cast<const float4*>(lm + m);
         const float4 y = *reinterpret_cast<const float4*>(d + m);
         s += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
@@ -463,11 +518,15 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   float ar[16], ai[16];
   load_pair(pb, ar, ai);
   for (int64_t pi = pb; pi < pe; ++pi) {
-    float nr[16], ni[16];
-    if (pi + 1 < pe) load_pair(pi + 1, nr, ni);     // next pair's PCM in flight during this one
-    process(pi, ar, ai);
+    if (HL_PF_LATE) {
+      process(pi, ar, ai);
+    } else {                     // round-3 form: a second register set, copied at the back edge
+      float nr[16], ni[16];
+      if (pi + 1 < pe) load_pair(pi + 1, nr, ni);
+      process(pi, ar, ai);
 #pragma unroll
-    for (int a = 0; a < 16; a++) { ar[a] = nr[a]; ai[a] = ni[a]; }
+      for (int a = 0; a < 16; a++) { ar[a] = nr[a]; ai[a] = ni[a]; }
+    }
   }
 }
 

@@ -251,8 +251,9 @@ bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
   t.window = (float*)upload(wf); t.tw1 = upload(tw1); t.tw2 = upload(tw2);
   t.chunk_ks = (int*)upload(ks); t.chunk_w = upload(cw); t.mel_src = (uint16_t*)upload(msrc);
   t.dct = (float*)upload(dct);
+  t.zeros = (float*)upload(std::vector<float>(1024, 0.f));
   t.J = J; t.JS = JS; t.NMP = NMP; t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc; t.max_src = max_src;
-  t.ok = t.window && t.tw1 && t.tw2 && t.chunk_ks && t.chunk_w && t.mel_src && t.dct;
+  t.ok = t.window && t.tw1 && t.tw2 && t.chunk_ks && t.chunk_w && t.mel_src && t.dct && t.zeros;
   return t.ok;
 }
 
@@ -442,6 +443,7 @@ void fill_pair_params(sonar_ctx* c, const PairTables& t, const sonar_fp_cfg* cfg
                       sonar::MfccPairParams& q) {
   q.window = t.window; q.tw1 = (const float2*)t.tw1; q.tw2 = (const float2*)t.tw2;
   q.chunk_ks = t.chunk_ks; q.chunk_w = (const float2*)t.chunk_w; q.mel_src = t.mel_src; q.dct = t.dct;
+  q.zeros = t.zeros;
   q.J = t.J; q.JS = t.JS; q.max_src = t.max_src; q.NMP = t.NMP; q.n_mels = t.n_mels; q.n_mfcc = t.n_mfcc;
   q.pow2 = cfg->mfcc_input_power != 0;
   auto al = [](int x) { return (x + 15) & ~15; };

@@ -1,0 +1,16 @@
+# Headline: next pair's PCM loaded after the windowing into the same registers, unconditionally
+# (frames past the signal read a zero buffer) -- 841 VALU per pair against 891.  Tests, then A/B
+# against the same source built with -DHL_PF_LATE=0 (lib_pfold), three alternating rounds.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_fingerprint_batch.py tests/test_gpu_mfcc_pair.py tests/test_gpu_golden.py tests/test_gpu_fullsize.py > gpurun_out/r04x_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r04x_tests.log; [ $rc -eq 0 ] || { echo "tests rc=$rc"; tail -40 gpurun_out/r04x_tests.log; exit 1; }
+NOLEGS="--no-cpu-baseline --no-f64 --dtw-len 0 --c5-pairs 0 --c3-seconds 0 --c4-seconds 0 --c6-gallery 0 --c7-seconds 0 --ingest-reps 0 --batch-signals 0"
+for round in 1 2 3; do
+for t in default pfold; do
+  if [ $t = default ]; then L=sonido-sonar_amd/lib/libsonar_gpu.so; else L=sonido-sonar_amd/lib_$t/libsonar_gpu.so; fi
+  SONAR_LIB=$PWD/$L timeout -k 10 120 python3 bench.py $NOLEGS > gpurun_out/r04x_ab_$t.json 2>/dev/null || { echo "fail $t"; exit 1; }
+  python3 -c "import json; d=json.load(open('gpurun_out/r04x_ab_$t.json')); print('hl $t', round(d['roofline']['kernel_ms'],4), 'ms', '%.4e' % d['value'], round(d['roofline']['frac'],4))"
+done
+done
