@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--seconds", type=float, default=3600.0, help="audio seconds per GPU (1 h config)")
     ap.add_argument("--dtw-len", type=int, default=51676, help="DTW sequence length (0 = skip); C3 = 51,676")
-    ap.add_argument("--dtw-steps", type=int, default=3)
+    ap.add_argument("--dtw-steps", type=int, default=5, help="C3 DTW repetitions (median reported)")
     ap.add_argument("--c5-pairs", type=int, default=1000, help="C5 stream pairs in total (0 = skip)")
     ap.add_argument("--c5-seconds", type=float, default=60.0)
     ap.add_argument("--c5-max-lag", type=float, default=20.0, help="maxOffsetSeconds (lags are drawn in [0, 20) s)")
