@@ -92,7 +92,8 @@ struct MfccPairParams {
   int lds_src, lds_dct, lds_wave0, lds_bytes;
   int waves_per_block;  // 4 (mfcc_pair_kernel)
   // sonar_fingerprint_batch: nseg > 0 signals, F = 2 x the batch's pairs, pcm / n / out unused;
-  // seg (device) = {pcm address[nseg], n[nseg], F[nseg], out address[nseg], first pair[nseg + 1]}
+  // seg (device) = {pcm address[nseg], frames inside the signal[nseg], F[nseg], out address[nseg],
+  // first pair[nseg + 1]}
   const int64_t* seg;
   int nseg;
 };

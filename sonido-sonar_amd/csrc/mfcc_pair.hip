@@ -260,16 +260,19 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 
   // ---- this wave's pairs -------------------------------------------------------
   const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-  const int64_t pb = gw * p.pairs_per_wave;
-  const int64_t NP = (p.F + 1) >> 1;
-  if (pb >= NP) return;
-  const int64_t pe = min(NP, pb + p.pairs_per_wave);
+  // pair indices are 32-bit (the host checks the count), so the wave-uniform compares stay scalar
+  const int NP = (int)((p.F + 1) >> 1);
+  if (gw * p.pairs_per_wave >= NP) return;
+  const int pb = (int)(gw * p.pairs_per_wave);
+  const int pe = (int)min((int64_t)NP, (int64_t)pb + p.pairs_per_wave);
   const int H = p.H;
 
   // The signal a pair belongs to (wave-uniform).  One signal: pairs [0, NP) of p.pcm / p.out.  SEG:
-  // seg = {pcm address[nseg], n[nseg], F[nseg], out address[nseg], first pair[nseg + 1]}; the
-  // loads (one pair ahead) and the processing each keep their own cursor, advanced monotonically.
-  struct Sig { const float* pcm; int64_t n, F; float* out; int64_t p0, p1; int s; };
+  // seg = {pcm address[nseg], frames inside the signal[nseg], F[nseg], out address[nseg], first
+  // pair[nseg + 1]}; the loads (one pair ahead) and the processing each keep their own cursor,
+  // advanced monotonically.  Fin: frames t with t H + W <= n (= F unless the signal is shorter than
+  // W: Go's frame count truncates toward zero), the rest read zeros.
+  struct Sig { const float* pcm; float* out; int Fin, F, p0, p1, s; };
   // The table is read with vector loads (the kernel's stores keep it off the scalar cache); the
   // values are wave-uniform, so readfirstlane parks them in SGPRs.
   auto ld = [&](int i) {
@@ -280,8 +283,8 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   auto sig_at = [&](int s) {
     const int ns = p.nseg;
     Sig g;
-    g.pcm = reinterpret_cast<const float*>(ld(s)); g.n = ld(ns + s); g.F = ld(2 * ns + s);
-    g.out = reinterpret_cast<float*>(ld(3 * ns + s)); g.p0 = ld(4 * ns + s); g.p1 = ld(4 * ns + s + 1);
+    g.pcm = reinterpret_cast<const float*>(ld(s)); g.Fin = (int)ld(ns + s); g.F = (int)ld(2 * ns + s);
+    g.out = reinterpret_cast<float*>(ld(3 * ns + s)); g.p0 = (int)ld(4 * ns + s); g.p1 = (int)ld(4 * ns + s + 1);
     g.s = s;
     return g;
   };
@@ -294,20 +297,21 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     }
     gl = sig_at(lo);
   } else {
-    gl = Sig{p.pcm, p.n, p.F, p.out, 0, NP, 0};
+    const int Fin = p.n >= 1024 ? (int)min(p.F, (p.n - 1024) / H + 1) : 0;
+    gl = Sig{p.pcm, p.out, Fin, (int)p.F, 0, NP, 0};
   }
   gp = gl;
-  auto advance = [&](Sig& g, int64_t pi) {
+  auto advance = [&](Sig& g, int pi) {
     if (SEG) while (pi >= g.p1) g = sig_at(g.s + 1);
   };
 
 #ifndef HL_PF_LATE
 #define HL_PF_LATE 1
 #endif
-  auto frame_ok = [&](const Sig& g, int64_t t) { return t < g.F && t * (int64_t)H + 1024 <= g.n; };
-  auto load_pair = [&](int64_t pi, float (&xr)[16], float (&xi)[16]) {
+  auto frame_ok = [&](const Sig& g, int t) { return t < g.Fin; };
+  auto load_pair = [&](int pi, float (&xr)[16], float (&xi)[16]) {
     advance(gl, pi);
-    const int64_t t = 2 * (pi - gl.p0);
+    const int t = 2 * (pi - gl.p0);
     if (HL_PF_LATE) {
       // unconditional loads: a frame past the signal (the last pair's second frame of an odd F, or
       // a frame of a signal shorter than W) reads p.zeros instead -- a wave-uniform pointer select,
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 #ifndef HL_PRIO
 #define HL_PRIO 1
 #endif
-  auto process = [&](int64_t pi, float (&xr)[16], float (&xi)[16]) {
+  auto process = [&](int pi, float (&xr)[16], float (&xi)[16]) {
     advance(gp, pi);
     if (HL_PRIO == 1 || HL_PRIO >= 3) __builtin_amdgcn_s_setprio(0);
     if (HL_PRIO == 2) __builtin_amdgcn_s_setprio(1);
@@ -517,7 +521,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 
   float ar[16], ai[16];
   load_pair(pb, ar, ai);
-  for (int64_t pi = pb; pi < pe; ++pi) {
+  for (int pi = pb; pi < pe; ++pi) {
     if (HL_PF_LATE) {
       process(pi, ar, ai);
     } else {                     // round-3 form: a second register set, copied at the back edge
@@ -533,6 +537,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   const int64_t NP = (p.F + 1) >> 1;
+  if (NP > INT32_MAX) return -4;                  // 32-bit pair indices in the kernel
   const int64_t waves = (NP + p.pairs_per_wave - 1) / p.pairs_per_wave;
   const int64_t grid = (waves + 3) / 4;
   const bool head = p.J == 12 && p.max_src <= 8 && p.NMP == 40;

@@ -761,7 +761,8 @@ int sonar_fingerprint_batch(sonar_ctx* c, const void* const* pcm, const int64_t*
   int64_t NP = 0, ns = 0, nf = 0;
   for (int i = 0; i < count; i++) {
     const int64_t F = go_frames(n[i], W, H);
-    seg[2 * (size_t)count + i] = F; seg[(size_t)count + i] = n[i];
+    // frames whose W samples lie inside the signal (F itself unless n < W: Go's count truncates)
+    seg[2 * (size_t)count + i] = F; seg[(size_t)count + i] = n[i] >= W ? std::min<int64_t>(F, (n[i] - W) / H + 1) : 0;
     seg[4 * (size_t)count + i] = NP;
     NP += (F + 1) / 2; ns += n[i]; nf += F;
   }
