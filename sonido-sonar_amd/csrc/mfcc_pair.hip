@@ -305,38 +305,17 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     if (SEG) while (pi >= g.p1) g = sig_at(g.s + 1);
   };
 
-#ifndef HL_PF_LATE
-#define HL_PF_LATE 1
-#endif
   auto frame_ok = [&](const Sig& g, int t) { return t < g.Fin; };
   auto load_pair = [&](int pi, float (&xr)[16], float (&xi)[16]) {
     advance(gl, pi);
     const int t = 2 * (pi - gl.p0);
-    if (HL_PF_LATE) {
-      // unconditional loads: a frame past the signal (the last pair's second frame of an odd F, or
-      // a frame of a signal shorter than W) reads p.zeros instead -- a wave-uniform pointer select,
-      // so the loaded registers have one definition and stay in place across the loop's back edge
-      const float* f0 = frame_ok(gl, t) ? gl.pcm + t * (int64_t)H : p.zeros;
-      const float* f1 = frame_ok(gl, t + 1) ? gl.pcm + (t + 1) * (int64_t)H : p.zeros;
+    // unconditional loads: a frame past the signal (the last pair's second frame of an odd F, or
+    // a frame of a signal shorter than W) reads p.zeros instead -- a wave-uniform pointer select,
+    // so the loaded registers have one definition and stay in place across the loop's back edge
+    const float* f0 = frame_ok(gl, t) ? gl.pcm + t * (int64_t)H : p.zeros;
+    const float* f1 = frame_ok(gl, t + 1) ? gl.pcm + (t + 1) * (int64_t)H : p.zeros;
 #pragma unroll
-      for (int a = 0; a < 16; a++) { xr[a] = f0[lane + 64 * a]; xi[a] = f1[lane + 64 * a]; }
-      return;
-    }
-    const float* b0p = gl.pcm + t * (int64_t)H + lane;
-    if (frame_ok(gl, t)) {
-#pragma unroll
-      for (int a = 0; a < 16; a++) xr[a] = b0p[64 * a];
-    } else {
-#pragma unroll
-      for (int a = 0; a < 16; a++) xr[a] = 0.f;
-    }
-    if (frame_ok(gl, t + 1)) {
-#pragma unroll
-      for (int a = 0; a < 16; a++) xi[a] = b0p[H + 64 * a];
-    } else {
-#pragma unroll
-      for (int a = 0; a < 16; a++) xi[a] = 0.f;
-    }
+    for (int a = 0; a < 16; a++) { xr[a] = f0[lane + 64 * a]; xi[a] = f1[lane + 64 * a]; }
   };
 
   // Phase-dependent issue priority (HL_PRIO).  1 (default): a wave in the LDS-bound epilogue
@@ -353,22 +332,13 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     if (HL_PRIO == 1 || HL_PRIO >= 3) __builtin_amdgcn_s_setprio(0);
     if (HL_PRIO == 2) __builtin_amdgcn_s_setprio(1);
     cf v[16];
-#ifndef HL_WFMA
-#define HL_WFMA 1
-#endif
-    if (HL_WFMA) {
-      dft16_windowed(xr, xi, win, v);            // window fused into pass 1's first butterflies
-    } else {
-#pragma unroll
-      for (int a = 0; a < 16; a++) v[a] = {xr[a] * win[a], xi[a] * win[a]};
-    }
+    // ---- pass 1: DFT16 over a (the window fused into its first butterflies), twiddle w_1024^{b k1}
+    dft16_windowed(xr, xi, win, v);
     // the next pair's PCM into the same registers, now that this pair's samples are windowed: in
     // flight during the whole pair, and no register copies across the loop's back edge
     // (unconditional, so the registers carry one definition round the loop: the last pair of the
     // wave's range loads itself again)
-    if (HL_PF_LATE) load_pair(pi + 1 < pe ? pi + 1 : pi, xr, xi);
-    // ---- pass 1: DFT16 over a, twiddle w_1024^{b k1} -----------------------------
-    if (!HL_WFMA) dft16(v);
+    load_pair(pi + 1 < pe ? pi + 1 : pi, xr, xi);
 #pragma unroll
     for (int k = 1; k < 16; k++) v[k] = cmul(v[k], tw1[k]);
     // ---- T1: register bits 0-2 <-> lane bits 3-5 --------------------------------
@@ -521,17 +491,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 
   float ar[16], ai[16];
   load_pair(pb, ar, ai);
-  for (int pi = pb; pi < pe; ++pi) {
-    if (HL_PF_LATE) {
-      process(pi, ar, ai);
-    } else {                     // round-3 form: a second register set, copied at the back edge
-      float nr[16], ni[16];
-      if (pi + 1 < pe) load_pair(pi + 1, nr, ni);
-      process(pi, ar, ai);
-#pragma unroll
-      for (int a = 0; a < 16; a++) { ar[a] = nr[a]; ai[a] = ni[a]; }
-    }
-  }
+  for (int pi = pb; pi < pe; ++pi) process(pi, ar, ai);
 }
 
 
