@@ -195,6 +195,15 @@ void sonar_fp_cfg_default(sonar_fp_cfg* cfg);
  * spectral descriptors -> SONAR_ERR_UNSUPPORTED), as go-dsp's FFTReal takes any length. */
 int sonar_fingerprint(sonar_ctx* ctx, const void* pcm, int64_t n, const sonar_fp_cfg* cfg,
                       sonar_fp_out* out);
+/* Which transform kernel sonar_fingerprint runs for (cfg, n): pure host logic, the decision the
+ * call itself makes (no device needed).  SONAR_PLAN_PAIR: mfcc_pair_kernel (float32 MFCC only,
+ * W = 1024, at most SONAR_PAIR_MAX_FRAMES frames -- its frame indices are 32-bit -- and a
+ * filterbank that fits its lane chunks, else the call takes fp_wave_kernel); SONAR_PLAN_WAVE:
+ * fp_wave_kernel; SONAR_PLAN_DFT: stft_dft_kernel (other W); SONAR_PLAN_NONE: no transform
+ * requested (ZCR / energy only).  < 0: the error code the call would return for (cfg, n). */
+enum { SONAR_PLAN_NONE = 0, SONAR_PLAN_PAIR = 1, SONAR_PLAN_WAVE = 2, SONAR_PLAN_DFT = 3 };
+#define SONAR_PAIR_MAX_FRAMES 2147483646LL
+int32_t sonar_fp_kernel_plan(const sonar_fp_cfg* cfg, int64_t n);
 /* SpectralAnalyzer.ComputeSTFTBatch (fingerprint/analyzers/spectral.go:234-285): sonar_fingerprint
  * of `count` signals with one configuration; out[i] receives signal i's outputs (sizes as for
  * sonar_fingerprint with n[i]).  count <= 0 -> SONAR_ERR_EMPTY "no signals provided"; the first

@@ -371,11 +371,12 @@ class YinTrack:
 def speech_features_reference(pcm, sample_rate, fc):
     """SpeechFeatureExtractor.ExtractFeatures (fingerprint/extractors/speech.go:135-550), fp64.
     fc: dict(sample_rate, window_size, hop_size, stft_window_size, stft_hop_size, enable_mfcc,
-    enable_speech_features, enable_temporal_features, mfcc_coefficients)."""
+    enable_speech_features, enable_temporal_features, mfcc_coefficients[, nthreads: the STFT's worker
+    threads, Go's worker-pool shape, default 8])."""
     pcm = _f64(pcm)
     csr = fc["sample_rate"]
     W, H = fc["stft_window_size"], fc["stft_hop_size"]
-    mag = stft_mag(pcm, W, H, nthreads=8)
+    mag = stft_mag(pcm, W, H, nthreads=fc.get("nthreads", 8))
     F = len(mag)
     pre = preemphasis(pcm, 0.97)
     out = {}
@@ -478,7 +479,8 @@ def music_features_reference(pcm, sample_rate, fc):
     """MusicFeatureExtractor.ExtractFeatures (fingerprint/extractors/music.go:178-583), fp64, composed
     from the oracle's pieces.  fc: dict(sample_rate, window_size, hop_size, stft_window_size,
     stft_hop_size).  Returns (features, panic): panic is Go's runtime error text where the reference
-    panics (music.go:383 integer divide by zero with no energy frame; music.go:403 index out of range
+    panics (music.go:348-352 slice bounds when a chroma frame starts past the signal, (F-1) hop > n;
+    music.go:383 integer divide by zero with no energy frame; music.go:403 index out of range
     for >= 2 RMS frames of 1024 / 512, i.e. >= 1536 samples), features then holding what was computed
     before the panic."""
     pcm = _f64(pcm)
@@ -501,6 +503,9 @@ def music_features_reference(pcm, sample_rate, fc):
     if fc["hop_size"] <= 0:                                             # stft.go:54-56 via :358-361
         raise ValueError("chroma feature extraction failed: chroma computation failed at frame 0: "
                          "hop size must be positive")
+    if (F - 1) * fc["hop_size"] > n:                                    # pcm[start:end] with start > n (:348-352)
+        f = n // fc["hop_size"] + 1
+        return out, f"runtime error: slice bounds out of range [{f * fc['hop_size']}:{n}]"
     out["chroma"] = chroma_music(pcm, F, fc["hop_size"], csr)           # (:327-376)
     rms = short_time_energy(y, fc["window_size"], fc["hop_size"])       # extractTemporalFeatures (:378-458)
     out["rms_energy"] = rms

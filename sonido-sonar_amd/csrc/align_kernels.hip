@@ -686,11 +686,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
   const int64_t nq = a.nq, nr = a.nr, S = a.S, S2 = (a.S + 1) >> 1;
   const int dim = D > 0 ? D : a.dim;
   constexpr uint64_t INF_BITS = 0x7FF0000000000000ull;
-#ifdef DTW_DBG_NOEDGE   // A/B timing builds only (wrong results): every band runs as if it were band 0
-  const uint64_t* Ein = nullptr;
-#else
   const uint64_t* Ein = b > 0 ? a.E + (b - 1) * (nr + 1) : nullptr;       // C[64b][j] at index j
-#endif
   const int64_t nblk = (nr + DTW_RBLK - 1) / DTW_RBLK;
   const int64_t i = 64 * b + 1 + lane;
   const bool row_ok = i <= nq;

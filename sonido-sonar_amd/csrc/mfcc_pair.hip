@@ -318,19 +318,16 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     for (int a = 0; a < 16; a++) { xr[a] = f0[lane + 64 * a]; xi[a] = f1[lane + 64 * a]; }
   };
 
-  // Phase-dependent issue priority (HL_PRIO).  1 (default): a wave in the LDS-bound epilogue
-  // (pass 3, power rows, filterbank, ln, DCT: five LDS phases, few VALU) issues ahead of the waves
-  // in the VALU-bound FFT passes, so its short VALU bursts between LDS round trips are not queued
-  // behind 3-6 wave-instructions of FFT arithmetic, and its LDS traffic overlaps their VALU work.
-  // Same-box A/B (profiles/r04n_ab.log): 0.475-0.481 ms against 0.505-0.509 ms at priority 0;
-  // 2 (the reverse) 0.483-0.492 ms.
-#ifndef HL_PRIO
-#define HL_PRIO 1
-#endif
+  // Phase-dependent issue priority: a wave in the LDS-bound epilogue (pass 3, power rows,
+  // filterbank, ln, DCT: five LDS phases, few VALU) runs at s_setprio 1 and issues ahead of the
+  // waves in the VALU-bound FFT passes (0), so its short VALU bursts between LDS round trips are not
+  // queued behind 3-6 wave-instructions of FFT arithmetic, and its LDS traffic overlaps their VALU
+  // work.  Same-box A/B (profiles/r04n_ab.log, r04x4_ab.log): 0.475-0.481 ms against 0.505-0.509 ms
+  // at one priority; the reverse order 0.483-0.492 ms; the epilogue at 3, or priority from the T2
+  // transpose on, no better.
   auto process = [&](int pi, float (&xr)[16], float (&xi)[16]) {
     advance(gp, pi);
-    if (HL_PRIO == 1 || HL_PRIO >= 3) __builtin_amdgcn_s_setprio(0);
-    if (HL_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(0);
     cf v[16];
     // ---- pass 1: DFT16 over a (the window fused into its first butterflies), twiddle w_1024^{b k1}
     dft16_windowed(xr, xi, win, v);
@@ -371,7 +368,6 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     dft8<8, 1>(v);
 #pragma unroll
     for (int c = 1; c < 8; c++) { v[c] = cmul(v[c], tw2[c]); v[8 + c] = cmul(v[8 + c], tw2[c]); }
-    if (HL_PRIO == 3) __builtin_amdgcn_s_setprio(1);     // A/B: from the T2 transpose on
     // ---- T2: LDS transpose into the combo layout ---------------------------------
     if (kl != 0) {
 #pragma unroll
@@ -393,9 +389,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       v[j] = {u.x, u.y};
     }
     wave_lds_sync();
-    if (HL_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-    if (HL_PRIO == 4) __builtin_amdgcn_s_setprio(3);     // A/B: the epilogue at the top level
-    if (HL_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(1);
     // ---- pass 3: DFT8 over b0 for both combos --------------------------------------
     dft8<0, 1>(v);    // A[c1] = Z[rA + 128 c1]
     dft8<8, 1>(v);    // B[c1] = Z[rB + 128 c1]
@@ -459,11 +453,6 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     }
     wave_lds_sync();
     // ---- DCT-II (+ lifter): lane = q + 16 f + 32 h, half h of the filters ----------------
-#ifdef MFCC_DBG_NODCT   // A/B diagnostics: the DCT's share of the kernel (the most MFMA could save)
-    if ((lane & 15) < p.n_mfcc && (lane >> 5) == 0 && 2 * (pi - gp.p0) + ((lane >> 4) & 1) < gp.F)
-      gp.out[(2 * (pi - gp.p0) + ((lane >> 4) & 1)) * p.n_mfcc + (lane & 15)] = reinterpret_cast<const float*>(wb + kLogOff)[lane & 15];
-    if (false)
-#endif
     {
       const int q = lane & 15, f = (lane >> 4) & 1, hh = lane >> 5;
       const int half = NH ? NH : (nmp >> 1);
@@ -497,7 +486,9 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
 
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   const int64_t NP = (p.F + 1) >> 1;
-  if (NP > INT32_MAX) return -4;                  // 32-bit pair indices in the kernel
+  // 32-bit pair AND frame indices in the kernel (t = 2 (pi - p0) + 1 <= 2 NP): the host routes larger
+  // calls to fp_wave_kernel (sonar_fp_kernel_plan), so this is a guard, reported as unsupported
+  if (2 * NP > SONAR_PAIR_MAX_FRAMES) return -4;
   const int64_t waves = (NP + p.pairs_per_wave - 1) / p.pairs_per_wave;
   const int64_t grid = (waves + 3) / 4;
   const bool head = p.J == 12 && p.max_src <= 8 && p.NMP == 40;

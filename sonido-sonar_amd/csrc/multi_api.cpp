@@ -214,12 +214,6 @@ bool feat_batch(sonar_ctx* w, const std::vector<PairGeo>& pg, int32_t sr, int32_
   }
   (void)sw;
   if (hipMemcpyAsync(dj, hj, jb + nb, hipMemcpyHostToDevice, s) != hipSuccess) return false;
-#ifdef SONAR_DBG_C5_NOFEAT   // A/B timing builds only (wrong records): the chroma is a constant fill
-  for (int k = 0; k < 2 * n; ++k)
-    if (hipMemsetD32Async((hipDeviceptr_t)mj[k].chroma, 0x3FE00000u, (size_t)mj[k].F * 24, s) != hipSuccess) return false;
-  (void)ncorr; (void)nj;
-  return true;
-#endif
   if (sonar::launch_music_features_batch(mj, (const sonar::MfJob*)dj, 2 * n, fw, hop, fs, (const double*)ct->win,
                                          (const double*)ct->trig, (const int*)ct->cls, s) != 0)
     return false;
@@ -371,10 +365,8 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   for (const auto& p : pg)
     max_el = std::max({max_el, (p.Fq + p.Fr) * 12, (int64_t)(sonar::dtw_edge_bytes(p.g) / 8)});
   if (sonar::launch_nonfinite_batch(dargs, n, max_el, s) != 0) return fail(w, SONAR_ERR_DEVICE, "dtw launch failed");
-#ifndef SONAR_DBG_C5_NODTW   // A/B timing builds only (wrong records): no DTW
   if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s, dmap) != 0)
     return fail(w, SONAR_ERR_DEVICE, "dtw batch launch failed");
-#endif
   HIP_TRY(w, hipMemcpyAsync(hstat, small, small_b, hipMemcpyDeviceToHost, s));
   std::vector<uint64_t> htr(trb ? (size_t)total_bands * 8 : 0);
   if (trb) HIP_TRY(w, hipMemcpyAsync(htr.data(), trb, htr.size() * 8, hipMemcpyDeviceToHost, s));

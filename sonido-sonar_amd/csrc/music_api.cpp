@@ -12,7 +12,9 @@
 // (n >= 1536 samples); and a signal with no energy frame divides by zero at music.go:383.  Such a
 // call returns SONAR_ERR_PANIC with Go's runtime message, and *out holds the arrays the Go call
 // had computed before the panic (spectral features, MFCC, chroma, rms_energy, envelope_shape,
-// peak / average amplitude); Go itself returns nothing.  Below 1536 samples every group is
+// peak / average amplitude); Go itself returns nothing.  A FeatureConfig hop above the
+// spectrogram's panics earlier, in extractChromaFeatures (slice bounds, :348-352), after the
+// spectral features and the MFCC.  Below 1536 samples every group is
 // computed as in Go, the harmonic block zero by F7 unless the frame is exactly 1024 samples.
 #include "../../include/sonar_gpu.h"
 
@@ -154,11 +156,17 @@ int sonar_extract_music_features(sonar_ctx* c, const double* pcm, int64_t n, int
   if (fc->hop_size <= 0)
     return fail(c, SONAR_ERR_INVALID,
                 "chroma feature extraction failed: chroma computation failed at frame 0: hop size must be positive");
-  rc = sonar_chroma_stft(c, dy, n, F, fc->hop_size, csr, 0, dchroma, 1);
-  if (rc != SONAR_OK) return rc;
+  // frame f reads processedPCM[f hop : min(f hop + n/F, n)] (:348-352): a start past the end
+  // (hop above the spectrogram's, so (F-1) hop > n) is Go's slice-bounds panic at the first such
+  // frame; the spectral group and the MFCC were computed before it
+  const int64_t chroma_bad = (F - 1) * (int64_t)fc->hop_size > n ? n / fc->hop_size + 1 : -1;
+  if (chroma_bad < 0) {
+    rc = sonar_chroma_stft(c, dy, n, F, fc->hop_size, csr, 0, dchroma, 1);
+    if (rc != SONAR_OK) return rc;
+  }
 
   // ---- temporal (:378-458): ShortTimeEnergy (FeatureConfig W / H), envelope, amplitudes ------
-  const int64_t Fe = sonar_energy_frames(n, fc->window_size, fc->hop_size);
+  const int64_t Fe = chroma_bad < 0 ? sonar_energy_frames(n, fc->window_size, fc->hop_size) : 0;
   double* den = (double*)dbuf(c, "mx.energy", (size_t)std::max<int64_t>(Fe, 1) * 8);
   double* dabs = (double*)dbuf(c, "mx.abs", 16);
   if (!den || !dabs) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (energy)");
@@ -171,19 +179,21 @@ int sonar_extract_music_features(sonar_ctx* c, const double* pcm, int64_t n, int
   if (!denv || !dpk) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (envelope)");
   if (Fenv > 0 && sonar::launch_energy(dy, 1, n, Fenv, (int)fse, fc->hop_size, 0.0, denv, 1, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "envelope launch failed");
-  if (sonar::launch_abs_stats(dy, n, dabs, s) != 0) return fail(c, SONAR_ERR_DEVICE, "amplitude launch failed");
+  if (chroma_bad < 0 && sonar::launch_abs_stats(dy, n, dabs, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "amplitude launch failed");
   if (Fe > 0 && sonar::launch_frame_peak(dy, n, Fe, fse, dpk, s) != 0) return fail(c, SONAR_ERR_DEVICE, "peak launch failed");
   // the harmonic block's one live case: a 1024-sample frame (DetectPitch's window, :539)
   const int64_t fsh = F > 0 ? n / F : 0;
   double* dyin = (double*)dbuf(c, "mx.yin", 16);
   if (!dyin) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (pitch)");
-  const bool harmonic_live = fsh == 1024 && n < 1536;
+  const bool harmonic_live = fsh == 1024 && n < 1536 && chroma_bad < 0;
   if (harmonic_live && sonar::launch_yin(dy, n, 1, 1024, csr, dyin, dyin + 1, nullptr, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
 
   std::vector<double> mfcc, spec, con, lh, chroma, energy, env, abss, peaks, yv;
   if (d2h(c, mfcc, dmfcc, Fz * 13) || d2h(c, spec, dspec, Fz * 9) || d2h(c, con, dcon, Fz * kContrastBands) ||
-      d2h(c, lh, dlh, Fz * 2) || d2h(c, chroma, dchroma, Fz * 12) || d2h(c, energy, den, (size_t)Fe) ||
+      d2h(c, lh, dlh, Fz * 2) || d2h(c, chroma, dchroma, chroma_bad < 0 ? Fz * 12 : 0) ||
+      d2h(c, energy, den, (size_t)Fe) ||
       d2h(c, env, denv, (size_t)Fenv) || d2h(c, abss, dabs, 2) || d2h(c, peaks, dpk, (size_t)Fe) ||
       d2h(c, yv, dyin, harmonic_live ? 2 : 0))
     return SONAR_ERR_DEVICE;
@@ -203,6 +213,13 @@ int sonar_extract_music_features(sonar_ctx* c, const double* pcm, int64_t n, int
   res->put("zero_crossing_rate", std::vector<double>(Fz, 0.0), F, 1);
   res->put("spectral_contrast", std::move(con), F, kContrastBands);
   res->put("mfcc", std::move(mfcc), F, 13);
+  if (chroma_bad >= 0) {
+    char msg[96];
+    std::snprintf(msg, sizeof(msg), "runtime error: slice bounds out of range [%lld:%lld]",
+                  (long long)(chroma_bad * fc->hop_size), (long long)n);
+    *out = res;
+    return fail(c, SONAR_ERR_PANIC, msg);
+  }
   res->put("chroma", std::move(chroma), F, 12);
   res->vec("rms_energy", energy);
   // numFrames := len(RMSEnergy); frameSize := len(pcm) / numFrames (:382-383)

@@ -458,7 +458,56 @@ void fill_pair_params(sonar_ctx* c, const PairTables& t, const sonar_fp_cfg* cfg
   const int64_t target_waves = (int64_t)dev_cus * 12;
   q.pairs_per_wave = std::max<int64_t>(1, (NP + target_waves - 1) / target_waves);
 }
+
+// The transform kernel of a validated sonar_fingerprint call over F frames (sonar_fp_kernel_plan):
+// mfcc_pair_kernel for the float32 MFCC-only configuration at W = 1024 while its 32-bit frame
+// indices hold (t = 2 pair + 1 <= F), the general fused kernel for the other fused window sizes,
+// the float64 DFT path for any other W.
+int fp_plan(const sonar_fp_cfg* cfg, int64_t F) {
+  const uint32_t flags = cfg->flags;
+  if (!(flags & (SONAR_FP_MFCC | SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_COMPLEX | SONAR_FP_PHASE)))
+    return SONAR_PLAN_NONE;
+  if (!sonar::fingerprint_supported(cfg->window_size)) return SONAR_PLAN_DFT;
+  const bool pair = cfg->precision != SONAR_F64 && cfg->pcm_dtype != SONAR_F64 && cfg->out_dtype != SONAR_F64 &&
+                    cfg->window_size == 1024 && (flags & SONAR_FP_MFCC) &&
+                    !(flags & (SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_COMPLEX | SONAR_FP_PHASE |
+                               SONAR_FP_GENERIC | 0x80000000u)) &&
+                    F <= SONAR_PAIR_MAX_FRAMES;
+  return pair ? SONAR_PLAN_PAIR : SONAR_PLAN_WAVE;
+}
+
+// ComputeSTFTWithWindow's argument checks (spectral.go:386-412) and the GPU path's own limits, in the
+// order sonar_fingerprint applies them: SONAR_OK and the frame count, or the error code + message
+int fp_validate(const sonar_fp_cfg* cfg, int64_t n, bool have_pcm, int64_t* F, std::string* msg) {
+  if (n <= 0 || !have_pcm) { *msg = "empty signal"; return SONAR_ERR_EMPTY; }
+  const int W = cfg->window_size, H = cfg->hop_size;
+  if (W <= 0) { *msg = "window size must be positive"; return SONAR_ERR_INVALID; }
+  if (H <= 0) { *msg = "hop size must be positive"; return SONAR_ERR_INVALID; }
+  *F = go_frames(n, W, H);
+  if (*F <= 0) { *msg = "signal too short for given window size and hop size"; return SONAR_ERR_TOO_SHORT; }
+  if (fp_plan(cfg, *F) == SONAR_PLAN_DFT) {
+    // other window lengths (go-dsp takes any W, spectral.go:131) run the generic DFT path; the
+    // spectral descriptors exist only in the fused kernels
+    if (cfg->flags & SONAR_FP_SPECTRAL) {
+      *msg = "spectral descriptors need a window of 128, 256, 512, 1024 or 2048 (got " + std::to_string(W) + ")";
+      return SONAR_ERR_UNSUPPORTED;
+    }
+    if (W > 8192) {
+      *msg = "window size " + std::to_string(W) + " above 8192 (generic STFT path)";
+      return SONAR_ERR_UNSUPPORTED;
+    }
+  }
+  return SONAR_OK;
+}
 }  // namespace
+
+extern "C" int32_t sonar_fp_kernel_plan(const sonar_fp_cfg* cfg, int64_t n) {
+  if (!cfg) return SONAR_ERR_INVALID;
+  int64_t F = 0;
+  std::string msg;
+  const int rc = fp_validate(cfg, n, true, &F, &msg);
+  return rc != SONAR_OK ? rc : fp_plan(cfg, F);
+}
 
 namespace sonar {
 namespace detail {
@@ -467,27 +516,21 @@ namespace detail {
 int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cfg* cfg, sonar_fp_out* out,
                      bool pcm_dev) {
   if (!c || !cfg || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
-  // ComputeSTFTWithWindow validation order (spectral.go:386-412)
-  if (n <= 0 || !pcm) return fail(c, SONAR_ERR_EMPTY, "empty signal");
+  // ComputeSTFTWithWindow validation order (spectral.go:386-412), then the GPU path's limits
+  int64_t F = 0;
+  {
+    std::string msg;
+    const int rc = fp_validate(cfg, n, pcm != nullptr, &F, &msg);
+    if (rc != SONAR_OK) return fail(c, rc, msg);
+  }
   const int W = cfg->window_size, H = cfg->hop_size;
-  if (W <= 0) return fail(c, SONAR_ERR_INVALID, "window size must be positive");
-  if (H <= 0) return fail(c, SONAR_ERR_INVALID, "hop size must be positive");
-  const int64_t F = go_frames(n, W, H);
-  if (F <= 0) return fail(c, SONAR_ERR_TOO_SHORT, "signal too short for given window size and hop size");
   const bool f64 = cfg->precision == SONAR_F64;
   const bool pcm64 = cfg->pcm_dtype == SONAR_F64;
   const bool o64 = cfg->out_dtype == SONAR_F64;
   const uint32_t flags = cfg->flags;
-  const bool need_fft = flags & (SONAR_FP_MFCC | SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_COMPLEX |
-                                 SONAR_FP_PHASE);
-  // other window lengths (go-dsp takes any W, spectral.go:131) run the generic DFT path; the
-  // spectral descriptors exist only in the fused kernels
-  const bool generic = need_fft && !sonar::fingerprint_supported(W);
-  if (generic && (flags & SONAR_FP_SPECTRAL))
-    return fail(c, SONAR_ERR_UNSUPPORTED, "spectral descriptors need a window of 128, 256, 512, 1024 or 2048 (got " +
-                                              std::to_string(W) + ")");
-  if (generic && W > 8192)
-    return fail(c, SONAR_ERR_UNSUPPORTED, "window size " + std::to_string(W) + " above 8192 (generic STFT path)");
+  const int plan = fp_plan(cfg, F);
+  const bool need_fft = plan != SONAR_PLAN_NONE;
+  const bool generic = plan == SONAR_PLAN_DFT;
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const size_t esz_in = pcm64 ? 8 : 4, esz_out = o64 ? 8 : 4;
@@ -587,11 +630,8 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     c->last_fp_kernel = "stft_dft_kernel";
   }
   // headline path: float32 MFCC only at W = 1024 (mfcc_pair.hip); SONAR_FP_GENERIC forces fp_kernel.hip
-  const bool pair_ok = !generic && need_fft && !f64 && !pcm64 && !o64 && W == 1024 && (flags & SONAR_FP_MFCC) &&
-                       !(flags & (SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_COMPLEX | SONAR_FP_PHASE |
-                                  SONAR_FP_GENERIC | 0x80000000u));
   bool pair_done = false;
-  if (pair_ok) {
+  if (plan == SONAR_PLAN_PAIR) {
     const PairTables& t = pair_tables_for(c, cfg);
     if (t.ok) {
       sonar::MfccPairParams q{};
@@ -599,7 +639,9 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
       q.pcm = (const float*)dpcm; q.n = n; q.F = F; q.H = H;
       q.out = (float*)d_mfcc;
       hipEvent_t tend = timed_begin(c, s);
-      if (sonar::launch_mfcc_pair(q, s) != 0)
+      const int lrc = sonar::launch_mfcc_pair(q, s);
+      if (lrc == -4) return fail(c, SONAR_ERR_UNSUPPORTED, "too many frames for one mfcc_pair_kernel launch");
+      if (lrc != 0)
         return fail(c, SONAR_ERR_DEVICE, std::string("mfcc kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
       timed_end(c, s, tend);
       pair_done = true;
@@ -736,8 +778,11 @@ int sonar_fingerprint_batch(sonar_ctx* c, const void* const* pcm, const int64_t*
       return sig_fail(i, SONAR_ERR_TOO_SHORT, "signal too short for given window size and hop size");
   }
   const bool dev = cfg->device_ptrs != 0;
+  int64_t pairs_total = 0;                 // the one launch's 32-bit frame indices run over the whole batch
+  for (int i = 0; i < count; i++) pairs_total += (go_frames(n[i], W, H) + 1) / 2;
   const bool one_launch = W == 1024 && cfg->flags == SONAR_FP_MFCC && cfg->precision == SONAR_F32 &&
-                          cfg->pcm_dtype == SONAR_F32 && cfg->out_dtype == SONAR_F32;
+                          cfg->pcm_dtype == SONAR_F32 && cfg->out_dtype == SONAR_F32 &&
+                          2 * pairs_total <= SONAR_PAIR_MAX_FRAMES;
   const PairTables* tp = one_launch ? &pair_tables_for(c, cfg) : nullptr;
   if (!tp || !tp->ok) {
     for (int i = 0; i < count; i++) {
@@ -795,7 +840,9 @@ int sonar_fingerprint_batch(sonar_ctx* c, const void* const* pcm, const int64_t*
   q.F = 2 * NP; q.H = H;
   q.seg = dseg; q.nseg = count;
   hipEvent_t tend = timed_begin(c, s);
-  if (sonar::launch_mfcc_pair(q, s) != 0)
+  const int lrc = sonar::launch_mfcc_pair(q, s);
+  if (lrc == -4) return fail(c, SONAR_ERR_UNSUPPORTED, "too many frames for one mfcc_pair_kernel launch");
+  if (lrc != 0)
     return fail(c, SONAR_ERR_DEVICE, std::string("mfcc kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
   timed_end(c, s, tend);
   c->last_fp_kernel = "mfcc_pair_kernel";

@@ -29,6 +29,12 @@ from ._abi import (  # noqa: F401
     stft_frames,
     energy_frames,
     pitch_frames,
+    fp_kernel_plan,
+    PLAN_NONE,
+    PLAN_PAIR,
+    PLAN_WAVE,
+    PLAN_DFT,
+    PAIR_MAX_FRAMES,
     FP_MFCC,
     FP_MAGNITUDE,
     FP_SPECTRAL,

@@ -198,6 +198,8 @@ def lib():
     L.sonar_pitch_frames.restype = C.c_int64
     L.sonar_fp_cfg_default.argtypes = [C.POINTER(FpConfig)]
     L.sonar_fp_cfg_default.restype = None
+    L.sonar_fp_kernel_plan.argtypes = [C.POINTER(FpConfig), C.c_int64]
+    L.sonar_fp_kernel_plan.restype = C.c_int32
     L.sonar_fingerprint.argtypes = [_vp, _vp, C.c_int64, C.POINTER(FpConfig), C.POINTER(FpOut)]
     L.sonar_fingerprint_batch.argtypes = [_vp, C.POINTER(_vp), C.POINTER(C.c_int64), C.c_int32,
                                           C.POINTER(FpConfig), C.POINTER(FpOut)]
@@ -286,6 +288,15 @@ def abi_version():
 
 def stft_frames(n, W, H):
     return int(lib().sonar_stft_frames(n, W, H))
+
+
+PLAN_NONE, PLAN_PAIR, PLAN_WAVE, PLAN_DFT = 0, 1, 2, 3
+PAIR_MAX_FRAMES = 2147483646          # SONAR_PAIR_MAX_FRAMES: mfcc_pair_kernel's 32-bit frame indices
+
+
+def fp_kernel_plan(cfg, n):
+    """sonar_fp_kernel_plan: the transform kernel sonar_fingerprint runs for (cfg, n) (host logic)."""
+    return int(lib().sonar_fp_kernel_plan(C.byref(cfg), n))
 
 
 def energy_frames(n, W, H):

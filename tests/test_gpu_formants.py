@@ -38,6 +38,21 @@ def test_formant_frames_match_oracle(ctx, sr, seconds):
     assert np.max(np.abs(got["lpc_coeffs"][ok] - ref["lpc_coeffs"][ok]) / scale) < 1e-6
 
 
+def test_formant_frames_full_c4_30min(ctx):
+    """BASELINE configs[3] at its own size: AnalyzeMultipleFrames (format.go:427-449) over the whole
+    30-min 16 kHz C4 signal (28,123 frames of 2,048 at hop 1,024), the bench's c4_formants call,
+    against the oracle frame by frame with the rules above (status, counts and frequencies exact)."""
+    x = synth.c4_speech(seconds=1800.0, sr=16000)
+    got = ctx.formants(x, 16000, want_lpc=True)
+    ref = O.formant_frames(x, 16000, want_lpc=True)
+    assert len(got["status"]) == len(ref["status"]) == 28123
+    _cmp(got, ref)
+    ok = ref["status"] == 0
+    assert np.count_nonzero(ok) > 0
+    scale = np.max(np.abs(ref["lpc_coeffs"][ok]), axis=1, keepdims=True)
+    assert np.max(np.abs(got["lpc_coeffs"][ok] - ref["lpc_coeffs"][ok]) / scale) < 1e-6
+
+
 def test_formant_frames_custom_geometry_and_edges(ctx):
     x = synth.c4_speech(seconds=6.0, sr=16000)
     for fs, hop in [(4096, 1000), (2048, 512), (1500, 700)]:          # 1500 < W: every frame rejected

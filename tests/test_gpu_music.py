@@ -103,6 +103,25 @@ def test_full_extractor_below_1536_samples(ctx, n, W, H, fw, fh):
     # (0.95) leaves a low tone below the noise there, so Go (and the oracle) report no pitch either
 
 
+@pytest.mark.parametrize("n,W,H,fw,fh", [(1300, 256, 64, 256, 512), (88200, 1024, 256, 1024, 512),
+                                          (5000, 1024, 256, 1024, 1000)])
+def test_chroma_hop_above_spectrogram_hop_panics(ctx, n, W, H, fw, fh):
+    """FeatureConfig.HopSize above the spectrogram's: extractChromaFeatures slices
+    processedPCM[f hop : min(f hop + n/F, n)] (music.go:348-352), so once (F - 1) hop > n Go panics
+    with 'slice bounds out of range [start:n]' at the first frame starting past the end; only the
+    spectral group and the MFCC were computed."""
+    rng = np.random.default_rng(n)
+    x = synth.sweep(n / 44100.0)[:n] + 0.01 * rng.standard_normal(n)
+    F = sonar.stft_frames(n, W, H)
+    assert (F - 1) * fh > n
+    got, err, ref, panic = _run(ctx, x, stft_window_size=W, stft_hop_size=H, window_size=fw, hop_size=fh)
+    assert panic == f"runtime error: slice bounds out of range [{(n // fh + 1) * fh}:{n}]"
+    assert err is not None and err.code == sonar.ERR_PANIC and err.msg == panic, (err, panic)
+    assert "chroma" not in got and "rms_energy" not in got
+    assert set(got) == set(ref), sorted(set(got) ^ set(ref))
+    _compare(got, ref)
+
+
 def test_short_signal_temporal_error(ctx):
     """<= 512 samples: the onset STFT (1024 / 512) fails and ExtractFeatures with it (:412-415)."""
     x = synth.sweep(0.011)[:500]
