@@ -215,6 +215,35 @@ int32_t sonar_fp_kernel_plan(const sonar_fp_cfg* cfg, int64_t n);
 int sonar_fingerprint_batch(sonar_ctx* ctx, const void* const* pcm, const int64_t* n, int32_t count,
                             const sonar_fp_cfg* cfg, sonar_fp_out* out);
 
+/* ---- STFTStreamer (fingerprint/analyzers/spectral.go:287-374) ---------------------------------
+ * SpectralAnalyzer.ComputeSTFTStreaming(W, H, windowType) + STFTStreamer.ProcessChunk.  The stream
+ * keeps Go's buffer (the samples not yet consumed, < W for H <= W) on the device; each push appends
+ * a chunk and emits every complete frame in ONE fused STFT launch over [buffer | chunk].  Rows are
+ * bit-identical to one sonar_fingerprint call over the concatenated stream with the same cfg plus
+ * SONAR_FP_GENERIC (the per-frame kernel; the headline pair kernel's bits depend on a frame's
+ * partner, which a push may not have yet).  Frame placement is Go's, including its quirk for
+ * H > W: a frame whose hop reaches past the buffered samples clears the buffer (:355-362), so the
+ * rest of that skip is not carried into the next chunk. */
+typedef struct sonar_stft_stream sonar_stft_stream;
+/* cfg: window_size, hop_size, window_type ({Normalize, Symmetric} and Go's zero Beta / Alpha, as
+ * :290-295), flags (SONAR_FP_MAGNITUDE / _PHASE / _COMPLEX -- SpectrogramFrame -- and SONAR_FP_MFCC
+ * with cfg's MFCC parameters), precision, pcm_dtype, out_dtype, device_ptrs (for every push's chunk
+ * and outputs).  Errors: "failed to generate window: window size must be positive: W" / "... too
+ * large: W" (windowing.go:180-187); other flags -> SONAR_ERR_UNSUPPORTED. */
+int sonar_stft_stream_create(sonar_ctx* ctx, const sonar_fp_cfg* cfg, sonar_stft_stream** out);
+/* Frames the next push of n samples will emit: 0 for n <= 0 or while fewer than W samples are held,
+ * else (buffered + n - W) / H + 1 (host arithmetic; size the outputs of the push with it). */
+int64_t sonar_stft_stream_frames(const sonar_stft_stream* st, int64_t n);
+/* STFTStreamer.ProcessChunk(chunk) (:322-366): n <= 0 emits nothing (Go returns nil, nil).  out's
+ * requested arrays receive *frames rows (laid out as sonar_fingerprint's for that many frames).
+ * H == 0 with a frame due -> SONAR_ERR_INVALID (Go's loop never advances); H < 0 -> SONAR_ERR_PANIC
+ * "runtime error: slice bounds out of range [H:]" (:359).  Host buffers: synchronous; device buffers:
+ * asynchronous on the ctx stream (the chunk may be reused once the stream has passed the push). */
+int sonar_stft_stream_push(sonar_stft_stream* st, const void* chunk, int64_t n, sonar_fp_out* out,
+                           int64_t* frames);
+int64_t sonar_stft_stream_buffered(const sonar_stft_stream* st);   /* len(s.buffer) */
+void sonar_stft_stream_destroy(sonar_stft_stream* st);
+
 /* ---- PCM ingest: the decoder's f64le byte stream -> device samples.
  * Replaces Decoder.bytesToFloat64 + processFFmpegOutput's empty check (transcode/decoder.go:850-871,
  * :782-787; ffmpeg "-f f64le" at :709): nbytes is trimmed to a multiple of 8, zero samples fail with

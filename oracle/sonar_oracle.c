@@ -253,8 +253,10 @@ int or_stft_mag_window(const double* pcm, int64_t n, int W, int H, const double*
 
 int or_stft_mag(const double* pcm, int64_t n, int W, int H, int window_type, int nthreads, double* mag) {
     double* win = malloc(sizeof(double) * W);
-    /* SpectralAnalyzer always asks for {Normalize:true, Symmetric:true} (spectral.go:415-420) */
-    if (or_window(window_type, W, 1, 1, 8.6, 0.5, win) != 0) { free(win); return -2; }
+    /* SpectralAnalyzer always asks for {Normalize:true, Symmetric:true} (spectral.go:415-420); the
+     * literal leaves Beta and Alpha at Go's zero value (not DefaultWindowConfig's 8.6 / 0.5,
+     * windowing.go:66-73): Kaiser is I0(0)/I0(0) = 1, Tukey has no taper -- both rectangular */
+    if (or_window(window_type, W, 1, 1, 0.0, 0.0, win) != 0) { free(win); return -2; }
     int rc = or_stft_mag_window(pcm, n, W, H, win, nthreads, mag);
     free(win);
     return rc;
@@ -268,7 +270,7 @@ int or_stft_complex(const double* pcm, int64_t n, int W, int H, int window_type,
     if (F < 0) return -1;
     int K = W / 2 + 1;
     double* win = malloc(sizeof(double) * W);
-    if (or_window(window_type, W, 1, 1, 8.6, 0.5, win) != 0) { free(win); return -2; }
+    if (or_window(window_type, W, 1, 1, 0.0, 0.0, win) != 0) { free(win); return -2; }   /* as or_stft_mag */
     double* buf = malloc(sizeof(double) * W);
     double* re = malloc(sizeof(double) * W); double* im = malloc(sizeof(double) * W);
     for (int64_t t = 0; t < F; t++) {
@@ -716,7 +718,7 @@ done:
 int or_chroma_frames(const double* y, int64_t n, int64_t F, int H, int fs, int sr, double* out) {
     if (fs <= 0) return -1;
     double* win = malloc(sizeof(double) * fs);
-    or_window(OR_WIN_HANN, fs, 1, 1, 8.6, 0.5, win);
+    or_window(OR_WIN_HANN, fs, 1, 1, 0.0, 0.0, win);     /* music.go:335-340 literal (Hann: no parameter) */
     int K = fs / 2 + 1;
     int* map = malloc(sizeof(int) * K);
     double res = (double)sr / (double)fs;                         /* FreqResolution stft.go:158 */

@@ -440,6 +440,7 @@ constexpr int DTW_RBLK = 16;               // rows per ring refill
 #define DTW_DQ_CFG 32
 #endif
 constexpr int DTW_DQ = DTW_DQ_CFG;         // steps of distances held in LDS (a power of two)
+constexpr int DTW_SWEEP_PRIO = 3;  // s_setprio of the sweep (the min-chain is the critical path)
 #ifndef DTW_CODE_PRIO
 #define DTW_CODE_PRIO 2           // s_setprio of the code wave (A/B: 0, 1, 2, 3)
 #endif
@@ -694,10 +695,14 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
   uint64_t spins_total = 0;
   uint32_t dead_ = 0;
   // spin (LDS only) until `cond` holds; bounded, see DTW_SPIN_CHECK.  A wave that gives up, or sees
-  // the block's abort word, sets dead_ and runs out its loop without waiting again.
-#define SONAR_SPIN_UNTIL(role, cond)                                                  \
+  // the block's abort word, sets dead_ and runs out its loop without waiting again.  `prio` is the
+  // wave's working s_setprio level (a constant): while it spins the wave drops to 0 and takes it back
+  // once `cond` holds, so a waiting wave never outranks the producer it waits for (DESIGN.md,
+  // Kernel 6, "Issue priorities and liveness").
+#define SONAR_SPIN_UNTIL(role, prio, cond)                                            \
   do {                                                                                \
     if (!dead_ && !(cond)) {                                                          \
+      if ((prio) > 0) __builtin_amdgcn_s_setprio(0);                                  \
       const uint64_t tr0_ = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;           \
       uint64_t w0_ = 0;                                                               \
       uint32_t sp_ = 0, rounds_ = 0;                                                  \
@@ -715,6 +720,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
         }                                                                             \
       }                                                                               \
       if (a.trace) spins_total += __builtin_amdgcn_s_memrealtime() - tr0_;            \
+      if ((prio) > 0) __builtin_amdgcn_s_setprio(prio);                               \
     }                                                                                 \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");                            \
   } while (0)
@@ -858,7 +864,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
     double ckv = 0.0;                                  // the lane's C at the latest multiple-of-64 column
     for (int64_t s0 = 0; s0 < S; s0 += DTW_ECH) {
       const int need = (int)(s0 + DTW_ECH < S ? s0 + DTW_ECH : S);
-      SONAR_SPIN_UNTIL(DTW_ROLE_CODE, SONAR_LDS_LD(prog) >= need);
+      SONAR_SPIN_UNTIL(DTW_ROLE_CODE, DTW_CODE_PRIO, SONAR_LDS_LD(prog) >= need);
       // steps s0-2 .. s0+7 as 5 pairs (the last value unused); lane 0's neighbour pairs are the
       // edge columns (t+2, t+3) at eqb slots (t+2, t+3) (per-lane addresses, no divergence)
       double cv[DTW_ECH + 2], nv[DTW_ECH + 2];
@@ -951,12 +957,12 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
     for (int64_t c = w; DTW_ECH * c < S; c += DTW_NDW) {
       const int64_t t0 = DTW_ECH * c;
       // ring slots of steps t0..t0+7 were last read by the sweep for steps t0-DQ..t0-DQ+7
-      SONAR_SPIN_UNTIL(DTW_ROLE_DIST, SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW_DQ);
+      SONAR_SPIN_UNTIL(DTW_ROLE_DIST, DTW_DIST_PRIO, SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW_DQ);
       double dv[DTW_ECH];
       if constexpr (D > 0) {
         const int64_t need = (t0 + DTW_ECH - 1) / DTW_RBLK;             // rows up to t0+7
         const int64_t needc = need < nblk - 1 ? need : nblk - 1;
-        SONAR_SPIN_UNTIL(DTW_ROLE_DIST, SONAR_LDS_LD(rdy) >= needc);
+        SONAR_SPIN_UNTIL(DTW_ROLE_DIST, DTW_DIST_PRIO, SONAR_LDS_LD(rdy) >= needc);
         // rows t0-l .. t0-l+7 sit at consecutive slots (mirror), so one base + immediate offsets;
         // steps past S and rows outside [0, nr) give values the sweep never stores.  The chunk's
         // cells advance together, one dimension at a time: each sum is Go's sequential chain,
@@ -1025,7 +1031,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
   // ---------------------------------------------------------------- sweep wave
   // the min-chain is the pipeline's critical path: it wins VALU arbitration over the distance
   // waves sharing its SIMD (MI355X_MICROARCH.md, "VALU issue is arbitrated ... by priority")
-  __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(DTW_SWEEP_PRIO);
   const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
   uint64_t t_first = 0;
   uint64_t* Eout = (b + 1 < a.nb) ? a.E + b * (nr + 1) : nullptr;         // C[64b+64][j]
@@ -1153,7 +1159,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
   if (!ready(0, kc)) {
     const int cause = a.trace ? spin_cause(0, kc) : 0;
     const uint64_t before = spins_total;
-    SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready(0, kc)));
+    SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, DTW_SWEEP_PRIO, (kc = load_ctr(), ready(0, kc)));
     if (a.trace) account(cause, before);
   }
   if (a.trace) t_first = __builtin_amdgcn_s_memrealtime();
@@ -1200,7 +1206,7 @@ __global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(
       {
         const int cause = a.trace ? spin_cause((int)s1, kc) : 0;
         const uint64_t before = spins_total;
-        SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, (kc = load_ctr(), ready((int)s1, kc)));
+        SONAR_SPIN_UNTIL(DTW_ROLE_SWEEP, DTW_SWEEP_PRIO, (kc = load_ctr(), ready((int)s1, kc)));
         if (a.trace) account(cause, before);
         load_chunk(s1, dcn, echn);
       }

@@ -87,6 +87,13 @@ void trim_buffers(sonar_ctx* c) {
 }  // namespace detail
 }  // namespace sonar
 
+// The WindowConfig literals of ComputeSTFTWithWindow / ComputeSTFTStreaming (spectral.go:290-295,
+// :415-420) and extractChromaFeatures (music.go:335-340) set only Type, Size, Normalize and Symmetric:
+// Beta and Alpha keep Go's zero value, not DefaultWindowConfig's 8.6 / 0.5 (windowing.go:66-73).  So a
+// Kaiser STFT window is I0(0)/I0(0) = 1 everywhere and a Tukey one has no taper (int(0 * N / 2) = 0):
+// both are rectangular.
+constexpr double kStftBeta = 0.0, kStftAlpha = 0.0;
+
 namespace {
 using namespace sonar::detail;
 
@@ -116,7 +123,7 @@ int64_t go_frames(int64_t n, int W, int H) { return (n - W) / H + 1; }
 bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
   const int W = 1024, K = W / 2 + 1;
   std::vector<double> win;
-  if (!sonar::host::make_window(cfg->window_type, W, true, true, 8.6, 0.5, win)) return false;
+  if (!sonar::host::make_window(cfg->window_type, W, true, true, kStftBeta, kStftAlpha, win)) return false;
   sonar::host::MfccTables mt;
   if (!sonar::host::make_mfcc_tables(cfg->sample_rate, cfg->n_mfcc, cfg->n_filters, cfg->filterbank, cfg->low_freq,
                                      cfg->high_freq, cfg->use_lifter != 0, cfg->lifter, W, mt))
@@ -583,7 +590,7 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     if (it == c->fp_tables.end()) {
       FpTables t;
       std::vector<double> win;
-      if (!sonar::host::make_window(cfg->window_type, W, true, true, 8.6, 0.5, win))
+      if (!sonar::host::make_window(cfg->window_type, W, true, true, kStftBeta, kStftAlpha, win))
         return fail(c, SONAR_ERR_INVALID, "failed to generate window: unsupported window type");
       std::vector<double> trig(2 * (size_t)W);
       for (int m = 0; m < W; ++m) {
@@ -673,7 +680,7 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     if (it == c->fp_tables.end()) {
       FpTables t;
       std::vector<double> win;
-      if (!sonar::host::make_window(cfg->window_type, W, true, true, 8.6, 0.5, win))
+      if (!sonar::host::make_window(cfg->window_type, W, true, true, kStftBeta, kStftAlpha, win))
         return fail(c, SONAR_ERR_INVALID, "failed to generate window: unsupported window type");
       t.window = upload_real(win, f64);
       sonar::host::MfccTables mt;
@@ -940,7 +947,7 @@ const sonar_ctx::ChromaT* chroma_tables_for(sonar_ctx* c, int fs, int sr) {
   auto it = c->chroma_tables.find(key);
   if (it == c->chroma_tables.end()) {
     std::vector<double> win;
-    sonar::host::make_window(SONAR_WIN_HANN, fs, true, true, 8.6, 0.5, win);
+    sonar::host::make_window(SONAR_WIN_HANN, fs, true, true, kStftBeta, kStftAlpha, win);
     std::vector<int> map = sonar::host::chroma_map(fs, sr);
     std::vector<double> trig(2 * (size_t)fs);
     for (int m = 0; m < fs; m++) {

@@ -198,6 +198,14 @@ def lib():
     L.sonar_pitch_frames.restype = C.c_int64
     L.sonar_fp_cfg_default.argtypes = [C.POINTER(FpConfig)]
     L.sonar_fp_cfg_default.restype = None
+    L.sonar_stft_stream_create.argtypes = [_vp, C.POINTER(FpConfig), C.POINTER(_vp)]
+    L.sonar_stft_stream_frames.argtypes = [_vp, C.c_int64]
+    L.sonar_stft_stream_frames.restype = C.c_int64
+    L.sonar_stft_stream_buffered.argtypes = [_vp]
+    L.sonar_stft_stream_buffered.restype = C.c_int64
+    L.sonar_stft_stream_push.argtypes = [_vp, _vp, C.c_int64, C.POINTER(FpOut), C.POINTER(C.c_int64)]
+    L.sonar_stft_stream_destroy.argtypes = [_vp]
+    L.sonar_stft_stream_destroy.restype = None
     L.sonar_fp_kernel_plan.argtypes = [C.POINTER(FpConfig), C.c_int64]
     L.sonar_fp_kernel_plan.restype = C.c_int32
     L.sonar_fingerprint.argtypes = [_vp, _vp, C.c_int64, C.POINTER(FpConfig), C.POINTER(FpOut)]
@@ -471,8 +479,11 @@ class Context:
                                                     C.byref(cfg), C.byref(out)))
         return res
 
-    def _fp_outputs(self, n, cfg):
-        F = stft_frames(n, cfg.window_size, cfg.hop_size) if n > 0 and cfg.window_size > 0 and cfg.hop_size > 0 else 0
+    def _fp_outputs(self, n, cfg, frames=None):
+        if frames is not None:
+            F = frames
+        else:
+            F = stft_frames(n, cfg.window_size, cfg.hop_size) if n > 0 and cfg.window_size > 0 and cfg.hop_size > 0 else 0
         od = np.float64 if cfg.out_dtype == F64 else np.float32
         out, res = FpOut(), {}
         if F > 0:
@@ -502,6 +513,12 @@ class Context:
                 res["energy"] = np.zeros(fe, od)
                 out.energy = res["energy"].ctypes.data if fe > 0 else None
         return res, out
+
+    def stft_stream(self, cfg: FpConfig):
+        """sonar_stft_stream_create: SpectralAnalyzer.ComputeSTFTStreaming (spectral.go:287-312)."""
+        h = C.c_void_p()
+        self._check(self._L.sonar_stft_stream_create(self._h, C.byref(cfg), C.byref(h)))
+        return StftStream(self, h, cfg)
 
     def fingerprint_device(self, pcm_ptr, n, cfg: FpConfig, **out_ptrs):
         """Device-pointer form (async on the ctx stream): out_ptrs name -> device address."""
@@ -753,6 +770,56 @@ class Context:
             q_pcm_len, r_pcm_len, sample_rate, feature_sample_rate, hop_size, window_size, max_lag_seconds,
             C.byref(h)))
         return self._result(h)
+
+
+class StftStream:
+    """STFTStreamer (fingerprint/analyzers/spectral.go:314-366) over sonar_stft_stream_*: push(chunk)
+    is ProcessChunk and returns the emitted frames as a dict of arrays (the cfg's outputs, rows =
+    frames; empty arrays when no frame is complete).  Host buffers (cfg.device_ptrs = 0) unless
+    push_device is used."""
+
+    def __init__(self, ctx, h, cfg):
+        self._ctx, self._h, self.cfg = ctx, h, cfg
+
+    def frames(self, n):
+        return int(self._ctx._L.sonar_stft_stream_frames(self._h, n))
+
+    @property
+    def buffered(self):
+        return int(self._ctx._L.sonar_stft_stream_buffered(self._h))
+
+    def push(self, chunk):
+        cfg = self.cfg
+        x = np.ascontiguousarray(chunk, dtype=np.float64 if cfg.pcm_dtype == F64 else np.float32)
+        n = len(x)
+        F = self.frames(n)
+        res, out = self._ctx._fp_outputs(n, cfg, frames=max(F, 0))
+        got = C.c_int64()
+        self._ctx._check(self._ctx._L.sonar_stft_stream_push(self._h, _ptr(x) if n else None, n, C.byref(out),
+                                                             C.byref(got)))
+        assert got.value == max(F, 0), (got.value, F)
+        return res
+
+    def push_device(self, ptr, n, **out_ptrs):
+        """Device chunk and outputs (cfg.device_ptrs must be 1): async on the ctx stream; returns the
+        number of frames written."""
+        out = FpOut()
+        for k, v in out_ptrs.items():
+            setattr(out, k, v)
+        got = C.c_int64()
+        self._ctx._check(self._ctx._L.sonar_stft_stream_push(self._h, C.c_void_p(ptr), n, C.byref(out), C.byref(got)))
+        return got.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._ctx._L.sonar_stft_stream_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Multi:

@@ -89,7 +89,7 @@ def test_no_energy_frame_divides_by_zero(ctx):
 
 
 @pytest.mark.parametrize("n,W,H,fw,fh", [(1024, 1024, 256, 1024, 256), (1300, 1024, 256, 512, 128),
-                                          (1535, 512, 128, 1024, 256), (700, 512, 128, 256, 64),
+                                          (1535, 512, 128, 1024, 128), (700, 512, 128, 256, 64),
                                           (1024, 512, 256, 256, 128)])
 def test_full_extractor_below_1536_samples(ctx, n, W, H, fw, fh):
     rng = np.random.default_rng(n + W)
@@ -104,6 +104,7 @@ def test_full_extractor_below_1536_samples(ctx, n, W, H, fw, fh):
 
 
 @pytest.mark.parametrize("n,W,H,fw,fh", [(1300, 256, 64, 256, 512), (88200, 1024, 256, 1024, 512),
+                                          (1535, 512, 128, 1024, 256),
                                           (5000, 1024, 256, 1024, 1000)])
 def test_chroma_hop_above_spectrogram_hop_panics(ctx, n, W, H, fw, fh):
     """FeatureConfig.HopSize above the spectrogram's: extractChromaFeatures slices

@@ -22,6 +22,21 @@ def test_hann_normalisation_factor():
     assert np.mean(w ** 2) == pytest.approx(1.0, rel=1e-12)    # unit power gain (windowing.go:427-437)
 
 
+def test_stft_kaiser_and_tukey_windows_are_rectangular():
+    """F16: ComputeSTFTWithWindow's WindowConfig literal (spectral.go:415-420) sets only Type, Size,
+    Normalize and Symmetric, so Beta and Alpha are Go's zero values, not DefaultWindowConfig's 8.6 /
+    0.5 (windowing.go:66-73): Kaiser = I0(0 * ...)/I0(0) = 1, Tukey taper int(0 * N / 2) = 0 -- the STFT
+    of either equals the rectangular one exactly.  The parameterised windows themselves still follow
+    windowing.go:304-340."""
+    x = np.random.default_rng(4).standard_normal(1024 * 6)
+    rect = O.stft_mag(x, 1024, 256, window_type="rectangular")
+    for kind in ("kaiser", "tukey"):
+        assert np.array_equal(O.stft_mag(x, 1024, 256, window_type=kind), rect), kind
+    assert not np.allclose(O.window("kaiser", 64, beta=8.6), O.window("rectangular", 64))
+    assert np.array_equal(O.window("kaiser", 64, beta=0.0), O.window("rectangular", 64))
+    assert np.array_equal(O.window("tukey", 64, alpha=0.0), O.window("rectangular", 64))
+
+
 def test_mel_bin_points_and_nnz():
     fb = O.filterbank(26, 1024, 44100, 0, 22050)
     assert np.count_nonzero(fb) == 933

@@ -3,9 +3,12 @@
 flight = 16 streams x batches of 8) --reps times and report, per repetition, the wall time, the
 band pipeline's liveness counters (sonar_dtw_counters: edge refresh fences, fences followed by new
 edge values, timed-out DTWs / waves) and the failure text of any pair whose pipeline timed out
-(its diagnostic record, see DtwArgs::diag).  One JSON line per repetition, then a summary line.
+(its diagnostic record, see DtwArgs::diag).  One JSON line per call (the warm-up included), then a
+summary line, on stdout and APPENDED to --out (every call's record is kept across runs and variants:
+a timeout's role, band and ticket survive the next run).  The library's single-pair redo of a
+timed-out band pipeline is off unless --retry 1 (SONAR_PAIR_RETRY), so a timeout fails the call.
 
-Usage: python tools/c5_stress.py [--reps 40] [--pairs 1000] [--seconds 60]
+Usage: python tools/c5_stress.py [--reps 40] [--pairs 1000] [--seconds 60] [--out gpurun_out/c5_stress.jsonl]
 """
 import argparse
 import json
@@ -30,7 +33,22 @@ def main():
     ap.add_argument("--pairs", type=int, default=1000)
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--workers", type=int, default=128)
+    ap.add_argument("--retry", default="0", help="SONAR_PAIR_RETRY for the run (0: a timeout fails the call)")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "c5_stress.jsonl"),
+                    help="JSON lines appended here too ('' = stdout only)")
+    ap.add_argument("--tag", default="", help="label stored in every line (variant name)")
     a = ap.parse_args()
+    os.environ["SONAR_PAIR_RETRY"] = a.retry
+    if a.out:
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+
+    def emit(d):
+        d = {"tag": a.tag, "pid": os.getpid(), "time": time.time(), **d}
+        line = json.dumps(d)
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "a") as f:
+                f.write(line + "\n")
     ctx = sonar.Context(0)
     data = [pairs.c5_pair_device(k, a.seconds, device="cuda") for k in range(a.pairs)]
     torch.cuda.synchronize()
@@ -52,8 +70,7 @@ def main():
         run()
     except sonar.SonarError as e:
         werr = str(e)
-        print(json.dumps({"warmup_error": werr}), flush=True)
-    print(json.dumps({"warmup": True, "s": round(time.perf_counter() - t0, 4), **counters(), "error": werr}), flush=True)
+    emit({"warmup": True, "s": round(time.perf_counter() - t0, 4), **counters(), "error": werr})
     fails, tot = 0, {}
     for i in range(a.reps):
         t0 = time.perf_counter()
@@ -67,9 +84,8 @@ def main():
         c = counters()
         for k, v in c.items():
             tot[k] = tot.get(k, 0) + v
-        print(json.dumps({"rep": i, "s": round(dt, 4), "pairs_per_s": round(a.pairs / dt, 1), **c, "error": err}),
-              flush=True)
-    print(json.dumps({"summary": True, "reps": a.reps, "failed_reps": fails, **tot}), flush=True)
+        emit({"rep": i, "s": round(dt, 4), "pairs_per_s": round(a.pairs / dt, 1), **c, "error": err})
+    emit({"summary": True, "reps": a.reps, "failed_reps": fails, "warmup_failed": werr is not None, **tot})
     ctx.close()
 
 
