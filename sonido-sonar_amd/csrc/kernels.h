@@ -99,6 +99,8 @@ struct MfccPairParams {
 };
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s);
 int mfcc_pair_wave_bytes();
+int mfcc_pair_waves_per_block();   // waves per block of mfcc_pair_kernel (its LDS carve: tables + waves x wave bytes)
+int mfcc_pair_waves_per_cu();      // resident waves per CU it is sized for
 int mfcc_pair_rows();
 bool fingerprint_supported(int W);
 int fp_batch_frames(int W);

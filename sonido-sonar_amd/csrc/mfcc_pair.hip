@@ -196,6 +196,12 @@ __host__ __device__ constexpr int prow(int k) { return k + 2 * (k >> 4); }
 constexpr int kPRows = 600;
 constexpr int kPartOff = kPRows * 8;    // partial sums [64 lanes][a0 a1 b0 b1]
 constexpr int kLogOff = kPartOff + 64 * 16;   // logmel [2][NMP]
+// HL_W4: 4 waves per SIMD (8-wave blocks, 2 per CU, <= 128 VGPRs): the twiddles are rebuilt per pair
+// from w^1, w^2, w^4, w^8 (and w64^{b0} ^ 1, 2, 4), and the DCT ring does not fit the LDS
+#ifndef HL_W4
+#define HL_W4 0
+#endif
+constexpr int kWaveStride = kWaveBytes;
 
 }  // namespace
 
@@ -203,8 +209,10 @@ constexpr int kLogOff = kPartOff + 64 * 16;   // logmel [2][NMP]
 // headline bank (40 mels at 44.1 kHz: 12 / 8 / 20); 0 = read from p (runtime loops).
 // SEG: a batch of signals (sonar_fingerprint_batch) -- p.seg is the segment table, the pair index
 // runs over all signals' frame pairs, and each wave follows its range across signal boundaries.
-template <bool POW2, int JT, int MS, int NH, bool SEG>
-__global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
+// HC: compile-time hop (256: frame t+1 is frame t shifted by four 64-sample rows, so a pair loads 20
+// rows instead of 32 and holds 20 PCM registers) or 0 (runtime p.H, both frames loaded).
+template <bool POW2, int JT, int MS, int NH, bool SEG, int HC>
+__global__ __launch_bounds__(HL_W4 ? 512 : 256, HL_W4 ? 4 : 3) void mfcc_pair_kernel(MfccPairParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -220,12 +228,12 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     s_src[i] = (uint16_t)((idx & 0x8000u) ? 64 * kT2Stride : kPartOff + 8 * (int)idx);
   }
   for (int i = threadIdx.x; i < 16 * (p.NMP + 4); i += blockDim.x) s_dct[i] = p.dct[i];
-  unsigned char* wb = smem + p.lds_wave0 + wave * kWaveBytes;
+  unsigned char* wb = smem + p.lds_wave0 + wave * kWaveStride;
   // Zero the wave's region once: the filterbank chunks read up to 11 rows past bin 512 with
   // zero weight, and some of those bytes (the unused 17th float2 of T2 lane rows 33/34) are
   // never written by this kernel -- stale LDS from an earlier launch can hold NaN/Inf, and
   // 0 * NaN would turn the last filter into ln(1e-10) (seen in tools/pair_stress2.py).
-  for (int i = lane; i < kWaveBytes / 16; i += 64)
+  for (int i = lane; i < kWaveStride / 16; i += 64)
     *reinterpret_cast<float4*>(wb + 16 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
 
@@ -233,13 +241,16 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   float win[16];
 #pragma unroll
   for (int a = 0; a < 16; a++) win[a] = p.window[64 * a + lane];
-  cf tw1[16];                                   // w_1024^{lane k1}
+  constexpr bool TWR = HL_W4;                   // twiddles rebuilt per pair from their powers of two
+  cf tw1[16];                                   // w_1024^{lane k1} (TWR: k = 1, 2, 4, 8 only)
 #pragma unroll
-  for (int k = 1; k < 16; k++) { const float2 v = p.tw1[lane * 16 + k]; tw1[k] = {v.x, v.y}; }
+  for (int k = 1; k < 16; k++)
+    if (!TWR || (k & (k - 1)) == 0) { const float2 v = p.tw1[lane * 16 + k]; tw1[k] = {v.x, v.y}; }
   const int b0 = lane & 7, kl = lane >> 3;
-  cf tw2[8];                                    // w_64^{b0 c0}
+  cf tw2[8];                                    // w_64^{b0 c0} (TWR: c = 1, 2, 4 only)
 #pragma unroll
-  for (int c = 1; c < 8; c++) { const float2 v = p.tw2[b0 * 8 + c]; tw2[c] = {v.x, v.y}; }
+  for (int c = 1; c < 8; c++)
+    if (!TWR || (c & (c - 1)) == 0) { const float2 v = p.tw2[b0 * 8 + c]; tw2[c] = {v.x, v.y}; }
   // lane masks for the bit-3 exchange: m_hi3 = lanes with bit 3 set, m_lo3 = the rest
   const uint64_t m_hi3 = 0xff00ff00ff00ff00ull, m_lo3 = ~m_hi3;
   // T2 write bases (regular lanes, kl != 0): h = 0 -> + 136 c0, h = 1 -> + 136 (7 - c0)
@@ -257,6 +268,17 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   const int p8 = 8 * (self ? prow(512) : 18 * (lane & 31) + 16 + (lane >> 5));   // bin 512, or a pad row
   const int ks = p.chunk_ks[lane];                           // mel chunk start bin
   const int nmp = p.NMP;
+  // the ln phase's source byte offsets, loop-invariant per lane: in registers when the hop-256 PCM
+  // reuse leaves room (HC = 256, MS known), so that phase is one LDS round trip instead of two
+#ifndef HL_SRC_REGS
+#define HL_SRC_REGS 1
+#endif
+  constexpr bool SRC_REGS = HL_SRC_REGS && HC == 256 && MS > 0;
+  uint32_t srco[SRC_REGS ? MS : 1];
+  if constexpr (SRC_REGS) {
+#pragma unroll
+    for (int i = 0; i < MS; i++) srco[i] = s_src[64 * i + lane];
+  }
 
   // ---- this wave's pairs -------------------------------------------------------
   const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
@@ -265,7 +287,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   if (gw * p.pairs_per_wave >= NP) return;
   const int pb = (int)(gw * p.pairs_per_wave);
   const int pe = (int)min((int64_t)NP, (int64_t)pb + p.pairs_per_wave);
-  const int H = p.H;
+  const int H = HC ? HC : p.H;
 
   // The signal a pair belongs to (wave-uniform).  One signal: pairs [0, NP) of p.pcm / p.out.  SEG:
   // seg = {pcm address[nseg], frames inside the signal[nseg], F[nseg], out address[nseg], first
@@ -306,16 +328,22 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   };
 
   auto frame_ok = [&](const Sig& g, int t) { return t < g.Fin; };
-  auto load_pair = [&](int pi, float (&xr)[16], float (&xi)[16]) {
+  // The pair's PCM: xr = frame t's 16 rows (sample 64 a + lane), xe = frame t+1's rows that frame t
+  // lacks (HC = 256: its last four, frame t+1 = frame t from row 4 on; else all 16).  Unconditional loads: a frame past the signal (the last
+  // pair's second frame of an odd F, or a frame of a signal shorter than W) reads p.zeros instead
+  // -- a wave-uniform pointer select, so the loaded registers have one definition and stay in place
+  // across the loop's back edge.
+  constexpr int NE = HC == 256 ? 4 : 16;
+  auto load_pair = [&](int pi, float (&xr)[16], float (&xe)[NE]) {
     advance(gl, pi);
     const int t = 2 * (pi - gl.p0);
-    // unconditional loads: a frame past the signal (the last pair's second frame of an odd F, or
-    // a frame of a signal shorter than W) reads p.zeros instead -- a wave-uniform pointer select,
-    // so the loaded registers have one definition and stay in place across the loop's back edge
+    const bool ok1 = frame_ok(gl, t + 1);
     const float* f0 = frame_ok(gl, t) ? gl.pcm + t * (int64_t)H : p.zeros;
-    const float* f1 = frame_ok(gl, t + 1) ? gl.pcm + (t + 1) * (int64_t)H : p.zeros;
+    const float* f1 = !ok1 ? p.zeros : (HC == 256 ? f0 + 1024 : gl.pcm + (t + 1) * (int64_t)H);
 #pragma unroll
-    for (int a = 0; a < 16; a++) { xr[a] = f0[lane + 64 * a]; xi[a] = f1[lane + 64 * a]; }
+    for (int a = 0; a < 16; a++) xr[a] = f0[lane + 64 * a];
+#pragma unroll
+    for (int a = 0; a < NE; a++) xe[a] = f1[lane + 64 * a];
   };
 
   // Phase-dependent issue priority: a wave in the LDS-bound epilogue (pass 3, power rows,
@@ -325,19 +353,50 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   // work.  Same-box A/B (profiles/r04n_ab.log, r04x4_ab.log): 0.475-0.481 ms against 0.505-0.509 ms
   // at one priority; the reverse order 0.483-0.492 ms; the epilogue at 3, or priority from the T2
   // transpose on, no better.
-  auto process = [&](int pi, float (&xr)[16], float (&xi)[16]) {
+  auto process = [&](int pi, float (&xr)[16], float (&xe)[NE]) {
     advance(gp, pi);
     __builtin_amdgcn_s_setprio(0);
     cf v[16];
     // ---- pass 1: DFT16 over a (the window fused into its first butterflies), twiddle w_1024^{b k1}
-    dft16_windowed(xr, xi, win, v);
+    if constexpr (HC == 256) {
+      // frame t+1 = rows 4..15 of frame t + its own last four.  Past the signal (the last pair of an
+      // odd F) xe is zero and the partner is frame t's tail: its row is never stored, and frame t's
+      // bits depend only on frame t's samples, identically in single and batched calls
+      float xi[16];
+#pragma unroll
+      for (int a = 0; a < 16; a++) xi[a] = a < 12 ? xr[a + 4] : xe[a - 12];
+      dft16_windowed(xr, xi, win, v);
+    } else {
+      dft16_windowed(xr, xe, win, v);
+    }
     // the next pair's PCM into the same registers, now that this pair's samples are windowed: in
     // flight during the whole pair, and no register copies across the loop's back edge
     // (unconditional, so the registers carry one definition round the loop: the last pair of the
     // wave's range loads itself again)
-    load_pair(pi + 1 < pe ? pi + 1 : pi, xr, xi);
+#ifndef HL_PF_EPI
+#define HL_PF_EPI HL_W4
+#endif
+    // HL_PF_EPI: the next pair's PCM is loaded once the power rows are written instead (the FFT then
+    // holds no prefetch registers; the loads still have the whole epilogue to land)
+    if (!HL_PF_EPI) load_pair(pi + 1 < pe ? pi + 1 : pi, xr, xe);
+    if constexpr (TWR) {
+      // the other powers as products (f32 rounding of a few ulp in the twiddle, far below the
+      // 1e-4 parity bound); opaque copies keep the products inside the loop
+      cf w[16];
 #pragma unroll
-    for (int k = 1; k < 16; k++) v[k] = cmul(v[k], tw1[k]);
+      for (int k = 1; k < 16; k <<= 1) {
+        w[k] = tw1[k];
+        asm volatile("" : "+v"(w[k].x), "+v"(w[k].y));
+      }
+      w[3] = cmul(w[1], w[2]); w[5] = cmul(w[1], w[4]); w[6] = cmul(w[2], w[4]); w[7] = cmul(w[3], w[4]);
+#pragma unroll
+      for (int k = 9; k < 16; k++) w[k] = cmul(w[k - 8], w[8]);
+#pragma unroll
+      for (int k = 1; k < 16; k++) v[k] = cmul(v[k], w[k]);
+    } else {
+#pragma unroll
+      for (int k = 1; k < 16; k++) v[k] = cmul(v[k], tw1[k]);
+    }
     // ---- T1: register bits 0-2 <-> lane bits 3-5 --------------------------------
 #pragma unroll
     for (int j = 0; j < 16; j++)
@@ -367,7 +426,19 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     dft8<0, 1>(v);
     dft8<8, 1>(v);
 #pragma unroll
-    for (int c = 1; c < 8; c++) { v[c] = cmul(v[c], tw2[c]); v[8 + c] = cmul(v[8 + c], tw2[c]); }
+    for (int c = 1; c < 8; c++) {
+      cf u = tw2[c];
+      if constexpr (TWR) {
+        if (c == 1 || c == 2 || c == 4) {
+          asm volatile("" : "+v"(u.x), "+v"(u.y));
+        } else {
+          cf u1 = tw2[1], u2 = tw2[2], u4 = tw2[4];
+          asm volatile("" : "+v"(u1.x), "+v"(u1.y), "+v"(u2.x), "+v"(u2.y), "+v"(u4.x), "+v"(u4.y));
+          u = c == 3 ? cmul(u1, u2) : c == 5 ? cmul(u1, u4) : c == 6 ? cmul(u2, u4) : cmul(cmul(u1, u2), u4);
+        }
+      }
+      v[c] = cmul(v[c], u); v[8 + c] = cmul(v[8 + c], u);
+    }
     // ---- T2: LDS transpose into the combo layout ---------------------------------
     if (kl != 0) {
 #pragma unroll
@@ -417,11 +488,16 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       *reinterpret_cast<float2*>(wb + p8) = POW2 ? make_float2(p0 * p0, p1 * p1) : make_float2(p0, p1);
     }
     wave_lds_sync();
+    if (HL_PF_EPI) load_pair(pi + 1 < pe ? pi + 1 : pi, xr, xe);
     // ---- filterbank: lane chunk [ks, ks + J) of one filter pair ----------------------
     {
       float a0 = 0.f, a1 = 0.f, c0 = 0.f, c1 = 0.f;
-      const unsigned char* pr = wb + prow(ks) * 8;
-      const int ib = 16 - (ks & 15);                          // first i past a pad pair
+      // (HL_W4: ks through an opaque copy, so the chunk's row addresses are rebuilt per pair instead
+      // of being hoisted out of the loop into a dozen registers)
+      int ksv = ks;
+      if (HL_W4) asm volatile("" : "+v"(ksv));
+      const unsigned char* pr = wb + prow(ksv) * 8;
+      const int ib = 16 - (ksv & 15);                         // first i past a pad pair
       const float2* cw = s_cw + lane * p.JS;
       const int J = JT ? JT : p.J;
 #pragma unroll
@@ -437,11 +513,11 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     // ---- ln of the filter sums (lane = filter) ----------------------------------------
     if (lane < nmp) {
       const int ms = MS ? MS : p.max_src;
-      const float2 q0 = *reinterpret_cast<const float2*>(wb + s_src[lane]);   // every filter has a source
+      const float2 q0 = *reinterpret_cast<const float2*>(wb + (SRC_REGS ? srco[0] : s_src[lane]));   // every filter has a source
       float m0 = q0.x, m1 = q0.y;
 #pragma unroll
       for (int i = 1; i < ms; i++) {
-        const float2 q = *reinterpret_cast<const float2*>(wb + s_src[64 * i + lane]);
+        const float2 q = *reinterpret_cast<const float2*>(wb + (SRC_REGS ? srco[SRC_REGS ? i : 0] : s_src[64 * i + lane]));
         m0 += q.x;
         m1 += q.y;
       }
@@ -452,8 +528,8 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       lm[lane] = l0; lm[nmp + lane] = l1;
     }
     wave_lds_sync();
-    // ---- DCT-II (+ lifter): lane = q + 16 f + 32 h, half h of the filters ----------------
     {
+      // ---- DCT-II (+ lifter): lane = q + 16 f + 32 h, half h of the filters ----------------
       const int q = lane & 15, f = (lane >> 4) & 1, hh = lane >> 5;
       const int half = NH ? NH : (nmp >> 1);
       const float* lm = reinterpret_cast<const float*>(wb + kLogOff) + f * nmp + hh * half;
@@ -474,13 +550,13 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       s += f_of(r[1]);                                          // lanes < 32: + lane + 32
       const int64_t t = 2 * (pi - gp.p0) + f;
       if (hh == 0 && q < p.n_mfcc && t < gp.F) gp.out[t * p.n_mfcc + q] = s;
+      wave_lds_sync();
     }
-    wave_lds_sync();
   };
 
-  float ar[16], ai[16];
-  load_pair(pb, ar, ai);
-  for (int pi = pb; pi < pe; ++pi) process(pi, ar, ai);
+  float ar[16], ae[NE];
+  load_pair(pb, ar, ae);
+  for (int pi = pb; pi < pe; ++pi) process(pi, ar, ae);
 }
 
 
@@ -490,21 +566,28 @@ int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   // calls to fp_wave_kernel (sonar_fp_kernel_plan), so this is a guard, reported as unsupported
   if (2 * NP > SONAR_PAIR_MAX_FRAMES) return -4;
   const int64_t waves = (NP + p.pairs_per_wave - 1) / p.pairs_per_wave;
-  const int64_t grid = (waves + 3) / 4;
+  const int64_t grid = (waves + mfcc_pair_waves_per_block() - 1) / mfcc_pair_waves_per_block();
   const bool head = p.J == 12 && p.max_src <= 8 && p.NMP == 40;
+#ifndef HL_HOP256
+#define HL_HOP256 1
+#endif
+  const bool h256 = HL_HOP256 && p.H == 256 && head;   // the headline configuration's hop
   auto pick = [&](auto seg) {
     constexpr bool S = decltype(seg)::value;
-    return p.pow2 ? (head ? mfcc_pair_kernel<true, 12, 8, 20, S> : mfcc_pair_kernel<true, 0, 0, 0, S>)
-                  : (head ? mfcc_pair_kernel<false, 12, 8, 20, S> : mfcc_pair_kernel<false, 0, 0, 0, S>);
+    if (h256) return p.pow2 ? mfcc_pair_kernel<true, 12, 8, 20, S, 256> : mfcc_pair_kernel<false, 12, 8, 20, S, 256>;
+    return p.pow2 ? (head ? mfcc_pair_kernel<true, 12, 8, 20, S, 0> : mfcc_pair_kernel<true, 0, 0, 0, S, 0>)
+                  : (head ? mfcc_pair_kernel<false, 12, 8, 20, S, 0> : mfcc_pair_kernel<false, 0, 0, 0, S, 0>);
   };
   auto kern = p.nseg > 0 ? pick(std::true_type{}) : pick(std::false_type{});
   if (p.lds_bytes > 64 * 1024)
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), p.lds_bytes, s, p);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * mfcc_pair_waves_per_block()), p.lds_bytes, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int mfcc_pair_wave_bytes() { return kWaveBytes; }
+int mfcc_pair_wave_bytes() { return kWaveStride; }
+int mfcc_pair_waves_per_block() { return HL_W4 ? 8 : 4; }
+int mfcc_pair_waves_per_cu() { return HL_W4 ? 16 : 12; }
 int mfcc_pair_rows() { return kPRows; }
 
 }  // namespace sonar

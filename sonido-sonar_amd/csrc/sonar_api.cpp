@@ -457,12 +457,12 @@ void fill_pair_params(sonar_ctx* c, const PairTables& t, const sonar_fp_cfg* cfg
   q.lds_src = al(64 * t.JS * 8);
   q.lds_dct = q.lds_src + 64 * 16 * 2;
   q.lds_wave0 = q.lds_dct + al(16 * (t.NMP + 4) * 4);
-  // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU
-  q.waves_per_block = 4;
+  // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU (HL_W4 builds: 8 and 2)
+  q.waves_per_block = sonar::mfcc_pair_waves_per_block();
   q.lds_bytes = q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes();
   int dev_cus = 256;
   hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  const int64_t target_waves = (int64_t)dev_cus * 12;
+  const int64_t target_waves = (int64_t)dev_cus * sonar::mfcc_pair_waves_per_cu();
   q.pairs_per_wave = std::max<int64_t>(1, (NP + target_waves - 1) / target_waves);
 }
 

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Instruction mix of one kernel's hottest loop in a hipcc --save-temps .s file.
+
+The loop is taken as the innermost-depth loop block range that contains the most VALU: from its
+header label (comment '=>This Loop Header') to the last branch back to it.  Prints VALU / LDS /
+VMEM / SALU / s_nop / s_waitcnt counts.  Usage: python tools/isa_count.py file.s kernel_symbol"""
+import re
+import sys
+
+
+def main():
+    path, sym = sys.argv[1], sys.argv[2]
+    lines = open(path).read().splitlines()
+    start = next(i for i, ln in enumerate(lines) if ln.startswith(sym + ":"))
+    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+    body = lines[start:end + 1]
+    # loops: header label -> the labels of blocks inside it ("in Loop: Header=BBx_y" on the line after
+    # a label, or "Loop Header" on the header's own line)
+    members = {}
+    for i, ln in enumerate(body):
+        m = re.match(r"^\.(LBB\w+):", ln)
+        if not m:
+            continue
+        lab = m.group(1)
+        if "Loop Header" in ln:
+            members.setdefault(lab[1:], set()).add(lab)
+        nxt = body[i + 1] if i + 1 < len(body) else ""
+        h = re.search(r"Header=(BB\w+)", ln + nxt)
+        if h:
+            members.setdefault(h.group(1), set()).add(lab)
+    best = None
+    for hdr, labs in members.items():
+        labs = labs | {"L" + hdr}
+        idx = [i for i, ln in enumerate(body) if re.match(r"^\.(LBB\w+):", ln) and re.match(r"^\.(LBB\w+):", ln).group(1) in labs]
+        brs = [j for j, ln in enumerate(body) if re.search(r"s_(cbranch\w*|branch)\s+\.(LBB\w+)", ln)
+               and re.search(r"s_(cbranch\w*|branch)\s+\.(LBB\w+)", ln).group(2) in labs]
+        if not idx or not brs:
+            continue
+        seg = body[min(idx):max(max(brs), max(idx)) + 1]
+        nv = sum(1 for ln in seg if re.match(r"^\s+v_", ln))
+        if best is None or nv > best[0]:
+            best = (nv, hdr, seg)
+    nv, lab, seg = best
+    cnt = lambda pat: sum(1 for ln in seg if re.match(pat, ln))  # noqa: E731
+    pats = {"dpp": r"^\s+v_\w+_dpp", "permlane": r"^\s+v_permlane", "vmov": r"^\s+v_mov", "lds": r"^\s+ds_",
+            "lds_read": r"^\s+ds_read", "lds_write": r"^\s+ds_write", "vmem": r"^\s+(global|buffer|flat)_",
+            "salu": r"^\s+s_(?!nop|waitcnt|cbranch|branch)", "s_nop": r"^\s+s_nop", "s_waitcnt": r"^\s+s_waitcnt",
+            "scratch": r"^\s+scratch_"}
+    c = {k: cnt(v) for k, v in pats.items()}
+    print(f"{sym}: loop {lab}, {len(seg)} lines")
+    print("  VALU %d (dpp %d, permlane %d, mov %d)  LDS %d (read %d, write %d)  VMEM %d  SALU %d  s_nop %d  "
+          "s_waitcnt %d  scratch %d" % (nv, c["dpp"], c["permlane"], c["vmov"], c["lds"], c["lds_read"],
+                                         c["lds_write"], c["vmem"], c["salu"], c["s_nop"], c["s_waitcnt"], c["scratch"]))
+
+if __name__ == "__main__":
+    main()
