@@ -196,12 +196,6 @@ __host__ __device__ constexpr int prow(int k) { return k + 2 * (k >> 4); }
 constexpr int kPRows = 600;
 constexpr int kPartOff = kPRows * 8;    // partial sums [64 lanes][a0 a1 b0 b1]
 constexpr int kLogOff = kPartOff + 64 * 16;   // logmel [2][NMP]
-// HL_W4: 4 waves per SIMD (8-wave blocks, 2 per CU, <= 128 VGPRs): the twiddles are rebuilt per pair
-// from w^1, w^2, w^4, w^8 (and w64^{b0} ^ 1, 2, 4), and the DCT ring does not fit the LDS
-#ifndef HL_W4
-#define HL_W4 0
-#endif
-constexpr int kWaveStride = kWaveBytes;
 
 }  // namespace
 
@@ -212,7 +206,7 @@ constexpr int kWaveStride = kWaveBytes;
 // HC: compile-time hop (256: frame t+1 is frame t shifted by four 64-sample rows, so a pair loads 20
 // rows instead of 32 and holds 20 PCM registers) or 0 (runtime p.H, both frames loaded).
 template <bool POW2, int JT, int MS, int NH, bool SEG, int HC>
-__global__ __launch_bounds__(HL_W4 ? 512 : 256, HL_W4 ? 4 : 3) void mfcc_pair_kernel(MfccPairParams p) {
+__global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -228,12 +222,12 @@ __global__ __launch_bounds__(HL_W4 ? 512 : 256, HL_W4 ? 4 : 3) void mfcc_pair_ke
     s_src[i] = (uint16_t)((idx & 0x8000u) ? 64 * kT2Stride : kPartOff + 8 * (int)idx);
   }
   for (int i = threadIdx.x; i < 16 * (p.NMP + 4); i += blockDim.x) s_dct[i] = p.dct[i];
-  unsigned char* wb = smem + p.lds_wave0 + wave * kWaveStride;
+  unsigned char* wb = smem + p.lds_wave0 + wave * kWaveBytes;
   // Zero the wave's region once: the filterbank chunks read up to 11 rows past bin 512 with
   // zero weight, and some of those bytes (the unused 17th float2 of T2 lane rows 33/34) are
   // never written by this kernel -- stale LDS from an earlier launch can hold NaN/Inf, and
   // 0 * NaN would turn the last filter into ln(1e-10) (seen in tools/pair_stress2.py).
-  for (int i = lane; i < kWaveStride / 16; i += 64)
+  for (int i = lane; i < kWaveBytes / 16; i += 64)
     *reinterpret_cast<float4*>(wb + 16 * i) = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
 
@@ -241,16 +235,13 @@ __global__ __launch_bounds__(HL_W4 ? 512 : 256, HL_W4 ? 4 : 3) void mfcc_pair_ke
   float win[16];
 #pragma unroll
   for (int a = 0; a < 16; a++) win[a] = p.window[64 * a + lane];
-  constexpr bool TWR = HL_W4;                   // twiddles rebuilt per pair from their powers of two
-  cf tw1[16];                                   // w_1024^{lane k1} (TWR: k = 1, 2, 4, 8 only)
+  cf tw1[16];                                   // w_1024^{lane k1}
 #pragma unroll
-  for (int k = 1; k < 16; k++)
-    if (!TWR || (k & (k - 1)) == 0) { const float2 v = p.tw1[lane * 16 + k]; tw1[k] = {v.x, v.y}; }
+  for (int k = 1; k < 16; k++) { const float2 v = p.tw1[lane * 16 + k]; tw1[k] = {v.x, v.y}; }
   const int b0 = lane & 7, kl = lane >> 3;
-  cf tw2[8];                                    // w_64^{b0 c0} (TWR: c = 1, 2, 4 only)
+  cf tw2[8];                                    // w_64^{b0 c0}
 #pragma unroll
-  for (int c = 1; c < 8; c++)
-    if (!TWR || (c & (c - 1)) == 0) { const float2 v = p.tw2[b0 * 8 + c]; tw2[c] = {v.x, v.y}; }
+  for (int c = 1; c < 8; c++) { const float2 v = p.tw2[b0 * 8 + c]; tw2[c] = {v.x, v.y}; }
   // lane masks for the bit-3 exchange: m_hi3 = lanes with bit 3 set, m_lo3 = the rest
   const uint64_t m_hi3 = 0xff00ff00ff00ff00ull, m_lo3 = ~m_hi3;
   // T2 write bases (regular lanes, kl != 0): h = 0 -> + 136 c0, h = 1 -> + 136 (7 - c0)
@@ -373,30 +364,9 @@ __global__ __launch_bounds__(HL_W4 ? 512 : 256, HL_W4 ? 4 : 3) void mfcc_pair_ke
     // flight during the whole pair, and no register copies across the loop's back edge
     // (unconditional, so the registers carry one definition round the loop: the last pair of the
     // wave's range loads itself again)
-#ifndef HL_PF_EPI
-#define HL_PF_EPI HL_W4
-#endif
-    // HL_PF_EPI: the next pair's PCM is loaded once the power rows are written instead (the FFT then
-    // holds no prefetch registers; the loads still have the whole epilogue to land)
-    if (!HL_PF_EPI) load_pair(pi + 1 < pe ? pi + 1 : pi, xr, xe);
-    if constexpr (TWR) {
-      // the other powers as products (f32 rounding of a few ulp in the twiddle, far below the
-      // 1e-4 parity bound); opaque copies keep the products inside the loop
-      cf w[16];
+    load_pair(pi + 1 < pe ? pi + 1 : pi, xr, xe);
 #pragma unroll
-      for (int k = 1; k < 16; k <<= 1) {
-        w[k] = tw1[k];
-        asm volatile("" : "+v"(w[k].x), "+v"(w[k].y));
-      }
-      w[3] = cmul(w[1], w[2]); w[5] = cmul(w[1], w[4]); w[6] = cmul(w[2], w[4]); w[7] = cmul(w[3], w[4]);
-#pragma unroll
-      for (int k = 9; k < 16; k++) w[k] = cmul(w[k - 8], w[8]);
-#pragma unroll
-      for (int k = 1; k < 16; k++) v[k] = cmul(v[k], w[k]);
-    } else {
-#pragma unroll
-      for (int k = 1; k < 16; k++) v[k] = cmul(v[k], tw1[k]);
-    }
+    for (int k = 1; k < 16; k++) v[k] = cmul(v[k], tw1[k]);
     // ---- T1: register bits 0-2 <-> lane bits 3-5 --------------------------------
 #pragma unroll
     for (int j = 0; j < 16; j++)
@@ -426,19 +396,7 @@ __global__ __launch_bounds__(HL_W4 ? 512 : 256, HL_W4 ? 4 : 3) void mfcc_pair_ke
     dft8<0, 1>(v);
     dft8<8, 1>(v);
 #pragma unroll
-    for (int c = 1; c < 8; c++) {
-      cf u = tw2[c];
-      if constexpr (TWR) {
-        if (c == 1 || c == 2 || c == 4) {
-          asm volatile("" : "+v"(u.x), "+v"(u.y));
-        } else {
-          cf u1 = tw2[1], u2 = tw2[2], u4 = tw2[4];
-          asm volatile("" : "+v"(u1.x), "+v"(u1.y), "+v"(u2.x), "+v"(u2.y), "+v"(u4.x), "+v"(u4.y));
-          u = c == 3 ? cmul(u1, u2) : c == 5 ? cmul(u1, u4) : c == 6 ? cmul(u2, u4) : cmul(cmul(u1, u2), u4);
-        }
-      }
-      v[c] = cmul(v[c], u); v[8 + c] = cmul(v[8 + c], u);
-    }
+    for (int c = 1; c < 8; c++) { v[c] = cmul(v[c], tw2[c]); v[8 + c] = cmul(v[8 + c], tw2[c]); }
     // ---- T2: LDS transpose into the combo layout ---------------------------------
     if (kl != 0) {
 #pragma unroll
@@ -488,16 +446,11 @@ __global__ __launch_bounds__(HL_W4 ? 512 : 256, HL_W4 ? 4 : 3) void mfcc_pair_ke
       *reinterpret_cast<float2*>(wb + p8) = POW2 ? make_float2(p0 * p0, p1 * p1) : make_float2(p0, p1);
     }
     wave_lds_sync();
-    if (HL_PF_EPI) load_pair(pi + 1 < pe ? pi + 1 : pi, xr, xe);
     // ---- filterbank: lane chunk [ks, ks + J) of one filter pair ----------------------
     {
       float a0 = 0.f, a1 = 0.f, c0 = 0.f, c1 = 0.f;
-      // (HL_W4: ks through an opaque copy, so the chunk's row addresses are rebuilt per pair instead
-      // of being hoisted out of the loop into a dozen registers)
-      int ksv = ks;
-      if (HL_W4) asm volatile("" : "+v"(ksv));
-      const unsigned char* pr = wb + prow(ksv) * 8;
-      const int ib = 16 - (ksv & 15);                         // first i past a pad pair
+      const unsigned char* pr = wb + prow(ks) * 8;
+      const int ib = 16 - (ks & 15);                          // first i past a pad pair
       const float2* cw = s_cw + lane * p.JS;
       const int J = JT ? JT : p.J;
 #pragma unroll
@@ -585,9 +538,9 @@ int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int mfcc_pair_wave_bytes() { return kWaveStride; }
-int mfcc_pair_waves_per_block() { return HL_W4 ? 8 : 4; }
-int mfcc_pair_waves_per_cu() { return HL_W4 ? 16 : 12; }
+int mfcc_pair_wave_bytes() { return kWaveBytes; }
+int mfcc_pair_waves_per_block() { return 4; }
+int mfcc_pair_waves_per_cu() { return 12; }
 int mfcc_pair_rows() { return kPRows; }
 
 }  // namespace sonar

@@ -457,7 +457,7 @@ void fill_pair_params(sonar_ctx* c, const PairTables& t, const sonar_fp_cfg* cfg
   q.lds_src = al(64 * t.JS * 8);
   q.lds_dct = q.lds_src + 64 * 16 * 2;
   q.lds_wave0 = q.lds_dct + al(16 * (t.NMP + 4) * 4);
-  // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU (HL_W4 builds: 8 and 2)
+  // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU
   q.waves_per_block = sonar::mfcc_pair_waves_per_block();
   q.lds_bytes = q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes();
   int dev_cus = 256;
