@@ -73,7 +73,7 @@ struct MfccPairParams {
   int64_t n;            // samples
   int64_t F;            // STFT frames
   int H;                // hop
-  int64_t pairs_per_wave;
+  int64_t pairs_per_block;   // contiguous pairs per block (one block per CU), claimed pair by pair by its waves
   const float* window;  // [1024]
   const float2* tw1;    // [64][16]  w_1024^{b k1}
   const float2* tw2;    // [8][8]    w_64^{b0 c0}
@@ -89,13 +89,14 @@ struct MfccPairParams {
   int n_mels, n_mfcc;   // n_mfcc <= 16
   int pow2;             // F5: MFCC.Compute fed |X|^2 -> filterbank of |X|^4
   float* out;           // [F][n_mfcc]
-  int lds_src, lds_dct, lds_wave0, lds_bytes;
-  int waves_per_block;  // 4 (mfcc_pair_kernel)
+  int lds_src, lds_dct, lds_ctr, lds_wave0, lds_bytes;
+  int waves_per_block;  // 12 (mfcc_pair_kernel)
   // sonar_fingerprint_batch: nseg > 0 signals, F = 2 x the batch's pairs, pcm / n / out unused;
   // seg (device) = {pcm address[nseg], frames inside the signal[nseg], F[nseg], out address[nseg],
   // first pair[nseg + 1]}
   const int64_t* seg;
   int nseg;
+  uint64_t* stamp;      // HL_STAMP diagnostics builds only: per wave {start, end, pairs}
 };
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s);
 int mfcc_pair_wave_bytes();

@@ -206,7 +206,7 @@ constexpr int kLogOff = kPartOff + 64 * 16;   // logmel [2][NMP]
 // HC: compile-time hop (256: frame t+1 is frame t shifted by four 64-sample rows, so a pair loads 20
 // rows instead of 32 and holds 20 PCM registers) or 0 (runtime p.H, both frames loaded).
 template <bool POW2, int JT, int MS, int NH, bool SEG, int HC>
-__global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
+__global__ __launch_bounds__(768, 1) void mfcc_pair_kernel(MfccPairParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -222,6 +222,8 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     s_src[i] = (uint16_t)((idx & 0x8000u) ? 64 * kT2Stride : kPartOff + 8 * (int)idx);
   }
   for (int i = threadIdx.x; i < 16 * (p.NMP + 4); i += blockDim.x) s_dct[i] = p.dct[i];
+  int* s_next = reinterpret_cast<int*>(smem + p.lds_ctr);                          // the block's pair counter
+  if (threadIdx.x == 0) *s_next = 0;
   unsigned char* wb = smem + p.lds_wave0 + wave * kWaveBytes;
   // Zero the wave's region once: the filterbank chunks read up to 11 rows past bin 512 with
   // zero weight, and some of those bytes (the unused 17th float2 of T2 lane rows 33/34) are
@@ -271,14 +273,23 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     for (int i = 0; i < MS; i++) srco[i] = s_src[64 * i + lane];
   }
 
-  // ---- this wave's pairs -------------------------------------------------------
-  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-  // pair indices are 32-bit (the host checks the count), so the wave-uniform compares stay scalar
+  // ---- this block's pairs, handed to its waves one at a time --------------------------
+  // The block (one per CU, 12 waves) owns the contiguous pairs [pb, pe); each wave takes the next
+  // unclaimed pair from an LDS counter.  A static split per wave left the kernel waiting for its
+  // slowest waves: the youngest of a SIMD's three waves loses every issue tie to the older two
+  // (arbitration is by priority, then age) and finished its equal share ~15 % later
+  // (tools/hl_stamp.py, profiles/r05j_stamp.log).  Pair indices are 32-bit (the host checks the
+  // count), so the wave-uniform compares stay scalar.
   const int NP = (int)((p.F + 1) >> 1);
-  if (gw * p.pairs_per_wave >= NP) return;
-  const int pb = (int)(gw * p.pairs_per_wave);
-  const int pe = (int)min((int64_t)NP, (int64_t)pb + p.pairs_per_wave);
+  const int64_t pb64 = (int64_t)blockIdx.x * p.pairs_per_block;
+  const int pb = (int)min((int64_t)NP, pb64);
+  const int pe = (int)min((int64_t)NP, pb64 + p.pairs_per_block);
   const int H = HC ? HC : p.H;
+  auto claim = [&]() -> int {
+    int v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(s_next, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return pb + __builtin_amdgcn_readfirstlane(v);
+  };
 
   // The signal a pair belongs to (wave-uniform).  One signal: pairs [0, NP) of p.pcm / p.out.  SEG:
   // seg = {pcm address[nseg], frames inside the signal[nseg], F[nseg], out address[nseg], first
@@ -344,7 +355,9 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
   // work.  Same-box A/B (profiles/r04n_ab.log, r04x4_ab.log): 0.475-0.481 ms against 0.505-0.509 ms
   // at one priority; the reverse order 0.483-0.492 ms; the epilogue at 3, or priority from the T2
   // transpose on, no better.
-  auto process = [&](int pi, float (&xr)[16], float (&xe)[NE]) {
+  // one pair; the next pair's PCM (nxt, claimed one pair ahead) is loaded during it, and the pair
+  // after that is claimed in its DCT phase, whose LDS drain returns the counter with the data
+  auto process = [&](int pi, int nxt, float (&xr)[16], float (&xe)[NE]) -> int {
     advance(gp, pi);
     __builtin_amdgcn_s_setprio(0);
     cf v[16];
@@ -364,7 +377,7 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
     // flight during the whole pair, and no register copies across the loop's back edge
     // (unconditional, so the registers carry one definition round the loop: the last pair of the
     // wave's range loads itself again)
-    load_pair(pi + 1 < pe ? pi + 1 : pi, xr, xe);
+    load_pair(nxt < pe ? nxt : pi, xr, xe);
 #pragma unroll
     for (int k = 1; k < 16; k++) v[k] = cmul(v[k], tw1[k]);
     // ---- T1: register bits 0-2 <-> lane bits 3-5 --------------------------------
@@ -503,13 +516,40 @@ __global__ __launch_bounds__(256, 3) void mfcc_pair_kernel(MfccPairParams p) {
       s += f_of(r[1]);                                          // lanes < 32: + lane + 32
       const int64_t t = 2 * (pi - gp.p0) + f;
       if (hh == 0 && q < p.n_mfcc && t < gp.F) gp.out[t * p.n_mfcc + q] = s;
+      int v = 0;
+      if (lane == 0) v = __hip_atomic_fetch_add(s_next, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       wave_lds_sync();
+      return pb + __builtin_amdgcn_readfirstlane(v);
     }
   };
 
-  float ar[16], ae[NE];
-  load_pair(pb, ar, ae);
-  for (int pi = pb; pi < pe; ++pi) process(pi, ar, ae);
+#ifdef HL_STAMP
+  const uint64_t t_begin = __builtin_amdgcn_s_memrealtime();
+  int done = 0;
+#endif
+  int cur = claim();
+  if (cur < pe) {
+    int nxt = claim();
+    float ar[16], ae[NE];
+    load_pair(cur, ar, ae);
+    for (;;) {
+      const int nn = process(cur, nxt, ar, ae);
+#ifdef HL_STAMP
+      ++done;
+#endif
+      if (nxt >= pe) break;
+      cur = nxt;
+      nxt = nn;
+    }
+  }
+#ifdef HL_STAMP
+  if (p.stamp && lane == 0) {
+    const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    p.stamp[3 * gw] = t_begin;
+    p.stamp[3 * gw + 1] = __builtin_amdgcn_s_memrealtime();
+    p.stamp[3 * gw + 2] = (uint64_t)done;
+  }
+#endif
 }
 
 
@@ -518,8 +558,7 @@ int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   // 32-bit pair AND frame indices in the kernel (t = 2 (pi - p0) + 1 <= 2 NP): the host routes larger
   // calls to fp_wave_kernel (sonar_fp_kernel_plan), so this is a guard, reported as unsupported
   if (2 * NP > SONAR_PAIR_MAX_FRAMES) return -4;
-  const int64_t waves = (NP + p.pairs_per_wave - 1) / p.pairs_per_wave;
-  const int64_t grid = (waves + mfcc_pair_waves_per_block() - 1) / mfcc_pair_waves_per_block();
+  const int64_t grid = (NP + p.pairs_per_block - 1) / p.pairs_per_block;
   const bool head = p.J == 12 && p.max_src <= 8 && p.NMP == 40;
 #ifndef HL_HOP256
 #define HL_HOP256 1
@@ -539,7 +578,7 @@ int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
 }
 
 int mfcc_pair_wave_bytes() { return kWaveBytes; }
-int mfcc_pair_waves_per_block() { return 4; }
+int mfcc_pair_waves_per_block() { return 12; }
 int mfcc_pair_waves_per_cu() { return 12; }
 int mfcc_pair_rows() { return kPRows; }
 

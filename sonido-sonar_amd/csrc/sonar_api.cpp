@@ -456,14 +456,15 @@ void fill_pair_params(sonar_ctx* c, const PairTables& t, const sonar_fp_cfg* cfg
   auto al = [](int x) { return (x + 15) & ~15; };
   q.lds_src = al(64 * t.JS * 8);
   q.lds_dct = q.lds_src + 64 * 16 * 2;
-  q.lds_wave0 = q.lds_dct + al(16 * (t.NMP + 4) * 4);
-  // mfcc_pair_kernel: 4 waves per block, 3 blocks per CU
+  q.lds_ctr = q.lds_dct + al(16 * (t.NMP + 4) * 4);
+  q.lds_wave0 = q.lds_ctr + 16;
+  // mfcc_pair_kernel: one 12-wave block per CU over a contiguous range of pairs
   q.waves_per_block = sonar::mfcc_pair_waves_per_block();
   q.lds_bytes = q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes();
   int dev_cus = 256;
   hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  const int64_t target_waves = (int64_t)dev_cus * sonar::mfcc_pair_waves_per_cu();
-  q.pairs_per_wave = std::max<int64_t>(1, (NP + target_waves - 1) / target_waves);
+  const int64_t blocks = (int64_t)dev_cus * sonar::mfcc_pair_waves_per_cu() / q.waves_per_block;
+  q.pairs_per_block = std::max<int64_t>(1, (NP + blocks - 1) / blocks);
 }
 
 // The transform kernel of a validated sonar_fingerprint call over F frames (sonar_fp_kernel_plan):
@@ -645,12 +646,25 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
       fill_pair_params(c, t, cfg, (F + 1) / 2, q);
       q.pcm = (const float*)dpcm; q.n = n; q.F = F; q.H = H;
       q.out = (float*)d_mfcc;
+#ifdef HL_STAMP
+      const char* stamp_path = std::getenv("SONAR_HL_STAMP");
+      const int64_t nw = ((F + 1) / 2 + q.pairs_per_block - 1) / q.pairs_per_block * q.waves_per_block;
+      if (stamp_path) q.stamp = (uint64_t*)dbuf(c, "hl.stamp", (size_t)nw * 24);
+#endif
       hipEvent_t tend = timed_begin(c, s);
       const int lrc = sonar::launch_mfcc_pair(q, s);
       if (lrc == -4) return fail(c, SONAR_ERR_UNSUPPORTED, "too many frames for one mfcc_pair_kernel launch");
       if (lrc != 0)
         return fail(c, SONAR_ERR_DEVICE, std::string("mfcc kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
       timed_end(c, s, tend);
+#ifdef HL_STAMP
+      if (q.stamp) {   // diagnostics: every wave's {start, end} appended to the file
+        std::vector<uint64_t> h((size_t)nw * 3);
+        HIP_TRY(c, hipMemcpyAsync(h.data(), q.stamp, h.size() * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipStreamSynchronize(s));
+        if (FILE* f = std::fopen(stamp_path, "ab")) { std::fwrite(h.data(), 8, h.size(), f); std::fclose(f); }
+      }
+#endif
       pair_done = true;
       c->last_fp_kernel = "mfcc_pair_kernel";
     }

@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 TAG=$1; shift
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_fingerprint_batch.py tests/test_gpu_mfcc_pair.py tests/test_gpu_golden.py tests/test_gpu_fullsize.py::test_c2_full_hour_mfcc tests/test_gpu_features_edges.py tests/test_gpu_multi.py > gpurun_out/${TAG}_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_fingerprint_batch.py tests/test_gpu_mfcc_pair.py tests/test_gpu_golden.py tests/test_gpu_fullsize.py::test_c2_full_hour_mfcc tests/test_gpu_features_edges.py tests/test_gpu_multi.py tests/test_gpu_stream.py tests/test_gpu_stft_mfcc.py > gpurun_out/${TAG}_tests.log 2>&1
 rc=$?; tail -2 gpurun_out/${TAG}_tests.log; [ $rc -eq 0 ] || { tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
 NOLEGS="--no-cpu-baseline --no-f64 --c1 0 --dtw-len 0 --c5-pairs 0 --c3-seconds 0 --c4-seconds 0 --c6-gallery 0 --c7-seconds 0 --ingest-reps 0 --batch-signals 0"
 for round in 1 2 3; do
