@@ -12,34 +12,22 @@ def main():
     path, sym = sys.argv[1], sys.argv[2]
     lines = open(path).read().splitlines()
     start = next(i for i, ln in enumerate(lines) if ln.startswith(sym + ":"))
-    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+    end = next(i for i in range(start + 1, len(lines)) if lines[i].startswith(".Lfunc_end"))
     body = lines[start:end + 1]
-    # loops: header label -> the labels of blocks inside it ("in Loop: Header=BBx_y" on the line after
-    # a label, or "Loop Header" on the header's own line)
-    members = {}
+    # loops: every "Loop Header" label, spanning to the last branch back to it
+    best = None
     for i, ln in enumerate(body):
         m = re.match(r"^\.(LBB\w+):", ln)
-        if not m:
+        if not m or "Loop Header" not in ln:
             continue
         lab = m.group(1)
-        if "Loop Header" in ln:
-            members.setdefault(lab[1:], set()).add(lab)
-        nxt = body[i + 1] if i + 1 < len(body) else ""
-        h = re.search(r"Header=(BB\w+)", ln + nxt)
-        if h:
-            members.setdefault(h.group(1), set()).add(lab)
-    best = None
-    for hdr, labs in members.items():
-        labs = labs | {"L" + hdr}
-        idx = [i for i, ln in enumerate(body) if re.match(r"^\.(LBB\w+):", ln) and re.match(r"^\.(LBB\w+):", ln).group(1) in labs]
-        brs = [j for j, ln in enumerate(body) if re.search(r"s_(cbranch\w*|branch)\s+\.(LBB\w+)", ln)
-               and re.search(r"s_(cbranch\w*|branch)\s+\.(LBB\w+)", ln).group(2) in labs]
-        if not idx or not brs:
+        brs = [j for j, x in enumerate(body) if re.search(r"s_(cbranch\w*|branch)\s+\." + lab + r"\b", x)]
+        if not brs:
             continue
-        seg = body[min(idx):max(max(brs), max(idx)) + 1]
-        nv = sum(1 for ln in seg if re.match(r"^\s+v_", ln))
+        seg = body[i:max(brs) + 1]
+        nv = sum(1 for x in seg if re.match(r"^\s+v_", x))
         if best is None or nv > best[0]:
-            best = (nv, hdr, seg)
+            best = (nv, lab, seg)
     nv, lab, seg = best
     cnt = lambda pat: sum(1 for ln in seg if re.match(pat, ln))  # noqa: E731
     pats = {"dpp": r"^\s+v_\w+_dpp", "permlane": r"^\s+v_permlane", "vmov": r"^\s+v_mov", "lds": r"^\s+ds_",
