@@ -2006,6 +2006,137 @@ int launch_nonfinite_batch(const DtwArgs* dargs, int n, int64_t max_elems, hipSt
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// sonar_align_pairs' scorer reductions on the device (alignment.go:380-643, correlation.go:526-667):
+// one wave per pair over its warping path and energy correlation -- host::path_sums and
+// host::corr_sums, bit for bit -- so a batch copies back ~150 bytes per pair instead of its path
+// (16 B per point) and correlation, and its host thread only combines scalars.  Counts, extrema
+// and the peak index (the first index of the largest |corr|, as Go's strict > scan) are order-free;
+// the float sums keep Go's sequential order: 64 terms are formed at once (a smoothed cost is Go's
+// window sum, a deviation is squared before it is added, as Go does) and then added one by one in
+// index order through v_readlane, four independent sums interleaved.
+namespace {
+__device__ __forceinline__ double rl(double v, int k) {           // lane k's v, wave-uniform
+  const int2 u = __builtin_bit_cast(int2, v);
+  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readlane(u.x, k), __builtin_amdgcn_readlane(u.y, k)));
+}
+__device__ __forceinline__ int64_t wave_isum(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// the largest a over the wave (ties: the smallest index); a = -1 for "none"
+__device__ __forceinline__ void wave_argmax(double& a, int64_t& i) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ao = __shfl_xor(a, o, 64);
+    const int64_t io = __shfl_xor(i, o, 64);
+    if (ao > a || (ao == a && io < i)) { a = ao; i = io; }
+  }
+}
+}  // namespace
+
+__global__ __launch_bounds__(64) void pair_score_kernel(const ScoreJob* jobs) {
+  const ScoreJob j = jobs[blockIdx.x];
+  const int lane = threadIdx.x;
+  // ---- warping path
+  const int64_t P = *j.plen;
+  host::PathSums ps;
+  ps.P = P;
+  if (P > 0) {
+    int64_t off = 0, dg = 0, ch = 0;
+    const int64_t w = max((int64_t)2, min((int64_t)5, P / 4)), h = w / 2;
+    auto smooth = [&](int64_t i) {                  // calculateCostConsistency's window mean
+      double t = 0.0;
+      const int64_t lo = max((int64_t)0, i - h), hi = min(P - 1, i + h);
+      for (int64_t q = lo; q <= hi; ++q) t += j.pc[q];
+      return t / (double)(hi - lo + 1);
+    };
+    double sc = 0.0, ss = 0.0;                       // Go's sequential sums (wave-uniform)
+    for (int64_t b = 0; b < P; b += 64) {
+      const int64_t i = b + lane;
+      double c = 0.0, m = 0.0;
+      if (i < P) {
+        off += j.pr[i] - j.pq[i];
+        c = j.pc[i];
+        if (P > 1) m = smooth(i);
+        if (i >= 1) {
+          const int d0 = j.pq[i] - j.pq[i - 1], d1 = j.pr[i] - j.pr[i - 1];
+          if (d0 > 0 && d1 > 0) dg++;
+          if (i >= 2 && (d0 != j.pq[i - 1] - j.pq[i - 2] || d1 != j.pr[i - 1] - j.pr[i - 2])) ch++;
+        }
+      }
+      const int cnt = (int)min((int64_t)64, P - b);
+      for (int k = 0; k < cnt; ++k) { sc += rl(c, k); ss += rl(m, k); }
+    }
+    ps.offset_sum = wave_isum(off);
+    ps.diag_steps = wave_isum(dg);
+    ps.changes = wave_isum(ch);
+    ps.sum_cost = sc;
+    ps.p0q = j.pq[0]; ps.p0r = j.pr[0]; ps.p1q = j.pq[P - 1]; ps.p1r = j.pr[P - 1];
+    if (P > 1) {
+      ps.sum_smooth = ss;
+      const double mean = ss / (double)P;
+      double vv = 0.0;
+      for (int64_t b = 0; b < P; b += 64) {
+        const int64_t i = b + lane;
+        double d2 = 0.0;
+        if (i < P) { const double d = smooth(i) - mean; d2 = d * d; }
+        const int cnt = (int)min((int64_t)64, P - b);
+        for (int k = 0; k < cnt; ++k) vv += rl(d2, k);
+      }
+      ps.var_smooth = vv;
+    }
+  }
+  if (lane == 0) *j.path = ps;
+  // ---- energy correlation
+  if (!j.corr) return;
+  const int64_t nl = j.nl;
+  host::CorrSums cs;
+  cs.num_lags = nl;
+  if (nl > 0) {
+    // findPeak: Go keeps corr[0] unless a strictly larger |corr| follows (a NaN corr[0] is kept)
+    double a = -1.0;
+    int64_t pi = nl;
+    for (int64_t i = lane; i < nl; i += 64) {
+      const double v = fabs(j.corr[i]);
+      if (v > a) { a = v; pi = i; }                  // NaN never wins
+    }
+    wave_argmax(a, pi);
+    const double c0 = j.corr[0];
+    if (isnan(c0) || !(a > fabs(c0))) pi = 0;        // nothing strictly larger than |corr[0]|
+    cs.peak_index = pi;
+    cs.peak = j.corr[pi];
+    double ns = 0.0, sa = -1.0, ms = 0.0;
+    int64_t nc = 0, si = nl;
+    for (int64_t b = 0; b < nl; b += 64) {
+      const int64_t i = b + lane;
+      double sq = 0.0;                               // terms outside the mask add an exact +0
+      if (i < nl) {
+        const double c = j.corr[i], v = fabs(c);
+        const int64_t d = i > pi ? i - pi : pi - i;
+        if (d > 5) { sq = c * c; nc++; }
+        if (i != pi && v > sa) { sa = v; si = i; }
+        if (d > 10 && v > ms) ms = v;
+      }
+      const int cnt = (int)min((int64_t)64, nl - b);
+      for (int k = 0; k < cnt; ++k) ns += rl(sq, k);
+    }
+    cs.noise_sum = ns;
+    cs.noise_count = wave_isum(nc);
+    wave_argmax(sa, si);
+    cs.second_peak = (si < nl && sa > 0.0) ? j.corr[si] : 0.0;   // Go starts from 0 with a strict >
+    int64_t mi = 0;
+    wave_argmax(ms, mi);                             // a max of non-negative values
+    cs.max_sidelobe = ms;
+    if (nl >= 3 && pi > 0 && pi < nl - 1) cs.sharpness = -(j.corr[pi + 1] - 2 * j.corr[pi] + j.corr[pi - 1]);
+  }
+  if (lane == 0) *j.corr_out = cs;
+}
+
+int launch_pair_scores(const ScoreJob* djobs, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(pair_score_kernel, dim3((unsigned)n), dim3(64), 0, s, djobs);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s) {
   if (n <= 0) return 0;
   int64_t blocks = (n + 255) / 256;

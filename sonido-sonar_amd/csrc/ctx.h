@@ -126,10 +126,12 @@ int dtw_finish(sonar_ctx* c, DtwPending* p, const int32_t** hq, const int32_t** 
 // selectBestAlignment and the time-stretch estimate, into a result handle and/or a pair record
 struct AlignIn {
   const double* corr = nullptr;   // energy correlation, 2L+1 lags (null: no correlation candidate)
+  const host::CorrSums* corr_sums = nullptr;   // or its reductions (the device scorer's), no array
   int64_t L = 0, nqe = 0, nre = 0, mlf = 0;
   bool has_dtw = false;           // chroma DTW candidate
   const int32_t *pq = nullptr, *pr = nullptr;
   const double* pc = nullptr;
+  const host::PathSums* path_sums = nullptr;   // or the path's reductions, no arrays
   int64_t P = 0, nqc = 0, nrc = 0;
   double dist = 0.0;
   int64_t q_pcm_len = 0, r_pcm_len = 0;

@@ -522,12 +522,13 @@ void align_finish(const AlignIn& in, sonar_result* res, sonar_pair_record* rec) 
   struct Cand { bool ok = false; int type = 0; sonar::host::AlignScores s; bool dtw = false;
                 int64_t p0q = 0, p0r = 0, p1q = 0, p1r = 0, plen = 0; };
   Cand corr, chroma;
-  if (in.corr) {     // alignWithFeatures (:357-410) on the energy correlation
-    const auto m = sonar::host::ncc_metrics(in.corr, 2 * in.L + 1, in.L, in.nqe, in.nre);
+  if (in.corr || in.corr_sums) {   // alignWithFeatures (:357-410) on the energy correlation
+    const auto m = in.corr_sums ? sonar::host::ncc_metrics(*in.corr_sums, in.L, in.nqe, in.nre)
+                                : sonar::host::ncc_metrics(in.corr, 2 * in.L + 1, in.L, in.nqe, in.nre);
     corr.ok = true; corr.type = 1;
     corr.s = sonar::host::xcorr_scores(m, in.hop, in.sample_rate, (int)in.mlf);
     if (rec) { rec->peak_lag = (double)m.peak_lag; rec->corr_offset_seconds = corr.s.offset_seconds; }
-    if (res) {
+    if (res && in.corr) {
       res->vec("correlations", std::vector<double>(in.corr, in.corr + 2 * in.L + 1));
       res->scalar("peak_lag", (double)m.peak_lag);
       res->scalar("peak_correlation", m.peak_corr);
@@ -545,11 +546,12 @@ void align_finish(const AlignIn& in, sonar_result* res, sonar_pair_record* rec) 
   if (in.has_dtw) {  // alignWithDTW (:129-148)
     const int64_t P = in.P;
     chroma.ok = true; chroma.type = 2; chroma.dtw = true;
-    chroma.s = sonar::host::dtw_scores(in.pq, in.pr, in.pc, P, in.nqc, in.nrc, in.dist, in.sample_rate);
+    const sonar::host::PathSums ps = in.path_sums ? *in.path_sums : sonar::host::path_sums(in.pq, in.pr, in.pc, P);
+    chroma.s = sonar::host::dtw_scores(ps, in.nqc, in.nrc, in.dist, in.sample_rate);
     chroma.plen = P;
-    if (P > 0) { chroma.p0q = in.pq[0]; chroma.p0r = in.pr[0]; chroma.p1q = in.pq[P - 1]; chroma.p1r = in.pr[P - 1]; }
+    if (P > 0) { chroma.p0q = ps.p0q; chroma.p0r = ps.p0r; chroma.p1q = ps.p1q; chroma.p1r = ps.p1r; }
     if (rec) rec->dtw_distance = in.dist;
-    if (res) {
+    if (res && in.pq) {
       std::vector<double> vq(P), vr(P), vc(P);
       for (int64_t i = 0; i < P; i++) { vq[i] = in.pq[i]; vr[i] = in.pr[i]; vc[i] = in.pc[i]; }
       res->scalar("dtw_distance", in.dist);

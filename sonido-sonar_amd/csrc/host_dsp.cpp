@@ -219,12 +219,30 @@ void YinTracker::step(double& pitch, double& conf, double& voicing) {
   pitch = p; conf = c; voicing = v;
 }
 
-NccMetrics ncc_metrics(const double* corr, int64_t nl, int64_t L, int64_t na, int64_t nb) {
-  NccMetrics m;
-  m.num_lags = nl;
-  if (nl <= 0) return m;
+CorrSums corr_sums(const double* corr, int64_t nl) {
+  CorrSums c;
+  c.num_lags = nl;
+  if (nl <= 0) return c;
   double pk = corr[0]; int64_t pidx = 0;                          // findPeak :526-544
   for (int64_t i = 0; i < nl; i++) if (std::fabs(corr[i]) > std::fabs(pk)) { pk = corr[i]; pidx = i; }
+  c.peak = pk; c.peak_index = pidx;
+  for (int64_t i = 0; i < nl; i++)                                // calculateSNR :572-601
+    if (std::llabs(i - pidx) > 5) { c.noise_sum += corr[i] * corr[i]; c.noise_count++; }
+  if (nl >= 3 && pidx > 0 && pidx < nl - 1)                        // calculateSharpness :611-619
+    c.sharpness = -(corr[pidx + 1] - 2 * corr[pidx] + corr[pidx - 1]);
+  for (int64_t i = 0; i < nl; i++)                                // findSecondPeak :622-636
+    if (i != pidx && std::fabs(corr[i]) > std::fabs(c.second_peak)) c.second_peak = corr[i];
+  for (int64_t i = 0; i < nl; i++)                                // calculatePeakToSidelobe :639-661
+    if (std::llabs(i - pidx) > 10 && std::fabs(corr[i]) > c.max_sidelobe) c.max_sidelobe = std::fabs(corr[i]);
+  return c;
+}
+
+NccMetrics ncc_metrics(const CorrSums& c, int64_t L, int64_t na, int64_t nb) {
+  NccMetrics m;
+  m.num_lags = c.num_lags;
+  if (c.num_lags <= 0) return m;
+  const double pk = c.peak;
+  const int64_t pidx = c.peak_index;
   m.peak_corr = pk; m.peak_index = pidx; m.peak_lag = pidx - L;
   const int64_t n = std::min(na, nb);                              // calculatePValue :547-569
   m.p_value = 1.0;
@@ -233,22 +251,16 @@ NccMetrics ncc_metrics(const double* corr, int64_t nl, int64_t L, int64_t na, in
     m.p_value = t > 2.0 ? 0.01 : t > 1.5 ? 0.05 : t > 1.0 ? 0.1 : 0.5;
   }
   {                                                               // calculateSNR :572-601
-    const double pv = std::fabs(corr[pidx]);
-    double ns = 0; int64_t nc = 0;
-    for (int64_t i = 0; i < nl; i++) if (std::llabs(i - pidx) > 5) { ns += corr[i] * corr[i]; nc++; }
-    if (nc > 0) {
-      const double lvl = std::sqrt(ns / (double)nc);
+    const double pv = std::fabs(pk);
+    if (c.noise_count > 0) {
+      const double lvl = std::sqrt(c.noise_sum / (double)c.noise_count);
       m.snr = lvl < 1e-10 ? INFINITY : 20.0 * std::log10(pv / lvl);
     }
   }
-  if (nl >= 3 && pidx > 0 && pidx < nl - 1)                        // calculateSharpness :611-619
-    m.sharpness = -(corr[pidx + 1] - 2 * corr[pidx] + corr[pidx - 1]);
-  for (int64_t i = 0; i < nl; i++)                                // findSecondPeak :622-636
-    if (i != pidx && std::fabs(corr[i]) > std::fabs(m.second_peak)) m.second_peak = corr[i];
+  m.sharpness = c.sharpness;
+  m.second_peak = c.second_peak;
   {                                                               // calculatePeakToSidelobe :639-661
-    const double pv = std::fabs(corr[pidx]);
-    double ms = 0;
-    for (int64_t i = 0; i < nl; i++) if (std::llabs(i - pidx) > 10 && std::fabs(corr[i]) > ms) ms = std::fabs(corr[i]);
+    const double pv = std::fabs(pk), ms = c.max_sidelobe;
     m.psl = ms < 1e-10 ? INFINITY : 20.0 * std::log10(pv / ms);
   }
   const int64_t lag = m.peak_lag;                                  // calculateOverlapLength :664-667
@@ -257,6 +269,10 @@ NccMetrics ncc_metrics(const double* corr, int64_t nl, int64_t L, int64_t na, in
   else { s1 = -lag; e1 = na; s2 = 0; e2 = nb; if (e1 > na) e1 = na; if (e2 > na + lag) e2 = na + lag; }
   m.overlap = std::min(e1 - s1, e2 - s2);
   return m;
+}
+
+NccMetrics ncc_metrics(const double* corr, int64_t nl, int64_t L, int64_t na, int64_t nb) {
+  return ncc_metrics(corr_sums(corr, nl), L, na, nb);
 }
 
 AlignScores xcorr_scores(const NccMetrics& m, int hop, int sr, int max_lag) {
@@ -293,74 +309,86 @@ AlignScores xcorr_scores(const NccMetrics& m, int hop, int sr, int max_lag) {
   return s;
 }
 
-namespace {
-double cost_consistency(const double* pc, int64_t P) {            // alignment.go:466-512
-  if (P <= 1) return 0.0;
-  int64_t w = std::min<int64_t>(5, P / 4);
-  w = std::max<int64_t>(w, 2);
-  std::vector<double> sm(P);
-  for (int64_t i = 0; i < P; i++) {
-    double s = 0; int64_t c = 0;
-    for (int64_t j = std::max<int64_t>(0, i - w / 2); j <= std::min<int64_t>(P - 1, i + w / 2); j++) { s += pc[j]; c++; }
-    sm[i] = s / (double)c;
-  }
-  double mean = 0; for (double v : sm) mean += v;
-  mean /= (double)P;
-  if (mean <= 1e-10) return 1.0;
-  double var = 0; for (double v : sm) { const double d = v - mean; var += d * d; }
-  var /= (double)P;
-  return 1.0 / (1.0 + std::sqrt(var) / mean);
-}
-double diagonal_bias(const int32_t* pq, const int32_t* pr, int64_t P) {   // :514-540
-  if (P <= 1) return 1.0;
-  int64_t dg = 0;
-  for (int64_t i = 1; i < P; i++) if (pq[i] - pq[i - 1] > 0 && pr[i] - pr[i - 1] > 0) dg++;
-  const double ratio = (double)dg / (double)(P - 1);
-  return 1.0 / (1.0 + std::exp(-10.0 * (ratio - 0.3)));
-}
-double path_changes_ratio(const int32_t* pq, const int32_t* pr, int64_t P) {   // :569-603 / :620-643
-  int64_t ch = 0; int pd0 = 0, pd1 = 0;
+PathSums path_sums(const int32_t* pq, const int32_t* pr, const double* pc, int64_t P) {
+  PathSums s;
+  s.P = P;
+  if (P <= 0) return s;
+  s.p0q = pq[0]; s.p0r = pr[0]; s.p1q = pq[P - 1]; s.p1r = pr[P - 1];
+  for (int64_t i = 0; i < P; i++) { s.offset_sum += pr[i] - pq[i]; s.sum_cost += pc[i]; }   // :530-541, :380-406
+  int pd0 = 0, pd1 = 0;
   for (int64_t i = 1; i < P; i++) {
     const int d0 = pq[i] - pq[i - 1], d1 = pr[i] - pr[i - 1];
-    if (i > 1 && (d0 != pd0 || d1 != pd1)) ch++;
+    if (d0 > 0 && d1 > 0) s.diag_steps++;                         // calculateDiagonalBias :514-540
+    if (i > 1 && (d0 != pd0 || d1 != pd1)) s.changes++;           // calculatePathChanges :569-603
     pd0 = d0; pd1 = d1;
   }
-  return (double)ch / (double)(P - 1);
+  if (P > 1) {                                                    // calculateCostConsistency :466-512
+    int64_t w = std::min<int64_t>(5, P / 4);
+    w = std::max<int64_t>(w, 2);
+    std::vector<double> sm(P);
+    for (int64_t i = 0; i < P; i++) {
+      double t = 0; int64_t c = 0;
+      for (int64_t j = std::max<int64_t>(0, i - w / 2); j <= std::min<int64_t>(P - 1, i + w / 2); j++) { t += pc[j]; c++; }
+      sm[i] = t / (double)c;
+    }
+    for (double v : sm) s.sum_smooth += v;
+    const double mean = s.sum_smooth / (double)P;
+    for (double v : sm) { const double d = v - mean; s.var_smooth += d * d; }
+  }
+  return s;
 }
-double dtw_quality(const int32_t* pq, const int32_t* pr, const double* pc, int64_t P, int64_t nq, int64_t nr) {
-  if (P == 0) return 0.0;                                         // calculateDTWQuality :543-566
-  double eff = (double)std::max(nq, nr) / (double)P;
+
+namespace {
+double cost_consistency(const PathSums& s) {                      // alignment.go:466-512
+  if (s.P <= 1) return 0.0;
+  const double mean = s.sum_smooth / (double)s.P;
+  if (mean <= 1e-10) return 1.0;
+  const double var = s.var_smooth / (double)s.P;
+  return 1.0 / (1.0 + std::sqrt(var) / mean);
+}
+double diagonal_bias(const PathSums& s) {                         // :514-540
+  if (s.P <= 1) return 1.0;
+  const double ratio = (double)s.diag_steps / (double)(s.P - 1);
+  return 1.0 / (1.0 + std::exp(-10.0 * (ratio - 0.3)));
+}
+double path_changes_ratio(const PathSums& s) {                    // :569-603 / :620-643
+  return (double)s.changes / (double)(s.P - 1);
+}
+double dtw_quality(const PathSums& s, int64_t nq, int64_t nr) {
+  if (s.P == 0) return 0.0;                                       // calculateDTWQuality :543-566
+  double eff = (double)std::max(nq, nr) / (double)s.P;
   eff = go_min(1.0, eff);
-  const double smooth = P <= 2 ? 1.0 : go_max(0.0, 1.0 - path_changes_ratio(pq, pr, P));
-  const double q = 0.3 * eff + 0.3 * diagonal_bias(pq, pr, P) + 0.2 * smooth + 0.2 * cost_consistency(pc, P);
+  const double smooth = s.P <= 2 ? 1.0 : go_max(0.0, 1.0 - path_changes_ratio(s));
+  const double q = 0.3 * eff + 0.3 * diagonal_bias(s) + 0.2 * smooth + 0.2 * cost_consistency(s);
   return go_min(1.0, go_max(0.0, q));
 }
 }  // namespace
 
-AlignScores dtw_scores(const int32_t* pq, const int32_t* pr, const double* pc, int64_t P, int64_t nq, int64_t nr,
-                       double dist, int sr) {
+AlignScores dtw_scores(const PathSums& ps, int64_t nq, int64_t nr, double dist, int sr) {
   AlignScores s;                                                  // alignWithDTW :129-148
+  const int64_t P = ps.P;
   const double avg = (double)(nq + nr) / 2.0;
   if (avg != 0) {                                                 // calculateSimilarityFromDTW :380-406
     const double ds = 1.0 / (1.0 + dist / avg);
-    double mc = 0; if (P > 0) { for (int64_t i = 0; i < P; i++) mc += pc[i]; mc /= (double)P; }
-    s.similarity = go_min(1.0, go_max(0.0, 0.5 * ds + 0.3 * dtw_quality(pq, pr, pc, P, nq, nr) + 0.2 * (1.0 / (1.0 + mc))));
+    double mc = 0; if (P > 0) mc = ps.sum_cost / (double)P;
+    s.similarity = go_min(1.0, go_max(0.0, 0.5 * ds + 0.3 * dtw_quality(ps, nq, nr) + 0.2 * (1.0 / (1.0 + mc))));
   }
   if (P > 0 && avg != 0) {                                        // calculateDTWConfidence :420-463
     const double c1 = std::exp(-(dist / avg) * 2.0);
     const double pe = go_min(1.0, (double)std::max(nq, nr) / (double)P);
-    s.confidence = go_min(1.0, go_max(0.0, 0.4 * c1 + 0.25 * pe + 0.2 * cost_consistency(pc, P) +
-                                               0.15 * diagonal_bias(pq, pr, P)));
+    s.confidence = go_min(1.0, go_max(0.0, 0.4 * c1 + 0.25 * pe + 0.2 * cost_consistency(ps) +
+                                               0.15 * diagonal_bias(ps)));
   }
-  if (P > 0) {                                                    // calculateAverageOffset :530-541
-    int64_t sum = 0;
-    for (int64_t i = 0; i < P; i++) sum += pr[i] - pq[i];
-    s.offset = sum / P;
-  }
+  if (P > 0) s.offset = ps.offset_sum / P;                        // calculateAverageOffset :530-541
   s.offset_seconds = (double)s.offset / (double)sr;               // F9: frames / sample rate
-  s.quality = dtw_quality(pq, pr, pc, P, nq, nr);
-  if (P >= 3) s.stability = go_max(0.0, 1.0 - path_changes_ratio(pq, pr, P));   // :620-643
+  s.quality = dtw_quality(ps, nq, nr);
+  if (P >= 3) s.stability = go_max(0.0, 1.0 - path_changes_ratio(ps));   // :620-643
   return s;
+}
+
+AlignScores dtw_scores(const int32_t* pq, const int32_t* pr, const double* pc, int64_t P, int64_t nq, int64_t nr,
+                       double dist, int sr) {
+  return dtw_scores(path_sums(pq, pr, pc, P), nq, nr, dist, sr);
 }
 
 double energy_variance(const std::vector<double>& e) {           // energy.go:96-117

@@ -47,7 +47,28 @@ struct NccMetrics {
   double peak_corr = 0, p_value = 1, snr = 0, sharpness = 0, second_peak = 0, psl = 0;
   int64_t peak_lag = 0, peak_index = 0, overlap = 0, num_lags = 0;
 };
+// The O(lags) part of those metrics: findPeak's index and value, calculateSNR's noise sum and count
+// (|i - peak| > 5), findSecondPeak's value, calculatePeakToSidelobe's sidelobe maximum (|i - peak|
+// > 10) and calculateSharpness's second difference (0 at the ends).  corr_sums runs Go's loops; the
+// batched pair path computes the same on the device (pair_score_kernel, align_kernels.hip), where
+// only the noise sum is reassociated.  Plain data, shared with the kernels.
+struct CorrSums {
+  int64_t num_lags = 0, peak_index = 0, noise_count = 0;
+  double peak = 0, noise_sum = 0, second_peak = 0, max_sidelobe = 0, sharpness = 0;
+};
+CorrSums corr_sums(const double* corr, int64_t nl);
+NccMetrics ncc_metrics(const CorrSums& c, int64_t L, int64_t na, int64_t nb);
 NccMetrics ncc_metrics(const double* corr, int64_t nl, int64_t L, int64_t na, int64_t nb);
+// The O(path) part of the DTW scorers (alignment.go:380-643): the path length and end points,
+// diagonal steps and direction changes (calculateDiagonalBias, calculatePathChanges), the offset
+// sum (calculateAverageOffset), the cost sum (calculateSimilarityFromDTW's mean cost) and
+// calculateCostConsistency's smoothed-cost sum and squared deviations from their mean
+struct PathSums {
+  int64_t P = 0, diag_steps = 0, changes = 0, offset_sum = 0;
+  int32_t p0q = 0, p0r = 0, p1q = 0, p1r = 0;
+  double sum_cost = 0, sum_smooth = 0, var_smooth = 0;
+};
+PathSums path_sums(const int32_t* pq, const int32_t* pr, const double* pc, int64_t P);
 
 // AlignmentAnalyzer scorers (algorithms/stats/alignment.go)
 struct AlignScores {
@@ -57,6 +78,7 @@ struct AlignScores {
 AlignScores xcorr_scores(const NccMetrics& m, int hop, int sample_rate, int max_lag);
 AlignScores dtw_scores(const int32_t* pq, const int32_t* pr, const double* pc, int64_t P, int64_t nq, int64_t nr,
                        double distance, int sample_rate);
+AlignScores dtw_scores(const PathSums& s, int64_t nq, int64_t nr, double distance, int sample_rate);
 
 // Energy helpers used by extractEnergyFeatures (algorithms/temporal/energy.go:96-178)
 double energy_variance(const std::vector<double>& e);

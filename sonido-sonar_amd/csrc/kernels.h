@@ -6,6 +6,7 @@
 #include <cstdint>
 
 #include "../../include/sonar_gpu.h"
+#include "host_dsp.h"
 
 namespace sonar {
 
@@ -277,6 +278,19 @@ int launch_dtw_path_tiles(const DtwArgs& a, int64_t P, hipStream_t s);
 int32_t dtw_dbg_stall_band(bool batch);   // SONAR_DTW_DBG_STALL (tests only), -1 when unset
 int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* dstart, int n, int64_t total_bands,
                      int64_t max_cap, int32_t* ticket, hipStream_t s, const int2* dmap = nullptr);
+// One pair of sonar_align_pairs' device-side scorer reductions (pair_score_kernel): the warping
+// path (length at *plen) and the energy correlation (nl lags, null: none) in, PathSums / CorrSums
+// (host_dsp.h) out
+struct ScoreJob {
+  const int32_t *pq, *pr;
+  const double* pc;
+  const int64_t* plen;
+  const double* corr;
+  int64_t nl;
+  host::PathSums* path;
+  host::CorrSums* corr_out;
+};
+int launch_pair_scores(const ScoreJob* djobs, int n, hipStream_t s);
 // sets *flag = 1 if any of the n values is not finite
 int launch_nonfinite(const double* x, int64_t n, int32_t* flag, hipStream_t s);
 // the same probe over q and r of every DTW of a batch (sets args[k].sync[2]); max_elems >= every

@@ -259,8 +259,10 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   // batch ticket, the per-pair band-kernel diagnostic records, then the DTW arguments, ticket
   // starts and the band-major ticket map
   const size_t stat_b = al256((size_t)n * 32 + 16), diag_b = al256((size_t)n * 8 * sonar::DTW_DIAG_WORDS),
+               ps_b = al256((size_t)n * sizeof(sonar::host::PathSums)),
+               cs_b = al256((size_t)n * sizeof(sonar::host::CorrSums)),
                args_b = al256((size_t)n * sizeof(sonar::DtwArgs)), start_b = al256((size_t)(n + 1) * 8),
-               map_b = al256((size_t)total_bands * 8);
+               map_b = al256((size_t)total_bands * 8), sj_b = al256((size_t)n * sizeof(sonar::ScoreJob));
   char* chroma = (char*)dbuf(w, "pb.chroma", chroma_b);
   char* CK = (char*)dbuf(w, "pb.CK", ck_b);
   char* runs = (char*)dbuf(w, "pb.runs", runs_b);
@@ -268,12 +270,17 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   char* E = (char*)dbuf(w, "pb.E", e_b);
   char* codes = (char*)dbuf(w, "pb.codes", codes_b);
   char* wst = (char*)dbuf(w, "pb.wstart", wst_b);
-  // small holds, in the pinned host buffer's layout: status words + ticket, diagnostic records, DTW
-  // arguments, ticket starts, band-major map, correlations, paths -- so the batch's results come
-  // back in ONE copy (each runtime copy is a blit kernel that needs a CU beside the band blocks)
-  const size_t small_b = stat_b + diag_b + args_b + start_b + map_b + corr_b + path_b;
+  // small holds, in the pinned host buffer's layout: status words + ticket, diagnostic records, the
+  // scorer reductions (PathSums, CorrSums), then DTW arguments, ticket starts, band-major map and
+  // score jobs (one upload), correlations, paths -- so the batch's results come back in ONE copy of
+  // the head (each runtime copy is a blit kernel that needs a CU beside the band blocks).  The
+  // scorers' O(path) loops run on the device (pair_score_kernel); SONAR_PAIR_HOST_SCORES=1 (A/B,
+  // tests) copies correlations and paths back instead and runs them on the host, as a
+  // SONAR_PAIR_DUMP does.
+  const size_t head_b = stat_b + diag_b + ps_b + cs_b, up_b = args_b + start_b + map_b + sj_b;
+  const size_t small_b = head_b + up_b + corr_b + path_b;
   char* small = (char*)dbuf(w, "pb.small", small_b);
-  char* corr = small ? small + (stat_b + diag_b + args_b + start_b + map_b) : nullptr;
+  char* corr = small ? small + (head_b + up_b) : nullptr;
   char* path = small ? corr + corr_b : nullptr;
   // SONAR_DTW_TRACE=<file> (diagnostics): every band's sweep timestamps (dtw_band_kernel's trace
   // words) appended to <file> as {pair, band, 8 trace words} records
@@ -286,7 +293,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   double* st = (double*)dbuf(w, "ncc.stats", 64);
   double* up_q = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.q", (size_t)maxn * 8);
   double* up_r = device_ptrs ? nullptr : (double*)dbuf(w, "pairs.r", (size_t)maxn * 8);
-  char* h = (char*)sonar::detail::hbuf(w, "pb.host", stat_b + diag_b + args_b + start_b + map_b + corr_b + path_b);
+  char* h = (char*)sonar::detail::hbuf(w, "pb.host", small_b);
   if (!chroma || !CK || !runs || !Dn || !E || !codes || !wst || !path || !corr || !small || !eq || !er || !xa || !xb ||
       !st || (!device_ptrs && (!up_q || !up_r)) || !h)
     return fail(w, SONAR_ERR_NOMEM, "allocation failed (pair batch)");
@@ -299,17 +306,26 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   int32_t* dstat = (int32_t*)small;                 // per pair: [0..1] plen, [2..3] C[nq][nr], [4..7] sync
   int32_t* ticket = (int32_t*)(small + (size_t)n * 32);
   uint64_t* ddiag = (uint64_t*)(small + stat_b);
-  const size_t ab = stat_b + diag_b;                 // where the arguments start
+  auto* dps = (sonar::host::PathSums*)(small + stat_b + diag_b);
+  auto* dcs = (sonar::host::CorrSums*)(small + stat_b + diag_b + ps_b);
+  const size_t ab = head_b;                          // where the arguments start
   sonar::DtwArgs* dargs = (sonar::DtwArgs*)(small + ab);
   int64_t* dstart = (int64_t*)(small + ab + args_b);
   char* hstat = h;
   const uint64_t* hdiag = (const uint64_t*)(h + stat_b);
+  const auto* hps = (const sonar::host::PathSums*)(h + stat_b + diag_b);
+  const auto* hcs = (const sonar::host::CorrSums*)(h + stat_b + diag_b + ps_b);
   sonar::DtwArgs* hargs = (sonar::DtwArgs*)(h + ab);
   int64_t* hstart = (int64_t*)(h + ab + args_b);
   int2* hmap = (int2*)(h + ab + args_b + start_b);
   int2* dmap = (int2*)(small + ab + args_b + start_b);
-  char* hcorr = h + ab + args_b + start_b + map_b;
+  auto* hsj = (sonar::ScoreJob*)(h + ab + args_b + start_b + map_b);
+  auto* dsj = (const sonar::ScoreJob*)(small + ab + args_b + start_b + map_b);
+  char* hcorr = h + head_b + up_b;
   char* hpath = hcorr + corr_b;
+  const char* dump_dir = std::getenv("SONAR_PAIR_DUMP");
+  const char* hs_env = std::getenv("SONAR_PAIR_HOST_SCORES");
+  const bool host_scores = dump_dir || (hs_env && std::atoi(hs_env) != 0);
   HIP_TRY(w, hipMemsetAsync(small, 0, stat_b + diag_b, s));
   // every pair's music features and energy NCC: batched launches over the whole batch when the
   // inputs are on the device and every signal fits the batched kernels (feat_batch), else pair by
@@ -346,6 +362,9 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     a.diag = ddiag + (size_t)i * sonar::DTW_DIAG_WORDS;
     a.trace = trb ? (uint64_t*)(trb + (size_t)acc * 64) : nullptr;
     a.dbg_stall = sonar::dtw_dbg_stall_band(true);
+    sonar::ScoreJob& sj = hsj[i];
+    sj = sonar::ScoreJob{a.pq, a.pr, a.pc, a.plen, p.corr ? (const double*)(corr + p.corr_off) : nullptr,
+                         2 * p.L + 1, dps + i, dcs + i};
     hstart[i] = acc;
     acc += p.g.nb;
   }
@@ -358,7 +377,7 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
       for (int i = 0; i < n; ++i)
         if (b < pg[i].g.nb) hmap[t++] = make_int2(i, (int)b);
   }
-  HIP_TRY(w, hipMemcpyAsync(dargs, hargs, args_b + start_b + map_b, hipMemcpyHostToDevice, s));
+  HIP_TRY(w, hipMemcpyAsync(dargs, hargs, up_b, hipMemcpyHostToDevice, s));
   // the non-finite probe of every pair's chroma in one launch (flags in each pair's sync[2]); the
   // same launch fills every pair's band-edge rows E with the band kernel's sentinel
   int64_t max_el = 0;
@@ -367,7 +386,8 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
   if (sonar::launch_nonfinite_batch(dargs, n, max_el, s) != 0) return fail(w, SONAR_ERR_DEVICE, "dtw launch failed");
   if (sonar::launch_dtw_batch(hargs, dargs, dstart, n, total_bands, max_cap, ticket, s, dmap) != 0)
     return fail(w, SONAR_ERR_DEVICE, "dtw batch launch failed");
-  HIP_TRY(w, hipMemcpyAsync(hstat, small, small_b, hipMemcpyDeviceToHost, s));
+  if (!host_scores && sonar::launch_pair_scores(dsj, n, s) != 0) return fail(w, SONAR_ERR_DEVICE, "score launch failed");
+  HIP_TRY(w, hipMemcpyAsync(hstat, small, host_scores ? small_b : head_b, hipMemcpyDeviceToHost, s));
   std::vector<uint64_t> htr(trb ? (size_t)total_bands * 8 : 0);
   if (trb) HIP_TRY(w, hipMemcpyAsync(htr.data(), trb, htr.size() * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(w, hipStreamSynchronize(s));
@@ -384,7 +404,6 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
       std::fclose(f);
     }
   }
-  const char* dump_dir = std::getenv("SONAR_PAIR_DUMP");
   for (int i = 0; i < n; ++i) {
     const PairGeo& p = pg[i];
     const char* ps = hstat + (size_t)i * 32;
@@ -429,9 +448,18 @@ int align_batch(sonar_ctx* w, const std::vector<PairGeo>& in, const double* cons
     }
     sonar::detail::AlignIn ai;
     ai.q_pcm_len = p.nq; ai.r_pcm_len = p.nr; ai.sample_rate = sr; ai.hop = hop;
-    if (p.corr) { ai.corr = (const double*)(hcorr + p.corr_off); ai.L = p.L; ai.nqe = p.Eq; ai.nre = p.Er; ai.mlf = p.mlf; }
-    const double* pc = (const double*)(hpath + p.path);
-    ai.has_dtw = true; ai.pc = pc; ai.pq = (const int32_t*)(pc + p.cap); ai.pr = ai.pq + p.cap;
+    if (p.corr) {
+      if (host_scores) ai.corr = (const double*)(hcorr + p.corr_off);
+      else ai.corr_sums = hcs + i;
+      ai.L = p.L; ai.nqe = p.Eq; ai.nre = p.Er; ai.mlf = p.mlf;
+    }
+    ai.has_dtw = true;
+    if (host_scores) {
+      const double* pc = (const double*)(hpath + p.path);
+      ai.pc = pc; ai.pq = (const int32_t*)(pc + p.cap); ai.pr = ai.pq + p.cap;
+    } else {
+      ai.path_sums = hps + i;
+    }
     ai.P = P; ai.nqc = p.Fq; ai.nrc = p.Fr; ai.dist = cnm / (double)P;   // dtw.go:88-91
     sonar::detail::align_finish(ai, nullptr, rec);
     rec->status = SONAR_OK;

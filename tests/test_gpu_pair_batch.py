@@ -139,3 +139,17 @@ def test_batched_features_equal_per_pair(ctx, monkeypatch, device_pairs, streams
     for f in sonar.PAIR_FIELDS:
         assert _same(got[f], ref[f]), f
         assert _same(per[f], ref[f]), f
+
+
+@pytest.mark.parametrize("streams", [1, 3])
+def test_device_scorer_equals_host_scorer(ctx, monkeypatch, device_pairs, streams):
+    """The batch's scorer reductions on the device (pair_score_kernel: path sums, correlation
+    peak / noise / sidelobes in Go's order) against the same batch scored on the host from the
+    copied-back paths and correlations (SONAR_PAIR_HOST_SCORES=1): identical records, bit for bit."""
+    qs, rs = device_pairs
+    qs, rs = qs[:-1], rs[:-1]
+    host = _run_dev(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=streams, SONAR_PAIR_HOST_SCORES=1)
+    dev = _run_dev(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=streams)
+    assert np.all(host["status"] == 0) and np.all(dev["status"] == 0)
+    for f in sonar.PAIR_FIELDS:
+        assert _same(dev[f], host[f]), f
