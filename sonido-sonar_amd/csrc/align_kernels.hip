@@ -445,8 +445,12 @@ constexpr int DTW_SWEEP_PRIO = 3;  // s_setprio of the sweep (the min-chain is t
 #define DTW_CODE_PRIO 2           // s_setprio of the code wave (A/B: 0, 1, 2, 3)
 #endif
 #ifndef DTW_DIST_PRIO
-#define DTW_DIST_PRIO 0           // s_setprio of the distance waves (A/B; 1 starved the feeder / edge
-                                  // poller into 1 s band timeouts, profiles/r04pq_ab.log)
+#define DTW_DIST_PRIO 1           // s_setprio of the distance waves while they compute.  Round 4's 1
+                                  // starved the feeder / edge poller into 1 s band timeouts
+                                  // (profiles/r04pq_ab.log) because the waves also SPUN at 1; since
+                                  // every wait drops to 0 (SONAR_SPIN_UNTIL), a distance wave only
+                                  // outranks them while it has cells to compute, at most DTW_DQ steps
+                                  // ahead of the sweep (profiles/r05q_dtw_prio_ab.log: C5 +1.3 %)
 #endif
 #ifndef DTW_AUX_PRIO
 #define DTW_AUX_PRIO 0            // s_setprio of the ring feeder and the edge poller (A/B)
