@@ -445,12 +445,13 @@ constexpr int DTW_SWEEP_PRIO = 3;  // s_setprio of the sweep (the min-chain is t
 #define DTW_CODE_PRIO 2           // s_setprio of the code wave (A/B: 0, 1, 2, 3)
 #endif
 #ifndef DTW_DIST_PRIO
-#define DTW_DIST_PRIO 1           // s_setprio of the distance waves while they compute.  Round 4's 1
-                                  // starved the feeder / edge poller into 1 s band timeouts
-                                  // (profiles/r04pq_ab.log) because the waves also SPUN at 1; since
-                                  // every wait drops to 0 (SONAR_SPIN_UNTIL), a distance wave only
-                                  // outranks them while it has cells to compute, at most DTW_DQ steps
-                                  // ahead of the sweep (profiles/r05q_dtw_prio_ab.log: C5 +1.3 %)
+#define DTW_DIST_PRIO 0           // s_setprio of the distance waves while they compute (A/B).  At 1,
+                                  // C5 ran 1.3 % faster (profiles/r05q_dtw_prio_ab.log) but a
+                                  // process's first C5 call lost DTWs to the 1 s bound again, in round
+                                  // 4 (profiles/r04pq_ab.log) and round 5 (r05s_c5_workers_ab.log),
+                                  // even with every wait at 0: busy distance waves of one band block
+                                  // outrank the OTHER block's edge poller on a shared SIMD (DESIGN.md,
+                                  // Kernel 6)
 #endif
 #ifndef DTW_AUX_PRIO
 #define DTW_AUX_PRIO 0            // s_setprio of the ring feeder and the edge poller (A/B)
