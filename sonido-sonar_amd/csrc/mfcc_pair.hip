@@ -359,7 +359,10 @@ __global__ __launch_bounds__(768, 1) void mfcc_pair_kernel(MfccPairParams p) {
   // after that is claimed in its DCT phase, whose LDS drain returns the counter with the data
   auto process = [&](int pi, int nxt, float (&xr)[16], float (&xe)[NE]) -> int {
     advance(gp, pi);
-    __builtin_amdgcn_s_setprio(0);
+#ifndef HL_PHASE_PRIO
+#define HL_PHASE_PRIO 1
+#endif
+    if (HL_PHASE_PRIO) __builtin_amdgcn_s_setprio(0);
     cf v[16];
     // ---- pass 1: DFT16 over a (the window fused into its first butterflies), twiddle w_1024^{b k1}
     if constexpr (HC == 256) {
@@ -431,7 +434,7 @@ __global__ __launch_bounds__(768, 1) void mfcc_pair_kernel(MfccPairParams p) {
       v[j] = {u.x, u.y};
     }
     wave_lds_sync();
-    __builtin_amdgcn_s_setprio(1);
+    if (HL_PHASE_PRIO) __builtin_amdgcn_s_setprio(1);
     // ---- pass 3: DFT8 over b0 for both combos --------------------------------------
     dft8<0, 1>(v);    // A[c1] = Z[rA + 128 c1]
     dft8<8, 1>(v);    // B[c1] = Z[rB + 128 c1]
