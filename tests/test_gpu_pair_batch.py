@@ -7,6 +7,7 @@ math.Min path and flags the record SONAR_PAIR_REDONE_NONFINITE).  Every batched 
 checks that no band pipeline timed out (the retry would hide it)."""
 import numpy as np
 import pytest
+import torch  # noqa: F401 -- before the library loads HIP (one HIP runtime in the process)
 
 import sonar
 from sonar import synth
@@ -93,7 +94,6 @@ def test_trim_releases_and_reallocates(ctx, monkeypatch, mixed_pairs):
 def device_pairs():
     """Device-resident pairs of 5-12 s (chroma frames of 256 samples: the batched feature launches
     take the whole batch), plus the same with one 3.3 s pair (257-sample frames: per-pair path)."""
-    import torch
     rng = np.random.default_rng(12)
     qs, rs = [], []
     for k, (sq, sr_) in enumerate([(6.0, 7.5), (9.0, 5.0), (12.0, 10.7), (5.5, 8.9), (7.0, 7.0), (3.3, 3.3)]):
@@ -151,5 +151,40 @@ def test_device_scorer_equals_host_scorer(ctx, monkeypatch, device_pairs, stream
     host = _run_dev(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=streams, SONAR_PAIR_HOST_SCORES=1)
     dev = _run_dev(ctx, monkeypatch, qs, rs, SONAR_PAIR_STREAMS=streams)
     assert np.all(host["status"] == 0) and np.all(dev["status"] == 0)
+    for f in sonar.PAIR_FIELDS:
+        assert _same(dev[f], host[f]), f
+
+
+def test_device_scorer_edge_pairs(ctx, monkeypatch):
+    """Device vs host scorer on pairs whose paths and correlations are degenerate: identical
+    streams (a pure diagonal, a correlation peak at lag 0), a silent query (an all-zero energy
+    correlation: no peak beyond index 0, zero sidelobes), a constant tone against itself shifted,
+    and the shortest streams the batch takes (paths of a few points)."""
+    rng = np.random.default_rng(21)
+    base, _ = synth.c3_pair(6.0, 0.7)[:2]
+    tone = (0.3 * np.sin(2 * np.pi * 440.0 * np.arange(int(5.0 * 44100)) / 44100.0)).astype(np.float64)
+    short = 0.2 * rng.standard_normal(1024 + 256 * 9)
+    qs = [base[: 5 * 44100], np.zeros(5 * 44100), tone, short, base[: 6 * 44100]]
+    rs = [base[: 5 * 44100].copy(), base[: 5 * 44100], np.roll(tone, 1234), short[::-1].copy(),
+          base[44100: 6 * 44100] + 1e-3 * rng.standard_normal(5 * 44100)]
+    qd = [torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64)).cuda() for x in qs]
+    rd = [torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64)).cuda() for x in rs]
+    torch.cuda.synchronize()
+
+    def run(**env):
+        env.setdefault("SONAR_PAIR_RETRY", 0)
+        for k, v in env.items():
+            monkeypatch.setenv(k, str(v))
+        try:
+            return ctx.align_pairs([q.data_ptr() for q in qd], [r.data_ptr() for r in rd],
+                                   nq=[q.numel() for q in qd], nr=[r.numel() for r in rd],
+                                   max_lag_seconds=2.0, workers=8, device_ptrs=True)
+        finally:
+            for k in env:
+                monkeypatch.delenv(k)
+
+    host = run(SONAR_PAIR_HOST_SCORES=1, SONAR_PAIR_STREAMS=1)
+    dev = run(SONAR_PAIR_STREAMS=1)
+    assert np.array_equal(host["status"], dev["status"])
     for f in sonar.PAIR_FIELDS:
         assert _same(dev[f], host[f]), f
