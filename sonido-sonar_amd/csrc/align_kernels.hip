@@ -470,6 +470,12 @@ constexpr int DTW_EAHEAD = 64;    // the feeder fetches edge columns up to min(p
 #ifndef DTW_DG
 #define DTW_DG 8                  // distance cells interleaved per pass (a divisor of DTW_ECH)
 #endif
+#ifndef DTW_BATCH_MINWAVES
+#define DTW_BATCH_MINWAVES 6      // the batched (C5) instance: 80 VGPRs instead of 98 (launch_dtw_batch)
+#endif
+#ifndef DTW_BATCH_PAD
+#define DTW_BATCH_PAD 2560        // dynamic LDS bytes per batched band block: unused, caps it at 2 per CU
+#endif
 #ifndef DTW_MINWAVES
 #define DTW_MINWAVES 4            // waves per SIMD the register budget must allow
 #endif
@@ -626,7 +632,8 @@ __device__ __forceinline__ void dtw_local_stall(int role, int32_t* sync, int* ct
 
 template <int D, bool FAST, bool BANDED, bool BATCH = false>
 // (2 blocks of 8 waves per CU: at least 4 waves per SIMD, <= 128 VGPRs)
-__global__ __launch_bounds__(64 * DTW_WAVES, DTW_MINWAVES) void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
+__global__ __launch_bounds__(64 * DTW_WAVES, BATCH ? DTW_BATCH_MINWAVES : DTW_MINWAVES)
+void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
   constexpr int DR = D > 0 ? D : 1;
   constexpr int DS = dtw_ring_stride<D>();
   constexpr int FEEDER_WAVE = DTW_FEEDER_WAVE;
@@ -1958,8 +1965,13 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
   if (total_bands > INT32_MAX) return -1;
   const DtwArgs none{};
   const DtwBatch bt{dargs, dstart, n, ticket, dmap};
-  hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES), 0, s,
-                     none, bt);
+  // the batched instance is built for 6 waves per SIMD (80 VGPRs) but launched with DTW_BATCH_PAD
+  // bytes of dynamic LDS it never touches, so LDS still holds it to 2 blocks per CU (3 x 52 KB would
+  // fit; 3 x 54.7 KB do not): the 18 registers per wave it gives up leave room on each SIMD for
+  // the other worker streams' short kernels beside two band blocks.  C5 2,143-2,162 ->
+  // 2,216-2,235 pairs/s (Kernel 6, "Register budget of the batched instance")
+  hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
+                     DTW_BATCH_PAD, s, none, bt);
   if (dtw_serial_walk()) {
     hipLaunchKernelGGL(dtw_walk_batch_kernel, dim3((unsigned)n), dim3(64), 0, s, dargs);
   } else {
