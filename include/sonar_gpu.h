@@ -165,7 +165,8 @@ typedef struct {
   int32_t energy_hop;      /* ShortTimeEnergy hop                                   */
   double preemph_alpha;    /* pre-emphasis for ZCR/energy (0.97 speech, pre_emphasis.go:116) */
   uint32_t flags;          /* SONAR_FP_*                                            */
-  int32_t precision;       /* SONAR_F32 (throughput) / SONAR_F64 (parity)           */
+  int32_t precision;       /* SONAR_F32 (throughput) / SONAR_F64 (parity); calls with
+                              SONAR_FP_SPECTRAL always run the f64 transform          */
   int32_t pcm_dtype;       /* SONAR_F32 / SONAR_F64                                 */
   int32_t out_dtype;       /* SONAR_F32 / SONAR_F64 element type of every output    */
   int32_t device_ptrs;     /* 0: host buffers (sync); 1: device buffers (async)     */
@@ -543,6 +544,46 @@ typedef struct {                     /* stats.AlignmentStats (alignment.go:700-7
 int sonar_alignment_consistency(sonar_ctx* ctx, const double* query, int64_t nq, const double* reference, int64_t nr,
                                 int32_t dim, int32_t method, int32_t max_lag, int32_t hop, int32_t sample_rate,
                                 int32_t num_trials, sonar_alignment_stats* out);
+
+/* ---- AlignmentAnalyzer.AlignFeatures / AlignAudio and AlignmentExtractor.AlignAudioFiles --------
+ * The analyzer's own entry (algorithms/stats/alignment.go:84-106) for method SONAR_ALIGN_DTW,
+ * SONAR_ALIGN_XCORR or SONAR_ALIGN_HYBRID (alignWithHybrid :308-337: the cross-correlation of the
+ * features' first component; when its confidence is <= 0.7 the DTW of the full rows, with Go's
+ * result aliasing F8: Confidence = 0.6 c + 0.4 c and Similarity = 0.7 s + 0.3 s of the DTW values,
+ * Offset / AlignmentQuality / Stability the DTW's, NoiseLevel the correlation's).  query /
+ * reference: row-major nq x dim / nr x dim float64 (device pointers if device_ptrs).  max_lag and
+ * hop as NewAlignmentAnalyzer (:60-81).  *out: scalars "method", "offset" (samples for the
+ * correlation, frames for the DTW, F9), "offset_seconds", "confidence", "similarity",
+ * "alignment_quality", "noise_level", "stability", "query_length", "reference_length",
+ * "sample_rate", "dtw_ran"; with the correlation "correlations" (2L+1) and its metrics
+ * ("peak_correlation", "peak_lag", ... as sonar_ncc); with the DTW "dtw_distance",
+ * "dtw_path_query", "dtw_path_reference", "dtw_path_cost".  Errors as Go: "empty feature sequences
+ * provided", "unsupported alignment method: N". */
+int sonar_analyzer_align_features(sonar_ctx* ctx, const double* query, int64_t nq, const double* reference,
+                                  int64_t nr, int32_t dim, int32_t method, int32_t max_lag, int32_t hop,
+                                  int32_t sample_rate, int32_t device_ptrs, sonar_result** out);
+
+/* AlignmentAnalyzer.AlignAudio (:108-126): extractEnergyFeatures (:341-361) of both float64 PCM
+ * streams -- numFrames = (len - window) / hop + 1 (truncating), RMS over [i hop, min(i hop + window,
+ * len)) -- then sonar_analyzer_align_features with dim 1.  Go panics are SONAR_ERR_PANIC with
+ * Go's text (hop 0: "integer divide by zero"; a negative frame count: "makeslice: len out of
+ * range"); window <= 0, hop < 0 or an empty stream: SONAR_ERR_UNSUPPORTED (Go divides 0 by 0). */
+int sonar_align_audio(sonar_ctx* ctx, const double* q_pcm, int64_t nq, const double* r_pcm, int64_t nr,
+                      int32_t method, int32_t max_lag, int32_t hop, int32_t window, int32_t sample_rate,
+                      int32_t device_ptrs, sonar_result** out);
+
+/* AlignmentExtractor.AlignAudioFiles (extractors/alignment.go:489-553) of an extractor built by
+ * NewAlignmentExtractorWithMaxLag (:99-136) from FeatureConfig{feature_sample_rate, hop, window}:
+ * ShortTimeEnergy (algorithms/temporal/energy.go:25-50) of both streams, then the Hybrid
+ * AlignFeatures at maxLagFrames = int(max_lag_seconds * feature_sample_rate) / hop.  *out: the
+ * sonar_analyzer_align_features keys (BestAlignment) plus the AlignmentFeatures fields
+ * "temporal_offset", "offset_confidence", "alignment_similarity", "alignment_quality",
+ * "feature_similarity_energy", "query_length_seconds", "reference_length_seconds", "time_stretch"
+ * (never set by Go: 0) and "max_lag_frames"; Method is always "energy_correlation".  Errors as Go:
+ * "alignment failed: empty feature sequences provided"; hop 0 panics ("integer divide by zero"). */
+int sonar_align_audio_files(sonar_ctx* ctx, const double* q_pcm, int64_t nq, const double* r_pcm, int64_t nr,
+                            int32_t sample_rate, int32_t feature_sample_rate, int32_t hop, int32_t window,
+                            double max_lag_seconds, int32_t device_ptrs, sonar_result** out);
 
 /* AlignmentExtractor.TruncateToAlignmentPCM (extractors/alignment.go:223-297) as sample indices:
  * the aligned segments are pcm1[start1 : start1+length] and pcm2[start2 : start2+length] (the

@@ -714,6 +714,102 @@ def align_offset_reference(query, reference, sample_rate, method, max_lag, hop):
     return int(align_dtw_metrics(res, len(q), len(r), sample_rate)["offset"])
 
 
+class GoPanic(RuntimeError):
+    """The Go reference panics on this input (the message is Go's runtime error text)."""
+
+
+def _go_div(a, b):
+    """Go's integer division: truncates toward zero; b == 0 panics."""
+    if b == 0:
+        raise GoPanic("runtime error: integer divide by zero")
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b > 0) else -q
+
+
+def analyzer_align_reference(query, reference, sample_rate, method, max_lag, hop, dtw_threads=8):
+    """AlignmentAnalyzer.AlignFeatures (stats/alignment.go:84-106) -> every AlignmentResult field.
+
+    alignWithCrossCorrelation (:151-181) on the first component (flatten2DFeatures :363-378), the
+    DTW (alignWithDTW :129-148) on the full rows, and alignWithHybrid (:308-337) with Go's result
+    aliasing (F8): alignWithCrossCorrelation and alignWithDTW both write into and return the SAME
+    *AlignmentResult, so after the DTW the "correlation" confidence and similarity being blended
+    are the DTW's own: Confidence = 0.6 c + 0.4 c, Similarity = 0.7 s + 0.3 s (float64, in that
+    order); Offset / AlignmentQuality / Stability are the DTW's, NoiseLevel stays the
+    correlation's (alignWithDTW never writes it).  The DTW is dtw_full (the same cells and
+    operation order as dtw(), stripe wavefront over `dtw_threads` threads)."""
+    q, r = _f64(query), _f64(reference)
+    if q.ndim == 1:
+        q = q[:, None]
+    if r.ndim == 1:
+        r = r[:, None]
+    if len(q) == 0 or len(r) == 0:
+        raise ValueError("empty feature sequences provided")
+    if method not in (ALIGN_DTW, ALIGN_XCORR, ALIGN_HYBRID):
+        raise ValueError(f"unsupported alignment method: {method}")
+    res = {"method": method, "query_length": len(q), "reference_length": len(r), "sample_rate": sample_rate,
+           "offset": 0, "offset_seconds": 0.0, "confidence": 0.0, "similarity": 0.0, "alignment_quality": 0.0,
+           "noise_level": 0.0, "stability": 0.0, "dtw_ran": 0}
+    if method in (ALIGN_XCORR, ALIGN_HYBRID):
+        corr, met = ncc(np.ascontiguousarray(q[:, 0]), np.ascontiguousarray(r[:, 0]), max_lag)
+        m = align_xcorr_metrics(met, hop, sample_rate, max_lag)
+        res.update(offset=int(m["offset"]), offset_seconds=m["offset_seconds"], similarity=m["similarity"],
+                   confidence=m["confidence"], alignment_quality=m["quality"], noise_level=m["noise_level"])
+        res["correlations"] = corr
+        res.update(met)
+        if method == ALIGN_XCORR or res["confidence"] > 0.7:
+            return res
+    d = dtw_full(q, r, nthreads=dtw_threads)
+    s = align_dtw_metrics(d, len(q), len(r), sample_rate)
+    res.update(offset=int(s["offset"]), offset_seconds=s["offset_seconds"], alignment_quality=s["quality"],
+               stability=s["stability"], dtw_ran=1, dtw_distance=d["distance"], dtw_path_query=d["path_q"],
+               dtw_path_reference=d["path_r"], dtw_path_cost=d["path_cost"])
+    if method == ALIGN_DTW:
+        res.update(confidence=s["confidence"], similarity=s["similarity"])
+    else:
+        c, sm = s["confidence"], s["similarity"]
+        res.update(confidence=0.6 * c + 0.4 * c, similarity=0.7 * sm + 0.3 * sm)
+    return res
+
+
+def analyzer_energy_features(pcm, window, hop):
+    """AlignmentAnalyzer.extractEnergyFeatures (stats/alignment.go:341-361): numFrames = (len - W)
+    / H + 1 with Go's truncating division, frame i = pcm[i H : min(i H + W, len)], RMS over its
+    own length."""
+    x = _f64(pcm)
+    nf = _go_div(len(x) - window, hop) + 1
+    if nf < 0:
+        raise GoPanic("runtime error: makeslice: len out of range")
+    if nf == 0:
+        return np.zeros(0)
+    if len(x) >= window:
+        return short_time_energy(x, window, hop)[:nf]
+    assert nf == 1 and len(x) > 0
+    return short_time_energy(x, len(x), hop)          # one frame over the whole (short) signal
+
+
+def align_audio_reference(q_pcm, r_pcm, sample_rate, method, max_lag, hop, window):
+    """AlignmentAnalyzer.AlignAudio (stats/alignment.go:108-126)."""
+    qe, re_ = analyzer_energy_features(q_pcm, window, hop), analyzer_energy_features(r_pcm, window, hop)
+    return analyzer_align_reference(qe[:, None], re_[:, None], sample_rate, method, max_lag, hop)
+
+
+def align_audio_files_reference(q_pcm, r_pcm, sample_rate, feature_sample_rate, hop, window, max_lag_seconds):
+    """AlignmentExtractor.AlignAudioFiles (extractors/alignment.go:489-553) with the extractor of
+    NewAlignmentExtractorWithMaxLag (:99-136): ShortTimeEnergy of both streams (energy.go:25-50),
+    then the Hybrid AlignFeatures at maxLagFrames = int(maxLagSeconds * SampleRate) / HopSize."""
+    mlf = _go_div(int(max_lag_seconds * feature_sample_rate), hop)
+    qe, re_ = short_time_energy(q_pcm, window, hop), short_time_energy(r_pcm, window, hop)
+    try:
+        res = analyzer_align_reference(qe[:, None], re_[:, None], sample_rate, ALIGN_HYBRID, mlf, hop)
+    except ValueError as e:
+        raise ValueError(f"alignment failed: {e}") from None
+    res.update(temporal_offset=res["offset_seconds"], offset_confidence=res["confidence"],
+               alignment_similarity=res["similarity"], feature_similarity_energy=res["similarity"],
+               query_length_seconds=len(q_pcm) / sample_rate, reference_length_seconds=len(r_pcm) / sample_rate,
+               time_stretch=0.0, max_lag_frames=mlf)
+    return res
+
+
 def alignment_consistency_reference(query, reference, sample_rate, method, max_lag, hop, num_trials=5):
     """AnalyzeAlignmentConsistency (stats/alignment.go:709-735) + calculateOffsetStats (:751-800).
     Every trial aligns the same deterministic perturbation, run here trial by trial as Go does."""

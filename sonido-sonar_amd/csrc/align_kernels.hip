@@ -17,6 +17,9 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include <cstdio>
+#include <mutex>
+
 #include "kernels.h"
 
 #pragma clang fp contract(off)
@@ -1970,6 +1973,17 @@ int launch_dtw_batch(const DtwArgs* hargs, const DtwArgs* dargs, const int64_t* 
   // fit; 3 x 54.7 KB do not): the 18 registers per wave it gives up leave room on each SIMD for
   // the other worker streams' short kernels beside two band blocks.  C5 2,143-2,162 ->
   // 2,216-2,235 pairs/s (Kernel 6, "Register budget of the batched instance")
+  // the 2-blocks-per-CU cap above rests on LDS arithmetic only (static LDS + DTW_BATCH_PAD > 160 KB / 3):
+  // checked once per process against the runtime's occupancy calculator, so a change of DTW_DQ or of
+  // the static LDS that lets a third block fit (measured slower) does not go unnoticed
+  static std::once_flag occ_once;
+  std::call_once(occ_once, [] {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, dtw_band_kernel<12, true, false, true>,
+                                                     64 * DTW_WAVES, DTW_BATCH_PAD) == hipSuccess && blocks != 2)
+      std::fprintf(stderr, "sonar: batched dtw_band_kernel fits %d blocks per CU (sized for 2: DTW_BATCH_PAD)\n",
+                   blocks);
+  });
   hipLaunchKernelGGL((dtw_band_kernel<12, true, false, true>), dim3((unsigned)total_bands), dim3(64 * DTW_WAVES),
                      DTW_BATCH_PAD, s, none, bt);
   if (dtw_serial_walk()) {

@@ -8,6 +8,7 @@
 #include "kernels.h"
 
 #include <map>
+#include <memory>
 #include <string>
 #include <utility>
 #include <vector>
@@ -73,20 +74,42 @@ struct sonar_ctx {
   hipEvent_t fpb_ev = nullptr;
 };
 
+// Named float64 arrays + scalars.  An array either owns its values (v) or points into a block the
+// result holds a reference to (ext + owners: pinned host memory the device copied into directly,
+// sonar::detail::pinned_block), so large outputs reach the caller without a host copy.
 struct sonar_result {
   struct Arr {
     std::string name;
     std::vector<double> v;
     int64_t rows = 0, cols = 0;
+    const double* ext = nullptr;
+    const double* data() const { return ext ? ext : v.data(); }
   };
   std::vector<Arr> arrays;
-  void put(const std::string& name, std::vector<double> v, int64_t rows, int64_t cols) {
+  std::vector<std::shared_ptr<void>> owners;
+  Arr& slot(const std::string& name) {
     for (auto& a : arrays)
-      if (a.name == name) { a.v = std::move(v); a.rows = rows; a.cols = cols; return; }
-    arrays.push_back({name, std::move(v), rows, cols});
+      if (a.name == name) return a;
+    arrays.push_back({name, {}, 0, 0, nullptr});
+    return arrays.back();
   }
+  void put(const std::string& name, std::vector<double> v, int64_t rows, int64_t cols) {
+    Arr& a = slot(name);
+    a.v = std::move(v); a.rows = rows; a.cols = cols; a.ext = nullptr;
+  }
+  // rows x cols values at p, inside a block this result holds (see hold)
+  void put_ext(const std::string& name, const double* p, int64_t rows, int64_t cols) {
+    Arr& a = slot(name);
+    a.v.clear(); a.rows = rows; a.cols = cols; a.ext = p;
+  }
+  void hold(std::shared_ptr<void> block) { owners.push_back(std::move(block)); }
   void scalar(const std::string& name, double x) { put(name, {x}, 1, 1); }
   void vec(const std::string& name, const std::vector<double>& v) { put(name, v, (int64_t)v.size(), 1); }
+  double get(const std::string& name, double dflt = 0.0) const {
+    for (auto& a : arrays)
+      if (a.name == name && a.rows * a.cols > 0) return a.data()[0];
+    return dflt;
+  }
 };
 
 namespace sonar {
@@ -96,6 +119,12 @@ void* dbuf(sonar_ctx* c, const std::string& name, size_t bytes);
 // frees every cached device / pinned host buffer of c (sonar_trim; the batch path's NOMEM retry)
 void trim_buffers(sonar_ctx* c);
 void* hbuf(sonar_ctx* c, const std::string& name, size_t bytes);
+// A block of `bytes` of pinned host memory from a process-wide pool (hipHostMalloc'd once, reused):
+// device-to-host copies land in it at DMA speed and result arrays can point into it; the block
+// returns to the pool when the last shared_ptr to it goes.  Null on allocation failure.
+std::shared_ptr<void> pinned_block(size_t bytes);
+// frees the pool's idle blocks (sonar_trim)
+void pinned_pool_trim();
 // chroma tables of frame size fs at sample rate sr, built once per context (sonar_api.cpp); null on
 // allocation failure
 const sonar_ctx::ChromaT* chroma_tables_for(sonar_ctx* c, int fs, int sr);

@@ -206,26 +206,54 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   if (fc->enable_speech_features && sonar::launch_tilt(dy, n, Fp, dtilt, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "tilt launch failed");
 
-  std::vector<double> mfcc, spec, zcr, energy, praw, craw, part, env, loud, tilt, head;
-  if (d2h(c, mfcc, dmfcc, fc->enable_mfcc ? Fz * nm : 0) || d2h(c, spec, dspec, Fz * 9) || d2h(c, zcr, dzcr, Fz) ||
-      d2h(c, energy, den, (size_t)Fe) || d2h(c, praw, dpit, (size_t)Fp) || d2h(c, craw, dcon, (size_t)Fp) ||
-      d2h(c, part, dpart, SB * 4) || d2h(c, env, denv, (size_t)std::max<int64_t>(Fenv, 0)) ||
-      d2h(c, loud, dld, (size_t)Fl) || d2h(c, tilt, dtilt, fc->enable_speech_features ? (size_t)Fp : 0) ||
-      d2h(c, head, dy, (size_t)std::min<int64_t>(n, 1024)))
+  // ---- results back: ONE pinned block from the pool, every array copied into it by DMA; the
+  // result's large arrays point into the block (no host copy, no page faults on fresh vectors) ----
+  const size_t Fe_z = (size_t)std::max<int64_t>(Fe, 0), Fp_z = (size_t)std::max<int64_t>(Fp, 0);
+  const size_t Fenv_z = (size_t)std::max<int64_t>(Fenv, 0), Fl_z = (size_t)std::max<int64_t>(Fl, 0);
+  const bool lohi_copy = (int64_t)Fe_z > F;                       // Go pads the ratios past the spectrogram
+  size_t off = 0;
+  auto take = [&](size_t cnt) { const size_t o = off; off += (cnt + 7) & ~size_t(7); return o; };
+  const size_t o_mfcc = take(fc->enable_mfcc ? Fz * nm : 0), o_spec = take(Fz * 9), o_zcr = take(Fz);
+  const size_t o_en = take(Fe_z), o_ent = take(Fe_z), o_praw = take(Fp_z), o_craw = take(Fp_z);
+  const size_t o_part = take(SB * 4), o_env = take(Fenv_z), o_loud = take(Fl_z);
+  const size_t o_tilt = take(fc->enable_speech_features ? Fp_z : 0), o_head = take((size_t)std::min<int64_t>(n, 1024));
+  const size_t o_trk = take(6 * Fp_z), o_lohi = take(lohi_copy ? 2 * Fe_z : 0);
+  std::shared_ptr<void> blk = sonar::detail::pinned_block(off * 8);
+  if (!blk) return fail(c, SONAR_ERR_NOMEM, "pinned host allocation failed (results)");
+  double* B = (double*)blk.get();
+  double* dent = (double*)dbuf(c, "sx.ent", std::max<size_t>(Fe_z, 1) * 8);
+  if (!dent) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (entropy)");
+  if (Fe_z && sonar::launch_energy_entropy(den, (int64_t)Fe_z, dent, s) != 0)
+    return fail(c, SONAR_ERR_DEVICE, "entropy launch failed");
+  auto d2h = [&](size_t o, const void* d, size_t cnt) -> int {
+    if (cnt) HIP_TRY(c, hipMemcpyAsync(B + o, d, cnt * 8, hipMemcpyDeviceToHost, s));
+    return SONAR_OK;
+  };
+  if (d2h(o_mfcc, dmfcc, fc->enable_mfcc ? Fz * nm : 0) || d2h(o_spec, dspec, Fz * 9) || d2h(o_zcr, dzcr, Fz) ||
+      d2h(o_en, den, Fe_z) || d2h(o_ent, dent, Fe_z) || d2h(o_praw, dpit, Fp_z) || d2h(o_craw, dcon, Fp_z) ||
+      d2h(o_part, dpart, SB * 4) || d2h(o_env, denv, Fenv_z) || d2h(o_loud, dld, Fl_z) ||
+      d2h(o_tilt, dtilt, fc->enable_speech_features ? Fp_z : 0) ||
+      d2h(o_head, dy, (size_t)std::min<int64_t>(n, 1024)))
     return SONAR_ERR_DEVICE;
   HIP_TRY(c, hipStreamSynchronize(s));
+  const double* energy = B + o_en;
+  const double* spec = B + o_spec;
+  const double* praw = B + o_praw;
+  const double* craw = B + o_craw;
+  const double* part = B + o_part;
 
   auto* res = new sonar_result();
-  if (fc->enable_mfcc) res->put("mfcc", std::move(mfcc), F, nm);
+  res->hold(blk);
+  if (fc->enable_mfcc) res->put_ext("mfcc", B + o_mfcc, F, nm);
   static const char* spec_names[9] = {"spectral_centroid", "spectral_rolloff", "spectral_bandwidth",
                                       "spectral_flatness", "spectral_crest", "spectral_slope", "spectral_flux",
                                       "", ""};
   for (int d = 0; d < 7; d++) {
     const int64_t cnt = d == 6 ? (F > 1 ? F - 1 : 0) : F;
     if (d == 6 && F <= 1) continue;                               // flux only when TimeFrames > 1 (:362-365)
-    res->put(spec_names[d], std::vector<double>(spec.begin() + d * Fz, spec.begin() + d * Fz + cnt), cnt, 1);
+    res->put_ext(spec_names[d], spec + d * Fz, cnt, 1);
   }
-  res->put("zero_crossing_rate", std::move(zcr), (int64_t)Fz, 1);
+  res->put_ext("zero_crossing_rate", B + o_zcr, (int64_t)Fz, 1);
 
   // whole-signal stats: partials reduced in block order
   double peak = 0, sabs = 0, ssq = 0, cross = 0;
@@ -240,7 +268,7 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   double thr10 = 0.0;                                             // percentile10_threshold(energy), once
   bool have_thr10 = false;
   auto energy_thr10 = [&]() {
-    if (!have_thr10) { thr10 = percentile10_threshold(energy); have_thr10 = true; }
+    if (!have_thr10) { thr10 = percentile10_threshold(std::vector<double>(energy, energy + Fe_z)); have_thr10 = true; }
     return thr10;
   };
   if (fc->enable_speech_features) {
@@ -249,7 +277,7 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     const double z = n <= 1 ? 0.0 : cross / (double)(n - 1);
     if (sp && (z < 0.01 || z > 0.3)) sp = false;
     if (sp && std::sqrt(ssq / (double)n) < 0.001) sp = false;
-    if (sp) sp = check_periodicity(head);
+    if (sp) sp = check_periodicity(std::vector<double>(B + o_head, B + o_head + std::min<int64_t>(n, 1024)));
     is_speech = sp;
     res->scalar("is_speech", sp ? 1.0 : 0.0);
     // AnalyzeSpeech -> FormantAnalyzer.AnalyzeFormants(preprocessed PCM) (speech_analysis.go:70-74,
@@ -260,15 +288,17 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
       const int W = csr >= 16000 ? 2048 : 1024, p = 12 + csr / 1000;
       sonar_formant_frame* dfm = (sonar_formant_frame*)dbuf(c, "sx.formant", sizeof(sonar_formant_frame));
       double* dham = (double*)dbuf(c, "sx.ham", W * 8);
-      if (!dfm || !dham) return fail(c, SONAR_ERR_NOMEM, "device allocation failed");
+      if (!dfm || !dham) { delete res; return fail(c, SONAR_ERR_NOMEM, "device allocation failed"); }
       std::vector<double> ham(W);
       for (int i = 0; i < W; i++) ham[i] = 0.54 - 0.46 * std::cos(2.0 * M_PI * (double)i / (double)(W - 1));
-      HIP_TRY(c, hipMemcpyAsync(dham, ham.data(), W * 8, hipMemcpyHostToDevice, s));
-      if (p > 64 || sonar::launch_formants(dy, 1, 0, W, p, csr, n >= W ? 1 : 0, dham, dfm, nullptr, nullptr, s) != 0)
-        return fail(c, SONAR_ERR_DEVICE, "formant launch failed");
       sonar_formant_frame fm;
-      HIP_TRY(c, hipMemcpyAsync(&fm, dfm, sizeof(fm), hipMemcpyDeviceToHost, s));
-      HIP_TRY(c, hipStreamSynchronize(s));
+      if (hipMemcpyAsync(dham, ham.data(), W * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+          p > 64 || sonar::launch_formants(dy, 1, 0, W, p, csr, n >= W ? 1 : 0, dham, dfm, nullptr, nullptr, s) != 0 ||
+          hipMemcpyAsync(&fm, dfm, sizeof(fm), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
+        delete res;
+        return fail(c, SONAR_ERR_DEVICE, "formant launch failed");
+      }
       if (fm.status == 0) {
         formants.assign(fm.frequency, fm.frequency + fm.n_formants);
         vtl = fm.vocal_tract_length;
@@ -291,11 +321,11 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
       // estimateSpeechRate (speech.go:779-797) on the energy frames of the pre-emphasised PCM
       const double dur = (double)n / (double)csr;
       double sil = 0.0;
-      if (!energy.empty()) {
+      if (Fe_z) {
         const double thr = energy_thr10();
         int64_t k = 0;
-        for (double e : energy) if (e <= thr) k++;
-        sil = (double)k / (double)energy.size();
+        for (size_t i = 0; i < Fe_z; i++) if (energy[i] <= thr) k++;
+        sil = (double)k / (double)Fe_z;
       }
       const double speech_time = dur * (1.0 - sil);
       res->scalar("speech_rate", speech_time > 0 ? 4.0 * speech_time / dur : 3.0);
@@ -303,49 +333,49 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
       res->scalar("speech_rate", 0.0);
     }
     if (sp) {
-      std::vector<double> voicing(Fp);                             // extractVoicingProbability (:530-550)
+      std::vector<double> voicing(Fp_z);                           // extractVoicingProbability (:530-550)
       for (int64_t i = 0; i < Fp; i++) {
         double p = praw[i], q = craw[i], v = 0;
         if (i * 512 + 1024 <= n) { tracker.step(p, q, v); voicing[i] = v; }
       }
       res->vec("voicing_probability", voicing);
-      res->vec("spectral_tilt", tilt);
+      res->put_ext("spectral_tilt", B + o_tilt, (int64_t)Fp_z, 1);
       // extractPauseDurations (:587-637)
       std::vector<double> pauses;
-      if (!energy.empty()) {
+      if (Fe_z) {
         const double thr = energy_thr10();
         const double fts = (double)fc->hop_size / (double)csr;
         bool in = false; int64_t st = 0;
-        for (int64_t i = 0; i < (int64_t)energy.size(); i++) {
+        for (int64_t i = 0; i < (int64_t)Fe_z; i++) {
           if (energy[i] <= thr) { if (!in) { in = true; st = i; } }
           else if (in) { const double d = (double)(i - st) * fts; if (d > 0.1) pauses.push_back(d); in = false; }
         }
-        if (in) { const double d = (double)((int64_t)energy.size() - st) * fts; if (d > 0.1) pauses.push_back(d); }
+        if (in) { const double d = (double)((int64_t)Fe_z - st) * fts; if (d > 0.1) pauses.push_back(d); }
       }
       res->vec("pause_duration", pauses);
     }
   }
 
   // ---- temporal features (extractTemporalFeatures :370-409) ---------------------
-  const double lrange = csr > 0 ? sonar::host::loudness_range_from_rms(loud) : 0.0;
+  const double lrange = csr > 0 ? sonar::host::loudness_range_from_rms(std::vector<double>(B + o_loud, B + o_loud + Fl_z)) : 0.0;
   if (fc->enable_temporal_features) {
-    res->vec("rms_energy", energy);
+    res->put_ext("rms_energy", energy, (int64_t)Fe_z, 1);
     res->scalar("dynamic_range", lrange);
     double sil = 0.0;
-    if (!energy.empty()) {                                        // calculateSilenceRatio (:639-665)
+    if (Fe_z) {                                                   // calculateSilenceRatio (:639-665)
       const double thr = energy_thr10();
       int64_t k = 0;
-      for (double e : energy) if (e <= thr) k++;
-      sil = (double)k / (double)energy.size();
+      for (size_t i = 0; i < Fe_z; i++) if (energy[i] <= thr) k++;
+      sil = (double)k / (double)Fe_z;
     }
     res->scalar("silence_ratio", sil);
     res->scalar("peak_amplitude", peak);
     res->scalar("average_amplitude", n > 0 ? sabs / (double)n : 0.0);
     // detectOnsets (:668-693) + calculateAdaptiveThreshold (:695-716)
     std::vector<int64_t> onsets;
-    if (energy.size() >= 3) {
-      std::vector<double> der(energy.size() - 1);
-      for (size_t i = 0; i + 1 < energy.size(); i++) der[i] = energy[i + 1] - energy[i];
+    if (Fe_z >= 3) {
+      std::vector<double> der(Fe_z - 1);
+      for (size_t i = 0; i + 1 < Fe_z; i++) der[i] = energy[i + 1] - energy[i];
       double sum = 0; for (double v : der) sum += v;
       const double mean = sum / (double)der.size();
       double var = 0; for (double v : der) { const double d = v - mean; var += d * d; }
@@ -365,44 +395,53 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
       if (att[i] > 0.1) att[i] = 0.1;
     }
     res->vec("attack_time", att);
-    res->vec("envelope_shape", env);
+    res->put_ext("envelope_shape", B + o_env, (int64_t)Fenv_z, 1);
   }
 
   // ---- energy features (extractEnergyFeatures :411-461) -------------------------
-  res->vec("short_time_energy", energy);
-  res->scalar("energy_variance", sonar::host::energy_variance(energy));
+  res->put_ext("short_time_energy", energy, (int64_t)Fe_z, 1);
+  res->scalar("energy_variance", sonar::host::energy_variance(energy, Fe_z));
   res->scalar("loudness_range", lrange);
-  {
-    const size_t ne = energy.size();
-    std::vector<double> ent(ne, 0.0), lo(ne, 0.0), hi(ne, 0.0);
-    for (size_t i = 0; i < ne; i++) {
-      if (energy[i] > 0) ent[i] = -energy[i] * std::log(energy[i] + 1e-10);
-      if ((int64_t)i < F) { lo[i] = spec[7 * Fz + i]; hi[i] = spec[8 * Fz + i]; }
+  res->put_ext("energy_entropy", B + o_ent, (int64_t)Fe_z, 1);
+  if (!lohi_copy) {                                               // every energy frame has a spectrogram row
+    res->put_ext("low_energy_ratio", spec + 7 * Fz, (int64_t)Fe_z, 1);
+    res->put_ext("high_energy_ratio", spec + 8 * Fz, (int64_t)Fe_z, 1);
+  } else {
+    double* lo = B + o_lohi;
+    double* hi = lo + Fe_z;
+    for (size_t i = 0; i < Fe_z; i++) {
+      lo[i] = (int64_t)i < F ? spec[7 * Fz + i] : 0.0;
+      hi[i] = (int64_t)i < F ? spec[8 * Fz + i] : 0.0;
     }
-    res->vec("energy_entropy", ent);
-    res->vec("low_energy_ratio", lo);
-    res->vec("high_energy_ratio", hi);
+    res->put_ext("low_energy_ratio", lo, (int64_t)Fe_z, 1);
+    res->put_ext("high_energy_ratio", hi, (int64_t)Fe_z, 1);
   }
 
   // ---- harmonic features (extractHarmonicFeatures :464-509) --------------------
   {
-    std::vector<double> pe(Fp, 0.0), pc(Fp, 0.0), vs(Fp, 0.0), hr(Fp), ih(Fp), tcen(Fp, 0.0);
+    double* pe = B + o_trk;
+    double* pc = pe + Fp_z;
+    double* vs = pc + Fp_z;
+    double* hr = vs + Fp_z;
+    double* ih = hr + Fp_z;
+    double* tcen = ih + Fp_z;
     for (int64_t i = 0; i < Fp; i++) {
+      double p = 0.0, q = 0.0, v = 0.0;
       if (i * 512 + 1024 <= n) {                                  // DetectPitch size check (pitch_detection.go:226)
-        double p = praw[i], q = craw[i], v = 0;
+        p = praw[i]; q = craw[i];
         tracker.step(p, q, v);
-        pe[i] = p; pc[i] = q; vs[i] = v;
       }
-      hr[i] = vs[i] * 10.0;
-      ih[i] = 1.0 - vs[i];
-      if (pe[i] > 0) tcen[i] = pe[i];
+      pe[i] = p; pc[i] = q; vs[i] = v;
+      hr[i] = v * 10.0;
+      ih[i] = 1.0 - v;
+      tcen[i] = p > 0 ? p : 0.0;
     }
-    res->vec("pitch_estimate", pe);
-    res->vec("pitch_confidence", pc);
-    res->vec("voicing_strength", vs);
-    res->vec("harmonic_ratio", hr);
-    res->vec("inharmonicity_ratio", ih);
-    res->vec("tonal_centroid", tcen);
+    res->put_ext("pitch_estimate", pe, (int64_t)Fp_z, 1);
+    res->put_ext("pitch_confidence", pc, (int64_t)Fp_z, 1);
+    res->put_ext("voicing_strength", vs, (int64_t)Fp_z, 1);
+    res->put_ext("harmonic_ratio", hr, (int64_t)Fp_z, 1);
+    res->put_ext("inharmonicity_ratio", ih, (int64_t)Fp_z, 1);
+    res->put_ext("tonal_centroid", tcen, (int64_t)Fp_z, 1);
   }
   (void)is_speech;
   *out = res;

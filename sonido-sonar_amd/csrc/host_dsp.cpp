@@ -183,20 +183,24 @@ std::vector<int> chroma_map(int fs, int sr) {
 }
 
 static double median_positive(const double* v, int n) {           // calculateMedian :975-1004
-  std::vector<double> tmp;
-  for (int i = 0; i < n; i++) if (v[i] > 0) tmp.push_back(v[i]);
-  if (tmp.empty()) return 0.0;
-  std::sort(tmp.begin(), tmp.end());
-  const size_t m = tmp.size();
+  double tmp[8];                                                  // n <= 5
+  int m = 0;
+  for (int i = 0; i < n; i++)
+    if (v[i] > 0) {                                               // insertion sort of the positives
+      int j = m++;
+      while (j > 0 && tmp[j - 1] > v[i]) { tmp[j] = tmp[j - 1]; --j; }
+      tmp[j] = v[i];
+    }
+  if (m == 0) return 0.0;
   return (m % 2 == 0) ? (tmp[m / 2 - 1] + tmp[m / 2]) / 2.0 : tmp[m / 2];
 }
 
 void YinTracker::step(double& pitch, double& conf, double& voicing) {
   double p = pitch, c = conf, v = conf;
-  if (p != 0.0 && !hist.empty()) {                                // applyOctaveCorrection :789-827
-    const int cnt = (int)std::min<size_t>(hist.size(), 5);
+  if (p != 0.0 && count > 0) {                                    // applyOctaveCorrection :789-827
+    const int cnt = std::min(count, 5);
     if (cnt >= 3) {
-      const double med = median_positive(hist.data() + hist.size() - cnt, cnt);
+      const double med = median_positive(hist + count - cnt, cnt);
       const double ratios[4] = {0.5, 2.0, 1.0 / 3.0, 3.0};
       for (double r : ratios) {
         const double ex = med * r;
@@ -208,11 +212,15 @@ void YinTracker::step(double& pitch, double& conf, double& voicing) {
     }
   }
   if (c < 0.5) { p = 0; c = 0; v = 0; }                          // MinConfidence :781-785
-  hist.push_back(p);                                              // updateTemporalTracking :876-899
-  if (hist.size() > 20) hist.erase(hist.begin());
-  if (hist.size() > 1) {                                          // applyTemporalSmoothing :903-921
-    const int cnt = (int)std::min<size_t>(hist.size(), 3);
-    if (cnt >= 3) p = median_positive(hist.data() + hist.size() - cnt, cnt);
+  if (count == 20) {                                              // updateTemporalTracking :876-899
+    for (int i = 1; i < 20; i++) hist[i - 1] = hist[i];
+    hist[19] = p;
+  } else {
+    hist[count++] = p;
+  }
+  if (count > 1) {                                                // applyTemporalSmoothing :903-921
+    const int cnt = std::min(count, 3);
+    if (cnt >= 3) p = median_positive(hist + count - cnt, cnt);
     else p = 0.3 * p + (1 - 0.3) * prev;
   }
   prev = p;
@@ -391,14 +399,14 @@ AlignScores dtw_scores(const int32_t* pq, const int32_t* pr, const double* pc, i
   return dtw_scores(path_sums(pq, pr, pc, P), nq, nr, dist, sr);
 }
 
-double energy_variance(const std::vector<double>& e) {           // energy.go:96-117
-  if (e.size() < 2) return 0.0;
+double energy_variance(const double* e, size_t n) {               // energy.go:96-117
+  if (n < 2) return 0.0;
   double mean = 0.0;
-  for (double v : e) mean += v;
-  mean /= (double)e.size();
+  for (size_t i = 0; i < n; i++) mean += e[i];
+  mean /= (double)n;
   double var = 0.0;
-  for (double v : e) { const double d = v - mean; var += d * d; }
-  return var / (double)(e.size() - 1);
+  for (size_t i = 0; i < n; i++) { const double d = e[i] - mean; var += d * d; }
+  return var / (double)(n - 1);
 }
 
 double loudness_range_from_rms(std::vector<double> v) {           // energy.go:145-205

@@ -36,8 +36,11 @@ void balance_groups(const MfccTables& t, int groups, std::vector<int>& off, std:
 std::vector<int> chroma_map(int fs, int sample_rate);
 
 // PitchDetector post-processing + temporal tracking (pitch_detection.go:767-921)
+// The history is Go's pitchHistory capped at 20 entries (only its last 5 are ever read), kept in a
+// fixed array: one step allocates nothing (a 1-hour call runs 310,000 steps).
 struct YinTracker {
-  std::vector<double> hist;
+  double hist[20] = {0};
+  int count = 0;                   // entries held (<= 20), oldest first
   double prev = 0.0;
   void step(double& pitch, double& conf, double& voicing);
 };
@@ -50,8 +53,9 @@ struct NccMetrics {
 // The O(lags) part of those metrics: findPeak's index and value, calculateSNR's noise sum and count
 // (|i - peak| > 5), findSecondPeak's value, calculatePeakToSidelobe's sidelobe maximum (|i - peak|
 // > 10) and calculateSharpness's second difference (0 at the ends).  corr_sums runs Go's loops; the
-// batched pair path computes the same on the device (pair_score_kernel, align_kernels.hip), where
-// only the noise sum is reassociated.  Plain data, shared with the kernels.
+// batched pair path computes the same on the device (pair_score_kernel, align_kernels.hip), every
+// sum in Go's index order with masked terms added as exact zeros, so the two are bit-identical
+// (test_device_scorer_equals_host_scorer).  Plain data, shared with the kernels.
 struct CorrSums {
   int64_t num_lags = 0, peak_index = 0, noise_count = 0;
   double peak = 0, noise_sum = 0, second_peak = 0, max_sidelobe = 0, sharpness = 0;
@@ -81,7 +85,7 @@ AlignScores dtw_scores(const int32_t* pq, const int32_t* pr, const double* pc, i
 AlignScores dtw_scores(const PathSums& s, int64_t nq, int64_t nr, double distance, int sample_rate);
 
 // Energy helpers used by extractEnergyFeatures (algorithms/temporal/energy.go:96-178)
-double energy_variance(const std::vector<double>& e);
+double energy_variance(const double* e, size_t n);
 // ComputeLoudnessRange tail: RMS of 400 ms / 100 ms frames -> LU -> 10th..95th percentile range
 double loudness_range_from_rms(std::vector<double> rms);
 

@@ -54,6 +54,7 @@ struct FpParams {
   int out_f64;
   void* out_mfcc;
   void* out_mag;
+  int mag_f64;          // element type of out_mag (the SPEC scratch rows are float64 whatever out_f64 says)
   void* out_spec[9];    // centroid, rolloff, bandwidth, flatness, crest, slope, flux(F-1), low, high
   void* out_cplx;       // F x K x 2 (re, im) straight from the FFT's real split (nullable)
   void* out_phase;      // F x K atan2(im, re) (nullable)
@@ -66,6 +67,21 @@ struct FpParams {
 };
 
 int launch_fingerprint(const FpParams& p, int precision_f64, hipStream_t s);
+
+// The per-frame spectral descriptors of SpeechFeatureExtractor.extractSpectralFeatures
+// (extractors/speech.go:320-367, :438-458) from float64 |X| rows already in HBM (the fused kernel's
+// magnitude output, or the DFT path's scratch): spec_rows_kernel (fp_kernel.hip), one wave per
+// frame at a time over a contiguous frame run, every lane a contiguous bin chunk.
+struct SpecParams {
+  const double* mag;    // [F][K] |X| rows
+  int64_t F;            // frames
+  int K;                // bins per row (W/2 + 1)
+  int sample_rate;
+  int64_t frames_per_wave;
+  int out_f64;
+  void* out_spec[9];    // centroid, rolloff, bandwidth, flatness, crest, slope, flux(F-1), low, high
+};
+int launch_spec_rows(const SpecParams& p, hipStream_t s);
 
 // Headline fused kernel (mfcc_pair.hip): float32, W = 1024, MFCC output only.
 // One wave transforms two consecutive frames as one 1024-point complex FFT.
@@ -123,6 +139,8 @@ int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H,
                void* out, int out_f64, hipStream_t s);
 int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H, double alpha,
                   void* out, int out_f64, hipStream_t s);
+// EnergyEntropy (extractors/speech.go:429-433) of the short-time energy frames (misc_kernels.hip)
+int launch_energy_entropy(const double* e, int64_t n, double* out, hipStream_t s);
 // YIN raw per-frame results (misc_kernels.hip); frames start at 0, hop, 2 hop, ...
 int launch_yin(const double* pcm, int64_t n, int64_t frames, int64_t hop, int sample_rate, double* pitch,
                double* conf, int32_t* tau, hipStream_t s);

@@ -11,6 +11,9 @@
 //
 // Decision-bearing arithmetic (sign tests, sums feeding thresholds) is float64
 // with explicit _rn intrinsics: no FMA contraction, Go's evaluation order.
+#include <algorithm>
+#include <atomic>
+
 #include "kernels.h"
 
 #pragma clang fp contract(off)
@@ -115,6 +118,9 @@ __global__ __launch_bounds__(256) void energy_wave_kernel(const void* pcm, int p
   const int64_t s = (f0 + lane) * (int64_t)H;                    // this lane's frame start
   double prev = (s > 0 && s - 1 < n) ? pre_x(pcm, pcm_f64, s - 1) : 0.0;
   double ss = 0.0;
+  // alpha 0 (the raw-PCM RMS of ShortTimeEnergy callers): no pre-emphasis at all, so a non-finite
+  // previous sample cannot turn 0 * x[n-1] into NaN
+  const bool pre = alpha != 0.0;
   for (int k0 = 0; k0 < W; k0 += kEnP) {
     {
       double nx[8];
@@ -133,13 +139,13 @@ __global__ __launch_bounds__(256) void energy_wave_kernel(const void* pcm, int p
     if (k0 + kEnP <= W) {
 #pragma unroll
       for (int j = 0; j < kEnP; ++j) {
-        const double y = __dsub_rn(cur[j], __dmul_rn(alpha, prev));
+        const double y = pre ? __dsub_rn(cur[j], __dmul_rn(alpha, prev)) : cur[j];
         prev = cur[j];
         ss = __dadd_rn(ss, __dmul_rn(y, y));
       }
     } else {
       for (int j = 0; j < W - k0; ++j) {
-        const double y = __dsub_rn(cur[j], __dmul_rn(alpha, prev));
+        const double y = pre ? __dsub_rn(cur[j], __dmul_rn(alpha, prev)) : cur[j];
         prev = cur[j];
         ss = __dadd_rn(ss, __dmul_rn(y, y));
       }
@@ -149,60 +155,120 @@ __global__ __launch_bounds__(256) void energy_wave_kernel(const void* pcm, int p
 }
 
 // YIN per 1024-sample frame (hop 512 for extractHarmonicFeatures, 256 for the voice-quality
-// period scan): one block of 256 threads per frame
+// period scan), PitchDetector.detectPitchYin (pitch_detection.go:349-420) after preprocessFrame
+// (:282-314).  One wave per frame (round 6; rounds 1-5: a 256-thread block per frame, two tau per
+// thread reading both operands of every term from LDS, and one thread running the CMNDF with 1,022
+// dependent divisions: 23 ms per hour of 44.1 kHz audio).
+//  * difference function d(tau) = sum_j (x_j - x_{j+tau})^2, j < 512: lane l owns tau = 8 l + r,
+//    r < 8, eight independent chains in Go's j order (unfused: bit-exact).  The operands x_{j+tau}
+//    of a lane's eight chains slide by one per j, so they stay in a 16-register window refilled
+//    with 8 LDS reads per 8 j; x_j is an LDS broadcast.  8 x 8 terms = 192 f64 VALU per 16 LDS
+//    reads: the kernel is FP64-VALU-bound (3 ops per term, 2.4e11 per hour at hop 512).
+//  * CMNDF running sum (:368-372) is Go's sequential chain over tau = 1..511: a wave-uniform add
+//    chain fed by v_readlane, each lane keeping the partial sums of its own tau; then the two
+//    divisions per tau in parallel across lanes.
+//  * the first tau below the threshold that is a local minimum (:375-384) by a ballot, parabolic
+//    interpolation and the frequency gate (:391-417, 743-764) on uniform values.
 __constant__ double c_yin_win[1024];
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
 
 __global__ __launch_bounds__(256) void yin_kernel(const double* pcm, int64_t n, int64_t frames, int64_t hop, int sr,
                                                   double* pitch, double* conf, int32_t* tau_out) {
-  __shared__ double xw[1024];
-  __shared__ double diff[512];
-  __shared__ double cm[512];
-  const int64_t fi = blockIdx.x;
+  __shared__ double xs[4][1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t fi = (int64_t)blockIdx.x * 4 + w;
   if (fi >= frames) return;
   const int64_t s = fi * hop;
-  const bool full = (s + 1024 <= n);
-  if (!full) {   // DetectPitch rejects frames != WindowSize (pitch_detection.go:226)
-    if (threadIdx.x == 0) { pitch[fi] = 0; conf[fi] = 0; if (tau_out) tau_out[fi] = -2; }
+  if (s + 1024 > n) {   // DetectPitch rejects frames != WindowSize (pitch_detection.go:226)
+    if (lane == 0) { pitch[fi] = 0; conf[fi] = 0; if (tau_out) tau_out[fi] = -2; }
     return;
   }
-  for (int i = threadIdx.x; i < 1024; i += 256) {  // applyPreEmphasis :296-310, window :289-291
+  double* xw = xs[w];
+  for (int i = lane; i < 1024; i += 64) {  // applyPreEmphasis :300-314 (fresh per frame), window :292-294
     const double x = pcm[s + i];
     const double y = (i == 0) ? x : __dsub_rn(x, __dmul_rn(0.97, pcm[s + i - 1]));
     xw[i] = __dmul_rn(y, c_yin_win[i]);
   }
-  __syncthreads();
-  for (int tau = threadIdx.x; tau < 512; tau += 256) {  // difference function :353-362
-    double sum = 0.0;
-    for (int j = 0; j < 512; ++j) {
-      const double d = __dsub_rn(xw[j], xw[j + tau]);
-      sum = __dadd_rn(sum, __dmul_rn(d, d));
-    }
-    diff[tau] = sum;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    cm[0] = 1.0;                                        // CMNDF :365-371
-    double run = 0.0;
-    for (int tau = 1; tau < 512; ++tau) {
-      run = __dadd_rn(run, diff[tau]);
-      cm[tau] = __ddiv_rn(diff[tau], __ddiv_rn(run, (double)tau));
-    }
-    int mt = -1;                                        // first local minimum below 0.15 :374-383
-    for (int tau = 1; tau < 512; ++tau)
-      if (cm[tau] < 0.15 && tau + 1 < 512 && cm[tau] < cm[tau + 1]) { mt = tau; break; }
-    double p = 0.0, c = 0.0;
-    if (mt > 0) {
-      double period = (double)mt;                       // parabolicInterpolation :743-764
-      if (mt < 511) {
-        const double y1 = cm[mt - 1], y2 = cm[mt], y3 = cm[mt + 1];
-        const double a = __ddiv_rn(__dadd_rn(__dsub_rn(y1, __dmul_rn(2.0, y2)), y3), 2.0);
-        const double b = __ddiv_rn(__dsub_rn(y3, y1), 2.0);
-        if (a != 0.0) period = __dadd_rn((double)mt, __ddiv_rn(-b, __dmul_rn(2.0, a)));
+  wave_lds_sync();
+  const int t0 = 8 * lane;
+  double acc[8], win[16];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) { acc[r] = 0.0; win[r] = xw[t0 + r]; }
+  for (int jb = 0; jb < 512; jb += 8) {                  // difference function :353-362
+#pragma unroll
+    for (int r = 0; r < 8; ++r) win[8 + r] = xw[jb + t0 + 8 + r];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const double xj = xw[jb + jj];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const double d = __dsub_rn(xj, win[jj + r]);
+        acc[r] = __dadd_rn(acc[r], __dmul_rn(d, d));
       }
-      const double f = __ddiv_rn((double)sr, period);
-      const double cf = __dsub_rn(1.0, cm[mt]);
-      if (f >= 80.0 && f <= 1000.0) { p = f; c = cf; }
     }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) win[r] = win[8 + r];
+  }
+  // CMNDF :364-372: runningSum over tau = 1..511 in order (wave-uniform chain)
+  double run = 0.0, myrun[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) myrun[r] = 0.0;
+  for (int L = 0; L < 64; ++L) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if (L == 0 && r == 0) continue;                    // tau = 0 is not summed
+      run = __dadd_rn(run, readlane_f64(acc[r], L));
+      myrun[r] = (lane == L) ? run : myrun[r];
+    }
+  }
+  double cm[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int tau = t0 + r;
+    cm[r] = tau == 0 ? 1.0 : __ddiv_rn(acc[r], __ddiv_rn(myrun[r], (double)tau));
+  }
+  // first tau in 1..510 with cm < 0.15 and cm[tau] < cm[tau + 1] (:375-384)
+  const double nxt0 = __shfl_down(cm[0], 1, 64);         // lane + 1's tau 8 (l + 1)
+  int fr = 8;
+#pragma unroll
+  for (int r = 7; r >= 0; --r) {
+    const int tau = t0 + r;
+    const double nx = r < 7 ? cm[r + 1] : nxt0;
+    if (tau >= 1 && cm[r] < 0.15 && tau + 1 < 512 && cm[r] < nx) fr = r;
+  }
+  const unsigned long long bal = __ballot(fr < 8);
+  int mt = -1;
+  if (bal) {
+    const int L = __ffsll((long long)bal) - 1;
+    mt = 8 * L + __builtin_amdgcn_readlane(fr, L);
+  }
+  double p = 0.0, c = 0.0;
+  if (mt > 0) {                                          // wave-uniform from here
+    auto cm_at = [&](int tau) {                         // cm of a uniform tau, without a dynamic index
+      const int r = tau & 7, L = tau >> 3;
+      double v = 0.0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { const double t = readlane_f64(cm[q], L); v = (r == q) ? t : v; }
+      return v;
+    };
+    const double y2 = cm_at(mt);
+    double period = (double)mt;                          // parabolicInterpolation :743-764
+    if (mt < 511) {
+      const double y1 = cm_at(mt - 1), y3 = cm_at(mt + 1);
+      const double a = __ddiv_rn(__dadd_rn(__dsub_rn(y1, __dmul_rn(2.0, y2)), y3), 2.0);
+      const double b = __ddiv_rn(__dsub_rn(y3, y1), 2.0);
+      if (a != 0.0) period = __dadd_rn((double)mt, __ddiv_rn(-b, __dmul_rn(2.0, a)));
+    }
+    const double f = __ddiv_rn((double)sr, period);
+    const double cf = __dsub_rn(1.0, y2);
+    if (f >= 80.0 && f <= 1000.0) { p = f; c = cf; }
+  }
+  if (lane == 0) {
     pitch[fi] = p; conf[fi] = c;
     if (tau_out) tau_out[fi] = mt;
   }
@@ -504,17 +570,36 @@ int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, in
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// EnergyEntropy of extractEnergyFeatures (extractors/speech.go:429-433): -e ln(e + 1e-10) where e > 0
+__global__ __launch_bounds__(256) void energy_entropy_kernel(const double* e, int64_t n, double* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = e[i];
+    out[i] = v > 0.0 ? -v * log(v + 1e-10) : 0.0;
+  }
+}
+
+int launch_energy_entropy(const double* e, int64_t n, double* out, hipStream_t s) {
+  if (n <= 0) return 0;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(energy_entropy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, e, n, out);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int launch_yin(const double* pcm, int64_t n, int64_t frames, int64_t hop, int sr, double* pitch, double* conf,
                int32_t* tau, hipStream_t s) {
-  static bool init = false;
-  if (!init) {   // symmetric Hann without normalisation, pitch_detection.go:314-318
+  // the window table is a per-device symbol: uploaded once per device of the process
+  static std::atomic<uint64_t> init_mask{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -5;
+  if (!(init_mask.load() & (1ull << dev))) {   // symmetric Hann without normalisation, pitch_detection.go:316-345
     double w[1024];
     for (int i = 0; i < 1024; i++) w[i] = 0.5 * (1.0 - cos(2.0 * M_PI * (double)i / 1023.0));
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_yin_win), w, sizeof(w)) != hipSuccess) return -5;
-    init = true;
+    init_mask.fetch_or(1ull << dev);
   }
   if (frames <= 0) return 0;
-  hipLaunchKernelGGL(yin_kernel, dim3((unsigned)frames), dim3(256), 0, s, pcm, n, frames, hop, sr, pitch, conf, tau);
+  hipLaunchKernelGGL(yin_kernel, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0, s, pcm, n, frames, hop, sr, pitch,
+                     conf, tau);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

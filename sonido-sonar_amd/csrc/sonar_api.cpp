@@ -13,6 +13,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -76,6 +78,56 @@ void timed_end(sonar_ctx* c, hipStream_t s, hipEvent_t end) {
 }
 
 // the cached buffers of one context (not its workers')
+namespace {
+// idle pinned blocks by capacity; at most kPinnedCache bytes stay cached
+struct PinnedPool {
+  std::mutex m;
+  std::multimap<size_t, void*> idle;
+  size_t cached = 0;
+};
+PinnedPool& pinned_pool() {
+  static PinnedPool* p = new PinnedPool();   // never destroyed: blocks may outlive static teardown
+  return *p;
+}
+constexpr size_t kPinnedCache = size_t(8) << 30;
+void pinned_release(void* ptr, size_t cap) {
+  PinnedPool& pp = pinned_pool();
+  std::lock_guard<std::mutex> g(pp.m);
+  if (pp.cached + cap > kPinnedCache) { hipHostFree(ptr); return; }
+  pp.idle.emplace(cap, ptr);
+  pp.cached += cap;
+}
+}  // namespace
+
+std::shared_ptr<void> pinned_block(size_t bytes) {
+  if (bytes == 0) bytes = 64;
+  PinnedPool& pp = pinned_pool();
+  void* ptr = nullptr;
+  size_t cap = 0;
+  {
+    std::lock_guard<std::mutex> g(pp.m);
+    auto it = pp.idle.lower_bound(bytes);
+    if (it != pp.idle.end() && it->first <= 2 * bytes + (size_t(64) << 20)) {
+      ptr = it->second; cap = it->first;
+      pp.cached -= cap;
+      pp.idle.erase(it);
+    }
+  }
+  if (!ptr) {
+    cap = (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+    if (hipHostMalloc(&ptr, cap, hipHostMallocPortable) != hipSuccess) return nullptr;
+  }
+  return std::shared_ptr<void>(ptr, [cap](void* q) { pinned_release(q, cap); });
+}
+
+void pinned_pool_trim() {
+  PinnedPool& pp = pinned_pool();
+  std::lock_guard<std::mutex> g(pp.m);
+  for (auto& kv : pp.idle) hipHostFree(kv.second);
+  pp.idle.clear();
+  pp.cached = 0;
+}
+
 void trim_buffers(sonar_ctx* c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
@@ -350,6 +402,7 @@ int sonar_trim(sonar_ctx* c) {
   if (!c) return SONAR_ERR_INVALID;
   for (sonar_ctx* w : c->workers) sonar::detail::trim_buffers(w);
   sonar::detail::trim_buffers(c);
+  sonar::detail::pinned_pool_trim();
   return SONAR_OK;
 }
 
@@ -484,6 +537,17 @@ int fp_plan(const sonar_fp_cfg* cfg, int64_t F) {
   return pair ? SONAR_PLAN_PAIR : SONAR_PLAN_WAVE;
 }
 
+// spec_rows_kernel over F float64 |X| rows of K bins into the descriptor outputs (nullable each)
+int launch_spec(const double* mag, int64_t F, int K, int sample_rate, bool o64, void* const* d_spec, hipStream_t s) {
+  sonar::SpecParams sp{};
+  sp.mag = mag; sp.F = F; sp.K = K; sp.sample_rate = sample_rate; sp.out_f64 = o64 ? 1 : 0;
+  for (int d = 0; d < 9; d++) sp.out_spec[d] = d_spec[d];
+  // ~24 resident waves per CU over 256 CUs, a contiguous frame run each
+  const int64_t target = 256 * 24;
+  sp.frames_per_wave = std::max<int64_t>(1, (F + target - 1) / target);
+  return sonar::launch_spec_rows(sp, s);
+}
+
 // ComputeSTFTWithWindow's argument checks (spectral.go:386-412) and the GPU path's own limits, in the
 // order sonar_fingerprint applies them: SONAR_OK and the frame count, or the error code + message
 int fp_validate(const sonar_fp_cfg* cfg, int64_t n, bool have_pcm, int64_t* F, std::string* msg) {
@@ -494,12 +558,8 @@ int fp_validate(const sonar_fp_cfg* cfg, int64_t n, bool have_pcm, int64_t* F, s
   *F = go_frames(n, W, H);
   if (*F <= 0) { *msg = "signal too short for given window size and hop size"; return SONAR_ERR_TOO_SHORT; }
   if (fp_plan(cfg, *F) == SONAR_PLAN_DFT) {
-    // other window lengths (go-dsp takes any W, spectral.go:131) run the generic DFT path; the
-    // spectral descriptors exist only in the fused kernels
-    if (cfg->flags & SONAR_FP_SPECTRAL) {
-      *msg = "spectral descriptors need a window of 128, 256, 512, 1024 or 2048 (got " + std::to_string(W) + ")";
-      return SONAR_ERR_UNSUPPORTED;
-    }
+    // other window lengths (go-dsp takes any W, spectral.go:131) run the generic DFT path (its
+    // |X| scratch feeds spec_rows_kernel for the spectral descriptors)
     if (W > 8192) {
       *msg = "window size " + std::to_string(W) + " above 8192 (generic STFT path)";
       return SONAR_ERR_UNSUPPORTED;
@@ -532,10 +592,14 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     if (rc != SONAR_OK) return fail(c, rc, msg);
   }
   const int W = cfg->window_size, H = cfg->hop_size;
-  const bool f64 = cfg->precision == SONAR_F64;
+  const uint32_t flags = cfg->flags;
+  // The spectral descriptors always take the float64 transform, whatever `precision` says: the
+  // flatness (exp of the mean ln over every bin above 1e-10, spectral_flatness.go:31-73) and the
+  // log-log slope (spectral_slope.go:24-63) read leakage bins that sit below an f32 FFT's rounding
+  // floor, so an f32 transform cannot hold them to 1e-4.  ~10 % of the kernel.
+  const bool f64 = cfg->precision == SONAR_F64 || (flags & SONAR_FP_SPECTRAL) != 0;
   const bool pcm64 = cfg->pcm_dtype == SONAR_F64;
   const bool o64 = cfg->out_dtype == SONAR_F64;
-  const uint32_t flags = cfg->flags;
   const int plan = fp_plan(cfg, F);
   const bool need_fft = plan != SONAR_PLAN_NONE;
   const bool generic = plan == SONAR_PLAN_DFT;
@@ -634,6 +698,8 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
                                 (const double*)t.dct, (const double*)t.lift, t.n_mfcc, cfg->mfcc_input_power, d_mfcc,
                                 o64, s) != 0)
       return fail(c, SONAR_ERR_DEVICE, "mfcc launch failed");
+    if ((flags & SONAR_FP_SPECTRAL) && launch_spec(mag, F, K, cfg->sample_rate, o64, d_spec, s) != 0)
+      return fail(c, SONAR_ERR_DEVICE, "spectral descriptor launch failed");
     timed_end(c, s, tend);
     c->last_fp_kernel = "stft_dft_kernel";
   }
@@ -670,18 +736,27 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     }
   }
   if (need_fft && !generic && !pair_done) {
-    const bool spec = (flags & SONAR_FP_SPECTRAL) != 0;
+    // Spectral descriptors (round 6): the transform writes float64 |X| rows to HBM (the caller's
+    // Magnitude output when it is float64, else a scratch of F x K doubles) and spec_rows_kernel
+    // reduces them.  The fused SPEC epilogue (one wave per SIMD) remains only for a float32
+    // Magnitude output beside the descriptors, or when the scratch cannot be allocated.
+    const bool spec_req = (flags & SONAR_FP_SPECTRAL) != 0;
+    double* spec_mag = nullptr;
+    if (spec_req && f64 && !(d_mag && !o64))
+      spec_mag = d_mag ? (double*)d_mag : (double*)dbuf(c, "fp.specmag", (size_t)F * K * 8);
+    const bool spec = spec_req && !spec_mag;            // the fused SPEC epilogue
     const int NB = sonar::fp_batch_frames(W);
     const int PRE = sonar::fp_pre_rows(W, spec);
     sonar::FpParams p{};
     p.pcm = dpcm; p.n = n; p.pcm_f64 = pcm64; p.F = F; p.W = W; p.H = H;
-    p.flags = flags;
+    p.flags = spec ? flags : (flags & ~(uint32_t)SONAR_FP_SPECTRAL);
     p.input_power = cfg->mfcc_input_power;
     p.n_groups = 64 / NB;
     p.sample_rate = cfg->sample_rate;
     p.out_f64 = o64;
     p.out_mfcc = d_mfcc;
-    p.out_mag = d_mag;
+    p.out_mag = spec_mag ? (void*)spec_mag : d_mag;
+    p.mag_f64 = spec_mag ? 1 : (int)o64;
     p.out_cplx = d_cplx;
     p.out_phase = d_phase;
     for (int d = 0; d < 9; d++) p.out_spec[d] = d_spec[d];
@@ -744,6 +819,8 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     const int rc = sonar::launch_fingerprint(p, f64, s);
     c->last_fp_kernel = "fp_wave_kernel";
     if (rc != 0) return fail(c, SONAR_ERR_DEVICE, std::string("fingerprint kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (spec_mag && launch_spec(spec_mag, F, K, cfg->sample_rate, o64, d_spec, s) != 0)
+      return fail(c, SONAR_ERR_DEVICE, "spectral descriptor launch failed");
     timed_end(c, s, tend);
   }
   if (flags & SONAR_FP_ZCR) {
@@ -1406,7 +1483,7 @@ int sonar_result_get(const sonar_result* r, const char* name, const double** dat
   if (!r || !name) return SONAR_ERR_INVALID;
   for (const auto& a : r->arrays)
     if (a.name == name) {
-      if (data) *data = a.v.data();
+      if (data) *data = a.data();
       if (rows) *rows = a.rows;
       if (cols) *cols = a.cols;
       return SONAR_OK;

@@ -60,9 +60,14 @@ int grow(sonar_stft_stream* st, int64_t need) {
       if (nb[0]) (void)hipFree(nb[0]);
       return fail(c, SONAR_ERR_NOMEM, "device allocation failed (stream buffer)");
     }
+  hipError_t e = hipSuccess;
   if (st->len > 0)
-    HIP_TRY(c, hipMemcpyAsync(nb[0], st->buf[st->cur], (size_t)st->len * st->esz, hipMemcpyDeviceToDevice, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+    e = hipMemcpyAsync(nb[0], st->buf[st->cur], (size_t)st->len * st->esz, hipMemcpyDeviceToDevice, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {                       // the old buffers stay; the new pair must not leak
+    for (int k = 0; k < 2; k++) (void)hipFree(nb[k]);
+    return fail(c, SONAR_ERR_DEVICE, std::string("stream buffer copy: ") + hipGetErrorString(e));
+  }
   for (int k = 0; k < 2; k++)
     if (st->buf[k]) (void)hipFree(st->buf[k]);
   st->buf[0] = nb[0]; st->buf[1] = nb[1];

@@ -157,8 +157,11 @@ func (x *Multi) Fingerprint(pcm []float64, windowSize, hopSize, sampleRate int, 
 		nc = 13
 	}
 	flat := make([]float64, frames*nc)
-	out := C.sonar_fp_out{mfcc: unsafe.Pointer(&flat[0])}
-	if rc := C.sonar_fingerprint_multi(x.m, unsafe.Pointer(&pcm[0]), C.int64_t(len(pcm)), &cfg, &out); rc != C.SONAR_OK {
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	out := mfccOut(&pin, flat)
+	defer C.free(unsafe.Pointer(out))
+	if rc := C.sonar_fingerprint_multi(x.m, unsafe.Pointer(&pcm[0]), C.int64_t(len(pcm)), &cfg, out); rc != C.SONAR_OK {
 		return nil, x.err(rc)
 	}
 	return split(flat, frames, nc), nil

@@ -32,6 +32,7 @@ import "C"
 import (
 	"errors"
 	"fmt"
+	"runtime"
 	"unsafe"
 )
 
@@ -405,8 +406,11 @@ func (x *Context) Fingerprint(pcm []float64, windowSize, hopSize, sampleRate int
 		nc = 13
 	}
 	flat := make([]float64, frames*nc)
-	out := C.sonar_fp_out{mfcc: unsafe.Pointer(&flat[0])}
-	if rc := C.sonar_fingerprint(x.c, unsafe.Pointer(&pcm[0]), C.int64_t(len(pcm)), &cfg, &out); rc != C.SONAR_OK {
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	out := mfccOut(&pin, flat)
+	defer C.free(unsafe.Pointer(out))
+	if rc := C.sonar_fingerprint(x.c, unsafe.Pointer(&pcm[0]), C.int64_t(len(pcm)), &cfg, out); rc != C.SONAR_OK {
 		return nil, x.err(rc)
 	}
 	return split(flat, frames, nc), nil
@@ -440,9 +444,17 @@ func (x *Context) ComputeSTFT(pcm []float64, windowSize, hopSize, windowType int
 	k := windowSize/2 + 1
 	mag, ph := make([]float64, frames*k), make([]float64, frames*k)
 	cx := make([]complex128, frames*k)
-	out := C.sonar_fp_out{magnitude: unsafe.Pointer(&mag[0]), phase: unsafe.Pointer(&ph[0]),
-		complex: unsafe.Pointer(&cx[0])}
-	if rc := C.sonar_fingerprint(x.c, unsafe.Pointer(&pcm[0]), C.int64_t(len(pcm)), &cfg, &out); rc != C.SONAR_OK {
+	// the output struct holds Go pointers: pinned for the call (cgo's check rejects a Go pointer to
+	// unpinned Go pointers), the struct itself in C memory
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	pin.Pin(&mag[0])
+	pin.Pin(&ph[0])
+	pin.Pin(&cx[0])
+	out := (*C.sonar_fp_out)(C.calloc(1, C.size_t(unsafe.Sizeof(C.sonar_fp_out{}))))
+	defer C.free(unsafe.Pointer(out))
+	out.magnitude, out.phase, out.complex = unsafe.Pointer(&mag[0]), unsafe.Pointer(&ph[0]), unsafe.Pointer(&cx[0])
+	if rc := C.sonar_fingerprint(x.c, unsafe.Pointer(&pcm[0]), C.int64_t(len(pcm)), &cfg, out); rc != C.SONAR_OK {
 		return nil, x.err(rc)
 	}
 	s := &Spectrogram{Magnitude: split(mag, frames, k), Phase: split(ph, frames, k),
@@ -480,9 +492,12 @@ func (x *Context) FingerprintDecoded(output []byte, windowSize, hopSize, sampleR
 		nc = 13
 	}
 	flat := make([]float64, frames*nc)
-	out := C.sonar_fp_out{mfcc: unsafe.Pointer(&flat[0])}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	out := mfccOut(&pin, flat)
+	defer C.free(unsafe.Pointer(out))
 	if rc := C.sonar_fingerprint_f64le(x.c, unsafe.Pointer(&output[0]), C.int64_t(len(output)),
-		C.SONAR_INGEST_HOST_CONVERT, &cfg, &out); rc != C.SONAR_OK {
+		C.SONAR_INGEST_HOST_CONVERT, &cfg, out); rc != C.SONAR_OK {
 		return nil, x.err(rc)
 	}
 	return split(flat, frames, nc), nil
@@ -564,4 +579,14 @@ func (x *Context) NCC(s1, s2 []float64, maxLag int) (*CorrelationResult, error) 
 	}
 	return &CorrelationResult{Correlations: corr, PeakCorrelation: m[0], PeakLag: int(m[1]), PeakIndex: int(m[2]),
 		PValue: m[3], SNR: m[4], Sharpness: m[5], SecondPeak: m[6], PSL: m[7], OverlapLength: int(m[8])}, nil
+}
+
+// mfccOut is a sonar_fp_out in C memory whose mfcc field points at flat, pinned by pin for the
+// call: cgo rejects a Go struct holding Go pointers, and C memory may hold a Go pointer only while
+// it is pinned.  The caller frees the struct (C.free) and unpins.
+func mfccOut(pin *runtime.Pinner, flat []float64) *C.sonar_fp_out {
+	out := (*C.sonar_fp_out)(C.calloc(1, C.size_t(unsafe.Sizeof(C.sonar_fp_out{}))))
+	pin.Pin(&flat[0])
+	out.mfcc = unsafe.Pointer(&flat[0])
+	return out
 }

@@ -1,12 +1,14 @@
 package sonargpu
 
 /*
+#include <stdlib.h>
 #include "sonar_gpu.h"
 */
 import "C"
 
 import (
 	"fmt"
+	"runtime"
 	"unsafe"
 )
 
@@ -56,16 +58,31 @@ func (s *STFTStreamer) ProcessChunk(chunk []float64) ([]*SpectrogramFrame, error
 		frames = 0 // the push reports the error
 	}
 	k := s.freqBins
-	mag, ph := make([]float64, frames*k+1), make([]float64, frames*k+1)
-	cx := make([]complex128, frames*k+1)
-	out := C.sonar_fp_out{magnitude: unsafe.Pointer(&mag[0]), phase: unsafe.Pointer(&ph[0]),
-		complex: unsafe.Pointer(&cx[0])}
+	// The output struct holds pointers to Go memory: cgo's pointer check rejects a Go pointer to
+	// unpinned Go pointers, so the row slices (and the chunk) are pinned for the call.
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	out := (*C.sonar_fp_out)(C.calloc(1, C.size_t(unsafe.Sizeof(C.sonar_fp_out{}))))
+	defer C.free(unsafe.Pointer(out))
+	var mag, ph []float64
+	var cx []complex128
+	if frames > 0 {
+		mag, ph, cx = make([]float64, frames*k), make([]float64, frames*k), make([]complex128, frames*k)
+		pin.Pin(&mag[0])
+		pin.Pin(&ph[0])
+		pin.Pin(&cx[0])
+		out.magnitude, out.phase, out.complex = unsafe.Pointer(&mag[0]), unsafe.Pointer(&ph[0]), unsafe.Pointer(&cx[0])
+	}
+	pin.Pin(&chunk[0])
 	var got C.int64_t
-	if rc := C.sonar_stft_stream_push(s.st, unsafe.Pointer(&chunk[0]), n, &out, &got); rc != C.SONAR_OK {
+	if rc := C.sonar_stft_stream_push(s.st, unsafe.Pointer(&chunk[0]), n, out, &got); rc != C.SONAR_OK {
 		return nil, s.x.err(rc)
 	}
 	if int(got) != frames {
 		return nil, fmt.Errorf("sonargpu: stream emitted %d frames, expected %d: %w", int(got), frames, ErrDevice)
+	}
+	if frames == 0 {
+		return nil, nil // Go's ProcessChunk returns a nil slice when no frame completes (spectral.go:331, 373)
 	}
 	res := make([]*SpectrogramFrame, frames)
 	for t := range res {

@@ -256,6 +256,12 @@ def lib():
                                                  C.POINTER(C.c_void_p)]
     L.sonar_alignment_consistency.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                               C.c_int32, C.c_int32, C.c_int32, C.POINTER(AlignmentStats)]
+    L.sonar_analyzer_align_features.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                                C.c_int32, C.c_int32, C.c_int32, C.POINTER(_vp)]
+    L.sonar_align_audio.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                    C.c_int32, C.c_int32, C.POINTER(_vp)]
+    L.sonar_align_audio_files.argtypes = [_vp, _vp, C.c_int64, _vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                          C.c_int32, C.c_double, C.c_int32, C.POINTER(_vp)]
     L.sonar_truncate_to_alignment.argtypes = [_vp, C.c_int64, C.c_int64, C.c_int32, C.c_double,
                                               C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.sonar_voice_quality.argtypes = [_vp, _vp, C.c_int64, C.c_int32, C.POINTER(VoiceQuality)]
@@ -350,6 +356,34 @@ def records_dict(recs):
 
 def _ptr(a):
     return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class _ResultOwner:
+    """Owns a sonar_result handle; freed (sonar_result_free) when no view of it remains."""
+    def __init__(self, L, h):
+        self._L, self._h = L, h
+
+    def __del__(self):
+        if self._h:
+            self._L.sonar_result_free(self._h)
+            self._h = None
+
+
+class _ResultView:
+    """numpy's array interface over one result array; the array's base keeps the owner alive."""
+    def __init__(self, owner, addr, shape):
+        self._owner = owner
+        self.__array_interface__ = {"shape": shape, "typestr": "<f8", "data": (addr, False), "version": 3}
+
+
+def _pcm_arg(x, device_ptrs):
+    """(pointer, length, owner) of a PCM argument: a host float64 array, or (device pointer, n); the
+    caller keeps `owner` alive across the call (a converted copy)."""
+    if device_ptrs:
+        p, n = x
+        return C.c_void_p(int(p)), int(n), None
+    a = _f64(x)
+    return (_ptr(a) if a.size else None), int(a.size), a
 
 
 def _f64(a):
@@ -626,6 +660,44 @@ class Context:
             q.shape[1] if q.size else 1, method, max_lag, hop, sample_rate, num_trials, C.byref(st)))
         return {k: getattr(st, k) for k, _ in AlignmentStats._fields_}
 
+    def analyzer_align_features(self, query, reference, sample_rate, method=ALIGN_HYBRID, max_lag=100, hop=256):
+        """AlignmentAnalyzer.AlignFeatures (stats/alignment.go:84-106) for DTW / CrossCorrelation /
+        Hybrid -> the AlignmentResult fields (+ "correlations", NCC metrics, "dtw_path_*")."""
+        q, r = _f64(query), _f64(reference)
+        if q.ndim == 1:
+            q = q[:, None]
+        if r.ndim == 1:
+            r = r[:, None]
+        h = C.c_void_p()
+        self._check(self._L.sonar_analyzer_align_features(
+            self._h, _ptr(q) if q.size else None, len(q) if q.size else 0, _ptr(r) if r.size else None,
+            len(r) if r.size else 0, q.shape[1] if q.size else 1, method, max_lag, hop, sample_rate, 0, C.byref(h)))
+        return self._result(h)
+
+    def align_audio(self, q_pcm, r_pcm, sample_rate, method=ALIGN_HYBRID, max_lag=100, hop=256, window=1024,
+                    device_ptrs=False):
+        """AlignmentAnalyzer.AlignAudio (stats/alignment.go:108-126): RMS energy frames of both signals
+        (extractEnergyFeatures :341-361), then AlignFeatures.  q_pcm / r_pcm: float64 arrays, or device
+        pointers (ints) with lengths as (ptr, n) tuples when device_ptrs."""
+        (qp, nq, qa), (rp, nr, ra) = _pcm_arg(q_pcm, device_ptrs), _pcm_arg(r_pcm, device_ptrs)
+        h = C.c_void_p()
+        self._check(self._L.sonar_align_audio(self._h, qp, nq, rp, nr, method, max_lag, hop, window, sample_rate,
+                                              int(device_ptrs), C.byref(h)))
+        del qa, ra
+        return self._result(h)
+
+    def align_audio_files(self, q_pcm, r_pcm, sample_rate, feature_sample_rate=None, hop=256, window=1024,
+                          max_lag_seconds=60.0, device_ptrs=False):
+        """AlignmentExtractor.AlignAudioFiles (extractors/alignment.go:489-553): ShortTimeEnergy of
+        both PCM streams, then the extractor's Hybrid AlignFeatures."""
+        (qp, nq, qa), (rp, nr, ra) = _pcm_arg(q_pcm, device_ptrs), _pcm_arg(r_pcm, device_ptrs)
+        fsr = sample_rate if feature_sample_rate is None else feature_sample_rate
+        h = C.c_void_p()
+        self._check(self._L.sonar_align_audio_files(self._h, qp, nq, rp, nr, sample_rate, fsr, hop, window,
+                                                    float(max_lag_seconds), int(device_ptrs), C.byref(h)))
+        del qa, ra
+        return self._result(h)
+
     def truncate_to_alignment(self, n1, n2, sample_rate, temporal_offset):
         """AlignmentExtractor.TruncateToAlignmentPCM -> (start1, start2, length)."""
         a, b, n = C.c_int64(), C.c_int64(), C.c_int64()
@@ -672,18 +744,19 @@ class Context:
 
     # -- Go API mirror -----------------------------------------------------
     def _result(self, h):
+        """The result's arrays as numpy views of its memory (no copy; large arrays live in pinned
+        host memory the device copied into); the handle is freed when the last view goes."""
         L = self._L
+        owner = _ResultOwner(L, h)
         out = {}
-        try:
-            for i in range(L.sonar_result_count(h)):
-                name = L.sonar_result_name(h, i).decode()
-                data, rows, cols = _d(), C.c_int64(), C.c_int64()
-                L.sonar_result_get(h, name.encode(), C.byref(data), C.byref(rows), C.byref(cols))
-                n = rows.value * cols.value
-                arr = np.ctypeslib.as_array(data, shape=(n,)).copy() if n else np.zeros(0)
-                out[name] = arr.reshape(rows.value, cols.value) if cols.value > 1 else arr
-        finally:
-            L.sonar_result_free(h)
+        for i in range(L.sonar_result_count(h)):
+            name = L.sonar_result_name(h, i).decode()
+            data, rows, cols = _d(), C.c_int64(), C.c_int64()
+            L.sonar_result_get(h, name.encode(), C.byref(data), C.byref(rows), C.byref(cols))
+            n = rows.value * cols.value
+            shape = (rows.value, cols.value) if cols.value > 1 else (n,)
+            addr = C.cast(data, C.c_void_p).value
+            out[name] = np.asarray(_ResultView(owner, addr, shape)) if n else np.zeros(0)
         return out
 
     @staticmethod

@@ -83,9 +83,23 @@ def test_speech_extractor_real_sample_rate_c4(ctx, prec, rtol):
     ref = O.speech_features_reference(x, 16000, fc)
     for k in ("pitch_estimate", "pitch_confidence", "voicing_strength", "zero_crossing_rate", "short_time_energy"):
         assert np.array_equal(got[k], ref[k]), k            # YIN tau/tracking and ZCR counts are exact
-    if prec == sonar.F32:
-        ref = {k: v for k, v in ref.items() if k not in ("spectral_slope",)}
-    _cmp(got, ref, rtol, mag=O.stft_mag(x, 512, 128, nthreads=8))
+    _cmp(got, ref, rtol, mag=O.stft_mag(x, 512, 128, nthreads=8))    # every field, slope included
+
+
+def test_generate_fingerprint_music_c1_f32(ctx):
+    """C1 in the f32 (throughput) mode: every GenerateFingerprint field within the north star's 1e-4
+    of the oracle composition, spectral flatness and slope included (the
+    descriptors take the f64 transform in either mode, spectral_flatness.go:31-73)."""
+    x = synth.sweep(10.0)
+    cfg = ctx.fingerprint_config(window_size=1024, hop_size=256, feature_window_size=1024, feature_hop_size=256,
+                                 precision=sonar.F32)
+    got = ctx.generate_fingerprint(x, 44100, "music", cfg)
+    ref = O.speech_features_reference(x, 44100, dict(sample_rate=0, window_size=1024, hop_size=256,
+                                                     stft_window_size=1024, stft_hop_size=256, enable_mfcc=1,
+                                                     enable_speech_features=0, enable_temporal_features=0,
+                                                     mfcc_coefficients=13))
+    assert "spectral_flatness" in ref and "spectral_slope" in ref
+    _cmp(got, ref, 1e-4)
 
 
 def test_align_features_c3_lag(ctx):

@@ -5,8 +5,9 @@ mfcc_rows_kernel) against the oracle (or_fft: Bluestein for non-powers of two).
 
 Tolerances: magnitude and complex 1e-10 of the frame's peak (direct DFT against Bluestein, both
 float64); phase where |X| > 1e-6 of the peak, bounded by |dX| / |X|; MFCC 1e-9 of the row norm.
-The spectral descriptors exist only in the fused kernels: W outside {128 .. 2048, powers of two}
-with SONAR_FP_SPECTRAL fails with SONAR_ERR_UNSUPPORTED, as does W > 8192."""
+The spectral descriptors of any W run on spec_rows_kernel over the DFT path's |X| rows (round 6;
+rounds 1-5 refused them outside the fused kernels' powers of two); W > 8192 is
+SONAR_ERR_UNSUPPORTED."""
 import numpy as np
 import pytest
 
@@ -57,11 +58,33 @@ def test_generic_mfcc_matches_oracle(ctx, W, H, n_mels):
     assert_mfcc(got["mfcc"], ref, 1e-9)
 
 
+SPEC = ["centroid", "rolloff", "bandwidth", "flatness", "crest", "slope", "flux", "low_ratio", "high_ratio"]
+
+
+@pytest.mark.parametrize("W,H,sr", [(1000, 250, 44100), (441, 147, 22050), (3000, 1000, 16000), (4096 + 7, 2048, 0)])
+@pytest.mark.parametrize("prec", [sonar.F64, sonar.F32])
+def test_generic_spectral_descriptors(ctx, W, H, sr, prec):
+    """extractSpectralFeatures (speech.go:320-367) on the DFT path's rows: 1e-9 in both modes (the
+    DFT path is float64 throughout; f32 rounds the outputs: 1e-6), rolloff bin exact."""
+    from parity import assert_rolloff
+    x = _sig(SR + 777, seed=W + 3)
+    got = ctx.fingerprint(x, ctx.config(window_size=W, hop_size=H, sample_rate=sr, precision=prec,
+                                        flags=sonar.FP_SPECTRAL | sonar.FP_MFCC))
+    assert ctx.last_fp_kernel() == "stft_dft_kernel"
+    mag = O.stft_mag(x, W, H)
+    ref = O.spectral_descriptors(mag, sr)
+    tol = 1e-9 if prec == sonar.F64 else 1e-6
+    for k in SPEC:
+        g, r = np.asarray(got[k], np.float64), ref[k]
+        assert g.shape == r.shape, k
+        if k == "rolloff":
+            assert_rolloff(g, r, mag, 1e-12)
+            continue
+        scale = np.maximum(np.abs(r), np.max(np.abs(r)) * 1e-6 + 1e-30)
+        assert np.max(np.abs(g - r) / scale) < (tol * 10 if k == "slope" else tol), k
+
+
 def test_generic_unsupported_cases(ctx):
-    x = _sig(20000)
-    with pytest.raises(sonar.SonarError) as e:
-        ctx.fingerprint(x, ctx.config(window_size=1000, hop_size=250, flags=sonar.FP_SPECTRAL))
-    assert "spectral descriptors" in e.value.msg
     with pytest.raises(sonar.SonarError):
         ctx.fingerprint(np.zeros(20000), ctx.config(window_size=9000, hop_size=1000, flags=sonar.FP_MAGNITUDE))
 

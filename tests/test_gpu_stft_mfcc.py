@@ -161,7 +161,8 @@ def test_spectral_descriptors_match_oracle(ctx, W, H, sr, prec):
             continue
         scale = np.maximum(np.abs(r), np.max(np.abs(r)) * 1e-6 + 1e-30)
         err = np.max(np.abs(g - r) / scale)
-        # slope is a log-log regression over every bin above 1e-10: in F32 the small bins carry
-        # large relative FFT error (error ~ 1e-7 of the frame PEAK), so F32 slope is checked at 5e-3
-        stol = tol * 10 if prec == sonar.F64 else 5e-3
+        # slope is a log-log regression over every bin above 1e-10 (f64: 10x the tolerance); in
+        # the F32 mode the descriptors take the f64 transform (round 6), so every field, slope
+        # included, is held to the north star's 1e-4
+        stol = tol * 10 if prec == sonar.F64 else tol
         assert err < (tol if k != "slope" else stol), (k, err)

@@ -43,5 +43,5 @@ def test_plan_validation_errors_in_go_order():
     assert sonar.fp_kernel_plan(_cfg(window_size=0), 4096) == sonar.ERR_INVALID
     assert sonar.fp_kernel_plan(_cfg(hop_size=0), 4096) == sonar.ERR_INVALID
     assert sonar.fp_kernel_plan(_cfg(), 700) == sonar.ERR_TOO_SHORT
-    assert sonar.fp_kernel_plan(_cfg(window_size=1000, flags=sonar.FP_SPECTRAL), 10 ** 5) == sonar._abi.ERR_UNSUPPORTED
+    assert sonar.fp_kernel_plan(_cfg(window_size=1000, flags=sonar.FP_SPECTRAL), 10 ** 5) == sonar.PLAN_DFT
     assert sonar.fp_kernel_plan(_cfg(window_size=9000, flags=sonar.FP_MFCC), 10 ** 5) == sonar._abi.ERR_UNSUPPORTED
