@@ -66,6 +66,10 @@ struct sonar_ctx {
   // events that order it: features done -> side, NCC done -> stream
   hipStream_t side = nullptr;
   hipEvent_t side_ev[2] = {nullptr, nullptr};
+  // the host-PCM pipeline of sonar_extract_speech_features: H2D chunks on `copy`, one event per
+  // chunk the compute streams wait on (go_api.cpp)
+  hipStream_t copy = nullptr;
+  std::vector<hipEvent_t> chunk_ev;
   // band-kernel liveness counters (sonar_dtw_counters): edge refresh fences, those followed by new
   // edge values, DTWs that timed out, waves that timed out
   long long dtw_ctr[4] = {0, 0, 0, 0};
@@ -178,8 +182,9 @@ void timed_end(sonar_ctx* c, hipStream_t s, hipEvent_t end);
 // frees the ingest ring and joins its host threads (ingest_api.cpp)
 void ingest_release(sonar_ctx* c);
 // sonar_fingerprint with the PCM already on the device and host outputs (sonar_api.cpp)
+// [f_lo, f_hi): only those frames of the whole signal's STFT (device outputs, per-frame kernel)
 int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cfg* cfg, sonar_fp_out* out,
-                     bool pcm_dev);
+                     bool pcm_dev, int64_t f_lo = 0, int64_t f_hi = -1);
 // VoiceQualityAnalyzer.AnalyzeVoiceQuality on device-resident float64 samples (voice_api.cpp)
 int voice_quality(sonar_ctx* c, const double* dsig, int64_t n, int32_t sr, sonar_voice_quality_result* out);
 }  // namespace detail

@@ -190,9 +190,9 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
 
   // ---- this wave's frame range and unit sequence ---------------------------
   const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-  const int64_t f_begin = gw * p.frames_per_wave;
-  if (f_begin >= p.F) return;
-  const int64_t f_end = min(p.F, f_begin + p.frames_per_wave);
+  const int64_t f_begin = p.f_first + gw * p.frames_per_wave;       // this launch: frames [f_first, f_last)
+  if (f_begin >= p.f_last) return;
+  const int64_t f_end = min(p.f_last, f_begin + p.frames_per_wave);
   const int64_t nbatch = (f_end - f_begin + NB - 1) / NB;
   const int pre = (SPEC && f_begin > 0) ? 1 : 0;
   const int64_t nunits = pre + nbatch * UPB;
@@ -655,9 +655,9 @@ __global__ __launch_bounds__(256) void spec_rows_kernel(SpecParams p) {
     for (int k = threadIdx.x; k < K; k += blockDim.x) xk[k] = k > 0 ? log((double)k * fscale) * inv_ln10 : 0.0;
   __syncthreads();
   const int64_t gw = (int64_t)blockIdx.x * nw + wave;
-  const int64_t fb = gw * p.frames_per_wave;
-  if (fb >= p.F) return;
-  const int64_t fe = min(p.F, fb + p.frames_per_wave);
+  const int64_t fb = p.f_first + gw * p.frames_per_wave;            // this launch: frames [f_first, f_last)
+  if (fb >= p.f_last) return;
+  const int64_t fe = min(p.f_last, fb + p.frames_per_wave);
   const int CH = (K + 63) >> 6;
   const int k0 = min(K, lane * CH), k1 = min(K, k0 + CH), nk = k1 - k0;
   const double* src = p.mag;
@@ -803,14 +803,14 @@ __global__ __launch_bounds__(256) void spec_rows_kernel(SpecParams p) {
 }
 
 int launch_spec_rows(const SpecParams& p, hipStream_t s) {
-  if (p.F <= 0) return 0;
+  if (p.F <= 0 || p.f_last <= p.f_first) return 0;
   if (p.K < 2 || p.frames_per_wave <= 0) return -4;
   const int CH = (p.K + 63) / 64;
   const int waves_per_block = 4;
   const int nt = CH <= 9 ? 1 : 2;
   const size_t lds = (size_t)(p.K + (p.K & 1)) * 8 + (size_t)waves_per_block * nt * p.K * 8;
   if (lds > 160 * 1024) return -4;
-  const int64_t waves = (p.F + p.frames_per_wave - 1) / p.frames_per_wave;
+  const int64_t waves = (p.f_last - p.f_first + p.frames_per_wave - 1) / p.frames_per_wave;
   const int64_t grid = (waves + waves_per_block - 1) / waves_per_block;
   const dim3 g((unsigned)grid), b(64 * waves_per_block);
 #define SPEC_ROWS(C)                                                                             \
@@ -837,7 +837,8 @@ static int launch_t(const FpParams& p, hipStream_t s) {
   auto kern = fp_wave_kernel<T, P, R, SPEC, CPLX>;
   if (p.lds_bytes > 64 * 1024)
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
-  const int64_t waves = (p.F + p.frames_per_wave - 1) / p.frames_per_wave;
+  if (p.f_last <= p.f_first) return 0;
+  const int64_t waves = (p.f_last - p.f_first + p.frames_per_wave - 1) / p.frames_per_wave;
   const int64_t grid = (waves + p.waves_per_block - 1) / p.waves_per_block;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * p.waves_per_block), p.lds_bytes, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -5;

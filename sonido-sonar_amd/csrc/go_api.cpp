@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -136,30 +137,38 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   const int64_t Fp = sonar_pitch_frames(n);
   (void)K;
 
-  // ---- device inputs -------------------------------------------------------
+  // ---- device buffers ------------------------------------------------------------
   double* dpcm = (double*)dbuf(c, "sx.pcm", n * 8);
   double* dy = (double*)dbuf(c, "sx.pre", n * 8);
   if (!dpcm || !dy) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (pcm)");
-  HIP_TRY(c, hipMemcpyAsync(dpcm, pcm, n * 8, hipMemcpyHostToDevice, s));
-  // preprocessForSpeech: PreEmphasis("speech") alpha 0.97, fresh state (speech.go:238-245)
-  if (sonar::launch_preemph(dpcm, 1, n, 0.97, dy, s) != 0) return fail(c, SONAR_ERR_DEVICE, "preemph launch failed");
-
-  // ---- fused STFT kernel: MFCC + descriptors, ZCR and short-time energy ---------
   const size_t fsz = (size_t)std::max<int64_t>(F, 1);
   double* dmfcc = (double*)dbuf(c, "sx.mfcc", fsz * nm * 8);
   double* dspec = (double*)dbuf(c, "sx.spec", fsz * 9 * 8);
   double* dzcr = (double*)dbuf(c, "sx.zcr", fsz * 8);
   double* den = (double*)dbuf(c, "sx.energy", std::max<int64_t>(Fe, 1) * 8);
   if (!dmfcc || !dspec || !dzcr || !den) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (features)");
+  double* dpit = (double*)dbuf(c, "sx.pitch", std::max<int64_t>(Fp, 1) * 8);
+  double* dcon = (double*)dbuf(c, "sx.conf", std::max<int64_t>(Fp, 1) * 8);
+  if (!dpit || !dcon) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (pitch)");
+  // extractSimpleEnvelope (speech.go:752-777): RMS 512/256 of the pre-emphasised PCM
+  const int64_t Fenv = sonar_energy_frames(n, 512, 256);
+  double* denv = (double*)dbuf(c, "sx.env", std::max<int64_t>(Fenv, 1) * 8);
+  // ComputeLoudnessRange (energy.go:145-178): 400 ms / 100 ms RMS frames when sr > 0
+  const int lw = (int)(0.4 * (double)csr);
+  const int lh = std::max(1, lw / 4);
+  const int64_t Fl = csr > 0 ? sonar_energy_frames(n, lw, lh) : 0;
+  double* dld = (double*)dbuf(c, "sx.loud", std::max<int64_t>(Fl, 1) * 8);
+  if (!denv || !dld) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (envelope)");
+
+  // the fused STFT kernel: MFCC + descriptors + ZCR (the energy frames are launched beside it)
   sonar_fp_cfg cfg;
   sonar_fp_cfg_default(&cfg);
   cfg.window_size = W; cfg.hop_size = H; cfg.window_type = fc->window_type;
   cfg.sample_rate = csr;                                          // NewMFCC(config.SampleRate, ...) etc.
   cfg.n_mfcc = nm; cfg.n_filters = 26; cfg.use_lifter = 1; cfg.lifter = 22.0;   // NewMFCC defaults (mfcc.go:44-54)
   cfg.low_freq = 0.0; cfg.high_freq = (double)csr / 2.0;
-  cfg.energy_window = fc->window_size; cfg.energy_hop = fc->hop_size;
   cfg.preemph_alpha = 0.97;
-  cfg.flags = SONAR_FP_SPECTRAL | SONAR_FP_ZCR | SONAR_FP_ENERGY | (fc->enable_mfcc ? SONAR_FP_MFCC : 0);
+  cfg.flags = SONAR_FP_SPECTRAL | SONAR_FP_ZCR | (fc->enable_mfcc ? SONAR_FP_MFCC : 0);
   cfg.precision = fc->precision; cfg.pcm_dtype = SONAR_F64; cfg.out_dtype = SONAR_F64; cfg.device_ptrs = 1;
   sonar_fp_out fo;
   std::memset(&fo, 0, sizeof(fo));
@@ -167,41 +176,88 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   const size_t Fz = (size_t)F;
   fo.centroid = dspec; fo.rolloff = dspec + Fz; fo.bandwidth = dspec + 2 * Fz; fo.flatness = dspec + 3 * Fz;
   fo.crest = dspec + 4 * Fz; fo.slope = dspec + 5 * Fz; fo.flux = dspec + 6 * Fz; fo.low_ratio = dspec + 7 * Fz;
-  fo.high_ratio = dspec + 8 * Fz; fo.zcr = dzcr; fo.energy = Fe > 0 ? den : nullptr;
-  // ---- YIN raw results on the pre-emphasised PCM (extractHarmonicFeatures :464) ---
-  // on the side stream, beside the fused STFT kernel (both only read the PCM); the main stream
-  // waits for it before the copies back
-  double* dpit = (double*)dbuf(c, "sx.pitch", std::max<int64_t>(Fp, 1) * 8);
-  double* dcon = (double*)dbuf(c, "sx.conf", std::max<int64_t>(Fp, 1) * 8);
-  if (!dpit || !dcon) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (pitch)");
+  fo.high_ratio = dspec + 8 * Fz; fo.zcr = dzcr;
   if (!c->side) {
     HIP_TRY(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     for (auto& e : c->side_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
-  HIP_TRY(c, hipEventRecord(c->side_ev[0], s));                  // dy is written
-  HIP_TRY(c, hipStreamWaitEvent(c->side, c->side_ev[0], 0));
-  if (sonar::launch_yin(dy, n, Fp, 512, csr, dpit, dcon, nullptr, c->side) != 0)
-    return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
+
+  // ---- the host PCM crosses PCIe in chunks on the copy stream; once chunk k has landed, every
+  // frame whose samples lie in [0, end of chunk k) is computed while the next chunk is in flight:
+  // pre-emphasis of the chunk, the fused STFT kernel + descriptors + ZCR over the frames it
+  // completes, the energy / envelope / loudness frames, and YIN (1024 / 512) on the side stream.
+  // Frames are independent (the flux reads the previous frame's |X| row, already written in stream
+  // order), so the results equal the one-shot schedule's.  The fused kernel takes frame ranges on
+  // the per-frame path (W = 128 .. 2048); other W run it once after the last chunk.
+  int64_t CH = n > ((int64_t)24 << 20) ? ((int64_t)8 << 20) : n;         // 8 M samples (64 MB) per chunk
+  if (const char* e = std::getenv("SONAR_PCM_CHUNK")) {                   // samples per chunk (tests)
+    const long long v = std::atoll(e);
+    if (v > 0) CH = std::min<int64_t>(n, v);
+  }
+  const int64_t NCH = (n + CH - 1) / CH;
+  if (NCH > 1) {
+    if (!c->copy) HIP_TRY(c, hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+    while ((int64_t)c->chunk_ev.size() < NCH) {
+      hipEvent_t e;
+      HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->chunk_ev.push_back(e);
+    }
+    HIP_TRY(c, hipEventRecord(c->side_ev[0], s));                // the buffers' previous readers
+    HIP_TRY(c, hipStreamWaitEvent(c->copy, c->side_ev[0], 0));
+  }
+  const bool fp_chunks = sonar::fingerprint_supported(W);
+  // frames t < total whose samples [t hop, t hop + win) lie below sample b (all of them at the end)
+  auto ready = [&](int64_t b, int64_t total, int64_t win, int64_t hop) -> int64_t {
+    if (b >= n) return total;
+    if (b < win || hop <= 0) return 0;
+    return std::min<int64_t>(total, (b - win) / hop + 1);
+  };
+  int64_t done_fp = 0, done_e = 0, done_p = 0, done_env = 0, done_l = 0;
+  for (int64_t k = 0; k < NCH; ++k) {
+    const int64_t a = k * CH, b = std::min<int64_t>(n, a + CH);
+    if (NCH > 1) {
+      HIP_TRY(c, hipMemcpyAsync(dpcm + a, pcm + a, (size_t)(b - a) * 8, hipMemcpyHostToDevice, c->copy));
+      HIP_TRY(c, hipEventRecord(c->chunk_ev[k], c->copy));
+      HIP_TRY(c, hipStreamWaitEvent(s, c->chunk_ev[k], 0));
+    } else {
+      HIP_TRY(c, hipMemcpyAsync(dpcm, pcm, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    }
+    // preprocessForSpeech: PreEmphasis("speech") alpha 0.97, fresh state (speech.go:238-245)
+    if (sonar::launch_preemph(dpcm, 1, n, 0.97, dy, s, a, b) != 0) return fail(c, SONAR_ERR_DEVICE, "preemph launch failed");
+    // YIN raw results on the pre-emphasised PCM (extractHarmonicFeatures :464), side stream
+    const int64_t pk = ready(b, Fp, 1024, 512);
+    if (pk > done_p) {
+      HIP_TRY(c, hipEventRecord(c->side_ev[0], s));
+      HIP_TRY(c, hipStreamWaitEvent(c->side, c->side_ev[0], 0));
+      if (sonar::launch_yin(dy, n, Fp, 512, csr, dpit, dcon, nullptr, c->side, done_p, pk) != 0)
+        return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
+      done_p = pk;
+    }
+    const int64_t fk = fp_chunks ? ready(b, F, W, H) : (b >= n ? F : 0);
+    if (fk > done_fp) {
+      const int rc = sonar::detail::fingerprint_impl(c, dpcm, n, &cfg, &fo, true, done_fp, fk);
+      if (rc != SONAR_OK) return rc;
+      done_fp = fk;
+    }
+    const int64_t ek = ready(b, Fe, fc->window_size, fc->hop_size);
+    if (ek > done_e && sonar::launch_energy(dpcm, 1, n, Fe, fc->window_size, fc->hop_size, 0.97, den, 1, s, done_e, ek) != 0)
+      return fail(c, SONAR_ERR_DEVICE, "energy launch failed");
+    done_e = std::max(done_e, ek);
+    const int64_t vk = ready(b, Fenv, 512, 256);
+    if (vk > done_env && sonar::launch_energy(dpcm, 1, n, Fenv, 512, 256, 0.97, denv, 1, s, done_env, vk) != 0)
+      return fail(c, SONAR_ERR_DEVICE, "envelope launch failed");
+    done_env = std::max(done_env, vk);
+    const int64_t lk = ready(b, Fl, lw, lh);
+    if (lk > done_l && sonar::launch_energy(dpcm, 1, n, Fl, lw, lh, 0.97, dld, 1, s, done_l, lk) != 0)
+      return fail(c, SONAR_ERR_DEVICE, "loudness launch failed");
+    done_l = std::max(done_l, lk);
+  }
   HIP_TRY(c, hipEventRecord(c->side_ev[1], c->side));
-  int rc = sonar_fingerprint(c, dpcm, n, &cfg, &fo);
-  if (rc != SONAR_OK) return rc;
   HIP_TRY(c, hipStreamWaitEvent(s, c->side_ev[1], 0));
   // whole-signal statistics of the pre-emphasised PCM
   const int SB = 256;
   double* dpart = (double*)dbuf(c, "sx.stats", SB * 4 * 8);
   if (sonar::launch_stats(dy, n, dpart, SB, s) != 0) return fail(c, SONAR_ERR_DEVICE, "stats launch failed");
-  // extractSimpleEnvelope (speech.go:752-777): RMS 512/256 of the pre-emphasised PCM
-  const int64_t Fenv = sonar_energy_frames(n, 512, 256);
-  double* denv = (double*)dbuf(c, "sx.env", std::max<int64_t>(Fenv, 1) * 8);
-  if (Fenv > 0 && sonar::launch_energy(dpcm, 1, n, Fenv, 512, 256, 0.97, denv, 1, s) != 0)
-    return fail(c, SONAR_ERR_DEVICE, "envelope launch failed");
-  // ComputeLoudnessRange (energy.go:145-178): 400 ms / 100 ms RMS frames when sr > 0
-  const int lw = (int)(0.4 * (double)csr);
-  const int lh = std::max(1, lw / 4);
-  const int64_t Fl = csr > 0 ? sonar_energy_frames(n, lw, lh) : 0;
-  double* dld = (double*)dbuf(c, "sx.loud", std::max<int64_t>(Fl, 1) * 8);
-  if (Fl > 0 && sonar::launch_energy(dpcm, 1, n, Fl, lw, lh, 0.97, dld, 1, s) != 0)
-    return fail(c, SONAR_ERR_DEVICE, "loudness launch failed");
   double* dtilt = (double*)dbuf(c, "sx.tilt", std::max<int64_t>(Fp, 1) * 8);
   if (fc->enable_speech_features && sonar::launch_tilt(dy, n, Fp, dtilt, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "tilt launch failed");

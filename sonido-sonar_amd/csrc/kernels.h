@@ -35,6 +35,7 @@ struct FpParams {
   int64_t F;            // STFT frames
   int W, H;             // window / hop
   int64_t frames_per_wave;   // multiple of the batch size
+  int64_t f_first, f_last;   // the frames this launch computes: [f_first, f_last) of F
   const void* window;   // W coefficients, precision T
   uint32_t flags;       // SONAR_FP_* bits (see sonar_gpu.h); bit 31: debug FFT-only
   // filterbank + MFCC
@@ -78,6 +79,7 @@ struct SpecParams {
   int K;                // bins per row (W/2 + 1)
   int sample_rate;
   int64_t frames_per_wave;
+  int64_t f_first, f_last;   // the frames this launch reduces: [f_first, f_last) of F (flux reads row f_first - 1)
   int out_f64;
   void* out_spec[9];    // centroid, rolloff, bandwidth, flatness, crest, slope, flux(F-1), low, high
 };
@@ -135,15 +137,16 @@ int launch_mfcc_rows(const double* mag, int64_t F, int K, const int* lo, const i
                      const double* w, int n_mels, const double* dct, const double* lift, int n_mfcc, int input_power,
                      void* out, int out_f64, hipStream_t s);
 // ZCR + short-time energy on the pre-emphasised PCM (misc_kernels.hip)
+// [f0, f1): only those frames (f1 < 0: to the end) -- the chunked host-PCM pipeline
 int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, double alpha, int sample_rate,
-               void* out, int out_f64, hipStream_t s);
+               void* out, int out_f64, hipStream_t s, int64_t f0 = 0, int64_t f1 = -1);
 int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H, double alpha,
-                  void* out, int out_f64, hipStream_t s);
+                  void* out, int out_f64, hipStream_t s, int64_t f0 = 0, int64_t f1 = -1);
 // EnergyEntropy (extractors/speech.go:429-433) of the short-time energy frames (misc_kernels.hip)
 int launch_energy_entropy(const double* e, int64_t n, double* out, hipStream_t s);
 // YIN raw per-frame results (misc_kernels.hip); frames start at 0, hop, 2 hop, ...
 int launch_yin(const double* pcm, int64_t n, int64_t frames, int64_t hop, int sample_rate, double* pitch,
-               double* conf, int32_t* tau, hipStream_t s);
+               double* conf, int32_t* tau, hipStream_t s, int64_t f0 = 0, int64_t f1 = -1);
 // VoiceQualityAnalyzer helpers (misc_kernels.hip): per-period RMS, 2048-lag HNR autocorrelation
 int launch_period_rms(const double* y, const int64_t* start, const int64_t* len, int64_t np, double* amp,
                       hipStream_t s);
@@ -155,7 +158,8 @@ int launch_chroma(const double* y, int64_t n, int64_t frames, int hop, int fs, c
 int launch_dc_preemph(const double* x, int64_t n, double R, double alpha, double* y, double* scratch, hipStream_t s);
 size_t dc_preemph_scratch_bytes(int64_t n);
 // speech-extractor helpers (misc_kernels.hip)
-int launch_preemph(const void* pcm, int pcm_f64, int64_t n, double alpha, double* y, hipStream_t s);
+int launch_preemph(const void* pcm, int pcm_f64, int64_t n, double alpha, double* y, hipStream_t s, int64_t i0 = 0,
+                   int64_t i1 = -1);
 int launch_stats(const double* y, int64_t n, double* part, int blocks, hipStream_t s);
 int launch_tilt(const double* y, int64_t n, int64_t frames, double* tilt, hipStream_t s);
 // PCM ingest: f64 -> f32 (RNE); both pointers 16-B aligned (misc_kernels.hip)

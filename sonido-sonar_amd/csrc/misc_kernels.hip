@@ -36,10 +36,10 @@ __device__ __forceinline__ void store_out(void* out, int f64, int64_t i, double 
 }  // namespace
 
 // one wave per frame; crossing count is an exact integer reduction
-__global__ __launch_bounds__(256) void zcr_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H,
-                                                  double alpha, int sr, void* out, int out_f64) {
+__global__ __launch_bounds__(256) void zcr_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t f0, int64_t F,
+                                                  int W, int H, double alpha, int sr, void* out, int out_f64) {
   const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t t = f0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // frames [f0, F)
   if (t >= F) return;
   const int64_t s = t * H;
   int64_t e = s + W; if (e > n) e = n;
@@ -93,9 +93,9 @@ constexpr int kEnP = 8;                  // samples per round
 constexpr int kEnRow = kEnP + 2;         // LDS row stride in doubles
 
 template <bool BJ>
-__global__ __launch_bounds__(256) void energy_wave_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W,
-                                                          int H, double alpha, void* out, int out_f64,
-                                                          const MfJob* jobs) {
+__global__ __launch_bounds__(256) void energy_wave_kernel(const void* pcm, int pcm_f64, int64_t n, int64_t fbase,
+                                                          int64_t Fe, int W, int H, double alpha, void* out,
+                                                          int out_f64, const MfJob* jobs) {
   SONAR_FEAT_PRIO();
   __shared__ __attribute__((aligned(16))) double tile[4][64 * kEnRow];
   if constexpr (BJ) {
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void energy_wave_kernel(const void* pcm, int p
     pcm = j.y; n = j.n; Fe = j.Fe; out = j.energy;
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t f0 = ((int64_t)blockIdx.x * 4 + w) * 64;        // this wave's first frame
+  const int64_t f0 = fbase + ((int64_t)blockIdx.x * 4 + w) * 64;   // this wave's first frame; frames [fbase, Fe)
   if (f0 >= Fe) return;
   double* tl = tile[w];
   // loader role: round sample (row r = 8 i + lane / 8, column c = lane % 8)
@@ -177,11 +177,11 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
-__global__ __launch_bounds__(256) void yin_kernel(const double* pcm, int64_t n, int64_t frames, int64_t hop, int sr,
-                                                  double* pitch, double* conf, int32_t* tau_out) {
+__global__ __launch_bounds__(256) void yin_kernel(const double* pcm, int64_t n, int64_t f0, int64_t frames, int64_t hop,
+                                                  int sr, double* pitch, double* conf, int32_t* tau_out) {
   __shared__ double xs[4][1024];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t fi = (int64_t)blockIdx.x * 4 + w;
+  const int64_t fi = f0 + (int64_t)blockIdx.x * 4 + w;       // frames [f0, frames)
   if (fi >= frames) return;
   const int64_t s = fi * hop;
   if (s + 1024 > n) {   // DetectPitch rejects frames != WindowSize (pitch_detection.go:226)
@@ -554,19 +554,21 @@ int launch_mfcc_rows(const double* mag, int64_t F, int K, const int* lo, const i
 }
 
 int launch_zcr(const void* pcm, int pcm_f64, int64_t n, int64_t F, int W, int H, double alpha, int sr, void* out,
-               int out_f64, hipStream_t s) {
-  if (F <= 0) return 0;
-  hipLaunchKernelGGL(zcr_kernel, dim3((unsigned)((F + 3) / 4)), dim3(256), 0, s, pcm, pcm_f64, n, F, W, H, alpha,
-                     sr, out, out_f64);
+               int out_f64, hipStream_t s, int64_t f0, int64_t f1) {
+  if (f1 < 0 || f1 > F) f1 = F;
+  if (f1 <= f0) return 0;
+  hipLaunchKernelGGL(zcr_kernel, dim3((unsigned)((f1 - f0 + 3) / 4)), dim3(256), 0, s, pcm, pcm_f64, n, f0, f1, W, H,
+                     alpha, sr, out, out_f64);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 int launch_energy(const void* pcm, int pcm_f64, int64_t n, int64_t Fe, int W, int H, double alpha, void* out,
-                  int out_f64, hipStream_t s) {
-  if (Fe <= 0) return 0;
+                  int out_f64, hipStream_t s, int64_t f0, int64_t f1) {
+  if (f1 < 0 || f1 > Fe) f1 = Fe;
+  if (f1 <= f0) return 0;
   if (W <= 0 || H <= 0) return -4;
-  hipLaunchKernelGGL(energy_wave_kernel<false>, dim3((unsigned)((Fe + 255) / 256)), dim3(256), 0, s, pcm, pcm_f64, n,
-                     Fe, W, H, alpha, out, out_f64, (const MfJob*)nullptr);
+  hipLaunchKernelGGL(energy_wave_kernel<false>, dim3((unsigned)((f1 - f0 + 255) / 256)), dim3(256), 0, s, pcm, pcm_f64,
+                     n, f0, f1, W, H, alpha, out, out_f64, (const MfJob*)nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -586,7 +588,7 @@ int launch_energy_entropy(const double* e, int64_t n, double* out, hipStream_t s
 }
 
 int launch_yin(const double* pcm, int64_t n, int64_t frames, int64_t hop, int sr, double* pitch, double* conf,
-               int32_t* tau, hipStream_t s) {
+               int32_t* tau, hipStream_t s, int64_t f0, int64_t f1) {
   // the window table is a per-device symbol: uploaded once per device of the process
   static std::atomic<uint64_t> init_mask{0};
   int dev = 0;
@@ -597,8 +599,9 @@ int launch_yin(const double* pcm, int64_t n, int64_t frames, int64_t hop, int sr
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_yin_win), w, sizeof(w)) != hipSuccess) return -5;
     init_mask.fetch_or(1ull << dev);
   }
-  if (frames <= 0) return 0;
-  hipLaunchKernelGGL(yin_kernel, dim3((unsigned)((frames + 3) / 4)), dim3(256), 0, s, pcm, n, frames, hop, sr, pitch,
+  if (f1 < 0 || f1 > frames) f1 = frames;
+  if (f1 <= f0) return 0;
+  hipLaunchKernelGGL(yin_kernel, dim3((unsigned)((f1 - f0 + 3) / 4)), dim3(256), 0, s, pcm, n, f0, f1, hop, sr, pitch,
                      conf, tau);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
@@ -839,7 +842,7 @@ int launch_music_features_batch(const MfJob* hjobs, const MfJob* djobs, int nj, 
   hipLaunchKernelGGL((dc_block_kernel<true, true>), gdc, dim3(256), 0, s, nullptr, 0, R, RL, alpha, nullptr, nullptr,
                      nullptr, djobs);
   hipLaunchKernelGGL((energy_wave_kernel<true>), dim3((unsigned)((maxFe + 255) / 256), (unsigned)nj), dim3(256), 0, s,
-                     nullptr, 1, 0, 0, W, H, 0.0, nullptr, 1, djobs);
+                     nullptr, 1, 0, 0, 0, W, H, 0.0, nullptr, 1, djobs);
   const dim3 gch((unsigned)((maxF + 3) / 4), (unsigned)nj);
   if (fs == 256)
     hipLaunchKernelGGL((chroma_wave_kernel<4, true>), gch, dim3(256), 0, s, nullptr, 0, 0, H, window, trig, cls, nullptr, djobs);
@@ -850,8 +853,8 @@ int launch_music_features_batch(const MfJob* hjobs, const MfJob* djobs, int nj, 
 
 // ---- speech-extractor helpers -------------------------------------------
 // y = PreEmphasis.ProcessBuffer(x) (pre_emphasis.go:184-190), float64 output
-__global__ void preemph_kernel(const void* pcm, int pcm_f64, int64_t n, double alpha, double* y) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+__global__ void preemph_kernel(const void* pcm, int pcm_f64, int64_t i0, int64_t i1, double alpha, double* y) {
+  for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x)
     y[i] = preemph(pcm, pcm_f64, i, alpha);
 }
 
@@ -894,10 +897,12 @@ __global__ void tilt_kernel(const double* y, int64_t n, int64_t frames, double* 
   tilt[i] = lo > 0 ? -10.0 * log10(hi / lo) : 0.0;
 }
 
-int launch_preemph(const void* pcm, int pcm_f64, int64_t n, double alpha, double* y, hipStream_t s) {
-  if (n <= 0) return 0;
-  int64_t blocks = (n + 255) / 256; if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(preemph_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pcm, pcm_f64, n, alpha, y);
+int launch_preemph(const void* pcm, int pcm_f64, int64_t n, double alpha, double* y, hipStream_t s, int64_t i0,
+                   int64_t i1) {
+  if (i1 < 0 || i1 > n) i1 = n;
+  if (i1 <= i0) return 0;
+  int64_t blocks = (i1 - i0 + 255) / 256; if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(preemph_kernel, dim3((unsigned)blocks), dim3(256), 0, s, pcm, pcm_f64, i0, i1, alpha, y);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 int launch_stats(const double* y, int64_t n, double* part, int blocks, hipStream_t s) {

@@ -370,6 +370,9 @@ void sonar_destroy(sonar_ctx* c) {
   for (auto& e : c->side_ev)
     if (e) hipEventDestroy(e);
   if (c->side) hipStreamDestroy(c->side);
+  for (auto e : c->chunk_ev)
+    if (e) hipEventDestroy(e);
+  if (c->copy) hipStreamDestroy(c->copy);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -538,13 +541,15 @@ int fp_plan(const sonar_fp_cfg* cfg, int64_t F) {
 }
 
 // spec_rows_kernel over F float64 |X| rows of K bins into the descriptor outputs (nullable each)
-int launch_spec(const double* mag, int64_t F, int K, int sample_rate, bool o64, void* const* d_spec, hipStream_t s) {
+int launch_spec(const double* mag, int64_t F, int K, int sample_rate, bool o64, void* const* d_spec, hipStream_t s,
+                int64_t f_lo, int64_t f_hi) {
   sonar::SpecParams sp{};
   sp.mag = mag; sp.F = F; sp.K = K; sp.sample_rate = sample_rate; sp.out_f64 = o64 ? 1 : 0;
+  sp.f_first = f_lo; sp.f_last = f_hi;
   for (int d = 0; d < 9; d++) sp.out_spec[d] = d_spec[d];
   // ~24 resident waves per CU over 256 CUs, a contiguous frame run each
   const int64_t target = 256 * 24;
-  sp.frames_per_wave = std::max<int64_t>(1, (F + target - 1) / target);
+  sp.frames_per_wave = std::max<int64_t>(1, (f_hi - f_lo + target - 1) / target);
   return sonar::launch_spec_rows(sp, s);
 }
 
@@ -582,7 +587,7 @@ namespace detail {
 // pcm_dev: pcm is already device memory even though the outputs are host buffers
 // (cfg->device_ptrs == 0) -- the sonar_fingerprint_f64le path (ingest_api.cpp)
 int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cfg* cfg, sonar_fp_out* out,
-                     bool pcm_dev) {
+                     bool pcm_dev, int64_t f_lo, int64_t f_hi) {
   if (!c || !cfg || !out) return fail(c, SONAR_ERR_INVALID, "null argument");
   // ComputeSTFTWithWindow validation order (spectral.go:386-412), then the GPU path's limits
   int64_t F = 0;
@@ -591,6 +596,14 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     const int rc = fp_validate(cfg, n, pcm != nullptr, &F, &msg);
     if (rc != SONAR_OK) return fail(c, rc, msg);
   }
+  // a frame range [f_lo, f_hi) of the whole signal's STFT (the chunked host-PCM pipeline of the
+  // speech extractor): device outputs, the per-frame fused kernel, no energy frames
+  if (f_hi < 0 || f_hi > F) f_hi = F;
+  if (f_lo < 0) f_lo = 0;
+  const bool ranged = f_lo > 0 || f_hi < F;
+  if (ranged && (cfg->device_ptrs == 0 || fp_plan(cfg, F) != SONAR_PLAN_WAVE || (cfg->flags & SONAR_FP_ENERGY)))
+    return fail(c, SONAR_ERR_UNSUPPORTED, "frame ranges need device outputs and the per-frame fused kernel");
+  if (f_hi <= f_lo) return SONAR_OK;
   const int W = cfg->window_size, H = cfg->hop_size;
   const uint32_t flags = cfg->flags;
   // The spectral descriptors always take the float64 transform, whatever `precision` says: the
@@ -698,7 +711,7 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
                                 (const double*)t.dct, (const double*)t.lift, t.n_mfcc, cfg->mfcc_input_power, d_mfcc,
                                 o64, s) != 0)
       return fail(c, SONAR_ERR_DEVICE, "mfcc launch failed");
-    if ((flags & SONAR_FP_SPECTRAL) && launch_spec(mag, F, K, cfg->sample_rate, o64, d_spec, s) != 0)
+    if ((flags & SONAR_FP_SPECTRAL) && launch_spec(mag, F, K, cfg->sample_rate, o64, d_spec, s, 0, F) != 0)
       return fail(c, SONAR_ERR_DEVICE, "spectral descriptor launch failed");
     timed_end(c, s, tend);
     c->last_fp_kernel = "stft_dft_kernel";
@@ -749,6 +762,7 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     const int PRE = sonar::fp_pre_rows(W, spec);
     sonar::FpParams p{};
     p.pcm = dpcm; p.n = n; p.pcm_f64 = pcm64; p.F = F; p.W = W; p.H = H;
+    p.f_first = f_lo; p.f_last = f_hi;
     p.flags = spec ? flags : (flags & ~(uint32_t)SONAR_FP_SPECTRAL);
     p.input_power = cfg->mfcc_input_power;
     p.n_groups = 64 / NB;
@@ -812,21 +826,21 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     int dev_cus = 256;
     hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
     const int64_t target_waves = (int64_t)dev_cus * 12;
-    int64_t fpw = (F + target_waves - 1) / target_waves;
+    int64_t fpw = (f_hi - f_lo + target_waves - 1) / target_waves;
     fpw = std::max<int64_t>(NB, (fpw + NB - 1) / NB * NB);
     p.frames_per_wave = fpw;
     hipEvent_t tend = timed_begin(c, s);
     const int rc = sonar::launch_fingerprint(p, f64, s);
     c->last_fp_kernel = "fp_wave_kernel";
     if (rc != 0) return fail(c, SONAR_ERR_DEVICE, std::string("fingerprint kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
-    if (spec_mag && launch_spec(spec_mag, F, K, cfg->sample_rate, o64, d_spec, s) != 0)
+    if (spec_mag && launch_spec(spec_mag, F, K, cfg->sample_rate, o64, d_spec, s, f_lo, f_hi) != 0)
       return fail(c, SONAR_ERR_DEVICE, "spectral descriptor launch failed");
     timed_end(c, s, tend);
   }
   if (flags & SONAR_FP_ZCR) {
     void* d = out_ptr(out->zcr, "zcr", (size_t)F);
     if (!d) return fail(c, SONAR_ERR_INVALID, "out->zcr is null");
-    if (sonar::launch_zcr(dpcm, pcm64, n, F, W, H, cfg->preemph_alpha, cfg->sample_rate, d, o64, s) != 0)
+    if (sonar::launch_zcr(dpcm, pcm64, n, F, W, H, cfg->preemph_alpha, cfg->sample_rate, d, o64, s, f_lo, f_hi) != 0)
       return fail(c, SONAR_ERR_DEVICE, "zcr launch failed");
   }
   if (flags & SONAR_FP_ENERGY) {

@@ -122,3 +122,37 @@ def test_align_features_c3_lag(ctx):
     assert got["method"] == ref["method"]
     for k in ("temporal_offset", "offset_confidence", "alignment_similarity", "alignment_quality"):
         assert got[k] == pytest.approx(ref[k], rel=1e-9, abs=1e-12), k
+
+
+@pytest.mark.parametrize("chunk", [1 << 20, 300_007])
+def test_generate_fingerprint_chunked_pcm_equals_one_shot(ctx, chunk, monkeypatch):
+    """The host-PCM pipeline (H2D in chunks on a copy stream, every frame computed once its samples
+    have landed) gives the same bits as the one-shot schedule: talk content (speech + temporal
+    blocks on) at 16 kHz with a real sample rate, and music at 44.1 kHz (F1)."""
+    for x, sr, ct in ((synth.c4_speech(seconds=90.0, sr=16000), 16000, "talk"),
+                      (synth.c2_hour(seconds=60.0).astype(np.float64), 44100, "music")):
+        cfg = ctx.fingerprint_config(window_size=1024, hop_size=256, feature_window_size=1024,
+                                     feature_hop_size=256, precision=sonar.F64)
+        monkeypatch.delenv("SONAR_PCM_CHUNK", raising=False)
+        one = ctx.generate_fingerprint(x, sr, ct, cfg)
+        monkeypatch.setenv("SONAR_PCM_CHUNK", str(chunk))
+        got = ctx.generate_fingerprint(x, sr, ct, cfg)
+        monkeypatch.delenv("SONAR_PCM_CHUNK")
+        assert got.keys() == one.keys()
+        for k in one:
+            assert np.array_equal(np.asarray(got[k]), np.asarray(one[k]), equal_nan=True), (ct, k)
+
+
+def test_extract_speech_chunked_pcm_real_rate(ctx, monkeypatch):
+    """The same at FeatureConfig.SampleRate 16000 (loudness frames, voicing, tilt, formants run)."""
+    x = synth.c4_speech(seconds=120.0, sr=16000)
+    fc = ctx.feature_config(sample_rate=16000, window_size=512, hop_size=128, stft_window_size=512, stft_hop_size=128,
+                            enable_mfcc=1, enable_speech_features=1, enable_temporal_features=1, is_news=0,
+                            precision=sonar.F64)
+    monkeypatch.delenv("SONAR_PCM_CHUNK", raising=False)
+    one = ctx.extract_speech_features(x, 16000, fc)
+    monkeypatch.setenv("SONAR_PCM_CHUNK", "500001")
+    got = ctx.extract_speech_features(x, 16000, fc)
+    assert got.keys() == one.keys()
+    for k in one:
+        assert np.array_equal(np.asarray(got[k]), np.asarray(one[k]), equal_nan=True), k
