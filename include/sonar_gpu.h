@@ -744,6 +744,27 @@ int sonar_find_best_matches(sonar_gallery* g, const int64_t* queries, int64_t nq
                             const int64_t* candidates, int64_t nc, const sonar_compare_cfg* cfg,
                             sonar_match* out, int64_t* n_matches);
 
+/* FindBestMatches over candidates split across ranks: lists[r] holds rank r's
+ * sonar_find_best_matches output (nq x max_candidates, row q at q * max_candidates) with
+ * counts[r * nq + q] valid entries and its candidates numbered from cand_base[r].  out / n_out:
+ * the result of ONE call over all ranks' candidates -- similarity descending (the single call's
+ * radix order), equal similarities in global candidate order, at most max_candidates, ranked
+ * from 1, candidate = cand_base[r] + local position.  Host-only (no device); the rank-local lists
+ * can come from other processes (torch.distributed all-gather) or sonar_find_best_matches_multi. */
+int sonar_merge_matches(const sonar_match* const* lists, const int64_t* counts, const int64_t* cand_base,
+                        int32_t nlists, int64_t nq, int32_t max_candidates, sonar_match* out, int64_t* n_out);
+
+/* FingerprintComparator.FindBestMatches (fingerprint/comparison.go:197-263) over rank-local
+ * galleries: galleries[g] lives on rank g's context (sonar_multi_ctx); queries[g] are the query
+ * fingerprints' indices in galleries[g] (every rank holds the queries); candidates[g] / nc[g] rank
+ * g's candidates (candidates NULL: every gallery whole, nc ignored).  Each rank ranks its own
+ * candidates, the per-rank top max_candidates travel through one RCCL all-gather, and
+ * sonar_merge_matches gives out[q * max_candidates + k] / n_matches[q] equal to one call over the
+ * concatenated candidates (rank g's numbered after those of ranks 0..g-1).  Synchronous. */
+int sonar_find_best_matches_multi(sonar_multi* m, sonar_gallery* const* galleries, const int64_t* const* queries,
+                                  int64_t nq, const int64_t* const* candidates, const int64_t* nc,
+                                  const sonar_compare_cfg* cfg, sonar_match* out, int64_t* n_matches);
+
 /* result accessors: rows*cols float64 values, row-major; scalars are 1x1 */
 int sonar_result_get(const sonar_result* res, const char* name, const double** data, int64_t* rows,
                      int64_t* cols);

@@ -27,6 +27,12 @@ struct sonar_gallery {
   std::vector<void*> seqs;            // kept SpectralCentroid / SpectralRolloff copies
 };
 
+namespace sonar {
+namespace detail {
+sonar_ctx* gallery_ctx(const sonar_gallery* g) { return g ? g->c : nullptr; }
+}  // namespace detail
+}  // namespace sonar
+
 namespace {
 
 constexpr double kNaN = std::numeric_limits<double>::quiet_NaN();
@@ -387,6 +393,48 @@ int sonar_find_best_matches(sonar_gallery* g, const int64_t* queries, int64_t nq
   }
   HIP_TRY(c, hipStreamSynchronize(s));
   for (int64_t q = 0; q < nq; q++) n_matches[q] = std::min<int64_t>(cnt[q], K);
+  return SONAR_OK;
+}
+
+// FindBestMatches over candidates split across ranks (comparison.go:197-263): the single call's
+// order is similarity descending -- in the radix order of its device sort, i.e. the doubles'
+// order-preserving 64-bit keys -- with ties in candidate order; a rank's top max_candidates hold
+// every match of the global top max_candidates that lies in that rank, so merging the per-rank
+// lists under the same order (candidates renumbered by their rank's base) is exact.
+int sonar_merge_matches(const sonar_match* const* lists, const int64_t* counts, const int64_t* cand_base,
+                        int32_t nlists, int64_t nq, int32_t max_candidates, sonar_match* out, int64_t* n_out) {
+  if (nlists < 0 || nq < 0 || max_candidates < 0) return SONAR_ERR_INVALID;
+  if (nq > 0 && (!n_out || (nlists > 0 && (!lists || !counts || !cand_base)))) return SONAR_ERR_INVALID;
+  const int64_t K = max_candidates;
+  if (K > 0 && nq > 0 && !out) return SONAR_ERR_INVALID;
+  auto key = [](double d) {
+    uint64_t u;
+    std::memcpy(&u, &d, 8);
+    return (u >> 63) ? ~u : (u | (uint64_t(1) << 63));
+  };
+  struct Item { uint64_t k; int64_t cand; const sonar_match* m; };
+  std::vector<Item> items;
+  for (int64_t q = 0; q < nq; ++q) {
+    items.clear();
+    for (int32_t r = 0; r < nlists; ++r) {
+      const int64_t cnt = std::min<int64_t>(counts[(int64_t)r * nq + q], K);
+      for (int64_t k = 0; k < cnt; ++k) {
+        const sonar_match* m = lists[r] + q * K + k;
+        items.push_back({key(m->similarity.overall_similarity), cand_base[r] + m->candidate, m});
+      }
+    }
+    std::sort(items.begin(), items.end(), [](const Item& a, const Item& b) {
+      return a.k != b.k ? a.k > b.k : a.cand < b.cand;
+    });
+    const int64_t take = std::min<int64_t>((int64_t)items.size(), K);
+    for (int64_t k = 0; k < take; ++k) {
+      sonar_match m = *items[k].m;
+      m.candidate = items[k].cand;
+      m.rank = (int32_t)(k + 1);
+      out[q * K + k] = m;
+    }
+    n_out[q] = take;
+  }
   return SONAR_OK;
 }
 

@@ -172,6 +172,8 @@ struct AlignIn {
 };
 void align_finish(const AlignIn& in, sonar_result* res, sonar_pair_record* rec);
 hipEvent_t timed_begin(sonar_ctx* c, hipStream_t s);
+// the context a comparator gallery lives on (compare_api.cpp)
+sonar_ctx* gallery_ctx(const sonar_gallery* g);
 // ContentDetector (content_api.cpp)
 int detect_from_audio(sonar_ctx* c, const double* pcm, int64_t n, int32_t sr, double thr, int32_t* out,
                       sonar_acoustic_features* feat);

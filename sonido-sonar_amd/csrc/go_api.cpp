@@ -254,10 +254,16 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   }
   HIP_TRY(c, hipEventRecord(c->side_ev[1], c->side));
   HIP_TRY(c, hipStreamWaitEvent(s, c->side_ev[1], 0));
-  // whole-signal statistics of the pre-emphasised PCM
+  // whole-signal statistics of the pre-emphasised PCM: read by detectSpeech and the temporal
+  // block only (the music generation config enables neither, content_config.go:108-140)
   const int SB = 256;
   double* dpart = (double*)dbuf(c, "sx.stats", SB * 4 * 8);
-  if (sonar::launch_stats(dy, n, dpart, SB, s) != 0) return fail(c, SONAR_ERR_DEVICE, "stats launch failed");
+  if (!dpart) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (stats)");
+  if (fc->enable_speech_features || fc->enable_temporal_features) {
+    if (sonar::launch_stats(dy, n, dpart, SB, s) != 0) return fail(c, SONAR_ERR_DEVICE, "stats launch failed");
+  } else {
+    HIP_TRY(c, hipMemsetAsync(dpart, 0, SB * 4 * 8, s));
+  }
   double* dtilt = (double*)dbuf(c, "sx.tilt", std::max<int64_t>(Fp, 1) * 8);
   if (fc->enable_speech_features && sonar::launch_tilt(dy, n, Fp, dtilt, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "tilt launch failed");

@@ -857,4 +857,76 @@ int sonar_align_pairs_multi(sonar_multi* m, int64_t npairs, const double* const*
   return first;
 }
 
+// FindBestMatches over rank-local galleries (comparison.go:197-263, 1107-1152):
+// device g ranks the candidates of its own gallery (sonar_find_best_matches on its context), its
+// top max_candidates per query travel to every device through one RCCL all-gather, and the lists
+// are merged in the single call's order (sonar_merge_matches).  Candidates are numbered globally:
+// device g's candidate c is sum_{h<g} nc[h] + c.
+int sonar_find_best_matches_multi(sonar_multi* m, sonar_gallery* const* galleries, const int64_t* const* queries,
+                                  int64_t nq, const int64_t* const* candidates, const int64_t* nc,
+                                  const sonar_compare_cfg* cfg, sonar_match* out, int64_t* n_matches) {
+  if (!m) return SONAR_ERR_INVALID;
+  if (!galleries || !queries || !nc || !cfg) return mfail(m, SONAR_ERR_INVALID, "null argument");
+  if (cfg->max_candidates < 0) return mfail(m, SONAR_ERR_INVALID, "max candidates must not be negative");
+  if (m->comm.size() != m->ctx.size()) return mfail(m, SONAR_ERR_DEVICE, "no RCCL communicator");
+  const int G = (int)m->ctx.size();
+  const int64_t K = cfg->max_candidates;
+  if (nq <= 0) return SONAR_OK;
+  if (!n_matches || (K > 0 && !out)) return mfail(m, SONAR_ERR_INVALID, "null output");
+  for (int g = 0; g < G; ++g)
+    if (!galleries[g] || sonar::detail::gallery_ctx(galleries[g]) != m->ctx[g])
+      return mfail(m, SONAR_ERR_INVALID, "gallery " + std::to_string(g) + " does not live on rank " + std::to_string(g));
+  // per rank: [nq * K matches][nq counts]
+  const size_t lb = (size_t)(nq * K) * sizeof(sonar_match), shard = lb + (size_t)nq * 8;
+  std::vector<std::vector<char>> local(G, std::vector<char>(shard, 0));
+  std::vector<int> rcs(G, SONAR_OK);
+  std::vector<std::thread> th;
+  for (int g = 0; g < G; ++g) {
+    th.emplace_back([&, g] {
+      hipSetDevice(m->dev[g]);
+      sonar_match* lm = reinterpret_cast<sonar_match*>(local[g].data());
+      int64_t* lc = reinterpret_cast<int64_t*>(local[g].data() + lb);
+      rcs[g] = sonar_find_best_matches(galleries[g], queries[g], nq, candidates ? candidates[g] : nullptr, nc[g], cfg,
+                                       K > 0 ? lm : nullptr, lc);
+    });
+  }
+  for (auto& x : th) x.join();
+  for (int g = 0; g < G; ++g)
+    if (rcs[g] != SONAR_OK) return mfail(m, rcs[g], "rank " + std::to_string(g) + ": " + m->ctx[g]->err);
+  std::vector<void*> send(G), recv(G);
+  for (int g = 0; g < G; ++g) {
+    sonar_ctx* c = m->ctx[g];
+    hipSetDevice(m->dev[g]);
+    send[g] = dbuf(c, "mm.send", std::max<size_t>(shard, 16));
+    recv[g] = dbuf(c, "mm.recv", std::max<size_t>(shard * G, 16));
+    if (!send[g] || !recv[g]) return mfail(m, SONAR_ERR_NOMEM, "device allocation failed");
+    if (hipMemcpyAsync(send[g], local[g].data(), shard, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+      return mfail(m, SONAR_ERR_DEVICE, "match upload failed");
+  }
+  if (ncclGroupStart() != ncclSuccess) return mfail(m, SONAR_ERR_DEVICE, "ncclGroupStart failed");
+  for (int g = 0; g < G; ++g) {
+    hipSetDevice(m->dev[g]);
+    if (ncclAllGather(send[g], recv[g], shard, ncclUint8, m->comm[g], m->ctx[g]->stream) != ncclSuccess) {
+      ncclGroupEnd();
+      return mfail(m, SONAR_ERR_DEVICE, "ncclAllGather failed");
+    }
+  }
+  if (ncclGroupEnd() != ncclSuccess) return mfail(m, SONAR_ERR_DEVICE, "ncclGroupEnd failed");
+  hipSetDevice(m->dev[0]);
+  std::vector<char> host(shard * G);
+  if (hipMemcpyAsync(host.data(), recv[0], host.size(), hipMemcpyDeviceToHost, m->ctx[0]->stream) != hipSuccess ||
+      hipStreamSynchronize(m->ctx[0]->stream) != hipSuccess)
+    return mfail(m, SONAR_ERR_DEVICE, "match download failed");
+  for (int g = 1; g < G; ++g) { hipSetDevice(m->dev[g]); hipStreamSynchronize(m->ctx[g]->stream); }
+  std::vector<const sonar_match*> lists(G);
+  std::vector<int64_t> counts((size_t)G * nq), base(G, 0);
+  for (int g = 0; g < G; ++g) {
+    lists[g] = reinterpret_cast<const sonar_match*>(host.data() + g * shard);
+    std::memcpy(counts.data() + (size_t)g * nq, host.data() + g * shard + lb, (size_t)nq * 8);
+    if (g > 0) base[g] = base[g - 1] + (candidates ? nc[g - 1] : sonar_gallery_size(galleries[g - 1]));
+  }
+  const int rc = sonar_merge_matches(lists.data(), counts.data(), base.data(), G, nq, (int32_t)K, out, n_matches);
+  return rc == SONAR_OK ? SONAR_OK : mfail(m, rc, "merge failed");
+}
+
 }  // extern "C"

@@ -14,6 +14,7 @@ package sonargpu
 import "C"
 
 import (
+	"fmt"
 	"runtime"
 	"unsafe"
 )
@@ -278,4 +279,130 @@ func (g *Gallery) FindBestMatches(queries, candidates []int64, cfg CompareConfig
 		}
 	}
 	return out, nil
+}
+
+// LocalMatches is one rank's FindBestMatches output in the C ABI's layout (nq x MaxCandidates
+// records, Counts[q] valid in row q): what a rank of a distributed gallery ships to the others.
+type LocalMatches struct {
+	Records    []C.sonar_match
+	Counts     []int64
+	Candidates int64 // this rank's candidate count (the next rank's numbering starts after it)
+}
+
+// FindBestMatchesLocal ranks this gallery's candidates for each query and keeps the raw lists
+// for MergeMatches (the rank-local half of a FindBestMatches over several galleries).
+func (g *Gallery) FindBestMatchesLocal(queries, candidates []int64, cfg CompareConfig) (*LocalMatches, error) {
+	c := cfgOf(cfg)
+	nq, nc, K := len(queries), len(candidates), cfg.MaxCandidates
+	if K < 0 {
+		K = 0
+	}
+	buf := make([]C.sonar_match, nq*K+1)
+	n := make([]int64, nq+1)
+	var qp, cp *C.int64_t
+	if nq > 0 {
+		qp = (*C.int64_t)(unsafe.Pointer(&queries[0]))
+	}
+	if nc > 0 {
+		cp = (*C.int64_t)(unsafe.Pointer(&candidates[0]))
+	}
+	if rc := C.sonar_find_best_matches(g.g, qp, C.int64_t(nq), cp, C.int64_t(nc), &c, &buf[0],
+		(*C.int64_t)(unsafe.Pointer(&n[0]))); rc != 0 {
+		return nil, g.x.err(rc)
+	}
+	return &LocalMatches{Records: buf[:nq*K], Counts: n[:nq], Candidates: int64(nc)}, nil
+}
+
+// MergeMatches gives the FindBestMatches result of one call over the concatenated candidates of
+// every rank (rank r's numbered after ranks 0..r-1): sonar_merge_matches, the single call's order.
+// Candidate in the returned matches is the global position.
+func MergeMatches(parts []*LocalMatches, nq, maxCandidates int) ([][]Match, error) {
+	K := maxCandidates
+	if K < 0 {
+		K = 0
+	}
+	R := len(parts)
+	lists := C.calloc(C.size_t(R+1), C.size_t(unsafe.Sizeof(uintptr(0))))
+	defer C.free(lists)
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	counts := make([]int64, R*nq+1)
+	base := make([]int64, R+1)
+	for r, p := range parts {
+		if len(p.Records) > 0 {
+			pin.Pin(&p.Records[0])
+			(*[1 << 28]unsafe.Pointer)(lists)[r] = unsafe.Pointer(&p.Records[0])
+		}
+		copy(counts[r*nq:], p.Counts)
+		if r > 0 {
+			base[r] = base[r-1] + parts[r-1].Candidates
+		}
+	}
+	out := make([]C.sonar_match, nq*K+1)
+	n := make([]int64, nq+1)
+	if rc := C.sonar_merge_matches((**C.sonar_match)(lists), (*C.int64_t)(unsafe.Pointer(&counts[0])),
+		(*C.int64_t)(unsafe.Pointer(&base[0])), C.int32_t(R), C.int64_t(nq), C.int32_t(K), &out[0],
+		(*C.int64_t)(unsafe.Pointer(&n[0]))); rc != 0 {
+		return nil, fmt.Errorf("sonar_merge_matches: %w", ErrInvalid)
+	}
+	res := make([][]Match, nq)
+	for q := range res {
+		for k := 0; k < int(n[q]); k++ {
+			m := &out[q*K+k]
+			res[q] = append(res[q], Match{Candidate: int64(m.candidate), Rank: int(m.rank),
+				MatchType: matchTypes[m.match_type], Similarity: simOf(&m.similarity)})
+		}
+	}
+	return res, nil
+}
+
+// FindBestMatches over rank-local galleries of one process's devices (sonar_find_best_matches_multi):
+// galleries[g] must live on x's rank g; queries[g] are the queries' indices there and candidates[g]
+// rank g's candidates.  The per-rank top lists travel through one RCCL all-gather.
+func (x *Multi) FindBestMatches(galleries []*Gallery, queries, candidates [][]int64, cfg CompareConfig) ([][]Match,
+	error) {
+	G := len(galleries)
+	if G == 0 || len(queries) != G || len(candidates) != G {
+		return nil, fmt.Errorf("one gallery, query list and candidate list per rank: %w", ErrInvalid)
+	}
+	nq := len(queries[0])
+	K := cfg.MaxCandidates
+	if K < 0 {
+		K = 0
+	}
+	c := cfgOf(cfg)
+	ptrs := C.calloc(C.size_t(3*G), C.size_t(unsafe.Sizeof(uintptr(0))))
+	defer C.free(ptrs)
+	arr := (*[1 << 28]unsafe.Pointer)(ptrs)
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	nc := make([]int64, G)
+	for g := 0; g < G; g++ {
+		arr[g] = unsafe.Pointer(galleries[g].g)
+		if len(queries[g]) > 0 {
+			pin.Pin(&queries[g][0])
+			arr[G+g] = unsafe.Pointer(&queries[g][0])
+		}
+		if len(candidates[g]) > 0 {
+			pin.Pin(&candidates[g][0])
+			arr[2*G+g] = unsafe.Pointer(&candidates[g][0])
+		}
+		nc[g] = int64(len(candidates[g]))
+	}
+	out := make([]C.sonar_match, nq*K+1)
+	n := make([]int64, nq+1)
+	if rc := C.sonar_find_best_matches_multi(x.m, (**C.sonar_gallery)(ptrs), (**C.int64_t)(unsafe.Pointer(&arr[G])),
+		C.int64_t(nq), (**C.int64_t)(unsafe.Pointer(&arr[2*G])), (*C.int64_t)(unsafe.Pointer(&nc[0])), &c, &out[0],
+		(*C.int64_t)(unsafe.Pointer(&n[0]))); rc != 0 {
+		return nil, x.err(rc)
+	}
+	res := make([][]Match, nq)
+	for q := range res {
+		for k := 0; k < int(n[q]); k++ {
+			m := &out[q*K+k]
+			res[q] = append(res[q], Match{Candidate: int64(m.candidate), Rank: int(m.rank),
+				MatchType: matchTypes[m.match_type], Similarity: simOf(&m.similarity)})
+		}
+	}
+	return res, nil
 }

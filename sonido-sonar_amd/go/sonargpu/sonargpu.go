@@ -376,6 +376,62 @@ func (x *Context) AlignFeatures(qEnergy, rEnergy []float64, qChroma, rChroma [][
 	return x.collect(res), nil
 }
 
+// AlignmentMethod values of stats.AlignmentMethod (algorithms/stats/alignment.go:12-17).
+const (
+	AlignmentDTW              = int(C.SONAR_ALIGN_DTW)
+	AlignmentCrossCorrelation = int(C.SONAR_ALIGN_XCORR)
+	AlignmentPhaseCorrelation = int(C.SONAR_ALIGN_PHASE)
+	AlignmentHybrid           = int(C.SONAR_ALIGN_HYBRID)
+)
+
+// AnalyzerAlignFeatures = stats.NewAlignmentAnalyzer(method, maxLag, _, hop, _, _).AlignFeatures(query,
+// reference, sampleRate) (algorithms/stats/alignment.go:84-106), including alignWithHybrid's result
+// aliasing (:308-337).  The Result holds the AlignmentResult scalars ("offset", "offset_seconds",
+// "confidence", "similarity", "alignment_quality", "noise_level", "stability", ...), the
+// CrossCorrResult ("correlations", "peak_lag", ...) and the DTWResult ("dtw_distance",
+// "dtw_path_query", "dtw_path_reference", "dtw_path_cost") where the method ran them.
+func (x *Context) AnalyzerAlignFeatures(query, reference [][]float64, sampleRate, method, maxLag,
+	hop int) (*Result, error) {
+	q, dim := rows2(query)
+	r, _ := rows2(reference)
+	var res *C.sonar_result
+	if rc := C.sonar_analyzer_align_features(x.c, f64p(q), C.int64_t(len(query)), f64p(r), C.int64_t(len(reference)),
+		C.int32_t(dim), C.int32_t(method), C.int32_t(maxLag), C.int32_t(hop), C.int32_t(sampleRate), 0,
+		&res); rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	return x.collect(res), nil
+}
+
+// AlignAudio = AlignmentAnalyzer.AlignAudio (algorithms/stats/alignment.go:108-126): the analyzer's
+// RMS energy frames of both signals (extractEnergyFeatures, window / hop), then AlignFeatures.
+func (x *Context) AlignAudio(queryPCM, referencePCM []float64, sampleRate, method, maxLag, hop,
+	window int) (*Result, error) {
+	var res *C.sonar_result
+	if rc := C.sonar_align_audio(x.c, f64p(queryPCM), C.int64_t(len(queryPCM)), f64p(referencePCM),
+		C.int64_t(len(referencePCM)), C.int32_t(method), C.int32_t(maxLag), C.int32_t(hop), C.int32_t(window),
+		C.int32_t(sampleRate), 0, &res); rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	return x.collect(res), nil
+}
+
+// AlignAudioFiles = AlignmentExtractor.AlignAudioFiles (fingerprint/extractors/alignment.go:489-553)
+// for an extractor built by NewAlignmentExtractorWithMaxLag(&FeatureConfig{featureSampleRate, window,
+// hop}, _, maxLagSeconds): ShortTimeEnergy of both streams, the Hybrid alignment, and the
+// AlignmentFeatures fields ("temporal_offset", "offset_confidence", "alignment_similarity",
+// "alignment_quality", "feature_similarity_energy", ...; Method is "energy_correlation").
+func (x *Context) AlignAudioFiles(queryPCM, referencePCM []float64, sampleRate, featureSampleRate, hop, window int,
+	maxLagSeconds float64) (*Result, error) {
+	var res *C.sonar_result
+	if rc := C.sonar_align_audio_files(x.c, f64p(queryPCM), C.int64_t(len(queryPCM)), f64p(referencePCM),
+		C.int64_t(len(referencePCM)), C.int32_t(sampleRate), C.int32_t(featureSampleRate), C.int32_t(hop),
+		C.int32_t(window), C.double(maxLagSeconds), 0, &res); rc != C.SONAR_OK {
+		return nil, x.err(rc)
+	}
+	return x.collect(res), nil
+}
+
 // MFCCParams mirrors spectral.MFCCParams (algorithms/spectral/mfcc.go:27-34).
 type MFCCParams struct {
 	NumCoefficients, NumFilters int

@@ -280,6 +280,11 @@ def lib():
     L.sonar_compare.argtypes = [_vp, _i64p, C.c_int64, _i64p, C.c_int64, C.POINTER(CompareCfg), _vp, C.c_int32]
     L.sonar_find_best_matches.argtypes = [_vp, _i64p, C.c_int64, _i64p, C.c_int64, C.POINTER(CompareCfg),
                                           C.POINTER(Match), _i64p]
+    L.sonar_merge_matches.argtypes = [C.POINTER(C.c_void_p), _i64p, _i64p, C.c_int32, C.c_int64, C.c_int32,
+                                      C.POINTER(Match), _i64p]
+    L.sonar_find_best_matches_multi.argtypes = [_vp, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int64,
+                                                C.POINTER(C.c_void_p), _i64p, C.POINTER(CompareCfg),
+                                                C.POINTER(Match), _i64p]
     L.sonar_result_get.argtypes = [_vp, C.c_char_p, C.POINTER(_d), _i64p, _i64p]
     L.sonar_result_count.argtypes = [_vp]
     L.sonar_result_name.argtypes = [_vp, C.c_int]
@@ -402,9 +407,20 @@ class Context:
         self._h = h
         self._L = L
 
+    @classmethod
+    def wrap(cls, handle, owner=None):
+        """A non-owning Context over an existing sonar_ctx (e.g. sonar_multi_ctx); `owner` is kept
+        alive with it.  close() does not destroy the handle."""
+        self = cls.__new__(cls)
+        self._h = handle if isinstance(handle, C.c_void_p) else C.c_void_p(handle)
+        self._L = lib()
+        self._borrowed = owner if owner is not None else True
+        return self
+
     def close(self):
         if getattr(self, "_h", None):
-            self._L.sonar_destroy(self._h)
+            if not getattr(self, "_borrowed", None):
+                self._L.sonar_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -924,6 +940,30 @@ class Multi:
 
     def size(self):
         return int(self._L.sonar_multi_size(self._h))
+
+    def ctx(self, rank):
+        """Rank `rank`'s context (sonar_multi_ctx) as a non-owning Context."""
+        return Context.wrap(self._L.sonar_multi_ctx(self._h, rank), owner=self)
+
+    def find_best_matches(self, galleries, queries, candidates, cfg):
+        """sonar_find_best_matches_multi: galleries[g] on rank g (sonar.compare.Gallery built on
+        Context wrappers of sonar_multi_ctx), queries[g] the queries' indices in galleries[g],
+        candidates[g] rank g's candidates (None: the whole gallery).  Returns per query the merged
+        Match list (candidates numbered globally, rank g's after ranks 0..g-1)."""
+        G = len(galleries)
+        nq = len(queries[0])
+        qs = [np.ascontiguousarray(q, dtype=np.int64) for q in queries]
+        cs = None if candidates is None else [np.ascontiguousarray(c, dtype=np.int64) for c in candidates]
+        nc = np.array([len(g) if cs is None else len(cs[i]) for i, g in enumerate(galleries)], dtype=np.int64)
+        gp = (C.c_void_p * G)(*[g._h.value for g in galleries])
+        qp = (C.c_void_p * G)(*[q.ctypes.data for q in qs])
+        cp = None if cs is None else (C.c_void_p * G)(*[c.ctypes.data if len(c) else None for c in cs])
+        K = max(0, cfg.max_candidates)
+        out = (Match * max(1, nq * K))()
+        nm = np.zeros(max(1, nq), dtype=np.int64)
+        self._check(self._L.sonar_find_best_matches_multi(self._h, gp, qp, nq, cp, nc.ctypes.data_as(_i64p),
+                                                          C.byref(cfg), out, nm.ctypes.data_as(_i64p)))
+        return [[out[i * K + k] for k in range(int(nm[i]))] for i in range(nq)]
 
     def fingerprint(self, pcm, cfg: FpConfig):
         """sonar_fingerprint_multi (host PCM, host outputs): MFCC / magnitude / descriptors."""

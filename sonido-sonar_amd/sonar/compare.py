@@ -253,6 +253,20 @@ class Gallery:
             C.c_void_p(out_ptr), 1))
         return nc
 
+    def find_best_matches_raw(self, queries, candidates, cfg: CompareCfg):
+        """sonar_find_best_matches as the C arrays: (Match array nq x K, counts[nq])."""
+        q = np.ascontiguousarray(queries, dtype=np.int64)
+        cand = None if candidates is None else np.ascontiguousarray(candidates, dtype=np.int64)
+        nc = len(self) if cand is None else len(cand)
+        K = max(0, cfg.max_candidates)
+        out = (Match * max(1, len(q) * K))()
+        nm = np.zeros(max(1, len(q)), dtype=np.int64)
+        self._ctx._check(self._L.sonar_find_best_matches(
+            self._h, q.ctypes.data_as(C.POINTER(C.c_int64)), len(q),
+            None if cand is None else cand.ctypes.data_as(C.POINTER(C.c_int64)), nc, C.byref(cfg), out,
+            nm.ctypes.data_as(C.POINTER(C.c_int64))))
+        return out, nm[: len(q)]
+
     def find_best_matches(self, queries, candidates, cfg: CompareCfg):
         q = np.ascontiguousarray(queries, dtype=np.int64)
         cand = None if candidates is None else np.ascontiguousarray(candidates, dtype=np.int64)
@@ -265,6 +279,51 @@ class Gallery:
             None if cand is None else cand.ctypes.data_as(C.POINTER(C.c_int64)), nc, C.byref(cfg), out,
             nm.ctypes.data_as(C.POINTER(C.c_int64))))
         return [[out[i * K + k] for k in range(int(nm[i]))] for i in range(len(q))]
+
+
+def merge_matches(lists, counts, cand_base, nq, max_candidates):
+    """sonar_merge_matches: rank-local FindBestMatches lists (ctypes Match arrays of nq x K, with
+    counts[r][q] valid rows) -> the single call's result over all ranks' candidates, as Match
+    lists per query (candidates numbered from cand_base[r])."""
+    L = lib()
+    R, K = len(lists), max(0, int(max_candidates))
+    lp = (C.c_void_p * max(1, R))(*[C.cast(x, C.c_void_p).value for x in lists])
+    cnt = np.ascontiguousarray(np.asarray(counts, dtype=np.int64).reshape(R * nq) if R else np.zeros(1, np.int64))
+    base = np.ascontiguousarray(np.asarray(cand_base, dtype=np.int64) if R else np.zeros(1, np.int64))
+    out = (Match * max(1, nq * K))()
+    nm = np.zeros(max(1, nq), dtype=np.int64)
+    rc = L.sonar_merge_matches(lp, cnt.ctypes.data_as(C.POINTER(C.c_int64)), base.ctypes.data_as(C.POINTER(C.c_int64)),
+                               R, nq, K, out, nm.ctypes.data_as(C.POINTER(C.c_int64)))
+    if rc != OK:
+        raise SonarError(rc, "sonar_merge_matches: invalid arguments")
+    return [[out[i * K + k] for k in range(int(nm[i]))] for i in range(nq)]
+
+
+def find_best_matches_distributed(local_lists, nq, max_candidates, n_local_candidates, group=None):
+    """FindBestMatches across torch.distributed ranks (comparison.go:197-263):
+    every rank passes its own gallery's top lists (Gallery.find_best_matches_raw), the fixed-size
+    byte records are all-gathered (RCCL on GPUs, gloo in the CPU tests) with each rank's candidate
+    count, and every rank merges them in the single call's order.  Returns the merged lists."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    K = max(0, int(max_candidates))
+    matches, counts = local_lists
+    raw = C.string_at(C.addressof(matches), nq * K * C.sizeof(Match)) if nq * K else b""
+    payload = torch.frombuffer(bytearray(raw + np.asarray(counts, np.int64).tobytes()
+                                         + np.int64(n_local_candidates).tobytes()), dtype=torch.uint8)
+    parts = [torch.empty_like(payload) for _ in range(world)]
+    dist.all_gather(parts, payload, group=group)
+    lists, cnts, base, b = [], [], [], 0
+    lb = nq * K * C.sizeof(Match)
+    for part in parts:
+        buf = part.numpy().tobytes()
+        arr = (Match * max(1, nq * K)).from_buffer_copy(buf[:lb] + bytes(max(0, C.sizeof(Match) * max(1, nq * K) - lb)))
+        lists.append(arr)
+        cnts.append(np.frombuffer(buf[lb:lb + 8 * nq], dtype=np.int64))
+        base.append(b)
+        b += int(np.frombuffer(buf[lb + 8 * nq:lb + 8 * nq + 8], dtype=np.int64)[0])
+    return merge_matches(lists, cnts, base, nq, K)
 
 
 class FingerprintComparator:
