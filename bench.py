@@ -151,8 +151,10 @@ def load_traffic(kernel_name):
 
 def bench_headline_f64(args, ctx, pcm, F, dev):
     """The headline configuration at the reference's precision: float64 PCM in, every stage in
-    float64 (fp_wave_kernel<double>), float64 MFCC out -- what the Go path computes.  HIP events
-    around 5 launches after 2 warm-ups; the PCM is converted to float64 on the device before."""
+    float64 (mfcc_pair_kernel<double> since round 6), float64 MFCC out -- what the Go path computes.
+    HIP events around 5 launches after 2 warm-ups; the PCM is converted to float64 on the device
+    before.  generic_kernel_ms: the general fused kernel (fp_wave_kernel<double>, SONAR_FP_GENERIC)
+    on the same bytes, the round-5 path, for comparison."""
     pcm64 = pcm.double()
     n = pcm64.numel()
     out64 = torch.empty((F, N_MFCC), dtype=torch.float64, device=dev)
@@ -176,6 +178,19 @@ def bench_headline_f64(args, ctx, pcm, F, dev):
            "fp64_frac": F * FLOPS_PER_FRAME / (kms * 1e-3) / 1e12 / FP64_PEAK_TFS,
            "hbm_gbs": F * (8 * H + 8 * N_MFCC) / (kms * 1e-3) / 1e9}
     host = out64.cpu().numpy()
+    gen = ctx.config(window_size=W, hop_size=H, sample_rate=SR, n_filters=N_MELS, n_mfcc=N_MFCC,
+                     precision=sonar.F64, pcm_dtype=sonar.F64, out_dtype=sonar.F64,
+                     flags=sonar.FP_MFCC | sonar.FP_GENERIC)
+    ctx.fingerprint_device(pcm64.data_ptr(), n, gen, mfcc=out64.data_ptr())
+    torch.cuda.synchronize()
+    ctx.last_kernel_ms()
+    ctx.enable_kernel_timing(True)
+    for _ in range(3):
+        ctx.fingerprint_device(pcm64.data_ptr(), n, gen, mfcc=out64.data_ptr())
+    torch.cuda.synchronize()
+    ctx.enable_kernel_timing(False)
+    res["generic_kernel_ms"] = ctx.last_kernel_ms()
+    res["generic_kernel"] = ctx.last_fp_kernel()
     del pcm64, out64
     return res, host
 

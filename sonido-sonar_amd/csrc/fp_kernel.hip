@@ -116,14 +116,22 @@ template <typename P> struct Vec2;
 template <> struct Vec2<float> { using type = float2; };
 template <> struct Vec2<double> { using type = double2; };
 
+#ifndef FP64_MIN_WAVES
+#define FP64_MIN_WAVES 1
+#endif
+// FP64_MIN_WAVES: waves per SIMD the float64 MFCC / magnitude instance at W = 1024 is compiled for
 template <typename T, typename P, int R, bool SPEC, bool CPLX = false>
-__global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
+__global__ __launch_bounds__(256, (sizeof(T) == 8 && !SPEC && !CPLX && R == 8) ? FP64_MIN_WAVES : 1)
+void fp_wave_kernel(FpParams p) {
   constexpr int FR = (R >= 8) ? 1 : 8 / R;   // frames per FFT unit
   constexpr int V = R * FR;                   // values per lane
   constexpr int G = V / 8;                    // 8-column groups
   constexpr int M = 64 * R;                   // complex FFT size
   constexpr int K = M + 1;                    // bins per frame (LDS row stride)
-  constexpr int NB = FR > 4 ? FR : 4;         // frames per epilogue batch
+  // frames per epilogue batch: float64 MFCC / magnitude launches take one FFT unit per batch (the
+  // whole wave on its filterbank, ln and DCT), so a wave's LDS is one unit's rows and three 4-wave
+  // blocks fit per CU; float32 and the fused SPEC epilogue batch at least four frames
+  constexpr int NB = (sizeof(T) == 8 && !SPEC) ? FR : (FR > 4 ? FR : 4);
   constexpr int NG = 64 / NB;                 // epilogue lanes per frame
   constexpr int UPB = NB / FR;                // units per batch
   constexpr int PRE = SPEC ? FR : 0;          // rows before the batch (flux predecessor unit)
@@ -235,12 +243,22 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
     }
   };
 
+  // the next unit's PCM in registers during the current FFT (PF); the float64 MFCC / magnitude
+  // instance runs more waves per SIMD instead (FP64_PREFETCH=1 restores it for A/B)
+#ifndef FP64_PREFETCH
+#define FP64_PREFETCH 1
+#endif
+#ifndef FP64_WINREG
+#define FP64_WINREG 1
+#endif
+  constexpr bool PF = !(sizeof(T) == 8 && !SPEC) || FP64_PREFETCH;
   T cur_e[FR][R], cur_o[FR][R];
-  load_unit(unit_frame(0), cur_e, cur_o);
+  if (PF) load_unit(unit_frame(0), cur_e, cur_o);
 
   for (int64_t ui = 0; ui < nunits; ++ui) {
     T nxt_e[FR][R], nxt_o[FR][R];
-    if (ui + 1 < nunits) load_unit(unit_frame(ui + 1), nxt_e, nxt_o);
+    if (PF) { if (ui + 1 < nunits) load_unit(unit_frame(ui + 1), nxt_e, nxt_o); }
+    else load_unit(unit_frame(ui), cur_e, cur_o);
     const int rb = unit_row(ui);
     T* S = rows + (int64_t)rb * K;              // scratch = the unit's own rows
 
@@ -250,7 +268,12 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
 #pragma unroll
       for (int fr = 0; fr < FR; fr++)
 #pragma unroll
-        for (int a = 0; a < R; a++) { xr[fr][a] = cur_e[fr][a] * we[a]; xi[fr][a] = cur_o[fr][a] * wo[a]; }
+        for (int a = 0; a < R; a++) {
+          // FP64_WINREG=0: the window read per unit (L1-resident) instead of 2R registers held
+          const T we_ = FP64_WINREG || sizeof(T) == 4 || SPEC ? we[a] : win[2 * (64 * a + lane)];
+          const T wo_ = FP64_WINREG || sizeof(T) == 4 || SPEC ? wo[a] : win[2 * (64 * a + lane) + 1];
+          xr[fr][a] = cur_e[fr][a] * we_; xi[fr][a] = cur_o[fr][a] * wo_;
+        }
       // step 1: R-point DFT over a, twiddle w_M^{lane c}
 #pragma unroll
       for (int fr = 0; fr < FR; fr++) {
@@ -405,10 +428,12 @@ __global__ __launch_bounds__(256) void fp_wave_kernel(FpParams p) {
       }
       wave_lds_sync();
     }
+    if (PF) {
 #pragma unroll
-    for (int fr = 0; fr < FR; fr++)
+      for (int fr = 0; fr < FR; fr++)
 #pragma unroll
-      for (int a = 0; a < R; a++) { cur_e[fr][a] = nxt_e[fr][a]; cur_o[fr][a] = nxt_o[fr][a]; }
+        for (int a = 0; a < R; a++) { cur_e[fr][a] = nxt_e[fr][a]; cur_o[fr][a] = nxt_o[fr][a]; }
+    }
 
     // ======================= batch epilogue (lane = frame x group) ==========
     const int64_t bi_ = pre ? ui - 1 : ui;
@@ -871,10 +896,10 @@ int launch_fingerprint(const FpParams& p, int f64, hipStream_t s) {
 }
 
 // batch geometry shared with the host (LDS carve)
-int fp_batch_frames(int W) {
+int fp_batch_frames(int W, int f64, int spec) {
   const int R = W / 128;
   const int FR = R >= 8 ? 1 : 8 / R;
-  return FR > 4 ? FR : 4;
+  return (f64 && !spec) ? FR : (FR > 4 ? FR : 4);
 }
 int fp_pre_rows(int W, int spec) {
   const int R = W / 128;

@@ -85,45 +85,48 @@ struct SpecParams {
 };
 int launch_spec_rows(const SpecParams& p, hipStream_t s);
 
-// Headline fused kernel (mfcc_pair.hip): float32, W = 1024, MFCC output only.
-// One wave transforms two consecutive frames as one 1024-point complex FFT.
+// Headline fused kernel (mfcc_pair.hip): W = 1024, MFCC output only, float32 (the headline) or
+// float64 arithmetic (f64 = 1: float64 tables and output, PCM float32 or float64 per pcm_f64).
+// One wave transforms two consecutive frames as one 1024-point complex FFT.  Table element type
+// T = float or double per f64; "complex" = {T re, T im}.
 struct MfccPairParams {
-  const float* pcm;     // device f32
+  const void* pcm;      // device PCM (float, or double when pcm_f64)
   int64_t n;            // samples
   int64_t F;            // STFT frames
   int H;                // hop
   int64_t pairs_per_block;   // contiguous pairs per block (one block per CU), claimed pair by pair by its waves
-  const float* window;  // [1024]
-  const float2* tw1;    // [64][16]  w_1024^{b k1}
-  const float2* tw2;    // [8][8]    w_64^{b0 c0}
+  const void* window;   // [1024] T
+  const void* tw1;      // [64][16] complex  w_1024^{b k1}
+  const void* tw2;      // [8][8]   complex  w_64^{b0 c0}
   const int* chunk_ks;  // [64] first bin of each lane's filterbank chunk
-  const float2* chunk_w;   // [64][JS] (weight of slot a, weight of slot b), 1/4 (or 1/16) folded
-  const uint16_t* mel_src; // [16][64] partial-sum float2 index (2 lane + slot), bit 15 = unused
-  const float* dct;     // [16][NMP + 4] DCT-II rows with the lifter folded in
-  const float* zeros;   // [1024] zeros: the samples of frames past the signal
+  const void* chunk_w;  // [64][JS] complex (weight of slot a, weight of slot b), 1/4 (or 1/16) folded
+  const uint16_t* mel_src; // [16][64] partial-sum pair index (2 lane + slot), bit 15 = unused
+  const void* dct;      // [16][NMP + 4] T: DCT-II rows with the lifter folded in
+  const void* zeros;    // [1024] zero PCM samples (8 KB): the samples of frames past the signal
   int J;                // bins per chunk (<= 16)
-  int JS;               // chunk_w row stride = J | 1 (odd: conflict-free b64 reads)
+  int JS;               // chunk_w row stride = J | 1 (odd: conflict-free reads)
   int max_src;          // most partial sums of one filter (<= 16)
   int NMP;              // n_mels padded to a multiple of 8 (<= 64)
   int n_mels, n_mfcc;   // n_mfcc <= 16
   int pow2;             // F5: MFCC.Compute fed |X|^2 -> filterbank of |X|^4
-  float* out;           // [F][n_mfcc]
-  int lds_src, lds_dct, lds_ctr, lds_wave0, lds_bytes;
-  int waves_per_block;  // 12 (mfcc_pair_kernel)
-  // sonar_fingerprint_batch: nseg > 0 signals, F = 2 x the batch's pairs, pcm / n / out unused;
-  // seg (device) = {pcm address[nseg], frames inside the signal[nseg], F[nseg], out address[nseg],
-  // first pair[nseg + 1]}
+  void* out;            // [F][n_mfcc] T
+  int lds_src, lds_dct, lds_ctr, lds_tw2, lds_wave0, lds_bytes;   // lds_tw2: float64 only (64 complex)
+  int waves_per_block;  // mfcc_pair_waves_per_block(f64)
+  // sonar_fingerprint_batch (float32 only): nseg > 0 signals, F = 2 x the batch's pairs, pcm / n /
+  // out unused; seg (device) = {pcm address[nseg], frames inside the signal[nseg], F[nseg], out
+  // address[nseg], first pair[nseg + 1]}
   const int64_t* seg;
   int nseg;
+  int f64, pcm_f64;
   uint64_t* stamp;      // HL_STAMP diagnostics builds only: per wave {start, end, pairs}
 };
 int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s);
-int mfcc_pair_wave_bytes();
-int mfcc_pair_waves_per_block();   // waves per block of mfcc_pair_kernel (its LDS carve: tables + waves x wave bytes)
-int mfcc_pair_waves_per_cu();      // resident waves per CU it is sized for
+int mfcc_pair_wave_bytes(int f64);
+int mfcc_pair_waves_per_block(int f64);   // waves per block of mfcc_pair_kernel (its LDS carve: tables + waves x wave bytes)
+int mfcc_pair_waves_per_cu(int f64);      // resident waves per CU it is sized for
 int mfcc_pair_rows();
 bool fingerprint_supported(int W);
-int fp_batch_frames(int W);
+int fp_batch_frames(int W, int f64, int spec);
 int fp_pre_rows(int W, int spec);
 
 // STFT for window lengths outside the fused kernels (any W <= 8192, misc_kernels.hip): direct

@@ -269,7 +269,7 @@ bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
   std::vector<int> lane_of(64);
   for (int l = 0; l < 64; l++) lane_of[order[l]] = l;
   std::vector<int> ks(64, 0);
-  std::vector<float> cw(64 * 2 * JS, 0.f);
+  std::vector<double> cw(64 * 2 * JS, 0.0);
   std::vector<std::vector<int>> src(64);
   for (size_t ci = 0; ci < chunks.size(); ci++) {   // chunk order = ascending bins
     const Chunk& ch = chunks[ci];
@@ -278,8 +278,8 @@ bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
     const int lane = lane_of[ci], k0 = ch.k0;
     ks[lane] = k0;
     for (int i = 0; i < J && k0 + i < g.k1; i++) {
-      cw[(lane * JS + i) * 2] = (float)(weight(g.a, k0 + i) * scale);
-      cw[(lane * JS + i) * 2 + 1] = g.b >= 0 ? (float)(weight(g.b, k0 + i) * scale) : 0.f;
+      cw[(lane * JS + i) * 2] = weight(g.a, k0 + i) * scale;
+      cw[(lane * JS + i) * 2 + 1] = g.b >= 0 ? weight(g.b, k0 + i) * scale : 0.0;
     }
     src[g.a].push_back(2 * lane);
     if (g.b >= 0) src[g.b].push_back(2 * lane + 1);
@@ -292,27 +292,31 @@ bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
     for (size_t i = 0; i < src[m].size(); i++) msrc[i * 64 + m] = (uint16_t)src[m][i];
   }
   const int NMP = (mt.n_mels + 7) / 8 * 8;
-  std::vector<float> dct(16 * (NMP + 4), 0.f);
+  std::vector<double> dct(16 * (NMP + 4), 0.0);
   for (int q = 0; q < mt.n_mfcc; q++)
-    for (int m = 0; m < mt.n_mels; m++)
-      dct[q * (NMP + 4) + m] = (float)(mt.dct[(size_t)q * mt.n_mels + m] * mt.lift[q]);
-  std::vector<float> tw1(64 * 16 * 2), tw2(64 * 2), wf(win.begin(), win.end());
+    for (int m = 0; m < mt.n_mels; m++) dct[q * (NMP + 4) + m] = mt.dct[(size_t)q * mt.n_mels + m] * mt.lift[q];
+  std::vector<double> tw1(64 * 16 * 2), tw2(64 * 2);
   for (int b = 0; b < 64; b++)
     for (int k = 0; k < 16; k++) {
       const double a = -2.0 * M_PI * (double)((b * k) % 1024) / 1024.0;
-      tw1[(b * 16 + k) * 2] = (float)std::cos(a); tw1[(b * 16 + k) * 2 + 1] = (float)std::sin(a);
+      tw1[(b * 16 + k) * 2] = std::cos(a); tw1[(b * 16 + k) * 2 + 1] = std::sin(a);
     }
   for (int b = 0; b < 8; b++)
     for (int c = 0; c < 8; c++) {
       const double a = -2.0 * M_PI * (double)(b * c) / 64.0;
-      tw2[(b * 8 + c) * 2] = (float)std::cos(a); tw2[(b * 8 + c) * 2 + 1] = (float)std::sin(a);
+      tw2[(b * 8 + c) * 2] = std::cos(a); tw2[(b * 8 + c) * 2 + 1] = std::sin(a);
     }
-  t.window = (float*)upload(wf); t.tw1 = upload(tw1); t.tw2 = upload(tw2);
-  t.chunk_ks = (int*)upload(ks); t.chunk_w = upload(cw); t.mel_src = (uint16_t*)upload(msrc);
-  t.dct = (float*)upload(dct);
-  t.zeros = (float*)upload(std::vector<float>(1024, 0.f));
+  // float32 tables = the float64 values rounded once; float64 tables as computed
+  auto f32 = [](const std::vector<double>& v) { return std::vector<float>(v.begin(), v.end()); };
+  t.window[0] = upload(f32(win)); t.tw1[0] = upload(f32(tw1)); t.tw2[0] = upload(f32(tw2));
+  t.chunk_w[0] = upload(f32(cw)); t.dct[0] = upload(f32(dct));
+  t.window[1] = upload(win); t.tw1[1] = upload(tw1); t.tw2[1] = upload(tw2);
+  t.chunk_w[1] = upload(cw); t.dct[1] = upload(dct);
+  t.chunk_ks = (int*)upload(ks); t.mel_src = (uint16_t*)upload(msrc);
+  t.zeros = upload(std::vector<double>(1024, 0.0));
   t.J = J; t.JS = JS; t.NMP = NMP; t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc; t.max_src = max_src;
-  t.ok = t.window && t.tw1 && t.tw2 && t.chunk_ks && t.chunk_w && t.mel_src && t.dct && t.zeros;
+  t.ok = t.chunk_ks && t.mel_src && t.zeros;
+  for (int i = 0; i < 2; i++) t.ok = t.ok && t.window[i] && t.tw1[i] && t.tw2[i] && t.chunk_w[i] && t.dct[i];
   return t.ok;
 }
 
@@ -503,23 +507,25 @@ const PairTables& pair_tables_for(sonar_ctx* c, const sonar_fp_cfg* cfg) {
 
 // tables, LDS carve and work split of one mfcc_pair_kernel launch over NP frame pairs
 void fill_pair_params(sonar_ctx* c, const PairTables& t, const sonar_fp_cfg* cfg, int64_t NP,
-                      sonar::MfccPairParams& q) {
-  q.window = t.window; q.tw1 = (const float2*)t.tw1; q.tw2 = (const float2*)t.tw2;
-  q.chunk_ks = t.chunk_ks; q.chunk_w = (const float2*)t.chunk_w; q.mel_src = t.mel_src; q.dct = t.dct;
-  q.zeros = t.zeros;
+                      sonar::MfccPairParams& q, bool f64 = false) {
+  const int e = f64 ? 1 : 0, es = f64 ? 8 : 4;
+  q.f64 = e;
+  q.window = t.window[e]; q.tw1 = t.tw1[e]; q.tw2 = t.tw2[e]; q.chunk_w = t.chunk_w[e]; q.dct = t.dct[e];
+  q.chunk_ks = t.chunk_ks; q.mel_src = t.mel_src; q.zeros = t.zeros;
   q.J = t.J; q.JS = t.JS; q.max_src = t.max_src; q.NMP = t.NMP; q.n_mels = t.n_mels; q.n_mfcc = t.n_mfcc;
   q.pow2 = cfg->mfcc_input_power != 0;
   auto al = [](int x) { return (x + 15) & ~15; };
-  q.lds_src = al(64 * t.JS * 8);
+  q.lds_src = al(64 * t.JS * 2 * es);
   q.lds_dct = q.lds_src + 64 * 16 * 2;
-  q.lds_ctr = q.lds_dct + al(16 * (t.NMP + 4) * 4);
-  q.lds_wave0 = q.lds_ctr + 16;
-  // mfcc_pair_kernel: one 12-wave block per CU over a contiguous range of pairs
-  q.waves_per_block = sonar::mfcc_pair_waves_per_block();
-  q.lds_bytes = q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes();
+  q.lds_ctr = q.lds_dct + al(16 * (t.NMP + 4) * es);
+  q.lds_tw2 = q.lds_ctr + 16;
+  q.lds_wave0 = q.lds_tw2 + (f64 ? 64 * 16 : 0);
+  // mfcc_pair_kernel: one block per CU (12 waves float32, 8 float64) over a contiguous range of pairs
+  q.waves_per_block = sonar::mfcc_pair_waves_per_block(e);
+  q.lds_bytes = q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes(e);
   int dev_cus = 256;
   hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  const int64_t blocks = (int64_t)dev_cus * sonar::mfcc_pair_waves_per_cu() / q.waves_per_block;
+  const int64_t blocks = (int64_t)dev_cus * sonar::mfcc_pair_waves_per_cu(e) / q.waves_per_block;
   q.pairs_per_block = std::max<int64_t>(1, (NP + blocks - 1) / blocks);
 }
 
@@ -532,8 +538,11 @@ int fp_plan(const sonar_fp_cfg* cfg, int64_t F) {
   if (!(flags & (SONAR_FP_MFCC | SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_COMPLEX | SONAR_FP_PHASE)))
     return SONAR_PLAN_NONE;
   if (!sonar::fingerprint_supported(cfg->window_size)) return SONAR_PLAN_DFT;
-  const bool pair = cfg->precision != SONAR_F64 && cfg->pcm_dtype != SONAR_F64 && cfg->out_dtype != SONAR_F64 &&
-                    cfg->window_size == 1024 && (flags & SONAR_FP_MFCC) &&
+  // the pair kernel computes in float32 with float32 PCM and output, or in float64 with float64
+  // output (PCM of either type)
+  const bool types = cfg->precision == SONAR_F64 ? cfg->out_dtype == SONAR_F64
+                                                  : cfg->pcm_dtype != SONAR_F64 && cfg->out_dtype != SONAR_F64;
+  const bool pair = types && cfg->window_size == 1024 && (flags & SONAR_FP_MFCC) &&
                     !(flags & (SONAR_FP_MAGNITUDE | SONAR_FP_SPECTRAL | SONAR_FP_COMPLEX | SONAR_FP_PHASE |
                                SONAR_FP_GENERIC | 0x80000000u)) &&
                     F <= SONAR_PAIR_MAX_FRAMES;
@@ -722,9 +731,9 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     const PairTables& t = pair_tables_for(c, cfg);
     if (t.ok) {
       sonar::MfccPairParams q{};
-      fill_pair_params(c, t, cfg, (F + 1) / 2, q);
-      q.pcm = (const float*)dpcm; q.n = n; q.F = F; q.H = H;
-      q.out = (float*)d_mfcc;
+      fill_pair_params(c, t, cfg, (F + 1) / 2, q, f64);
+      q.pcm = dpcm; q.pcm_f64 = pcm64 ? 1 : 0; q.n = n; q.F = F; q.H = H;
+      q.out = d_mfcc;
 #ifdef HL_STAMP
       const char* stamp_path = std::getenv("SONAR_HL_STAMP");
       const int64_t nw = ((F + 1) / 2 + q.pairs_per_block - 1) / q.pairs_per_block * q.waves_per_block;
@@ -758,7 +767,7 @@ int fingerprint_impl(sonar_ctx* c, const void* pcm, int64_t n, const sonar_fp_cf
     if (spec_req && f64 && !(d_mag && !o64))
       spec_mag = d_mag ? (double*)d_mag : (double*)dbuf(c, "fp.specmag", (size_t)F * K * 8);
     const bool spec = spec_req && !spec_mag;            // the fused SPEC epilogue
-    const int NB = sonar::fp_batch_frames(W);
+    const int NB = sonar::fp_batch_frames(W, f64 ? 1 : 0, spec ? 1 : 0);
     const int PRE = sonar::fp_pre_rows(W, spec);
     sonar::FpParams p{};
     p.pcm = dpcm; p.n = n; p.pcm_f64 = pcm64; p.F = F; p.W = W; p.H = H;

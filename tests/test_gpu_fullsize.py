@@ -36,7 +36,7 @@ def test_c2_full_hour_mfcc(ctx):
 
 def test_c2_f64_headline_10min(ctx):
     """The headline configuration at the reference's precision (float64 in, every stage float64,
-    fp_wave_kernel<double>) on 10 min of C2, against the oracle on the same bytes, at the 1e-9
+    mfcc_pair_kernel<double> since round 6) on 10 min of C2, against the oracle on the same bytes, at the 1e-9
     row-norm tolerance of the f64 MFCC tests (tests/parity.py's f64 tiers: 1e-8 / 1e-7 / 1e-6).
     VERDICT r04 item 1: the bench's whole-hour f64 error (3.1e-8) came from a host regeneration of
     the PCM that differs from the device one by an f32 ulp in ~1/1,500 samples; on identical bytes
@@ -45,7 +45,7 @@ def test_c2_f64_headline_10min(ctx):
     cfg = ctx.config(window_size=1024, hop_size=256, sample_rate=SR, n_filters=40, n_mfcc=13,
                      precision=sonar.F64, pcm_dtype=sonar.F64, out_dtype=sonar.F64, flags=sonar.FP_MFCC)
     got = ctx.fingerprint(x, cfg)["mfcc"]
-    assert ctx.last_fp_kernel() == "fp_wave_kernel"
+    assert ctx.last_fp_kernel() == "mfcc_pair_kernel"
     assert got.shape == (103356, 13)
     ref = O.mfcc_frames(O.stft_mag(x, 1024, 256, nthreads=16), SR, n_coef=13, n_mels=40)
     assert_mfcc(got, ref, 1e-9)

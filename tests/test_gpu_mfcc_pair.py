@@ -130,3 +130,63 @@ def test_pair_vs_generic_kernel_long(ctx):
     b = _fp(ctx, x, _cfg(ctx, flags=sonar.FP_MFCC | sonar.FP_GENERIC), "fp_wave_kernel").astype(np.float64)
     assert a.shape == b.shape
     assert _err(a, b) < 1e-4
+
+
+# ---- float64 (round 6): the same kernel templated on double -- float64 tables, arithmetic and
+# output, PCM float32 (widened exactly) or float64 -- at the f64 MFCC tolerance (1e-9 of the row
+# norm, tests/parity.py's f64 tiers).  VERDICT r05 item 4: the headline configuration at the
+# reference's precision.
+def _cfg64(ctx, pcm64=True, **kw):
+    return _cfg(ctx, precision=sonar.F64, pcm_dtype=sonar.F64 if pcm64 else sonar.F32, out_dtype=sonar.F64, **kw)
+
+
+def _x64(x, pcm64):
+    return x.astype(np.float64) if pcm64 else x.astype(np.float32)
+
+
+@pytest.mark.parametrize("pcm64", [True, False])
+@pytest.mark.parametrize("H", [256, 100, 1000])
+def test_pair_kernel_f64_matches_oracle(ctx, pcm64, H):
+    x = _x64(synth.c2_hour(seconds=7.3), pcm64)
+    got = _fp(ctx, x, _cfg64(ctx, pcm64, hop_size=H))
+    assert got.dtype == np.float64
+    ref = _ref(x, H=H)
+    assert got.shape == ref.shape
+    assert_mfcc(got, ref, 1e-9)
+
+
+@pytest.mark.parametrize("n_extra", [0, 1, 255, 257])
+def test_pair_kernel_f64_odd_even_frames(ctx, n_extra):
+    x = synth.c2_hour(seconds=0.5)[: 1024 + 256 * 40 + n_extra].astype(np.float64)
+    got = _fp(ctx, x, _cfg64(ctx))
+    ref = _ref(x)
+    assert got.shape == ref.shape == (sonar.stft_frames(len(x), 1024, 256), 13)
+    assert_mfcc(got, ref, 1e-9)
+
+
+@pytest.mark.parametrize("sr,nm,nc,power,win", [(44100, 26, 13, 0, "hann"), (22050, 32, 16, 0, "hamming"),
+                                                (16000, 26, 12, 1, "blackman"), (44100, 20, 1, 0, "rectangular"),
+                                                (48000, 64, 13, 0, "hann")])
+def test_pair_kernel_f64_banks(ctx, sr, nm, nc, power, win):
+    x = synth.c2_hour(seconds=2.0).astype(np.float64)
+    got = _fp(ctx, x, _cfg64(ctx, sample_rate=sr, n_filters=nm, n_mfcc=nc, mfcc_input_power=power, window_type=win),
+              "fp_wave_kernel" if nm == 64 else None)
+    assert_mfcc(got, _ref(x, sr=sr, nm=nm, nc=nc, power=bool(power), win=win), 1e-9)
+
+
+def test_pair_kernel_f64_sample_rate_zero_and_short(ctx):
+    x = synth.sweep(1.0).astype(np.float64)
+    got = _fp(ctx, x, _cfg64(ctx, sample_rate=0, n_filters=26))
+    assert np.allclose(got[:, 0], np.sqrt(26) * np.log(1e-10), rtol=1e-12, atol=0)
+    assert np.abs(got[:, 1:]).max() < 1e-9
+    one = _fp(ctx, x[:1000], _cfg64(ctx, n_filters=26))
+    assert one.shape == (1, 13)
+    assert_mfcc(one, _ref(x[:1000], nm=26), 1e-9)
+
+
+def test_pair_vs_generic_kernel_f64_long(ctx):
+    """60 s: the f64 pair kernel against fp_wave_kernel<double> on the same bytes."""
+    x = synth.c2_hour(seconds=60.0).astype(np.float64)
+    a = _fp(ctx, x, _cfg64(ctx))
+    b = _fp(ctx, x, _cfg64(ctx, flags=sonar.FP_MFCC | sonar.FP_GENERIC), "fp_wave_kernel")
+    assert_mfcc(a, b, 1e-9)

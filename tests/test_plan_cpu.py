@@ -29,7 +29,12 @@ def test_pair_kernel_frame_limit():
 
 
 def test_plan_routes_like_the_call():
-    assert sonar.fp_kernel_plan(_cfg(precision=sonar.F64), 10 ** 6) == sonar.PLAN_WAVE
+    assert sonar.fp_kernel_plan(_cfg(precision=sonar.F64), 10 ** 6) == sonar.PLAN_WAVE     # f32 output
+    # float64 arithmetic + output: the pair kernel's double instantiation, PCM of either type
+    assert sonar.fp_kernel_plan(_cfg(precision=sonar.F64, out_dtype=sonar.F64), 10 ** 6) == sonar.PLAN_PAIR
+    assert sonar.fp_kernel_plan(_cfg(precision=sonar.F64, pcm_dtype=sonar.F64, out_dtype=sonar.F64),
+                                10 ** 6) == sonar.PLAN_PAIR
+    assert sonar.fp_kernel_plan(_cfg(pcm_dtype=sonar.F64), 10 ** 6) == sonar.PLAN_WAVE
     assert sonar.fp_kernel_plan(_cfg(out_dtype=sonar.F64), 10 ** 6) == sonar.PLAN_WAVE
     assert sonar.fp_kernel_plan(_cfg(flags=sonar.FP_MFCC | sonar.FP_SPECTRAL), 10 ** 6) == sonar.PLAN_WAVE
     assert sonar.fp_kernel_plan(_cfg(flags=sonar.FP_MFCC | sonar.FP_GENERIC), 10 ** 6) == sonar.PLAN_WAVE

@@ -18,7 +18,13 @@ variants = {
     "mfcc_w2048": dict(flags=sonar.FP_MFCC, window_size=2048, hop_size=512),
     "mfcc_w512": dict(flags=sonar.FP_MFCC, window_size=512, hop_size=128),
     "mfcc_f64": dict(flags=sonar.FP_MFCC, precision=sonar.F64),
+    # float64 arithmetic and output (the pair kernel's double instantiation; _generic: fp_wave_kernel<double>)
+    "mfcc_f64o": dict(flags=sonar.FP_MFCC, precision=sonar.F64, out_dtype=sonar.F64),
+    "mfcc_f64p": dict(flags=sonar.FP_MFCC, precision=sonar.F64, out_dtype=sonar.F64, pcm_dtype=sonar.F64),
+    "mfcc_f64p_generic": dict(flags=sonar.FP_MFCC | sonar.FP_GENERIC, precision=sonar.F64, out_dtype=sonar.F64,
+                              pcm_dtype=sonar.F64),
 }
+pcm64 = None
 sel = sys.argv[1:] or list(variants)
 for name in sel:
     kw = dict(window_size=1024, hop_size=256, sample_rate=44100, n_filters=40, n_mfcc=13, precision=sonar.F32,
@@ -26,18 +32,22 @@ for name in sel:
     kw.update(variants[name])
     cfg = ctx.config(**kw)
     F = sonar.stft_frames(n, cfg.window_size, cfg.hop_size)
-    outs = {"mfcc": torch.empty((F, 13), dtype=torch.float32, device=dev)}
+    odt = torch.float64 if cfg.out_dtype == sonar.F64 else torch.float32
+    if cfg.pcm_dtype == sonar.F64 and pcm64 is None:
+        pcm64 = pcm.double()
+    src = pcm64 if cfg.pcm_dtype == sonar.F64 else pcm
+    outs = {"mfcc": torch.empty((F, 13), dtype=odt, device=dev)}
     ptrs = {"mfcc": outs["mfcc"].data_ptr()}
     if cfg.flags & sonar.FP_SPECTRAL:
         for k in ["centroid", "rolloff", "bandwidth", "flatness", "crest", "slope", "flux", "low_ratio", "high_ratio"]:
-            outs[k] = torch.empty(F, dtype=torch.float32, device=dev)
+            outs[k] = torch.empty(F, dtype=odt, device=dev)
             ptrs[k] = outs[k].data_ptr()
     for _ in range(3):
-        ctx.fingerprint_device(pcm.data_ptr(), n, cfg, **ptrs)
+        ctx.fingerprint_device(src.data_ptr(), n, cfg, **ptrs)
     torch.cuda.synchronize(); ctx.last_kernel_ms()
     ctx.enable_kernel_timing(True)
     for _ in range(int(os.environ.get("ITERS", "100"))):
-        ctx.fingerprint_device(pcm.data_ptr(), n, cfg, **ptrs)
+        ctx.fingerprint_device(src.data_ptr(), n, cfg, **ptrs)
     torch.cuda.synchronize()
     ctx.enable_kernel_timing(False)
     ms = ctx.last_kernel_ms()
