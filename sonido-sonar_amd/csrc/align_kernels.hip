@@ -443,7 +443,10 @@ constexpr int DTW_RBLK = 16;               // rows per ring refill
 #define DTW_DQ_CFG 32
 #endif
 constexpr int DTW_DQ = DTW_DQ_CFG;         // steps of distances held in LDS (a power of two)
-constexpr int DTW_SWEEP_PRIO = 3;  // s_setprio of the sweep (the min-chain is the critical path)
+#ifndef DTW_SWEEP_PRIO_CFG
+#define DTW_SWEEP_PRIO_CFG 3
+#endif
+constexpr int DTW_SWEEP_PRIO = DTW_SWEEP_PRIO_CFG;  // s_setprio of the sweep (the min-chain is the critical path)
 #ifndef DTW_CODE_PRIO
 #define DTW_CODE_PRIO 2           // s_setprio of the code wave (A/B: 0, 1, 2, 3)
 #endif
@@ -457,7 +460,13 @@ constexpr int DTW_SWEEP_PRIO = 3;  // s_setprio of the sweep (the min-chain is t
                                   // Kernel 6)
 #endif
 #ifndef DTW_AUX_PRIO
-#define DTW_AUX_PRIO 0            // s_setprio of the ring feeder and the edge poller (A/B)
+#define DTW_AUX_PRIO 0            // s_setprio of the ring feeder (A/B)
+#endif
+#ifndef DTW_EDGE_PRIO
+#define DTW_EDGE_PRIO 3           // s_setprio of the edge poller (round 6): the top level, the same as
+                                  // the sweep that produces the edge it polls.  The edge poll is the
+                                  // kernel's only wait on ANOTHER block; at the top level no wave of any
+                                  // block outranks it (Kernel 6, "Liveness by construction")
 #endif
 #ifndef DTW_OQ_CFG
 #define DTW_OQ_CFG 32
@@ -742,7 +751,11 @@ void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
 
   if (wave == FEEDER_WAVE || wave == EDGE_WAVE) {
     // ------------------------------------------------ ring feeder / edge poller
-    if (DTW_AUX_PRIO) __builtin_amdgcn_s_setprio(DTW_AUX_PRIO);
+    if (wave == FEEDER_WAVE) {
+      if (DTW_AUX_PRIO) __builtin_amdgcn_s_setprio(DTW_AUX_PRIO);
+    } else {
+      if (DTW_EDGE_PRIO) __builtin_amdgcn_s_setprio(DTW_EDGE_PRIO);
+    }
     // two waves, so the edge poll's global-load latency never delays a ring refill
     const bool do_ring = wave == FEEDER_WAVE;
     int64_t nextblk = 0, have = 0;

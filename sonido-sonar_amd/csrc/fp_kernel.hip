@@ -117,9 +117,13 @@ template <> struct Vec2<float> { using type = float2; };
 template <> struct Vec2<double> { using type = double2; };
 
 #ifndef FP64_MIN_WAVES
-#define FP64_MIN_WAVES 1
+#define FP64_MIN_WAVES 3
 #endif
-// FP64_MIN_WAVES: waves per SIMD the float64 MFCC / magnitude instance at W = 1024 is compiled for
+// FP64_MIN_WAVES: waves per SIMD the float64 MFCC / magnitude instance at W = 1024 is compiled for.
+// 3 (168 VGPRs + 220 B of scratch) against 1 (2 waves per SIMD, 222-228 VGPRs, no scratch): the hour's
+// f64 MFCC 3.28 -> 3.00 ms and the f64 transform of MFCC + descriptors 6.75 -> 6.42 ms, same box, two
+// alternating rounds (profiles/r06f_fp64_ab.log: default = 1, w3 = 3; nopf / nopfw = FP64_PREFETCH /
+// FP64_WINREG at 0, both no faster)
 template <typename T, typename P, int R, bool SPEC, bool CPLX = false>
 __global__ __launch_bounds__(256, (sizeof(T) == 8 && !SPEC && !CPLX && R == 8) ? FP64_MIN_WAVES : 1)
 void fp_wave_kernel(FpParams p) {
@@ -243,8 +247,8 @@ void fp_wave_kernel(FpParams p) {
     }
   };
 
-  // the next unit's PCM in registers during the current FFT (PF); the float64 MFCC / magnitude
-  // instance runs more waves per SIMD instead (FP64_PREFETCH=1 restores it for A/B)
+  // the next unit's PCM in registers during the current FFT (PF); FP64_PREFETCH=0 drops it for the
+  // float64 MFCC / magnitude instance (A/B knob, measured no faster)
 #ifndef FP64_PREFETCH
 #define FP64_PREFETCH 1
 #endif
