@@ -53,10 +53,12 @@ def test_complex_and_phase_match_oracle(ctx, W, H, prec):
 
 
 def test_complex_with_mfcc_in_one_call(ctx):
-    """Requesting the spectrum next to the MFCC leaves the MFCC unchanged (same fused kernel)."""
+    """Requesting the spectrum next to the MFCC leaves the MFCC unchanged (same fused kernel:
+    SONAR_FP_GENERIC keeps the MFCC-only reference call on fp_wave_kernel, where the f64 MFCC-only
+    configuration would otherwise take mfcc_pair_kernel<double>)."""
     x = _sig(44100 * 3)
     base = dict(window_size=1024, hop_size=256, precision=sonar.F64)
-    ref = ctx.fingerprint(x, ctx.config(flags=sonar.FP_MFCC, **base))["mfcc"]
+    ref = ctx.fingerprint(x, ctx.config(flags=sonar.FP_MFCC | sonar.FP_GENERIC, **base))["mfcc"]
     got = ctx.fingerprint(x, ctx.config(flags=sonar.FP_MFCC | sonar.FP_COMPLEX | sonar.FP_PHASE, **base))
     assert np.array_equal(got["mfcc"], ref)
     ref_c, ref_p = O.stft_complex(x, 1024, 256)
