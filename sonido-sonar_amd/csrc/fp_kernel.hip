@@ -117,13 +117,14 @@ template <> struct Vec2<float> { using type = float2; };
 template <> struct Vec2<double> { using type = double2; };
 
 #ifndef FP64_MIN_WAVES
-#define FP64_MIN_WAVES 3
+#define FP64_MIN_WAVES 2
 #endif
 // FP64_MIN_WAVES: waves per SIMD the float64 MFCC / magnitude instance at W = 1024 is compiled for.
-// 3 (168 VGPRs + 220 B of scratch) against 1 (2 waves per SIMD, 222-228 VGPRs, no scratch): the hour's
-// f64 MFCC 3.28 -> 3.00 ms and the f64 transform of MFCC + descriptors 6.75 -> 6.42 ms, same box, two
-// alternating rounds (profiles/r06f_fp64_ab.log: default = 1, w3 = 3; nopf / nopfw = FP64_PREFETCH /
-// FP64_WINREG at 0, both no faster)
+// 2 against 1 and 3 on the final code, same box, two alternating rounds (profiles/r06n_fp64_minwaves_ab.log):
+// float64 PCM, MFCC only 3.17-3.19 / 3.30-3.31 / 3.73 ms per hour; float64 PCM, MFCC + descriptors
+// (the GenerateFingerprint transform) 6.62-6.63 / 6.79-6.81 / 7.47-7.50 ms; float32 PCM equal at 1
+// and 2.  (An earlier A/B, profiles/r06f_fp64_ab.log, had 3 ahead on the float32-PCM instance.)
+// FP64_PREFETCH / FP64_WINREG at 0 (no PCM prefetch / the window re-read): no faster (r06f).
 template <typename T, typename P, int R, bool SPEC, bool CPLX = false>
 __global__ __launch_bounds__(256, (sizeof(T) == 8 && !SPEC && !CPLX && R == 8) ? FP64_MIN_WAVES : 1)
 void fp_wave_kernel(FpParams p) {

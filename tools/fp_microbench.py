@@ -23,6 +23,9 @@ variants = {
     "mfcc_f64p": dict(flags=sonar.FP_MFCC, precision=sonar.F64, out_dtype=sonar.F64, pcm_dtype=sonar.F64),
     "mfcc_f64p_generic": dict(flags=sonar.FP_MFCC | sonar.FP_GENERIC, precision=sonar.F64, out_dtype=sonar.F64,
                               pcm_dtype=sonar.F64),
+    # the GenerateFingerprint transform: f64 PCM, MFCC + descriptors (two passes: |X| rows + spec_rows_kernel)
+    "spec_f64p": dict(flags=sonar.FP_MFCC | sonar.FP_SPECTRAL, precision=sonar.F64, out_dtype=sonar.F64,
+                      pcm_dtype=sonar.F64),
 }
 pcm64 = None
 sel = sys.argv[1:] or list(variants)
