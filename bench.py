@@ -672,6 +672,49 @@ def feature_parity(got, ref, rtol):
     return {"pass": bool(ok), "rtol": rtol, "fields": out}
 
 
+def load_gf_kernels(F, n):
+    """Per-kernel time of one GenerateFingerprint hour call (f64) from the newest committed
+    rocprofv3 timeline (profiles/<round>_gf_timeline.json: tools/gpu_gf_profile.sh, a kernel +
+    memory-copy trace of tools/gf_hour_probe.py, placed inside each call by tools/gf_timeline.py),
+    and each kernel's roofline: the transform and YIN against the FP64 VALU roof, the descriptor
+    pass against HBM, the H2D copy against the PCIe rate of the same run's pageable copy.  A kernel
+    trace cannot run inside this process, so these come from the committed profile."""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gf_timeline.json")), reverse=True)
+    if not paths:
+        return None
+    calls = [c for c in json.load(open(paths[0])) if c.get("precision") == "f64"]
+    if not calls:
+        return None
+
+    def med(pat):
+        v = [sum(o["ms"] for k, o in c["ops"].items() if pat in k) for c in calls]
+        return float(np.median(v)) if v else None
+    K = W // 2 + 1
+    yin_frames = (n - 1024) // 512 + 1
+    t_fft, t_spec, t_yin, t_h2d = (med("fp_wave_kernel<double"), med("spec_rows_kernel"), med("yin_kernel"),
+                                   med("HOST_TO_DEVICE"))
+    out = {"source": os.path.relpath(paths[0], ROOT), "calls": len(calls),
+           "note": "kernel ms summed over the call's chunked launches, median over the profiled f64 calls"}
+    if t_fft:
+        out["transform"] = {"kernel": "fp_wave_kernel<double, double, 8, false>", "ms": t_fft, "bound": "fp64_valu",
+                            "achieved_tflops": F * FLOPS_PER_FRAME / t_fft / 1e9,
+                            "frac": F * FLOPS_PER_FRAME / t_fft / 1e9 / FP64_PEAK_TFS,
+                            "flops_per_frame": FLOPS_PER_FRAME}
+    if t_spec:
+        b = F * K * 8 + F * 9 * 8
+        out["descriptors"] = {"kernel": "spec_rows_kernel", "ms": t_spec, "bound": "hbm",
+                              "achieved_gbs": b / t_spec / 1e6, "frac": b / t_spec / 1e6 / 8000.0,
+                              "bytes_per_frame": K * 8 + 9 * 8}
+    if t_yin:
+        ops = 512 * 512 * 3
+        out["yin"] = {"kernel": "yin_kernel", "ms": t_yin, "frames": yin_frames, "bound": "fp64_valu",
+                      "achieved_tflops": yin_frames * ops / t_yin / 1e9,
+                      "frac": yin_frames * ops / t_yin / 1e9 / FP64_PEAK_TFS, "ops_per_frame": ops}
+    if t_h2d:
+        out["h2d"] = {"ms": t_h2d, "gbs": 8 * n / t_h2d / 1e6}
+    return out
+
+
 def bench_c1(args, ctx):
     """BASELINE configs[0] -- the north star's own claim, music fingerprinting in frames/s: the
     product entry sonar_generate_fingerprint (FingerprintGenerator.GenerateFingerprint,
@@ -709,6 +752,45 @@ def bench_c1(args, ctx):
             ctx.generate_fingerprint(x2[: SR * 20], SR, "music", cfg)
             med, lo, hi = timed_runs(lambda: ctx.generate_fingerprint(x2, SR, "music", cfg), reps=args.reps, warmup=1)
             r2[name] = {"ms": med * 1e3, "ms_spread": [lo * 1e3, hi * 1e3], "frames_per_s": F2 / med}
+        # the call is bound by the host -> device copy of the float64 PCM (DESIGN.md Kernel 1b,
+        # "GenerateFingerprint pipeline"): its roof is a plain copy of the same pageable bytes
+        dev = torch.device("cuda", torch.cuda.current_device())
+        xt = torch.from_numpy(x2)
+        xt.to(dev)
+        torch.cuda.synchronize()
+        cmed, _, _ = timed_runs(lambda: (xt.to(dev), torch.cuda.synchronize()), reps=3, warmup=0)
+        nbytes = 8 * len(x2)
+        r2["roofline"] = {"bound": "pcie", "unit": "GB/s", "achieved": nbytes / r2["f64"]["ms"] / 1e6,
+                          "peak": nbytes / cmed / 1e9, "frac": cmed * 1e3 / r2["f64"]["ms"],
+                          "traffic": nbytes, "peak_source": "torch pageable H2D copy of the same float64 PCM, "
+                                                            "median of 3, same process",
+                          "h2d_copy_ms": cmed * 1e3}
+        # the call's float64 transform + descriptor pass alone on device-resident PCM (HIP events, one
+        # timed region over fp_wave_kernel<double> and spec_rows_kernel): inside the call these
+        # kernels share the GPU with YIN and the copies, so the timeline's sums overstate them
+        xd = xt.to(dev)
+        outs_d = {"mfcc": torch.empty((F2, 13), dtype=torch.float64, device=dev)}
+        for k in ("centroid", "rolloff", "bandwidth", "flatness", "crest", "slope", "flux", "low_ratio", "high_ratio"):
+            outs_d[k] = torch.empty(F2, dtype=torch.float64, device=dev)
+        cfg_t = ctx.config(window_size=W, hop_size=H, sample_rate=SR, n_filters=26, n_mfcc=13, precision=sonar.F64,
+                           pcm_dtype=sonar.F64, out_dtype=sonar.F64, flags=sonar.FP_MFCC | sonar.FP_SPECTRAL)
+        ptrs = {k: v.data_ptr() for k, v in outs_d.items()}
+        ctx.fingerprint_device(xd.data_ptr(), len(x2), cfg_t, **ptrs)
+        torch.cuda.synchronize()
+        ctx.last_kernel_ms()
+        ctx.enable_kernel_timing(True)
+        for _ in range(3):
+            ctx.fingerprint_device(xd.data_ptr(), len(x2), cfg_t, **ptrs)
+        torch.cuda.synchronize()
+        ctx.enable_kernel_timing(False)
+        t_iso = ctx.last_kernel_ms()
+        r2["transform_isolated"] = {"kernels": "fp_wave_kernel<double, double, 8, false> + spec_rows_kernel",
+                                    "ms": t_iso, "bound": "fp64_valu",
+                                    "achieved_tflops": F2 * FLOPS_PER_FRAME / t_iso / 1e9,
+                                    "frac": F2 * FLOPS_PER_FRAME / t_iso / 1e9 / FP64_PEAK_TFS,
+                                    "note": "MFCC + descriptors in float64 on device-resident float64 PCM, mean of 3"}
+        del xt, xd, outs_d
+        r2["kernels"] = load_gf_kernels(F2, len(x2))
         res["c1_generate_fingerprint"]["c2_hour"] = r2
         del x2
     if not args.no_cpu_baseline:

@@ -69,6 +69,8 @@ struct sonar_ctx {
   // chunk the compute streams wait on (go_api.cpp)
   hipStream_t copy = nullptr;
   std::vector<hipEvent_t> chunk_ev;
+  // ... and chunk k's pitch rows on the host (side stream), for the early tracker
+  std::vector<hipEvent_t> back_ev;
   // band-kernel liveness counters (sonar_dtw_counters): edge refresh fences, those followed by new
   // edge values, DTWs that timed out, waves that timed out
   long long dtw_ctr[4] = {0, 0, 0, 0};

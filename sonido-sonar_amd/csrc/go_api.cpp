@@ -182,6 +182,24 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     for (auto& e : c->side_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
 
+  // ---- results: ONE pinned block from the pool, every array copied into it by DMA; the result's
+  // large arrays point into the block (no host copy, no page faults on fresh vectors).  The
+  // per-frame arrays travel chunk by chunk during the pipeline below, the rest after it ----
+  const size_t Fe_z = (size_t)std::max<int64_t>(Fe, 0), Fp_z = (size_t)std::max<int64_t>(Fp, 0);
+  const size_t Fenv_z = (size_t)std::max<int64_t>(Fenv, 0), Fl_z = (size_t)std::max<int64_t>(Fl, 0);
+  const bool lohi_copy = (int64_t)Fe_z > F;                       // Go pads the ratios past the spectrogram
+  const int SB = 256;
+  size_t off = 0;
+  auto take = [&](size_t cnt) { const size_t o = off; off += (cnt + 7) & ~size_t(7); return o; };
+  const size_t o_mfcc = take(fc->enable_mfcc ? Fz * nm : 0), o_spec = take(Fz * 9), o_zcr = take(Fz);
+  const size_t o_en = take(Fe_z), o_ent = take(Fe_z), o_praw = take(Fp_z), o_craw = take(Fp_z);
+  const size_t o_part = take(SB * 4), o_env = take(Fenv_z), o_loud = take(Fl_z);
+  const size_t o_tilt = take(fc->enable_speech_features ? Fp_z : 0), o_head = take((size_t)std::min<int64_t>(n, 1024));
+  const size_t o_trk = take(6 * Fp_z), o_lohi = take(lohi_copy ? 2 * Fe_z : 0);
+  std::shared_ptr<void> blk = sonar::detail::pinned_block(off * 8);
+  if (!blk) return fail(c, SONAR_ERR_NOMEM, "pinned host allocation failed (results)");
+  double* B = (double*)blk.get();
+
   // ---- the host PCM crosses PCIe in chunks on the copy stream; once chunk k has landed, every
   // frame whose samples lie in [0, end of chunk k) is computed while the next chunk is in flight:
   // pre-emphasis of the chunk, the fused STFT kernel + descriptors + ZCR over the frames it
@@ -195,13 +213,18 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     if (v > 0) CH = std::min<int64_t>(n, v);
   }
   const int64_t NCH = (n + CH - 1) / CH;
-  if (NCH > 1) {
-    if (!c->copy) HIP_TRY(c, hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
-    while ((int64_t)c->chunk_ev.size() < NCH) {
+  auto grow_ev = [&](std::vector<hipEvent_t>& v, int64_t cnt) -> int {
+    while ((int64_t)v.size() < cnt) {
       hipEvent_t e;
       HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      c->chunk_ev.push_back(e);
+      v.push_back(e);
     }
+    return SONAR_OK;
+  };
+  if (grow_ev(c->back_ev, NCH)) return SONAR_ERR_DEVICE;
+  if (NCH > 1) {
+    if (!c->copy) HIP_TRY(c, hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+    if (grow_ev(c->chunk_ev, NCH)) return SONAR_ERR_DEVICE;
     HIP_TRY(c, hipEventRecord(c->side_ev[0], s));                // the buffers' previous readers
     HIP_TRY(c, hipStreamWaitEvent(c->copy, c->side_ev[0], 0));
   }
@@ -212,7 +235,12 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     if (b < win || hop <= 0) return 0;
     return std::min<int64_t>(total, (b - win) / hop + 1);
   };
+  // the harmonic features' tracker runs chunk by chunk during the pipeline (below) when the speech
+  // block does not need the pitch rows first (SONAR_GF_EARLY=0: after the last chunk)
+  static const int gf_early = [] { const char* e = std::getenv("SONAR_GF_EARLY"); return e ? std::atoi(e) : 1; }();
+  const bool trk_early = !fc->enable_speech_features && gf_early != 0;
   int64_t done_fp = 0, done_e = 0, done_p = 0, done_env = 0, done_l = 0;
+  std::vector<int64_t> p_end(NCH, 0);                              // pitch frames complete after chunk k
   for (int64_t k = 0; k < NCH; ++k) {
     const int64_t a = k * CH, b = std::min<int64_t>(n, a + CH);
     if (NCH > 1) {
@@ -229,7 +257,8 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     if (pk > done_p) {
       HIP_TRY(c, hipEventRecord(c->side_ev[0], s));
       HIP_TRY(c, hipStreamWaitEvent(c->side, c->side_ev[0], 0));
-      if (sonar::launch_yin(dy, n, Fp, 512, csr, dpit, dcon, nullptr, c->side, done_p, pk) != 0)
+      if (sonar::launch_yin(dy, n, Fp, 512, csr, trk_early ? B + o_praw : dpit, trk_early ? B + o_craw : dcon, nullptr,
+                            c->side, done_p, pk) != 0)
         return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
       done_p = pk;
     }
@@ -250,13 +279,18 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     const int64_t lk = ready(b, Fl, lw, lh);
     if (lk > done_l && sonar::launch_energy(dpcm, 1, n, Fl, lw, lh, 0.97, dld, 1, s, done_l, lk) != 0)
       return fail(c, SONAR_ERR_DEVICE, "loudness launch failed");
+    // the tracker's input: with trk_early, YIN writes this chunk's pitch rows straight into the
+    // pinned result block (mapped host memory) and the event marks them complete.  A DMA copy per
+    // chunk instead queues behind the next chunk's H2D on the copy engine and serialises the
+    // pipeline: 41-42 against 30 ms per hour (profiles/r06r_gf_early_ab.log)
+    if (trk_early) HIP_TRY(c, hipEventRecord(c->back_ev[k], c->side));
+    p_end[k] = done_p;
     done_l = std::max(done_l, lk);
   }
   HIP_TRY(c, hipEventRecord(c->side_ev[1], c->side));
   HIP_TRY(c, hipStreamWaitEvent(s, c->side_ev[1], 0));
   // whole-signal statistics of the pre-emphasised PCM: read by detectSpeech and the temporal
   // block only (the music generation config enables neither, content_config.go:108-140)
-  const int SB = 256;
   double* dpart = (double*)dbuf(c, "sx.stats", SB * 4 * 8);
   if (!dpart) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (stats)");
   if (fc->enable_speech_features || fc->enable_temporal_features) {
@@ -268,21 +302,6 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   if (fc->enable_speech_features && sonar::launch_tilt(dy, n, Fp, dtilt, s) != 0)
     return fail(c, SONAR_ERR_DEVICE, "tilt launch failed");
 
-  // ---- results back: ONE pinned block from the pool, every array copied into it by DMA; the
-  // result's large arrays point into the block (no host copy, no page faults on fresh vectors) ----
-  const size_t Fe_z = (size_t)std::max<int64_t>(Fe, 0), Fp_z = (size_t)std::max<int64_t>(Fp, 0);
-  const size_t Fenv_z = (size_t)std::max<int64_t>(Fenv, 0), Fl_z = (size_t)std::max<int64_t>(Fl, 0);
-  const bool lohi_copy = (int64_t)Fe_z > F;                       // Go pads the ratios past the spectrogram
-  size_t off = 0;
-  auto take = [&](size_t cnt) { const size_t o = off; off += (cnt + 7) & ~size_t(7); return o; };
-  const size_t o_mfcc = take(fc->enable_mfcc ? Fz * nm : 0), o_spec = take(Fz * 9), o_zcr = take(Fz);
-  const size_t o_en = take(Fe_z), o_ent = take(Fe_z), o_praw = take(Fp_z), o_craw = take(Fp_z);
-  const size_t o_part = take(SB * 4), o_env = take(Fenv_z), o_loud = take(Fl_z);
-  const size_t o_tilt = take(fc->enable_speech_features ? Fp_z : 0), o_head = take((size_t)std::min<int64_t>(n, 1024));
-  const size_t o_trk = take(6 * Fp_z), o_lohi = take(lohi_copy ? 2 * Fe_z : 0);
-  std::shared_ptr<void> blk = sonar::detail::pinned_block(off * 8);
-  if (!blk) return fail(c, SONAR_ERR_NOMEM, "pinned host allocation failed (results)");
-  double* B = (double*)blk.get();
   double* dent = (double*)dbuf(c, "sx.ent", std::max<size_t>(Fe_z, 1) * 8);
   if (!dent) return fail(c, SONAR_ERR_NOMEM, "device allocation failed (entropy)");
   if (Fe_z && sonar::launch_energy_entropy(den, (int64_t)Fe_z, dent, s) != 0)
@@ -291,17 +310,53 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     if (cnt) HIP_TRY(c, hipMemcpyAsync(B + o, d, cnt * 8, hipMemcpyDeviceToHost, s));
     return SONAR_OK;
   };
-  if (d2h(o_mfcc, dmfcc, fc->enable_mfcc ? Fz * nm : 0) || d2h(o_spec, dspec, Fz * 9) || d2h(o_zcr, dzcr, Fz) ||
-      d2h(o_en, den, Fe_z) || d2h(o_ent, dent, Fe_z) || d2h(o_praw, dpit, Fp_z) || d2h(o_craw, dcon, Fp_z) ||
-      d2h(o_part, dpart, SB * 4) || d2h(o_env, denv, Fenv_z) || d2h(o_loud, dld, Fl_z) ||
+  // everything but the pitch rows
+  if ((!trk_early && (d2h(o_praw, dpit, Fp_z) || d2h(o_craw, dcon, Fp_z))) ||
+      d2h(o_mfcc, dmfcc, fc->enable_mfcc ? Fz * nm : 0) || d2h(o_spec, dspec, Fz * 9) || d2h(o_zcr, dzcr, Fz) ||
+      d2h(o_en, den, Fe_z) || d2h(o_env, denv, Fenv_z) || d2h(o_loud, dld, Fl_z))
+    return SONAR_ERR_DEVICE;
+  if (d2h(o_ent, dent, Fe_z) || d2h(o_part, dpart, SB * 4) ||
       d2h(o_tilt, dtilt, fc->enable_speech_features ? Fp_z : 0) ||
       d2h(o_head, dy, (size_t)std::min<int64_t>(n, 1024)))
     return SONAR_ERR_DEVICE;
+  // Without the speech block (the GenerateFingerprint content configs for music / news / sports,
+  // content_config.go:108-140) the harmonic features' sequential tracker is the only consumer of the
+  // pitch frames before the end: it runs chunk by chunk as each chunk's pitch rows land, while the
+  // device and PCIe work on (the speech block's voicing pass must see the tracker first, so with it
+  // the tracker runs after the sync, below)
+  int64_t trk_done = 0;
+  sonar::host::YinTracker tracker;
+  const double* praw = B + o_praw;
+  const double* craw = B + o_craw;
+  double* pe = B + o_trk;
+  double* pc = pe + Fp_z;
+  double* vs = pc + Fp_z;
+  double* hr = vs + Fp_z;
+  double* ih = hr + Fp_z;
+  double* tcen = ih + Fp_z;
+  auto track = [&](int64_t hi) {                                  // extractHarmonicFeatures :464-509
+    for (int64_t i = trk_done; i < hi; i++) {
+      double p = 0.0, q = 0.0, v = 0.0;
+      if (i * 512 + 1024 <= n) {                                  // DetectPitch size check (pitch_detection.go:226)
+        p = praw[i]; q = craw[i];
+        tracker.step(p, q, v);
+      }
+      pe[i] = p; pc[i] = q; vs[i] = v;
+      hr[i] = v * 10.0;
+      ih[i] = 1.0 - v;
+      tcen[i] = p > 0 ? p : 0.0;
+    }
+    trk_done = std::max(trk_done, hi);
+  };
+  if (trk_early) {
+    for (int64_t k = 0; k < NCH; ++k) {
+      HIP_TRY(c, hipEventSynchronize(c->back_ev[k]));
+      track(p_end[k]);
+    }
+  }
   HIP_TRY(c, hipStreamSynchronize(s));
   const double* energy = B + o_en;
   const double* spec = B + o_spec;
-  const double* praw = B + o_praw;
-  const double* craw = B + o_craw;
   const double* part = B + o_part;
 
   auto* res = new sonar_result();
@@ -325,7 +380,6 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   // cross-block sign changes at block boundaries are counted inside each block (i > 0 uses y[i-1])
 
   // ---- speech features (extractSpeechFeatures :272-313) -------------------------
-  sonar::host::YinTracker tracker;
   bool is_speech = false;
   double thr10 = 0.0;                                             // percentile10_threshold(energy), once
   bool have_thr10 = false;
@@ -481,23 +535,7 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
 
   // ---- harmonic features (extractHarmonicFeatures :464-509) --------------------
   {
-    double* pe = B + o_trk;
-    double* pc = pe + Fp_z;
-    double* vs = pc + Fp_z;
-    double* hr = vs + Fp_z;
-    double* ih = hr + Fp_z;
-    double* tcen = ih + Fp_z;
-    for (int64_t i = 0; i < Fp; i++) {
-      double p = 0.0, q = 0.0, v = 0.0;
-      if (i * 512 + 1024 <= n) {                                  // DetectPitch size check (pitch_detection.go:226)
-        p = praw[i]; q = craw[i];
-        tracker.step(p, q, v);
-      }
-      pe[i] = p; pc[i] = q; vs[i] = v;
-      hr[i] = v * 10.0;
-      ih[i] = 1.0 - v;
-      tcen[i] = p > 0 ? p : 0.0;
-    }
+    track(Fp);                                                    // the rest (all of it after the speech block)
     res->put_ext("pitch_estimate", pe, (int64_t)Fp_z, 1);
     res->put_ext("pitch_confidence", pc, (int64_t)Fp_z, 1);
     res->put_ext("voicing_strength", vs, (int64_t)Fp_z, 1);

@@ -377,6 +377,8 @@ void sonar_destroy(sonar_ctx* c) {
   for (auto e : c->chunk_ev)
     if (e) hipEventDestroy(e);
   if (c->copy) hipStreamDestroy(c->copy);
+  for (auto e : c->back_ev)
+    if (e) hipEventDestroy(e);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }

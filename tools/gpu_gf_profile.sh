@@ -1,6 +1,6 @@
 # GenerateFingerprint at hour scale: the changed GPU tests, the plain probe,
 # the probe under a kernel + memory-copy trace (timeline), and SQ / traffic PMC passes over a
-# 10-minute probe (fp_wave_kernel SPEC and yin_kernel).  Summaries go to gpurun_out/<tag>_*.
+# 10-minute probe (the float64 transform, spec_rows_kernel and yin_kernel).  Summaries go to gpurun_out/<tag>_*.
 # Usage (GPU box): bash tools/gpu_gf_profile.sh <tag> [tests...]
 set -o pipefail
 TAG=${1:-r06a}; shift
@@ -23,7 +23,7 @@ f=$(find "$OUT/trace" -name '*kernel_stats.csv' | head -1); cp "$f" gpurun_out/$
 rm -f "$OUT"/trace/*/*_kernel_trace.csv "$OUT"/trace/*_kernel_trace.csv
 echo "timeline done"
 ITERS=1 timeout -k 10 900 bash tools/pmc_run.sh "${TAG}_gf" tools/gf_hour_probe.py 600 1 || exit 1
-for k in "fp_wave_kernel<double, double, 8, true" yin_kernel; do
+for k in "fp_wave_kernel<double, double, 8, false" spec_rows_kernel yin_kernel; do
   python3 tools/pmc_summary.py "gpurun_out/pmc_${TAG}_gf" "$k"
 done > gpurun_out/${TAG}_gf_pmc.txt
 echo "pmc done"
