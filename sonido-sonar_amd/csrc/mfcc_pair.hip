@@ -727,7 +727,8 @@ int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
   else kern = pick(f64t, f32t, std::false_type{});
   if (p.lds_bytes > 64 * 1024)
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, p.lds_bytes);
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * mfcc_pair_waves_per_block(p.f64)), p.lds_bytes, s, p);
+  if (p.waves_per_block < 1 || p.waves_per_block > mfcc_pair_waves_per_block(p.f64) || p.lds_bytes > 160 * 1024) return -5;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * p.waves_per_block), p.lds_bytes, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

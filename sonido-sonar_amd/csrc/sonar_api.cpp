@@ -523,11 +523,15 @@ void fill_pair_params(sonar_ctx* c, const PairTables& t, const sonar_fp_cfg* cfg
   q.lds_tw2 = q.lds_ctr + 16;
   q.lds_wave0 = q.lds_tw2 + (f64 ? 64 * 16 : 0);   // float64: the stage-2 twiddle table
   // mfcc_pair_kernel: one block per CU (12 waves float32, 8 float64) over a contiguous range of pairs
+  // One block per CU.  The float64 waves' 17.4 KB regions beside the largest tables (J = 16,
+  // NMP = 64: 29 KB) exceed the 160 KiB of LDS at 8 waves; such a bank runs 7 (or fewer) waves
   q.waves_per_block = sonar::mfcc_pair_waves_per_block(e);
+  while (q.waves_per_block > 1 && q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes(e) > 160 * 1024)
+    --q.waves_per_block;
   q.lds_bytes = q.lds_wave0 + q.waves_per_block * sonar::mfcc_pair_wave_bytes(e);
   int dev_cus = 256;
   hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
-  const int64_t blocks = (int64_t)dev_cus * sonar::mfcc_pair_waves_per_cu(e) / q.waves_per_block;
+  const int64_t blocks = (int64_t)dev_cus * std::max(1, sonar::mfcc_pair_waves_per_cu(e) / q.waves_per_block);
   q.pairs_per_block = std::max<int64_t>(1, (NP + blocks - 1) / blocks);
 }
 

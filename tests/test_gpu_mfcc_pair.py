@@ -190,3 +190,17 @@ def test_pair_vs_generic_kernel_f64_long(ctx):
     a = _fp(ctx, x, _cfg64(ctx))
     b = _fp(ctx, x, _cfg64(ctx, flags=sonar.FP_MFCC | sonar.FP_GENERIC), "fp_wave_kernel")
     assert_mfcc(a, b, 1e-9)
+
+
+@pytest.mark.parametrize("sr,nm", [(8000, 20), (11025, 40), (16000, 48), (22050, 56), (44100, 60), (32000, 64),
+                                   (96000, 40), (44100, 8)])
+def test_pair_kernel_f64_bank_sweep(ctx, sr, nm):
+    """Banks of every shape the pair kernel takes (the widest chunks and largest DCT tables shrink
+    the float64 block to fewer waves to fit LDS), or the general kernel where it does not."""
+    x = synth.c2_hour(seconds=1.5).astype(np.float64)
+    cfg = _cfg64(ctx, sample_rate=sr, n_filters=nm)
+    got = ctx.fingerprint(x, cfg)["mfcc"]
+    assert ctx.last_fp_kernel() in ("mfcc_pair_kernel", "fp_wave_kernel")
+    assert_mfcc(got, _ref(x, sr=sr, nm=nm), 1e-9)
+    got32 = ctx.fingerprint(x.astype(np.float32), _cfg(ctx, sample_rate=sr, n_filters=nm))["mfcc"]
+    assert _err(got32, _ref(x.astype(np.float32), sr=sr, nm=nm)) < 1e-4
