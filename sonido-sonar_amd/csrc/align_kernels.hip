@@ -2077,9 +2077,42 @@ __device__ __forceinline__ void wave_argmax(double& a, int64_t& i) {
 }
 }  // namespace
 
+// Sequential sums of 64 terms at a time (acc += v[lane 0], += v[lane 1], ... in lane order, for
+// NC independent sums at once).  PAIR_SCORE_LDS (round 6): the terms go through LDS and every lane
+// runs the add chain on broadcast reads, so a term costs one dependent v_add_f64 (the reads are
+// independent and issued ahead) instead of two v_readlane + the SGPR hazard + the add.
+#ifndef PAIR_SCORE_LDS
+#define PAIR_SCORE_LDS 1
+#endif
+template <int NC>
+__device__ __forceinline__ void seq_add(double (&acc)[NC], const double (&v)[NC], int cnt, double* buf) {
+  if constexpr (PAIR_SCORE_LDS) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) buf[64 * c + lane] = v[c];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll 16
+    for (int k = 0; k < cnt; ++k) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[c] += buf[64 * c + k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the next block's stores after every read
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  } else {
+    for (int k = 0; k < cnt; ++k) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[c] += rl(v[c], k);
+    }
+  }
+}
+
 __global__ __launch_bounds__(64) void pair_score_kernel(const ScoreJob* jobs) {
   const ScoreJob j = jobs[blockIdx.x];
   const int lane = threadIdx.x;
+  __shared__ double sbuf[2 * 64];
   // ---- warping path
   const int64_t P = *j.plen;
   host::PathSums ps;
@@ -2108,7 +2141,10 @@ __global__ __launch_bounds__(64) void pair_score_kernel(const ScoreJob* jobs) {
         }
       }
       const int cnt = (int)min((int64_t)64, P - b);
-      for (int k = 0; k < cnt; ++k) { sc += rl(c, k); ss += rl(m, k); }
+      double acc[2] = {sc, ss};
+      const double v[2] = {c, m};
+      seq_add<2>(acc, v, cnt, sbuf);
+      sc = acc[0]; ss = acc[1];
     }
     ps.offset_sum = wave_isum(off);
     ps.diag_steps = wave_isum(dg);
@@ -2124,7 +2160,10 @@ __global__ __launch_bounds__(64) void pair_score_kernel(const ScoreJob* jobs) {
         double d2 = 0.0;
         if (i < P) { const double d = smooth(i) - mean; d2 = d * d; }
         const int cnt = (int)min((int64_t)64, P - b);
-        for (int k = 0; k < cnt; ++k) vv += rl(d2, k);
+        double acc[1] = {vv};
+        const double v[1] = {d2};
+        seq_add<1>(acc, v, cnt, sbuf);
+        vv = acc[0];
       }
       ps.var_smooth = vv;
     }
@@ -2161,7 +2200,10 @@ __global__ __launch_bounds__(64) void pair_score_kernel(const ScoreJob* jobs) {
         if (d > 10 && v > ms) ms = v;
       }
       const int cnt = (int)min((int64_t)64, nl - b);
-      for (int k = 0; k < cnt; ++k) ns += rl(sq, k);
+      double acc[1] = {ns};
+      const double v[1] = {sq};
+      seq_add<1>(acc, v, cnt, sbuf);
+      ns = acc[0];
     }
     cs.noise_sum = ns;
     cs.noise_count = wave_isum(nc);
