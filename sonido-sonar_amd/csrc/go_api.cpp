@@ -238,7 +238,18 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   // the harmonic features' tracker runs chunk by chunk during the pipeline (below) when the speech
   // block does not need the pitch rows first (SONAR_GF_EARLY=0: after the last chunk)
   static const int gf_early = [] { const char* e = std::getenv("SONAR_GF_EARLY"); return e ? std::atoi(e) : 1; }();
-  const bool trk_early = !fc->enable_speech_features && gf_early != 0;
+  // the device's address of the block's pitch rows (mapped pinned memory); none -> the late order
+  double *hpit = nullptr, *hcon = nullptr;
+  if (!fc->enable_speech_features && gf_early != 0 && Fp_z) {
+    void* dB = nullptr;
+    if (hipHostGetDevicePointer(&dB, B, 0) == hipSuccess && dB) {
+      hpit = (double*)dB + o_praw;
+      hcon = (double*)dB + o_craw;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
+  const bool trk_early = hpit != nullptr;
   int64_t done_fp = 0, done_e = 0, done_p = 0, done_env = 0, done_l = 0;
   std::vector<int64_t> p_end(NCH, 0);                              // pitch frames complete after chunk k
   for (int64_t k = 0; k < NCH; ++k) {
@@ -257,7 +268,7 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     if (pk > done_p) {
       HIP_TRY(c, hipEventRecord(c->side_ev[0], s));
       HIP_TRY(c, hipStreamWaitEvent(c->side, c->side_ev[0], 0));
-      if (sonar::launch_yin(dy, n, Fp, 512, csr, trk_early ? B + o_praw : dpit, trk_early ? B + o_craw : dcon, nullptr,
+      if (sonar::launch_yin(dy, n, Fp, 512, csr, trk_early ? hpit : dpit, trk_early ? hcon : dcon, nullptr,
                             c->side, done_p, pk) != 0)
         return fail(c, SONAR_ERR_DEVICE, "yin launch failed");
       done_p = pk;
