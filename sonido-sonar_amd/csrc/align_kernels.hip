@@ -462,6 +462,9 @@ constexpr int DTW_SWEEP_PRIO = DTW_SWEEP_PRIO_CFG;  // s_setprio of the sweep (t
 #ifndef DTW_AUX_PRIO
 #define DTW_AUX_PRIO 0            // s_setprio of the ring feeder (A/B)
 #endif
+#ifndef DTW_EDGE_SLEEP
+#define DTW_EDGE_SLEEP 1          // s_sleep of the edge poller between empty polls (64 clk units)
+#endif
 #ifndef DTW_EDGE_PRIO
 #define DTW_EDGE_PRIO 3           // s_setprio of the edge poller (round 6): the top level, the same as
                                   // the sweep that produces the edge it polls.  The edge poll is the
@@ -843,7 +846,9 @@ void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
         idle = 0;
       } else {
         fenced = false;
-        __builtin_amdgcn_s_sleep(1);
+        // an idle poll sleeps; the edge poller at the top level sleeps DTW_EDGE_SLEEP (A/B knob)
+        if (do_ring) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(DTW_EDGE_SLEEP);
         if ((++idle & 63) == 0) {
           if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) {
             // a wave of this block timed out (SONAR_SPIN_UNTIL): write its diagnostic record here
