@@ -462,9 +462,6 @@ constexpr int DTW_SWEEP_PRIO = DTW_SWEEP_PRIO_CFG;  // s_setprio of the sweep (t
 #ifndef DTW_AUX_PRIO
 #define DTW_AUX_PRIO 0            // s_setprio of the ring feeder (A/B)
 #endif
-#ifndef DTW_EDGE_SLEEP
-#define DTW_EDGE_SLEEP 1          // s_sleep of the edge poller between empty polls (64 clk units)
-#endif
 #ifndef DTW_EDGE_PRIO
 #define DTW_EDGE_PRIO 3           // s_setprio of the edge poller (round 6): the top level, the same as
                                   // the sweep that produces the edge it polls.  The edge poll is the
@@ -846,9 +843,7 @@ void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
         idle = 0;
       } else {
         fenced = false;
-        // an idle poll sleeps; the edge poller at the top level sleeps DTW_EDGE_SLEEP (A/B knob)
-        if (do_ring) __builtin_amdgcn_s_sleep(1);
-        else __builtin_amdgcn_s_sleep(DTW_EDGE_SLEEP);
+        __builtin_amdgcn_s_sleep(1);   // (the poller at 2 or 4: no different, profiles/r06z_*)
         if ((++idle & 63) == 0) {
           if (SONAR_LDS_LD(ctr[DTW_CTR_ABORT])) {
             // a wave of this block timed out (SONAR_SPIN_UNTIL): write its diagnostic record here
@@ -2062,12 +2057,8 @@ int launch_nonfinite_batch(const DtwArgs* dargs, int n, int64_t max_elems, hipSt
 // and the peak index (the first index of the largest |corr|, as Go's strict > scan) are order-free;
 // the float sums keep Go's sequential order: 64 terms are formed at once (a smoothed cost is Go's
 // window sum, a deviation is squared before it is added, as Go does) and then added one by one in
-// index order through v_readlane, four independent sums interleaved.
+// index order (seq_add below).
 namespace {
-__device__ __forceinline__ double rl(double v, int k) {           // lane k's v, wave-uniform
-  const int2 u = __builtin_bit_cast(int2, v);
-  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readlane(u.x, k), __builtin_amdgcn_readlane(u.y, k)));
-}
 __device__ __forceinline__ int64_t wave_isum(int64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
@@ -2083,35 +2074,25 @@ __device__ __forceinline__ void wave_argmax(double& a, int64_t& i) {
 }  // namespace
 
 // Sequential sums of 64 terms at a time (acc += v[lane 0], += v[lane 1], ... in lane order, for
-// NC independent sums at once).  PAIR_SCORE_LDS (round 6): the terms go through LDS and every lane
-// runs the add chain on broadcast reads, so a term costs one dependent v_add_f64 (the reads are
-// independent and issued ahead) instead of two v_readlane + the SGPR hazard + the add.
-#ifndef PAIR_SCORE_LDS
-#define PAIR_SCORE_LDS 1
-#endif
+// NC independent sums at once).  Round 6: the terms go through LDS and every lane runs the add chain
+// on broadcast reads, so a term costs one dependent v_add_f64 (the reads are independent and issue
+// ahead) instead of two v_readlane + the SGPR hazard + the add (3.2 -> 2.0 ms per launch).
 template <int NC>
 __device__ __forceinline__ void seq_add(double (&acc)[NC], const double (&v)[NC], int cnt, double* buf) {
-  if constexpr (PAIR_SCORE_LDS) {
-    const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) buf[64 * c + lane] = v[c];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  for (int c = 0; c < NC; ++c) buf[64 * c + lane] = v[c];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #pragma unroll 16
-    for (int k = 0; k < cnt; ++k) {
+  for (int k = 0; k < cnt; ++k) {
 #pragma unroll
-      for (int c = 0; c < NC; ++c) acc[c] += buf[64 * c + k];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the next block's stores after every read
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  } else {
-    for (int k = 0; k < cnt; ++k) {
-#pragma unroll
-      for (int c = 0; c < NC; ++c) acc[c] += rl(v[c], k);
-    }
+    for (int c = 0; c < NC; ++c) acc[c] += buf[64 * c + k];
   }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // the next block's stores after every read
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 __global__ __launch_bounds__(64) void pair_score_kernel(const ScoreJob* jobs) {

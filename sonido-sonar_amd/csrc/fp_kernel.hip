@@ -124,7 +124,7 @@ template <> struct Vec2<double> { using type = double2; };
 // float64 PCM, MFCC only 3.17-3.19 / 3.30-3.31 / 3.73 ms per hour; float64 PCM, MFCC + descriptors
 // (the GenerateFingerprint transform) 6.62-6.63 / 6.79-6.81 / 7.47-7.50 ms; float32 PCM equal at 1
 // and 2.  (An earlier A/B, profiles/r06f_fp64_ab.log, had 3 ahead on the float32-PCM instance.)
-// FP64_PREFETCH / FP64_WINREG at 0 (no PCM prefetch / the window re-read): no faster (r06f).
+// Dropping the PCM prefetch or re-reading the window instead of holding it: no faster (r06f).
 template <typename T, typename P, int R, bool SPEC, bool CPLX = false>
 __global__ __launch_bounds__(256, (sizeof(T) == 8 && !SPEC && !CPLX && R == 8) ? FP64_MIN_WAVES : 1)
 void fp_wave_kernel(FpParams p) {
@@ -248,22 +248,13 @@ void fp_wave_kernel(FpParams p) {
     }
   };
 
-  // the next unit's PCM in registers during the current FFT (PF); FP64_PREFETCH=0 drops it for the
-  // float64 MFCC / magnitude instance (A/B knob, measured no faster)
-#ifndef FP64_PREFETCH
-#define FP64_PREFETCH 1
-#endif
-#ifndef FP64_WINREG
-#define FP64_WINREG 1
-#endif
-  constexpr bool PF = !(sizeof(T) == 8 && !SPEC) || FP64_PREFETCH;
+  // the next unit's PCM in registers during the current FFT
   T cur_e[FR][R], cur_o[FR][R];
-  if (PF) load_unit(unit_frame(0), cur_e, cur_o);
+  load_unit(unit_frame(0), cur_e, cur_o);
 
   for (int64_t ui = 0; ui < nunits; ++ui) {
     T nxt_e[FR][R], nxt_o[FR][R];
-    if (PF) { if (ui + 1 < nunits) load_unit(unit_frame(ui + 1), nxt_e, nxt_o); }
-    else load_unit(unit_frame(ui), cur_e, cur_o);
+    if (ui + 1 < nunits) load_unit(unit_frame(ui + 1), nxt_e, nxt_o);
     const int rb = unit_row(ui);
     T* S = rows + (int64_t)rb * K;              // scratch = the unit's own rows
 
@@ -274,10 +265,7 @@ void fp_wave_kernel(FpParams p) {
       for (int fr = 0; fr < FR; fr++)
 #pragma unroll
         for (int a = 0; a < R; a++) {
-          // FP64_WINREG=0: the window read per unit (L1-resident) instead of 2R registers held
-          const T we_ = FP64_WINREG || sizeof(T) == 4 || SPEC ? we[a] : win[2 * (64 * a + lane)];
-          const T wo_ = FP64_WINREG || sizeof(T) == 4 || SPEC ? wo[a] : win[2 * (64 * a + lane) + 1];
-          xr[fr][a] = cur_e[fr][a] * we_; xi[fr][a] = cur_o[fr][a] * wo_;
+          xr[fr][a] = cur_e[fr][a] * we[a]; xi[fr][a] = cur_o[fr][a] * wo[a];
         }
       // step 1: R-point DFT over a, twiddle w_M^{lane c}
 #pragma unroll
@@ -433,12 +421,10 @@ void fp_wave_kernel(FpParams p) {
       }
       wave_lds_sync();
     }
-    if (PF) {
 #pragma unroll
-      for (int fr = 0; fr < FR; fr++)
+    for (int fr = 0; fr < FR; fr++)
 #pragma unroll
-        for (int a = 0; a < R; a++) { cur_e[fr][a] = nxt_e[fr][a]; cur_o[fr][a] = nxt_o[fr][a]; }
-    }
+      for (int a = 0; a < R; a++) { cur_e[fr][a] = nxt_e[fr][a]; cur_o[fr][a] = nxt_o[fr][a]; }
 
     // ======================= batch epilogue (lane = frame x group) ==========
     const int64_t bi_ = pre ? ui - 1 : ui;

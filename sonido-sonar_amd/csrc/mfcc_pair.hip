@@ -276,28 +276,6 @@ template <typename T> struct template_ty { using type = T; };
 
 }  // namespace
 
-#ifndef P64_WIN_G
-#define P64_WIN_G 1
-#endif
-#ifndef P64_TW1_R
-#define P64_TW1_R 1
-#endif
-#ifndef P64_TW2_L
-#define P64_TW2_L 1
-#endif
-// the same three moves for the float32 kernel (A/B knobs, default off) and its waves per block
-#ifndef HL_F32_WIN_G
-#define HL_F32_WIN_G 0
-#endif
-#ifndef HL_F32_TW1_R
-#define HL_F32_TW1_R 0
-#endif
-#ifndef HL_F32_TW2_L
-#define HL_F32_TW2_L 0
-#endif
-#ifndef HL_F32_WAVES
-#define HL_F32_WAVES 12
-#endif
 
 // JT / MS / NH: compile-time chunk length, sources per filter and DCT half-length for the
 // headline bank (40 mels at 44.1 kHz: 12 / 8 / 20); 0 = read from p (runtime loops).
@@ -307,7 +285,7 @@ template <typename T> struct template_ty { using type = T; };
 // rows instead of 32 and holds 20 PCM registers) or 0 (runtime p.H, both frames loaded).
 // T: arithmetic / output type (float: the headline; double: 8 waves per block); P: PCM type.
 template <typename T, typename P, bool POW2, int JT, int MS, int NH, bool SEG, int HC>
-__global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 64 * HL_F32_WAVES, 1) void mfcc_pair_kernel(MfccPairParams p) {
+__global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 768, 1) void mfcc_pair_kernel(MfccPairParams p) {
   using L = Lay<T>;
   using C = cx<T>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -327,7 +305,7 @@ __global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 64 * HL_F32_WAVES, 1) void m
   }
   const T* g_dct = reinterpret_cast<const T*>(p.dct);
   for (int i = threadIdx.x; i < 16 * (p.NMP + 4); i += blockDim.x) s_dct[i] = g_dct[i];
-  if (sizeof(T) == 8 ? P64_TW2_L : HL_F32_TW2_L) {
+  if (sizeof(T) == 8) {   // the float64 instance's stage-2 twiddle table
     C* t = reinterpret_cast<C*>(smem + p.lds_tw2);
     for (int i = threadIdx.x; i < 64; i += blockDim.x) t[i] = reinterpret_cast<const C*>(p.tw2)[i];
   }
@@ -344,13 +322,13 @@ __global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 64 * HL_F32_WAVES, 1) void m
 
   // ---- per-lane constants ---------------------------------------------------------
   // float64 register budget (8 waves per CU = 256 VGPRs each): the per-lane constants that the
-  // float32 kernel keeps in registers are re-read or derived per pair instead --
-  //   P64_WIN_G:  the window from global memory (L1/L2-resident 8 KB) at each pair's pass 1;
-  //   P64_TW1_R:  w_1024^{lane k1} from four held powers (k1 = 1, 2, 4, 8) by 11 complex products;
-  //   P64_TW2_L:  w_64^{b0 c0} from an LDS table (8 distinct rows per wave: broadcast reads).
+  // float32 kernel keeps in registers are re-read or derived per pair instead -- the window from
+  // global memory (L1/L2-resident 8 KB) at each pair's pass 1 (WIN_G), w_1024^{lane k1} from four
+  // held powers (k1 = 1, 2, 4, 8) by 11 complex products (TW1_R), w_64^{b0 c0} from an LDS table
+  // (TW2_L: 8 distinct rows per wave, broadcast reads).  The same moves in the float32 kernel (16
+  // waves per CU at 128 VGPRs) measured slower (DESIGN.md Kernel 1a, profiles/r06y_*).
   constexpr bool D = sizeof(T) == 8;
-  constexpr bool WIN_G = D ? P64_WIN_G : HL_F32_WIN_G, TW1_R = D ? P64_TW1_R : HL_F32_TW1_R,
-                 TW2_L = D ? P64_TW2_L : HL_F32_TW2_L;
+  constexpr bool WIN_G = D, TW1_R = D, TW2_L = D;
   const T* g_win = reinterpret_cast<const T*>(p.window);
   T win[16];
   if constexpr (!WIN_G) {
@@ -525,10 +503,6 @@ __global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 64 * HL_F32_WAVES, 1) void m
     if constexpr (TW1_R) {
       C w[16];
       w[1] = tw1[1]; w[2] = tw1[2]; w[4] = tw1[4]; w[8] = tw1[8];
-      if constexpr (!D) {   // keep the products in the loop (hoisted, they would hold 11 more pairs)
-#pragma unroll
-        for (int k = 1; k <= 8; k <<= 1) { T x = w[k].x, y = w[k].y; asm volatile("" : "+v"(x), "+v"(y)); w[k] = C{x, y}; }
-      }
       w[3] = cmul(w[1], w[2]); w[5] = cmul(w[4], w[1]); w[6] = cmul(w[4], w[2]); w[7] = cmul(w[4], w[3]);
 #pragma unroll
       for (int k = 9; k < 16; k++) w[k] = cmul(w[8], w[k - 8]);
@@ -751,8 +725,8 @@ int launch_mfcc_pair(const MfccPairParams& p, hipStream_t s) {
 }
 
 int mfcc_pair_wave_bytes(int f64) { return f64 ? Lay<double>::WaveBytes : Lay<float>::WaveBytes; }
-int mfcc_pair_waves_per_block(int f64) { return f64 ? 8 : HL_F32_WAVES; }
-int mfcc_pair_waves_per_cu(int f64) { return f64 ? 8 : HL_F32_WAVES; }
+int mfcc_pair_waves_per_block(int f64) { return f64 ? 8 : 12; }
+int mfcc_pair_waves_per_cu(int f64) { return f64 ? 8 : 12; }
 int mfcc_pair_rows() { return kPRows; }
 
 }  // namespace sonar

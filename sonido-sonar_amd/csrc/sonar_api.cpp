@@ -521,7 +521,7 @@ void fill_pair_params(sonar_ctx* c, const PairTables& t, const sonar_fp_cfg* cfg
   q.lds_dct = q.lds_src + 64 * 16 * 2;
   q.lds_ctr = q.lds_dct + al(16 * (t.NMP + 4) * es);
   q.lds_tw2 = q.lds_ctr + 16;
-  q.lds_wave0 = q.lds_tw2 + 64 * 16;            // the stage-2 twiddle table (float64; float32 knob)
+  q.lds_wave0 = q.lds_tw2 + (f64 ? 64 * 16 : 0);   // float64: the stage-2 twiddle table
   // mfcc_pair_kernel: one block per CU (12 waves float32, 8 float64) over a contiguous range of pairs
   // One block per CU.  The float64 waves' 17.4 KB regions beside the largest tables (J = 16,
   // NMP = 64: 29 KB) exceed the 160 KiB of LDS at 8 waves; such a bank runs 7 (or fewer) waves
