@@ -2085,20 +2085,40 @@ __device__ __forceinline__ void seq_add(double (&acc)[NC], const double (&v)[NC]
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#pragma unroll 16
-  for (int k = 0; k < cnt; ++k) {
+  // 32 terms per sum into registers with every read issued up front, then the adds in order
+  for (int k0 = 0; k0 < cnt; k0 += 32) {
+    double r[NC][32];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) acc[c] += buf[64 * c + k];
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int q = 0; q < 32; q += 2) {
+        const double2 v2 = *reinterpret_cast<const double2*>(&buf[64 * c + k0 + q]);
+        r[c][q] = v2.x; r[c][q + 1] = v2.y;
+      }
+    if (k0 + 32 <= cnt) {
+#pragma unroll
+      for (int q = 0; q < 32; ++q)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c] += r[c][q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 32; ++q)
+        if (k0 + q < cnt) {
+#pragma unroll
+          for (int c = 0; c < NC; ++c) acc[c] += r[c][q];
+        }
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");     // the next block's stores after every read
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+constexpr int SU = 4;   // 64-term steps whose terms are formed before their adds (loads in flight)
 __global__ __launch_bounds__(64) void pair_score_kernel(const ScoreJob* jobs) {
   const ScoreJob j = jobs[blockIdx.x];
   const int lane = threadIdx.x;
-  __shared__ double sbuf[2 * 64];
+  __shared__ __attribute__((aligned(16))) double sbuf[2 * 64];
   // ---- warping path
   const int64_t P = *j.plen;
   host::PathSums ps;
@@ -2113,24 +2133,36 @@ __global__ __launch_bounds__(64) void pair_score_kernel(const ScoreJob* jobs) {
       return t / (double)(hi - lo + 1);
     };
     double sc = 0.0, ss = 0.0;                       // Go's sequential sums (wave-uniform)
-    for (int64_t b = 0; b < P; b += 64) {
-      const int64_t i = b + lane;
-      double c = 0.0, m = 0.0;
-      if (i < P) {
-        off += j.pr[i] - j.pq[i];
-        c = j.pc[i];
-        if (P > 1) m = smooth(i);
-        if (i >= 1) {
-          const int d0 = j.pq[i] - j.pq[i - 1], d1 = j.pr[i] - j.pr[i - 1];
-          if (d0 > 0 && d1 > 0) dg++;
-          if (i >= 2 && (d0 != j.pq[i - 1] - j.pq[i - 2] || d1 != j.pr[i - 1] - j.pr[i - 2])) ch++;
+    // SU steps of 64 terms are formed first (their path loads all in flight at once), then added
+    for (int64_t b0 = 0; b0 < P; b0 += 64 * SU) {
+      double cu[SU], mu[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int64_t i = b0 + 64 * u + lane;
+        double c = 0.0, m = 0.0;
+        if (i < P) {
+          off += j.pr[i] - j.pq[i];
+          c = j.pc[i];
+          if (P > 1) m = smooth(i);
+          if (i >= 1) {
+            const int d0 = j.pq[i] - j.pq[i - 1], d1 = j.pr[i] - j.pr[i - 1];
+            if (d0 > 0 && d1 > 0) dg++;
+            if (i >= 2 && (d0 != j.pq[i - 1] - j.pq[i - 2] || d1 != j.pr[i - 1] - j.pr[i - 2])) ch++;
+          }
+        }
+        cu[u] = c; mu[u] = m;
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int64_t b = b0 + 64 * u;
+        if (b < P) {
+          const int cnt = (int)min((int64_t)64, P - b);
+          double acc[2] = {sc, ss};
+          const double v[2] = {cu[u], mu[u]};
+          seq_add<2>(acc, v, cnt, sbuf);
+          sc = acc[0]; ss = acc[1];
         }
       }
-      const int cnt = (int)min((int64_t)64, P - b);
-      double acc[2] = {sc, ss};
-      const double v[2] = {c, m};
-      seq_add<2>(acc, v, cnt, sbuf);
-      sc = acc[0]; ss = acc[1];
     }
     ps.offset_sum = wave_isum(off);
     ps.diag_steps = wave_isum(dg);
@@ -2141,15 +2173,26 @@ __global__ __launch_bounds__(64) void pair_score_kernel(const ScoreJob* jobs) {
       ps.sum_smooth = ss;
       const double mean = ss / (double)P;
       double vv = 0.0;
-      for (int64_t b = 0; b < P; b += 64) {
-        const int64_t i = b + lane;
-        double d2 = 0.0;
-        if (i < P) { const double d = smooth(i) - mean; d2 = d * d; }
-        const int cnt = (int)min((int64_t)64, P - b);
-        double acc[1] = {vv};
-        const double v[1] = {d2};
-        seq_add<1>(acc, v, cnt, sbuf);
-        vv = acc[0];
+      for (int64_t b0 = 0; b0 < P; b0 += 64 * SU) {
+        double du[SU];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int64_t i = b0 + 64 * u + lane;
+          double d2 = 0.0;
+          if (i < P) { const double d = smooth(i) - mean; d2 = d * d; }
+          du[u] = d2;
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int64_t b = b0 + 64 * u;
+          if (b < P) {
+            const int cnt = (int)min((int64_t)64, P - b);
+            double acc[1] = {vv};
+            const double v[1] = {du[u]};
+            seq_add<1>(acc, v, cnt, sbuf);
+            vv = acc[0];
+          }
+        }
       }
       ps.var_smooth = vv;
     }
@@ -2175,21 +2218,32 @@ __global__ __launch_bounds__(64) void pair_score_kernel(const ScoreJob* jobs) {
     cs.peak = j.corr[pi];
     double ns = 0.0, sa = -1.0, ms = 0.0;
     int64_t nc = 0, si = nl;
-    for (int64_t b = 0; b < nl; b += 64) {
-      const int64_t i = b + lane;
-      double sq = 0.0;                               // terms outside the mask add an exact +0
-      if (i < nl) {
-        const double c = j.corr[i], v = fabs(c);
-        const int64_t d = i > pi ? i - pi : pi - i;
-        if (d > 5) { sq = c * c; nc++; }
-        if (i != pi && v > sa) { sa = v; si = i; }
-        if (d > 10 && v > ms) ms = v;
+    for (int64_t b0 = 0; b0 < nl; b0 += 64 * SU) {
+      double qu[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int64_t i = b0 + 64 * u + lane;
+        double sq = 0.0;                             // terms outside the mask add an exact +0
+        if (i < nl) {
+          const double c = j.corr[i], v = fabs(c);
+          const int64_t d = i > pi ? i - pi : pi - i;
+          if (d > 5) { sq = c * c; nc++; }
+          if (i != pi && v > sa) { sa = v; si = i; }
+          if (d > 10 && v > ms) ms = v;
+        }
+        qu[u] = sq;
       }
-      const int cnt = (int)min((int64_t)64, nl - b);
-      double acc[1] = {ns};
-      const double v[1] = {sq};
-      seq_add<1>(acc, v, cnt, sbuf);
-      ns = acc[0];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int64_t b = b0 + 64 * u;
+        if (b < nl) {
+          const int cnt = (int)min((int64_t)64, nl - b);
+          double acc[1] = {ns};
+          const double v[1] = {qu[u]};
+          seq_add<1>(acc, v, cnt, sbuf);
+          ns = acc[0];
+        }
+      }
     }
     cs.noise_sum = ns;
     cs.noise_count = wave_isum(nc);
