@@ -1204,6 +1204,10 @@ def main():
     if args.batch_signals > 0:
         leg("fp_batch", lambda: bench_fp_batch(args, ctx, dev, cfg))
     if args.c5_pairs > 0:
+        # the earlier legs' device buffers (the hour's |X| scratch, the C3 DTW's codes and
+        # checkpoints: several GB) are released first, so C5 runs in the memory state it has alone
+        ctx.trim()
+        torch.cuda.empty_cache()
         leg("c5", lambda: bench_c5(args, world, rank, dev, ctx))
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             leg("c5_cpu_baseline", lambda: {"c5_cpu_baseline": c5_cpu_baseline(args)})
