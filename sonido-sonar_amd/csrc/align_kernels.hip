@@ -442,7 +442,16 @@ constexpr int DTW_RBLK = 16;               // rows per ring refill
 #ifndef DTW_DQ_CFG
 #define DTW_DQ_CFG 32
 #endif
-constexpr int DTW_DQ = DTW_DQ_CFG;         // steps of distances held in LDS (a power of two)
+constexpr int DTW_DQ = DTW_DQ_CFG;         // steps of distances held in LDS (a power of two), batched
+#ifndef DTW_DQ_SINGLE_CFG
+#define DTW_DQ_SINGLE_CFG 64
+#endif
+// ... and for the single-DTW instance (C3): 64 steps let the distance waves run further ahead of the
+// sweep.  Same box, three rounds (profiles/r06ah_dtw_rings_ab.log): C3 band 14.9-15.2 against
+// 15.7-16.1 ms; in the batched instance the larger LDS footprint costs C5 4 % (2,134-2,146 against
+// 2,216-2,229 pairs/s), so it keeps 32.  The split confirmed on another box (r06ai_dtw_dq_single_ab.log):
+// C3 band 14.9-15.1 against 15.6-16.3 ms, C5 unchanged.  68.5 KB of LDS, 104-108 VGPRs: still 2 per CU
+constexpr int DTW_DQ_SINGLE = DTW_DQ_SINGLE_CFG;
 #ifndef DTW_SWEEP_PRIO_CFG
 #define DTW_SWEEP_PRIO_CFG 3
 #endif
@@ -652,7 +661,8 @@ void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
   constexpr int CODE_WAVE = DTW_CODE_WAVE;
   constexpr int EDGE_WAVE = DTW_EDGE_WAVE;
   __shared__ __attribute__((aligned(16))) double ring[(DTW_RROWS + DTW_RMIR) * DS];
-  __shared__ __attribute__((aligned(16))) double dring[64][DTW_DROW];   // distance of step t at [l][t % DQ]
+  constexpr int DQ = BATCH ? DTW_DQ : DTW_DQ_SINGLE;
+  __shared__ __attribute__((aligned(16))) double dring[64][DQ + 2];     // distance of step t at [l][t % DQ]
   __shared__ __attribute__((aligned(16))) double oring[64][DTW_OROW];   // C of step t at [l][t % OQ]
   __shared__ __attribute__((aligned(16))) double eqa[DTW_EQ];           // C[64b][c] at slot c - 1
   __shared__ __attribute__((aligned(16))) double eqb[DTW_EQ];           // C[64b][c] at slot c
@@ -985,7 +995,7 @@ void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
     for (int64_t c = w; DTW_ECH * c < S; c += DTW_NDW) {
       const int64_t t0 = DTW_ECH * c;
       // ring slots of steps t0..t0+7 were last read by the sweep for steps t0-DQ..t0-DQ+7
-      SONAR_SPIN_UNTIL(DTW_ROLE_DIST, DTW_DIST_PRIO, SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DTW_DQ);
+      SONAR_SPIN_UNTIL(DTW_ROLE_DIST, DTW_DIST_PRIO, SONAR_LDS_LD(prog) >= t0 + DTW_ECH - DQ);
       double dv[DTW_ECH];
       if constexpr (D > 0) {
         const int64_t need = (t0 + DTW_ECH - 1) / DTW_RBLK;             // rows up to t0+7
@@ -1045,7 +1055,7 @@ void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
 #pragma unroll
         for (int u = 0; u < DTW_ECH; ++u) dv[u] = dist_rt(t0 + u);
       }
-      double* drow = &dring[lane][t0 & (DTW_DQ - 1)];
+      double* drow = &dring[lane][t0 & (DQ - 1)];
 #pragma unroll
       for (int u = 0; u < DTW_ECH; u += 2)
         *reinterpret_cast<double2*>(drow + u) = make_double2(dv[u], dv[u + 1]);
@@ -1132,7 +1142,7 @@ void dtw_band_kernel(DtwArgs a_in, DtwBatch bt) {
   typedef double d2v __attribute__((ext_vector_type(2)));
   typedef __attribute__((address_space(3))) volatile d2v lds_d2;
   auto load_chunk = [&](int64_t s0, double (&dc)[DTW_ECH], double (&ech)[DTW_ECH]) {
-    const double* dr = &dring[lane][s0 & (DTW_DQ - 1)];
+    const double* dr = &dring[lane][s0 & (DQ - 1)];
     const double* er = &eqa[s0 & (DTW_EQ - 1)];        // columns s0+1 .. s0+8
 #pragma unroll
     for (int u = 0; u < DTW_ECH; u += 2) {
