@@ -105,3 +105,23 @@ def test_multi_align_pairs_equals_single(ctx, multi, pair_set):
     b = multi.align_pairs(qs, rs, max_lag_seconds=8.0, workers=2)
     for f in list(sonar.PAIR_FIELDS) + ["status"]:
         assert _same(a[f], b[f]), f
+
+
+def test_frame_shards_reproduce_whole_f64_pair(ctx):
+    """The float64 pair kernel (round 6) under frame sharding: the shards' inner boundaries are even,
+    so every shard pairs its frames as the whole does and its rows are the whole's, bit for bit."""
+    x = synth.c2_hour(seconds=30.0).astype(np.float64)
+    cfg = ctx.config(window_size=1024, hop_size=256, sample_rate=SR, n_filters=40, n_mfcc=13,
+                     precision=sonar.F64, pcm_dtype=sonar.F64, out_dtype=sonar.F64, flags=sonar.FP_MFCC)
+    whole = ctx.fingerprint(x, cfg)["mfcc"]
+    assert ctx.last_fp_kernel() == "mfcc_pair_kernel"
+    for g in range(3):
+        f0, f1, s0, s1 = sonar.multi_shard(len(x), 1024, 256, 3, g)
+        assert np.array_equal(ctx.fingerprint(x[s0:s1], cfg)["mfcc"], whole[f0:f1]), g
+
+
+def test_multi_fingerprint_f64_pair_equals_single(ctx, multi):
+    x = synth.c2_hour(seconds=20.0).astype(np.float64)
+    cfg = ctx.config(window_size=1024, hop_size=256, sample_rate=SR, n_filters=40, n_mfcc=13,
+                     precision=sonar.F64, pcm_dtype=sonar.F64, out_dtype=sonar.F64, flags=sonar.FP_MFCC)
+    assert np.array_equal(ctx.fingerprint(x, cfg)["mfcc"], multi.fingerprint(x, cfg)["mfcc"])
