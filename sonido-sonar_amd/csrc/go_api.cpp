@@ -237,7 +237,8 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
   };
   // the harmonic features' tracker runs chunk by chunk during the pipeline (below) when the speech
   // block does not need the pitch rows first (SONAR_GF_EARLY=0: after the last chunk)
-  static const int gf_early = [] { const char* e = std::getenv("SONAR_GF_EARLY"); return e ? std::atoi(e) : 1; }();
+  const char* gf_env = std::getenv("SONAR_GF_EARLY");
+  const int gf_early = gf_env ? std::atoi(gf_env) : 1;
   // the device's address of the block's pitch rows (mapped pinned memory); none -> the late order
   double *hpit = nullptr, *hcon = nullptr;
   if (!fc->enable_speech_features && gf_early != 0 && Fp_z) {

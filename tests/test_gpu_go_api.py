@@ -156,3 +156,19 @@ def test_extract_speech_chunked_pcm_real_rate(ctx, monkeypatch):
     assert got.keys() == one.keys()
     for k in one:
         assert np.array_equal(np.asarray(got[k]), np.asarray(one[k]), equal_nan=True), k
+
+
+def test_generate_fingerprint_early_tracker_equals_late(ctx, monkeypatch):
+    """Music content (no speech block): the harmonic tracker runs per chunk on YIN rows written
+    straight into the pinned result block (round 6); SONAR_GF_EARLY=0 runs it after the last chunk.
+    Same bits either way, chunked and one-shot."""
+    x = synth.c2_hour(seconds=60.0).astype(np.float64)
+    cfg = ctx.fingerprint_config(window_size=1024, hop_size=256, feature_window_size=1024, feature_hop_size=256,
+                                 precision=sonar.F64)
+    monkeypatch.setenv("SONAR_PCM_CHUNK", "400000")
+    early = ctx.generate_fingerprint(x, 44100, "music", cfg)
+    monkeypatch.setenv("SONAR_GF_EARLY", "0")
+    late = ctx.generate_fingerprint(x, 44100, "music", cfg)
+    assert early.keys() == late.keys()
+    for k in early:
+        assert np.array_equal(np.asarray(early[k]), np.asarray(late[k]), equal_nan=True), k
