@@ -251,6 +251,12 @@ int sonar_extract_speech_features(sonar_ctx* c, const double* pcm, int64_t n, in
     }
   }
   const bool trk_early = hpit != nullptr;
+  // YIN writes into the pinned block: on any early return the side stream is drained before the
+  // block goes back to the pool (declared after `blk`, so it runs first)
+  struct SideDrain {
+    hipStream_t st;
+    ~SideDrain() { if (st) (void)hipStreamSynchronize(st); }
+  } side_drain{trk_early ? c->side : nullptr};
   int64_t done_fp = 0, done_e = 0, done_p = 0, done_env = 0, done_l = 0;
   std::vector<int64_t> p_end(NCH, 0);                              // pitch frames complete after chunk k
   for (int64_t k = 0; k < NCH; ++k) {
