@@ -29,10 +29,11 @@ struct FpTables {
 // tables of the headline kernel (mfcc_pair.hip); ok = false -> configuration unsupported there
 struct PairTables {
   bool ok = false;
-  // [0] float32 tables (the headline), [1] float64 (the same bank at the reference's precision)
+  // [0] float32 tables (the headline), [1] float64 (the same bank at the reference's precision; its
+  // own chunk lane order, searched for its 16-byte power-row reads)
   void *window[2] = {}, *tw1[2] = {}, *tw2[2] = {}, *chunk_w[2] = {}, *dct[2] = {};
-  int* chunk_ks = nullptr;
-  uint16_t* mel_src = nullptr;
+  int* chunk_ks[2] = {};
+  uint16_t* mel_src[2] = {};
   void* zeros = nullptr;    // 1024 zero samples of either PCM type (8 KB)
   int J = 0, JS = 0, NMP = 0, n_mels = 0, n_mfcc = 0, max_src = 0;
 };

@@ -101,7 +101,7 @@ struct MfccPairParams {
   const int* chunk_ks;  // [64] first bin of each lane's filterbank chunk
   const void* chunk_w;  // [64][JS] complex (weight of slot a, weight of slot b), 1/4 (or 1/16) folded
   const uint16_t* mel_src; // [16][64] partial-sum pair index (2 lane + slot), bit 15 = unused
-  const void* dct;      // [16][NMP + 4] T: DCT-II rows with the lifter folded in
+  const void* dct;      // [16][NMP + mfcc_pair_dct_pad] T: DCT-II rows with the lifter folded in
   const void* zeros;    // [1024] zero PCM samples (8 KB): the samples of frames past the signal
   int J;                // bins per chunk (<= 16)
   int JS;               // chunk_w row stride = J | 1 (odd: conflict-free reads)
@@ -110,7 +110,7 @@ struct MfccPairParams {
   int n_mels, n_mfcc;   // n_mfcc <= 16
   int pow2;             // F5: MFCC.Compute fed |X|^2 -> filterbank of |X|^4
   void* out;            // [F][n_mfcc] T
-  int lds_src, lds_dct, lds_ctr, lds_tw2, lds_wave0, lds_bytes;   // lds_tw2: float64 only (64 complex)
+  int lds_src, lds_dct, lds_ctr, lds_tw2, lds_wave0, lds_bytes;   // lds_tw2: float64 only ([8][kPairTw2Row] complex)
   int waves_per_block;  // mfcc_pair_waves_per_block(f64)
   // sonar_fingerprint_batch (float32 only): nseg > 0 signals, F = 2 x the batch's pairs, pcm / n /
   // out unused; seg (device) = {pcm address[nseg], frames inside the signal[nseg], F[nseg], out
@@ -125,6 +125,14 @@ int mfcc_pair_wave_bytes(int f64);
 int mfcc_pair_waves_per_block(int f64);   // waves per block of mfcc_pair_kernel (its LDS carve: tables + waves x wave bytes)
 int mfcc_pair_waves_per_cu(int f64);      // resident waves per CU it is sized for
 int mfcc_pair_rows();
+// Per-instance LDS layout of mfcc_pair_kernel, shared with the host tables (bank-conflict-free
+// strides for its 8-B float32 and 16-B float64 accesses: tools/pair_lds_model.py):
+//   pad rows after every 16 power rows: float32 2 (18 rows x 8 B = 36 dwords per 16 bins), float64
+//   1 (17 x 16 B = 68 dwords: 8-lane ds_write_b128 groups of rows 18 apart collide mod 32);
+//   DCT row stride NMP + 4 (float32) / NMP + 2 (float64), stage-2 twiddle rows of 9 complex (float64).
+constexpr int mfcc_pair_pad_rows(int f64) { return f64 ? 1 : 2; }
+constexpr int mfcc_pair_dct_pad(int f64) { return f64 ? 2 : 4; }
+constexpr int kPairTw2Row = 9;
 bool fingerprint_supported(int W);
 int fp_batch_frames(int W, int f64, int spec);
 int fp_pre_rows(int W, int spec);

@@ -233,10 +233,11 @@ constexpr int kT2Irreg[2][8] = {
     {63 * 136, 60 * 136, 61 * 136, 62 * 136, 63 * 136 + 64, 62 * 136 + 64, 61 * 136 + 64, 60 * 136 + 64},
     {56 * 136, 57 * 136, 58 * 136, 59 * 136, 59 * 136 + 64, 58 * 136 + 64, 57 * 136 + 64, 56 * 136 + 64}};
 
-// power rows [bin][2 frames]: bin k at row k + 2 (k >> 4) -- two pad rows per 16 bins make the
-// split's stores (bins k1 + 16 c0 across a lane group) conflict-free; rows cover the chunk
-// over-read up to bin 527; the pad rows take the dummy bin-512 stores of lanes != 63
-__host__ __device__ constexpr int prow(int k) { return k + 2 * (k >> 4); }
+// power rows [bin][2 frames]: bin k at row k + PAD (k >> 4) -- pad rows after every 16 bins make the
+// split's stores (bins k1 + 16 c0 across a lane group) conflict-free: two for the float32 kernel's
+// 8-B rows, one for the float64 kernel's 16-B rows (mfcc_pair_pad_rows); rows cover the chunk
+// over-read up to bin 527; with two pad rows they take the dummy bin-512 stores of lanes != 63
+template <int PAD = 2> __host__ __device__ constexpr int prow(int k) { return k + PAD * (k >> 4); }
 constexpr int kPRows = 600;
 
 // one wave's LDS region for arithmetic type T (bytes)
@@ -245,7 +246,10 @@ template <typename T> struct Lay {
   static constexpr int T2Stride = 17 * CB;                     // bytes per lane row of the T2 buffer (17 complex)
   static constexpr int WaveBytes = 64 * T2Stride + 16;         // + a complex that stays zero (unused filter sources)
   static constexpr int PB = 2 * ES;                            // power row: [2 frames]
-  static constexpr int PartOff = kPRows * PB;                  // partial sums [64 lanes][a0 a1 b0 b1]
+  static constexpr int PadR = mfcc_pair_pad_rows(ES == 8);     // pad rows per 16 power rows
+  // partial sums: float32 [64 lanes][a0 a1 b0 b1]; float64 two planes [2][64 lanes][2] (16-B lane
+  // stride: a 32-B stride puts an 8-lane ds_write_b128 group on every bank twice)
+  static constexpr int PartOff = kPRows * PB;
   static constexpr int LogOff = PartOff + 64 * 4 * ES;         // logmel [2][NMP]
   static_assert(LogOff + 2 * 64 * ES <= WaveBytes, "wave region");
 };
@@ -294,20 +298,23 @@ __global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 768, 1) void mfcc_pair_kerne
   // ---- shared tables -> LDS ---------------------------------------------------
   C* s_cw = reinterpret_cast<C*>(smem);                                            // [64][J] (wa, wb)
   uint16_t* s_src = reinterpret_cast<uint16_t*>(smem + p.lds_src);                 // [16][64] source byte offsets
-  T* s_dct = reinterpret_cast<T*>(smem + p.lds_dct);                               // [16][NMP + 4], lifter folded
+  T* s_dct = reinterpret_cast<T*>(smem + p.lds_dct);                               // [16][NMP + DP], lifter folded
+  constexpr int DP = mfcc_pair_dct_pad(sizeof(T) == 8);
   const C* g_cw = reinterpret_cast<const C*>(p.chunk_w);
   for (int i = threadIdx.x; i < 64 * p.JS; i += blockDim.x) s_cw[i] = g_cw[i];
   // as byte offsets into the wave's region: a partial sum's pair (PartOff + 2 ES idx), or for an
   // unused source (bit 15) the complex that stays zero past the T2 rows
   for (int i = threadIdx.x; i < 64 * 16; i += blockDim.x) {
     const uint32_t idx = p.mel_src[i];
-    s_src[i] = (uint16_t)((idx & 0x8000u) ? 64 * L::T2Stride : L::PartOff + 2 * L::ES * (int)idx);
+    s_src[i] = (uint16_t)((idx & 0x8000u) ? 64 * L::T2Stride
+                          : L::PartOff + (sizeof(T) == 8 ? 16 * (int)(idx >> 1) + 1024 * (int)(idx & 1)
+                                                         : 2 * L::ES * (int)idx));
   }
   const T* g_dct = reinterpret_cast<const T*>(p.dct);
-  for (int i = threadIdx.x; i < 16 * (p.NMP + 4); i += blockDim.x) s_dct[i] = g_dct[i];
-  if (sizeof(T) == 8) {   // the float64 instance's stage-2 twiddle table
+  for (int i = threadIdx.x; i < 16 * (p.NMP + DP); i += blockDim.x) s_dct[i] = g_dct[i];
+  if (sizeof(T) == 8) {   // the float64 instance's stage-2 twiddle table, rows of kPairTw2Row complex
     C* t = reinterpret_cast<C*>(smem + p.lds_tw2);
-    for (int i = threadIdx.x; i < 64; i += blockDim.x) t[i] = reinterpret_cast<const C*>(p.tw2)[i];
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) t[(i >> 3) * kPairTw2Row + (i & 7)] = reinterpret_cast<const C*>(p.tw2)[i];
   }
   int* s_next = reinterpret_cast<int*>(smem + p.lds_ctr);                          // the block's pair counter
   if (threadIdx.x == 0) *s_next = 0;
@@ -343,7 +350,9 @@ __global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 768, 1) void mfcc_pair_kerne
     if (!TW1_R || k == 1 || k == 2 || k == 4 || k == 8) tw1[k] = g_tw1[lane * 16 + k];
   const int b0 = lane & 7, kl = lane >> 3;
   C tw2[8];                                     // w_64^{b0 c0}
-  const C* s_tw2 = reinterpret_cast<const C*>(smem + p.lds_tw2) + b0 * 8;
+  // (rows of 9 complex: the 8 rows a wave reads at once land on distinct banks -- rows of 8 put
+  // them all on one bank of the ds_read2_b64's mod-32 banking, 8-way)
+  const C* s_tw2 = reinterpret_cast<const C*>(smem + p.lds_tw2) + b0 * kPairTw2Row;
   if constexpr (!TW2_L) {
 #pragma unroll
     for (int c = 1; c < 8; c++) tw2[c] = g_tw2[b0 * 8 + c];
@@ -361,8 +370,9 @@ __global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 768, 1) void mfcc_pair_kerne
   else rA = 0;
   const int rB = (lane == 63) ? 64 : 128 - rA;
   const bool self = (lane == 63);
-  const int pA = prow(rA) * L::PB, pB = prow(rB) * L::PB;    // power row byte offsets (+144 rows per 128 bins)
-  const int p8 = L::PB * (self ? prow(512) : 18 * (lane & 31) + 16 + (lane >> 5));   // bin 512, or a pad row
+  constexpr int PR = L::PadR;
+  const int pA = prow<PR>(rA) * L::PB, pB = prow<PR>(rB) * L::PB;   // power row byte offsets (+(128 + 8 PR) rows per 128 bins)
+  const int p8 = L::PB * (self ? prow<PR>(512) : 18 * (lane & 31) + 16 + (lane >> 5));   // bin 512, or a pad row (PR = 2)
   const int ks = p.chunk_ks[lane];                           // mel chunk start bin
   const int nmp = p.NMP;
   // the ln phase's source byte offsets, loop-invariant per lane: in registers when the hop-256 PCM
@@ -575,7 +585,7 @@ __global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 768, 1) void mfcc_pair_kerne
       if (POW2) { p0 *= p0; p1 *= p1; }
       st2<T>(wb + off, p0, p1);
     };
-    constexpr int R128 = 144 * L::PB;                           // power rows of 128 bins (pad rows included)
+    constexpr int R128 = (128 + 8 * PR) * L::PB;                // power rows of 128 bins (pad rows included)
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       const C sec = self ? v[(8 - c) & 7] : v[15 - c];         // B[7 - c], or A[(8 - c) & 7] on lane 63
@@ -589,25 +599,32 @@ __global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 768, 1) void mfcc_pair_kerne
     }
     {                                                           // bin 512 (lane 63: (A4, A4))
       const T p0 = v[4].x * v[4].x * (T)4, p1 = v[4].y * v[4].y * (T)4;   // |2 a|^2 -> 4 a^2
-      if (POW2) st2<T>(wb + p8, p0 * p0, p1 * p1); else st2<T>(wb + p8, p0, p1);
+      if (PR == 2 || self) {                                    // one pad row: lane 63 alone
+        if (POW2) st2<T>(wb + p8, p0 * p0, p1 * p1); else st2<T>(wb + p8, p0, p1);
+      }
     }
     wave_lds_sync();
     // ---- filterbank: lane chunk [ks, ks + J) of one filter pair ----------------------
     {
       T a0 = 0, a1 = 0, c0 = 0, c1 = 0;
-      const unsigned char* pr = wb + prow(ks) * L::PB;
+      const unsigned char* pr = wb + prow<PR>(ks) * L::PB;
       const int ib = 16 - (ks & 15);                          // first i past a pad pair
       const C* cw = s_cw + lane * p.JS;
       const int J = JT ? JT : p.J;
 #pragma unroll
       for (int i = 0; i < J; i++) {
-        const C pp = ld2<T>(pr + L::PB * i + (i >= ib ? 2 * L::PB : 0));
+        const C pp = ld2<T>(pr + L::PB * i + (i >= ib ? PR * L::PB : 0));
         const C w = cw[i];
         a0 += w.x * pp.x; a1 += w.x * pp.y;
         c0 += w.y * pp.x; c1 += w.y * pp.y;
       }
-      st2<T>(wb + L::PartOff + 4 * L::ES * lane, a0, a1);
-      st2<T>(wb + L::PartOff + 4 * L::ES * lane + 2 * L::ES, c0, c1);
+      if constexpr (sizeof(T) == 8) {
+        st2<T>(wb + L::PartOff + 16 * lane, a0, a1);
+        st2<T>(wb + L::PartOff + 1024 + 16 * lane, c0, c1);
+      } else {
+        st2<T>(wb + L::PartOff + 4 * L::ES * lane, a0, a1);
+        st2<T>(wb + L::PartOff + 4 * L::ES * lane + 2 * L::ES, c0, c1);
+      }
     }
     wave_lds_sync();
     // ---- ln of the filter sums (lane = filter) ----------------------------------------
@@ -633,7 +650,7 @@ __global__ __launch_bounds__(sizeof(T) == 8 ? 512 : 768, 1) void mfcc_pair_kerne
       const int q = lane & 15, f = (lane >> 4) & 1, hh = lane >> 5;
       const int half = NH ? NH : (nmp >> 1);
       const T* lm = reinterpret_cast<const T*>(wb + L::LogOff) + f * nmp + hh * half;
-      const T* d = s_dct + q * (nmp + 4) + hh * half;         // row stride NMP + 4
+      const T* d = s_dct + q * (nmp + DP) + hh * half;        // row stride NMP + DP
       auto dot4 = [&](int m) -> T {                             // 4 terms, in the float32 kernel's order
         if constexpr (sizeof(T) == 4) {
           const float4 x = *reinterpret_cast<const float4*>(lm + m);

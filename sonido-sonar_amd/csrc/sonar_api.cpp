@@ -226,75 +226,91 @@ bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
   for (size_t gi = 0; gi < segs.size(); gi++)
     for (int k0 = segs[gi].k0; k0 < segs[gi].k1; k0 += J) chunks.push_back({k0, (int)gi});
   chunks.resize(64, Chunk{0, -1});                 // idle lanes read bin 0 with zero weights
-  // Lane order of the chunks.  The filterbank's ds_read_b64 of power row prow(ks + i) is serviced
-  // in two 32-lane groups, bank (byte / 4) mod 64: chunks whose rows fall on the same banks in one
-  // group serialise (modelled and counted in tools/scratch/pair_lds_model.py: 59 extra LDS cycles
-  // per pair in ascending order at the headline bank, the bulk of SQ_LDS_BANK_CONFLICT).  A swap
-  // search between the two groups lowers that; the filters still sum their chunks in ascending-bin
-  // order (the source lists below follow the chunk order, not the lanes).
-  std::vector<int> order(64);
-  for (int l = 0; l < 64; l++) order[l] = l;
-  auto prow_h = [](int k) { return k + 2 * (k >> 4); };
-  auto fb_conflicts = [&](const std::vector<int>& o) {
-    int extra = 0;
-    for (int i = 0; i < J; i++)
-      for (int g = 0; g < 2; g++) {
-        int used[64][32], nu[64] = {0};
-        for (int l = 32 * g; l < 32 * g + 32; l++) {
-          const int k = chunks[o[l]].k0;
-          const int dw = 2 * prow_h(k) + 2 * i + ((i >= 16 - (k & 15)) ? 4 : 0);
-          for (int d = 0; d < 2; d++) {
+  // Lane order of the chunks, per instance.  The filterbank's power-row reads ld2(prow(ks + i)) are
+  // ds_read_b64 in the float32 kernel (two 32-lane groups) and ds_read_b128 in the float64 kernel
+  // (four 16-lane groups), bank (byte / 4) mod 64: chunks whose rows fall on the same banks in one
+  // group serialise (tools/pair_lds_model.py: 59 extra LDS cycles per pair in ascending order at the
+  // headline bank in float32, the bulk of its SQ_LDS_BANK_CONFLICT).  A swap search between groups
+  // lowers that; the filters still sum their chunks in ascending-bin order (the source lists below
+  // follow the chunk order, not the lanes), so the order changes no result bit.
+  static const int kB128Group[64] = {0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 1, 1, 1, 1, 0, 0,
+                                     0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3,
+                                     2, 2, 2, 2, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2, 3, 3, 3, 3};
+  for (int e = 0; e < 2; e++) {
+    const int pad = sonar::mfcc_pair_pad_rows(e), ew = e ? 4 : 2;   // dwords per lane access
+    auto group_of = [&](int l) { return e ? kB128Group[l] : l >> 5; };
+    auto fb_conflicts = [&](const std::vector<int>& o) {
+      int extra = 0;
+      for (int i = 0; i < J; i++) {
+        int used[4][64][32], nu[4][64] = {};
+        for (int l = 0; l < 64; l++) {
+          const int k = chunks[o[l]].k0, g = group_of(l);
+          const int dw = ew * (k + pad * (k >> 4)) + ew * i + ((i >= 16 - (k & 15)) ? ew * pad : 0);
+          for (int d = 0; d < ew; d++) {
             const int b = (dw + d) & 63;
             bool seen = false;
-            for (int u = 0; u < nu[b]; u++) seen |= used[b][u] == dw + d;
-            if (!seen && nu[b] < 32) used[b][nu[b]++] = dw + d;
+            for (int u = 0; u < nu[g][b]; u++) seen |= used[g][b][u] == dw + d;
+            if (!seen && nu[g][b] < 32) used[g][b][nu[g][b]++] = dw + d;
           }
         }
-        int mx = 1;
-        for (int b = 0; b < 64; b++) mx = std::max(mx, nu[b]);
-        extra += mx - 1;
+        for (int g = 0; g < (e ? 4 : 2); g++) {
+          int mx = 1;
+          for (int b = 0; b < 64; b++) mx = std::max(mx, nu[g][b]);
+          extra += mx - 1;
+        }
       }
-    return extra;
-  };
-  for (int best = fb_conflicts(order), improved = 1; improved;) {
-    improved = 0;
-    for (int a = 0; a < 32; a++)
-      for (int b = 32; b < 64; b++) {
-        std::swap(order[a], order[b]);
-        const int c = fb_conflicts(order);
-        if (c < best) { best = c; improved = 1; }
-        else std::swap(order[a], order[b]);
-      }
-  }
-  std::vector<int> lane_of(64);
-  for (int l = 0; l < 64; l++) lane_of[order[l]] = l;
-  std::vector<int> ks(64, 0);
-  std::vector<double> cw(64 * 2 * JS, 0.0);
-  std::vector<std::vector<int>> src(64);
-  for (size_t ci = 0; ci < chunks.size(); ci++) {   // chunk order = ascending bins
-    const Chunk& ch = chunks[ci];
-    if (ch.seg < 0) continue;
-    const Seg& g = segs[ch.seg];
-    const int lane = lane_of[ci], k0 = ch.k0;
-    ks[lane] = k0;
-    for (int i = 0; i < J && k0 + i < g.k1; i++) {
-      cw[(lane * JS + i) * 2] = weight(g.a, k0 + i) * scale;
-      cw[(lane * JS + i) * 2 + 1] = g.b >= 0 ? weight(g.b, k0 + i) * scale : 0.0;
+      return extra;
+    };
+    std::vector<int> order(64);
+    for (int l = 0; l < 64; l++) order[l] = l;
+    for (int best = fb_conflicts(order), improved = 1; improved;) {
+      improved = 0;
+      for (int a = 0; a < 64; a++)
+        for (int b = a + 1; b < 64; b++) {
+          if (group_of(a) == group_of(b)) continue;
+          std::swap(order[a], order[b]);
+          const int c = fb_conflicts(order);
+          if (c < best) { best = c; improved = 1; }
+          else std::swap(order[a], order[b]);
+        }
     }
-    src[g.a].push_back(2 * lane);
-    if (g.b >= 0) src[g.b].push_back(2 * lane + 1);
-  }
-  std::vector<uint16_t> msrc(64 * 16, 0x8000);
-  int max_src = 1;
-  for (int m = 0; m < mt.n_mels; m++) {
-    if (src[m].size() > 16) return false;
-    max_src = std::max(max_src, (int)src[m].size());
-    for (size_t i = 0; i < src[m].size(); i++) msrc[i * 64 + m] = (uint16_t)src[m][i];
+    std::vector<int> lane_of(64);
+    for (int l = 0; l < 64; l++) lane_of[order[l]] = l;
+    std::vector<int> ks(64, 0);
+    std::vector<double> cw(64 * 2 * JS, 0.0);
+    std::vector<std::vector<int>> src(64);
+    for (size_t ci = 0; ci < chunks.size(); ci++) {   // chunk order = ascending bins
+      const Chunk& ch = chunks[ci];
+      if (ch.seg < 0) continue;
+      const Seg& g = segs[ch.seg];
+      const int lane = lane_of[ci], k0 = ch.k0;
+      ks[lane] = k0;
+      for (int i = 0; i < J && k0 + i < g.k1; i++) {
+        cw[(lane * JS + i) * 2] = weight(g.a, k0 + i) * scale;
+        cw[(lane * JS + i) * 2 + 1] = g.b >= 0 ? weight(g.b, k0 + i) * scale : 0.0;
+      }
+      src[g.a].push_back(2 * lane);
+      if (g.b >= 0) src[g.b].push_back(2 * lane + 1);
+    }
+    std::vector<uint16_t> msrc(64 * 16, 0x8000);
+    int max_src = 1;
+    for (int m = 0; m < mt.n_mels; m++) {
+      if (src[m].size() > 16) return false;
+      max_src = std::max(max_src, (int)src[m].size());
+      for (size_t i = 0; i < src[m].size(); i++) msrc[i * 64 + m] = (uint16_t)src[m][i];
+    }
+    t.max_src = max_src;
+    t.chunk_w[e] = e ? upload(cw) : upload(std::vector<float>(cw.begin(), cw.end()));
+    t.chunk_ks[e] = (int*)upload(ks); t.mel_src[e] = (uint16_t*)upload(msrc);
   }
   const int NMP = (mt.n_mels + 7) / 8 * 8;
-  std::vector<double> dct(16 * (NMP + 4), 0.0);
-  for (int q = 0; q < mt.n_mfcc; q++)
-    for (int m = 0; m < mt.n_mels; m++) dct[q * (NMP + 4) + m] = mt.dct[(size_t)q * mt.n_mels + m] * mt.lift[q];
+  auto dct_rows = [&](int e) {             // [16][NMP + pad]
+    const int st = NMP + sonar::mfcc_pair_dct_pad(e);
+    std::vector<double> dct(16 * st, 0.0);
+    for (int q = 0; q < mt.n_mfcc; q++)
+      for (int m = 0; m < mt.n_mels; m++) dct[q * st + m] = mt.dct[(size_t)q * mt.n_mels + m] * mt.lift[q];
+    return dct;
+  };
   std::vector<double> tw1(64 * 16 * 2), tw2(64 * 2);
   for (int b = 0; b < 64; b++)
     for (int k = 0; k < 16; k++) {
@@ -309,14 +325,14 @@ bool build_pair_tables(const sonar_fp_cfg* cfg, PairTables& t) {
   // float32 tables = the float64 values rounded once; float64 tables as computed
   auto f32 = [](const std::vector<double>& v) { return std::vector<float>(v.begin(), v.end()); };
   t.window[0] = upload(f32(win)); t.tw1[0] = upload(f32(tw1)); t.tw2[0] = upload(f32(tw2));
-  t.chunk_w[0] = upload(f32(cw)); t.dct[0] = upload(f32(dct));
+  t.dct[0] = upload(f32(dct_rows(0)));
   t.window[1] = upload(win); t.tw1[1] = upload(tw1); t.tw2[1] = upload(tw2);
-  t.chunk_w[1] = upload(cw); t.dct[1] = upload(dct);
-  t.chunk_ks = (int*)upload(ks); t.mel_src = (uint16_t*)upload(msrc);
+  t.dct[1] = upload(dct_rows(1));
   t.zeros = upload(std::vector<double>(1024, 0.0));
-  t.J = J; t.JS = JS; t.NMP = NMP; t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc; t.max_src = max_src;
-  t.ok = t.chunk_ks && t.mel_src && t.zeros;
-  for (int i = 0; i < 2; i++) t.ok = t.ok && t.window[i] && t.tw1[i] && t.tw2[i] && t.chunk_w[i] && t.dct[i];
+  t.J = J; t.JS = JS; t.NMP = NMP; t.n_mels = mt.n_mels; t.n_mfcc = mt.n_mfcc;
+  t.ok = t.zeros != nullptr;
+  for (int i = 0; i < 2; i++)
+    t.ok = t.ok && t.window[i] && t.tw1[i] && t.tw2[i] && t.chunk_w[i] && t.dct[i] && t.chunk_ks[i] && t.mel_src[i];
   return t.ok;
 }
 
@@ -361,6 +377,13 @@ void sonar_destroy(sonar_ctx* c) {
     for (void* p : {(void*)t.window, (void*)t.mel_lo, (void*)t.mel_hi, (void*)t.mel_woff, (void*)t.grp_off,
                     (void*)t.grp_mels, t.mel_w, t.dct, t.lift, t.trig})
       if (p) hipFree(p);
+  }
+  for (auto& kv : c->pair_tables) {
+    PairTables& t = kv.second;
+    for (int i = 0; i < 2; i++)
+      for (void* p : {t.window[i], t.tw1[i], t.tw2[i], t.chunk_w[i], t.dct[i], (void*)t.chunk_ks[i], (void*)t.mel_src[i]})
+        if (p) hipFree(p);
+    if (t.zeros) hipFree(t.zeros);
   }
   for (auto& kv : c->chroma_tables) {
     hipFree(kv.second.win); hipFree(kv.second.trig); hipFree(kv.second.map); hipFree(kv.second.cls);
@@ -513,15 +536,15 @@ void fill_pair_params(sonar_ctx* c, const PairTables& t, const sonar_fp_cfg* cfg
   const int e = f64 ? 1 : 0, es = f64 ? 8 : 4;
   q.f64 = e;
   q.window = t.window[e]; q.tw1 = t.tw1[e]; q.tw2 = t.tw2[e]; q.chunk_w = t.chunk_w[e]; q.dct = t.dct[e];
-  q.chunk_ks = t.chunk_ks; q.mel_src = t.mel_src; q.zeros = t.zeros;
+  q.chunk_ks = t.chunk_ks[e]; q.mel_src = t.mel_src[e]; q.zeros = t.zeros;
   q.J = t.J; q.JS = t.JS; q.max_src = t.max_src; q.NMP = t.NMP; q.n_mels = t.n_mels; q.n_mfcc = t.n_mfcc;
   q.pow2 = cfg->mfcc_input_power != 0;
   auto al = [](int x) { return (x + 15) & ~15; };
   q.lds_src = al(64 * t.JS * 2 * es);
   q.lds_dct = q.lds_src + 64 * 16 * 2;
-  q.lds_ctr = q.lds_dct + al(16 * (t.NMP + 4) * es);
+  q.lds_ctr = q.lds_dct + al(16 * (t.NMP + sonar::mfcc_pair_dct_pad(e)) * es);
   q.lds_tw2 = q.lds_ctr + 16;
-  q.lds_wave0 = q.lds_tw2 + (f64 ? 64 * 16 : 0);   // float64: the stage-2 twiddle table
+  q.lds_wave0 = q.lds_tw2 + (f64 ? 8 * sonar::kPairTw2Row * 16 : 0);   // float64: the stage-2 twiddle table
   // mfcc_pair_kernel: one block per CU (12 waves float32, 8 float64) over a contiguous range of pairs
   // One block per CU.  The float64 waves' 17.4 KB regions beside the largest tables (J = 16,
   // NMP = 64: 29 KB) exceed the 160 KiB of LDS at 8 waves; such a bank runs 7 (or fewer) waves
