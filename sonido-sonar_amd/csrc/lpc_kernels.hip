@@ -93,6 +93,9 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
     if (lane == 0) Rp[0][m] = v;
   }
   __syncthreads();
+#ifdef FMT_DBG_STOP_R
+  return;
+#endif
 
   if (tid == 0) {
     const double* R = Rp[0];
@@ -123,6 +126,9 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
   __syncthreads();
   const int status = (int)red[0];
   const double E = red[1];
+#ifdef FMT_DBG_STOP_LEV
+  return;
+#endif
   if (status != 0) {
     if (tid == 0) clear_record(o, status, p);
     return;
@@ -130,51 +136,89 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
   if (coeffs) for (int i = tid; i <= p; i += 256) coeffs[f * (p + 1) + i] = a[i];
   if (refl) for (int i = tid; i < p; i += 256) refl[f * p + i] = kr[i];
   // spectral envelope, nfft = 1024 (findFormantsFromLPC format.go:150)
+  // (cos, sin) of the angles -i w by the rotation recurrence from (cos w, -sin w): within
+  // ~i ulp of cos(-i w) (the libm calls cost ~150 VALU each and were ~80 % of the kernel;
+  // tools/formant_microbench.py, DESIGN.md Kernel 5); Go's sums in Go's order
   for (int kk = tid; kk <= 512; kk += 256) {
     const double w = 2.0 * M_PI * (double)kk / 1024.0;
+    const double c1 = cos(w), s1 = -sin(w);
+    double cr = c1, si = s1;
     double rp = 1.0, ip = 0.0;
     for (int i = 1; i <= p; ++i) {
-      const double ang = -(double)i * w;
-      rp += a[i] * cos(ang);
-      ip += a[i] * sin(ang);
+      rp += a[i] * cr;
+      ip += a[i] * si;
+      const double nc = cr * c1 - si * s1, ns = si * c1 + cr * s1;
+      cr = nc;
+      si = ns;
     }
     const double mg = sqrt(rp * rp + ip * ip);
     env[kk] = mg > 0 ? 1.0 / mg : 0.0;
   }
   __syncthreads();
-  if (tid != 0) return;
-
+  // findSpectralPeaks + bandwidths + confidences (format.go:148-300) by the first wave: every
+  // search is wave-parallel with the serial loop's exact outcome (the same comparisons; a ballot's
+  // lowest set lane is the loop's first hit), so no LDS read sits in a one-lane dependent chain
+  if (tid >= 64) return;
   int stable = 1;
-  for (int i = 1; i <= p; ++i) if (fabs(a[i]) >= 1.0) stable = 0;
+  {
+    bool bad = false;
+    for (int i = lane + 1; i <= p; i += 64) bad = bad || fabs(a[i]) >= 1.0;
+    if (__ballot(bad)) stable = 0;
+  }
   const double res = (double)sr / 1024.0;
-  double maxv = 0.0;
-  for (int i = 0; i < 513; ++i) if (env[i] > maxv) maxv = env[i];
+  double maxv = 0.0;                                  // Go's strict '>' scan from 0: NaN never taken
+  for (int i = lane; i < 513; i += 64) { const double e = env[i]; if (e > maxv) maxv = e; }
+  for (int sh = 32; sh > 0; sh >>= 1) { const double o = __shfl_xor(maxv, sh, 64); if (o > maxv) maxv = o; }
   double fq[4], bw[4], am[4], cf[4];
   int nf = 0;
   if (maxv != 0) {
-    for (int i = 1; i < 512 && nf < 4; ++i) {       // peaks are ascending: the first 4 survive the cut
-      if (!(env[i] > env[i - 1] && env[i] > env[i + 1])) continue;
-      if (!(env[i] / maxv > 0.1)) continue;
-      const double fr = (double)i * res;
-      if (fr < 50.0 || fr > (double)sr / 2.0) continue;
-      const double hh = env[i] / 2.0;
-      int li = i, ri = i;
-      for (int t = i - 1; t >= 0; --t) if (env[t] <= hh) { li = t; break; }
-      for (int t = i + 1; t < 513; ++t) if (env[t] <= hh) { ri = t; break; }
-      double b = (double)(ri - li) * res;
-      if (b < 50.0) b = 50.0; else if (b > 500.0) b = 500.0;
-      double c = 1.0;
-      if (fr >= 300 && fr <= 3500) c *= 1.0;
-      else if (fr >= 100 && fr <= 5000) c *= 0.7;
-      else c *= 0.3;
-      c *= dmin(env[i], 1.0);
-      if (b >= 50 && b <= 300) c *= 1.0;
-      else if (b >= 30 && b <= 500) c *= 0.8;
-      else c *= 0.5;
-      c = dmax(0.0, dmin(1.0, c));
-      fq[nf] = fr; bw[nf] = b; am[nf] = env[i]; cf[nf] = c; ++nf;
+    for (int base = 1; base < 512 && nf < 4; base += 64) {   // peaks are ascending: the first 4 survive the cut
+      const int i = base + lane;
+      bool ok = false;
+      if (i < 512) {
+        const double e = env[i];
+        ok = e > env[i - 1] && e > env[i + 1] && e / maxv > 0.1;
+        const double fr = (double)i * res;
+        ok = ok && !(fr < 50.0 || fr > (double)sr / 2.0);
+      }
+      uint64_t bal = __ballot(ok);
+      while (bal && nf < 4) {
+        const int pk = base + __ffsll((long long)bal) - 1;
+        bal &= bal - 1;
+        const double ei = env[pk], fr = (double)pk * res, hh = ei / 2.0;
+        int li = pk, ri = pk;
+        for (int t0 = pk - 1; t0 >= 0; t0 -= 64) {      // the nearest t < pk with env[t] <= hh
+          const int t = t0 - lane;
+          const uint64_t q = __ballot(t >= 0 && env[t] <= hh);
+          if (q) { li = t0 - (__ffsll((long long)q) - 1); break; }
+        }
+        for (int t0 = pk + 1; t0 < 513; t0 += 64) {     // the nearest t > pk with env[t] <= hh
+          const int t = t0 + lane;
+          const uint64_t q = __ballot(t < 513 && env[t] <= hh);
+          if (q) { ri = t0 + (__ffsll((long long)q) - 1); break; }
+        }
+        double b = (double)(ri - li) * res;
+        if (b < 50.0) b = 50.0; else if (b > 500.0) b = 500.0;
+        double c = 1.0;
+        if (fr >= 300 && fr <= 3500) c *= 1.0;
+        else if (fr >= 100 && fr <= 5000) c *= 0.7;
+        else c *= 0.3;
+        c *= dmin(ei, 1.0);
+        if (b >= 50 && b <= 300) c *= 1.0;
+        else if (b >= 30 && b <= 500) c *= 0.8;
+        else c *= 0.5;
+        c = dmax(0.0, dmin(1.0, c));
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (u == nf) { fq[u] = fr; bw[u] = b; am[u] = ei; cf[u] = c; }
+        ++nf;
+      }
     }
   }
+  if (lane != 0) return;
+#ifdef FMT_DBG_STOP_ENV
+  return;
+#endif
   double vf[4], vb[4], va[4], vc[4];
   int nv = 0;
   for (int i = 0; i < nf; ++i) {
