@@ -67,6 +67,7 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
     if (tid == 0) { clear_record(o, 1, p); o->gain = 0.0; o->residual_energy = 0.0; }
     return;
   }
+  #pragma unroll 8
   for (int i = tid; i < W; i += 256) {
     const double v = i == 0 ? sig[0] : sig[i] - 0.97 * sig[i - 1];
     x[i] = v * ham[i];
@@ -74,12 +75,15 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
   __syncthreads();
   // normalize (correlation.go:464-501): mean, population variance, z-score
   double s = 0.0;
+  #pragma unroll 8
   for (int i = tid; i < W; i += 256) s += x[i];
   const double mean = block_sum<256>(s, red) / (double)W;
   s = 0.0;
+  #pragma unroll 8
   for (int i = tid; i < W; i += 256) { const double d = x[i] - mean; s += d * d; }
   const double sd = sqrt(block_sum<256>(s, red) / (double)W);
   __syncthreads();
+  #pragma unroll 8
   for (int i = tid; i < W; i += 256) x[i] = sd < 1e-10 ? x[i] - mean : (x[i] - mean) / sd;
   __syncthreads();
   // R[m] = r(L - m), L = min(1024, W-1)
@@ -88,6 +92,7 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
   for (int m = wv; m <= p; m += 4) {                  // wave wv: lags L-m for m = wv, wv+4, ...
     const int k = L - m;
     double v = 0.0;
+    #pragma unroll 4
     for (int i = lane; i + k < W; i += 64) v += x[i] * x[i + k];
     for (int sh = 32; sh > 0; sh >>= 1) v += __shfl_xor(v, sh, 64);
     if (lane == 0) Rp[0][m] = v;
@@ -144,6 +149,7 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
     const double c1 = cos(w), s1 = -sin(w);
     double cr = c1, si = s1;
     double rp = 1.0, ip = 0.0;
+#pragma unroll 4
     for (int i = 1; i <= p; ++i) {
       rp += a[i] * cr;
       ip += a[i] * si;
