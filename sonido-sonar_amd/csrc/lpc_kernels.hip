@@ -98,9 +98,6 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
     if (lane == 0) Rp[0][m] = v;
   }
   __syncthreads();
-#ifdef FMT_DBG_STOP_R
-  return;
-#endif
 
   if (tid == 0) {
     const double* R = Rp[0];
@@ -131,9 +128,6 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
   __syncthreads();
   const int status = (int)red[0];
   const double E = red[1];
-#ifdef FMT_DBG_STOP_LEV
-  return;
-#endif
   if (status != 0) {
     if (tid == 0) clear_record(o, status, p);
     return;
@@ -143,7 +137,7 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
   // spectral envelope, nfft = 1024 (findFormantsFromLPC format.go:150)
   // (cos, sin) of the angles -i w by the rotation recurrence from (cos w, -sin w): within
   // ~i ulp of cos(-i w) (the libm calls cost ~150 VALU each and were ~80 % of the kernel;
-  // tools/formant_microbench.py, DESIGN.md Kernel 5); Go's sums in Go's order
+  // tools/formant_microbench.py, DESIGN.md Kernel 3c); Go's sums in Go's order
   for (int kk = tid; kk <= 512; kk += 256) {
     const double w = 2.0 * M_PI * (double)kk / 1024.0;
     const double c1 = cos(w), s1 = -sin(w);
@@ -222,9 +216,6 @@ __global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t
     }
   }
   if (lane != 0) return;
-#ifdef FMT_DBG_STOP_ENV
-  return;
-#endif
   double vf[4], vb[4], va[4], vc[4];
   int nv = 0;
   for (int i = 0; i < nf; ++i) {
