@@ -10,9 +10,10 @@
 //     same sums evaluated directly, r(k) = sum_i z[i] z[i+k] for the p+1 lags
 //     k = L .. L-p (F11: the array starts at lag -L), one partial per thread
 //   levinsonDurbin (lpc.go:85-135)  lane 0, in place as written
-//   GetSpectralEnvelope (lpc.go:233-265)  513 points across the block
-//   findSpectralPeaks / bandwidth / confidence / validate / spacing / VTL /
-//     quality (format.go:148-411)  lane 0 over the LDS envelope
+//   GetSpectralEnvelope (lpc.go:233-265)  513 points across the block, the angles by
+//     rotation recurrence
+//   findSpectralPeaks / bandwidth / confidence (format.go:148-300)  the first wave, by ballots
+//     with the serial scans' exact outcome; validate / spacing / VTL / quality (:300-411) lane 0
 #include "../../include/sonar_gpu.h"
 #include "kernels.h"
 
