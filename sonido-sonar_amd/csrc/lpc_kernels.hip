@@ -51,7 +51,10 @@ __device__ double block_sum(double v, double* red) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void formant_kernel(const double* pcm, int64_t hop, int W, int p, int sr,
+#ifndef FMT_MIN_BLOCKS
+#define FMT_MIN_BLOCKS 5   // 0.614-0.618 against 0.635-0.641 ms at 1 (profiles/r06bg_formant_minblocks_ab.log)
+#endif
+__global__ __launch_bounds__(256, FMT_MIN_BLOCKS) void formant_kernel(const double* pcm, int64_t hop, int W, int p, int sr,
                                                       int frame_ok_len, const double* ham, sonar_formant_frame* out,
                                                       double* coeffs, double* refl) {
   __shared__ double x[2048];
